@@ -1,0 +1,156 @@
+/* mmvae_capi.h — C-ABI of the MI355X-native mmvae training engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (YPARK/mm-vae) has no FFI: its boundary is the C++ template
+ *   train_vae_model<MODEL_PTR, VISITOR, DATA_BLOCK, LOSS>(...)   include/mmvae_alg.hh:200-210
+ * whose per-batch body (mmvae_alg.hh:264-311) gathers a batch (DATA_BLOCK::read,
+ * include/mmvae_io.hh:208-245), runs MODEL::forward + LOSS + autograd backward +
+ * clip_grad_norm_ + Adam.  Every entry point below replaces one piece of that body; the
+ * comment on each names the reference interface it replaces.  A host loop mirroring
+ * train_vae_model (mm-vae_amd/host/) and the Python binding (mm-vae_amd/py/) sit on top.
+ *
+ * Conventions: plain C types; every call returns 0 on success or a negative MMVAE_E_*
+ * code, with a message retrievable by mmvae_last_error(h) (no exceptions cross the ABI,
+ * replacing the reference's CHK/ASSERT -> exit(1), include/utils/util.hh:35-56).  Host
+ * buffers are caller-owned; device memory is owned by the handle.  One host thread per
+ * handle.  All work is stream-ordered on the handle's HIP stream; the only host syncs are
+ * mmvae_sync() and non-NULL scalar outputs of mmvae_run().
+ */
+#ifndef MMVAE_CAPI_H_
+#define MMVAE_CAPI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mmvae_engine* mmvae_h;
+
+enum {
+    MMVAE_OK = 0,
+    MMVAE_E_ARG = -1,    /* invalid argument / shape mismatch */
+    MMVAE_E_HIP = -2,    /* HIP runtime failure (no device, OOM, launch error) */
+    MMVAE_E_STATE = -3,  /* call out of order (e.g. step before upload) */
+    MMVAE_E_COMM = -4,   /* RCCL failure */
+    MMVAE_E_NAME = -5    /* unknown parameter name */
+};
+
+enum { MMVAE_MODEL_NB = 0, MMVAE_MODEL_VMF = 1 };
+/* Operand precision of the encoder/decoder GEMMs; every epilogue, reduction, gradient and
+ * optimiser update is fp32.  F32 is the parity mode (exact f32 MFMA). */
+enum { MMVAE_DTYPE_F32 = 0, MMVAE_DTYPE_BF16 = 1 };
+
+typedef struct mmvae_cfg {
+    int32_t model;       /* MMVAE_MODEL_NB (src/nb_vae_main.cc) / MMVAE_MODEL_VMF (src/vmf_vae_main.cc) */
+    int32_t dtype;       /* MMVAE_DTYPE_* */
+    int64_t D;           /* genes: data_dim, nb.hh:214 / vmf.hh:200 (= MatrixMarket rows) */
+    int64_t C;           /* covariate dim: covar_dim (1 for the auto ones-file, nb_vae_main.cc:68-73) */
+    int64_t K;           /* NB --mean_latent (nb.hh:59) / vMF --latent (vmf.hh:60) */
+    int64_t H;           /* NB --overdisp_encoding (nb.hh:60); ignored for vMF */
+    int64_t R;           /* NB --overdispersion_latent (nb.hh:61); ignored for vMF */
+    int64_t max_batch;   /* largest B passed to mmvae_run on this handle */
+    float lr;            /* --lr (mmvae_alg.hh:19) default 1e-3 */
+    float weight_decay;  /* AdamOptions.weight_decay, mmvae_alg.hh:236: 1e-4 */
+    float grad_clip;     /* clip_grad_norm_ max norm, mmvae_alg.hh:308 (always 1.0 there: Q7) */
+    float kappa_min;     /* vMF --kappa_min (vmf.hh:61) */
+    float kappa_max;     /* vMF --kappa_max (vmf.hh:62) */
+    uint64_t seed;       /* Philox seed for the reparameterisation noise when none is injected */
+} mmvae_cfg;
+
+/* Fill a cfg with the reference defaults (mmvae_alg.hh:19-23, nb.hh:58-61, vmf.hh:59-63). */
+void mmvae_cfg_default(mmvae_cfg* cfg, int32_t model);
+
+/* Create an engine on HIP device `device`.  Replaces constructing nbvae_t / vmf_vae_t
+ * (nb.hh:299-401, vmf.hh:307-389) plus the torch::optim::Adam of mmvae_alg.hh:234-237.
+ * Parameters start at zero; load them with mmvae_set_param or mmvae_init_params. */
+int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out);
+int mmvae_destroy(mmvae_h h);
+/* Message for the last failing call on h (h may be NULL for mmvae_create failures). */
+const char* mmvae_last_error(mmvae_h h);
+
+/* ---- dataset (HBM-resident) --------------------------------------------------------
+ * Replaces mtx_data_block_t (mmvae_io.hh:49-141) for the data AND the covariate blocks:
+ * instead of re-reading BGZF per batch, the whole cell-major CSR is uploaded once
+ * (rows = cells = MatrixMarket columns, 0-based gene ids, sorted within a row).
+ * covar: [N, C] row-major (NULL -> all ones, the reference's auto covariate). */
+int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
+                     int64_t N, int64_t D, const float* covar);
+/* Device-side synthetic dataset (bench / smoke): SURVEY §8(d) count distribution. */
+int mmvae_synth_csr(mmvae_h h, int64_t N, double lib_size, uint64_t seed, int64_t* nnz_out);
+/* Copy dataset rows back to the host (recorder / CPU baseline sampling).  rowptr_out
+ * [nrows+1]; col/val sized by *nnz_io (in: capacity, out: needed). */
+int mmvae_get_rows(mmvae_h h, const int64_t* rows, int64_t nrows, int64_t* rowptr_out,
+                   int32_t* col_out, float* val_out, int64_t* nnz_io);
+
+/* ---- parameters (names = LibTorch named_parameters() keys) -------------------------
+ * Registered parameters (Adam + clip) keep their reference keys, e.g.
+ * "mu_representation_mean.weight"; the frozen, unregistered Sequentials (Q1) are exposed
+ * as "mu_enc.mu_encoding.weight|bias", "mu_dec.mu_decoding.weight|bias" (NB) and
+ * "z_enc.0.weight", "z_dec.decoding.weight|bias" (vMF). */
+int mmvae_num_params(mmvae_h h, int32_t* count);
+int mmvae_param_info(mmvae_h h, int32_t idx, const char** name, int64_t* numel, int32_t* registered);
+int mmvae_set_param(mmvae_h h, const char* name, const float* host, int64_t numel);
+int mmvae_get_param(mmvae_h h, const char* name, float* host, int64_t numel);
+/* Pre-clip gradient of a registered parameter from the last update step (parity tests). */
+int mmvae_get_grad(mmvae_h h, const char* name, float* host, int64_t numel);
+/* Reference-default initialisation (torch::nn::Linear kaiming-uniform(a=sqrt 5) bounds,
+ * zeros/ones per nb.hh:312-315, vmf.hh:321-323) from a seeded generator. */
+int mmvae_init_params(mmvae_h h, uint64_t seed);
+/* Reset the Adam moments and step counter. */
+int mmvae_reset_optimizer(mmvae_h h);
+
+/* ---- the ELBO step ------------------------------------------------------------------ */
+typedef struct mmvae_step_args {
+    const int64_t* cell_ids;  /* host [B]: dataset rows of this rank's batch (mmvae_alg.hh:264-266) */
+    const int64_t* ridx;      /* host [B] or NULL: bootstrap resample, rows = cell_ids[ridx]
+                                 (mmvae_alg.hh:292-301) */
+    int64_t B;                /* rows on this rank */
+    int64_t n_total;          /* rows over all ranks = the loss divisor n (nb.hh:543); 0 -> B */
+    int64_t row_offset;       /* global index of this rank's first row (noise key) */
+    float beta;               /* KL weight, nb_loss_t / vmf_loss_t (nb_vae_main.cc:26-32) */
+    const float* eps;         /* host noise or NULL (Philox): NB [B*K] then [B*R] (nb.hh:480-492);
+                                 vMF [B*K] (vmf.hh:299) */
+    uint64_t step_id;         /* Philox counter when eps == NULL */
+    int32_t update;           /* 1: forward+backward+all-reduce+clip+Adam (mmvae_alg.hh:303-310)
+                                 0: forward-only train-mode loss (the eval pass, Q12, :277-285) */
+} mmvae_step_args;
+
+/* Run one step.  loss_out (nullable) receives the rank-local loss (sum over this rank's
+ * rows / n_total; sum over ranks = the reference's loss).  total_norm_out (nullable)
+ * receives the clip_grad_norm_ total norm.  Non-NULL outputs synchronise the stream. */
+int mmvae_run(mmvae_h h, const mmvae_step_args* args, float* loss_out, double* total_norm_out);
+
+/* Recorder encoder (nb.hh:419-431 encode_mu(x); vmf.hh:267-281 encode(x)): mean/lnvar
+ * [B*K] row-major, no covariate, no noise. */
+int mmvae_encode(mmvae_h h, const int64_t* cell_ids, int64_t B, float* mean, float* lnvar);
+int mmvae_sync(mmvae_h h);
+
+/* ---- data parallel (RCCL over xGMI) -------------------------------------------------
+ * One process per GPU.  Rank 0 creates the 128-byte unique id and shares it out of band;
+ * every rank then calls mmvae_comm_init.  Afterwards each update step SUM-all-reduces the
+ * registered gradients before clip + Adam (new: the reference has no distribution). */
+int mmvae_comm_unique_id(void* out128);
+int mmvae_comm_init(mmvae_h h, int32_t rank, int32_t world, const void* id128);
+
+/* ---- instrumentation -----------------------------------------------------------------
+ * HIP-event timing of every kernel launch on the handle's stream. */
+int mmvae_timing_enable(mmvae_h h, int32_t on);
+int mmvae_timing_count(mmvae_h h, int32_t* n);
+int mmvae_timing_get(mmvae_h h, int32_t idx, const char** name, double* total_ms, int64_t* launches);
+int mmvae_timing_reset(mmvae_h h);
+
+/* ---- operators.hh (vMF observation model scalars) ----------------------------------
+ * lbessel(kappa, nu): piecewise log I_nu(kappa) approximation (operators.hh:49-101) with
+ * P. Mineiro's fasterlgamma (fastgamma.h:58-60); its custom backward returns the Baricz
+ * bound 0.5(sqrt(k^2 nu/(nu+1)+nu^2)+sqrt(k^2+nu^2))/k, ignoring the upstream gradient
+ * (operators.hh:20-40).  Host scalars, fp32. */
+float mmvae_lbessel(float kappa, float nu);
+float mmvae_lbessel_grad(float kappa, float nu);
+float mmvae_fasterlog(float x);     /* fastlog.h:75-85 */
+float mmvae_fasterlgamma(float x);  /* fastgamma.h:58-60 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMVAE_CAPI_H_ */

@@ -1,0 +1,654 @@
+// C-ABI implementation (include/mmvae_capi.h): handle lifecycle, parameter registry,
+// dataset upload, step orchestration, RCCL gradient all-reduce, kernel timing.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "engine.hpp"
+
+using namespace mmvae;
+
+static thread_local std::string g_last_error;
+
+#define FAIL(e, code, msg)                         \
+    do {                                           \
+        std::string _m = (msg);                    \
+        if (e) (e)->err = _m;                      \
+        g_last_error = _m;                         \
+        return (code);                             \
+    } while (0)
+
+#define HIPCHK(e, expr)                                                                             \
+    do {                                                                                            \
+        hipError_t _er = (expr);                                                                    \
+        if (_er != hipSuccess)                                                                      \
+            FAIL(e, MMVAE_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_er));               \
+    } while (0)
+
+namespace mmvae {
+
+void timer_begin(Engine* e, const char* name, hipEvent_t* a) {
+    auto it = e->timer_index.find(name);
+    int idx;
+    if (it == e->timer_index.end()) {
+        idx = (int)e->timers.size();
+        e->timers.push_back(TimerRec{name, 0.0, 0});
+        e->timer_index[name] = idx;
+    } else {
+        idx = it->second;
+    }
+    hipEvent_t ev0, ev1;
+    if (e->event_pool.size() >= 2) {
+        ev0 = e->event_pool.back();
+        e->event_pool.pop_back();
+        ev1 = e->event_pool.back();
+        e->event_pool.pop_back();
+    } else {
+        hipEventCreate(&ev0);
+        hipEventCreate(&ev1);
+    }
+    hipEventRecord(ev0, e->stream);
+    e->pending.push_back({idx, ev0, ev1});
+    *a = ev1;
+}
+
+void timer_end(Engine* e, hipEvent_t a) { hipEventRecord(a, e->stream); }
+
+}  // namespace mmvae
+
+static void timer_collect(Engine* e) {
+    if (e->pending.empty()) return;
+    hipStreamSynchronize(e->stream);
+    for (auto& p : e->pending) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        e->timers[p.idx].total_ms += ms;
+        e->timers[p.idx].launches += 1;
+        e->event_pool.push_back(p.a);
+        e->event_pool.push_back(p.b);
+    }
+    e->pending.clear();
+}
+
+// ---------------------------------------------------------------------------------------
+// parameter registry — LibTorch named_parameters() order (nb.hh:318-400, vmf.hh:325-388)
+// ---------------------------------------------------------------------------------------
+static void add_slot(Engine* e, const std::string& n, std::vector<int64_t> shape, bool reg) {
+    ParamSlot s;
+    s.name = n;
+    s.shape = shape;
+    s.numel = 1;
+    for (auto v : shape) s.numel *= v;
+    s.registered = reg;
+    if (reg) {
+        s.off = e->P_reg;
+        e->P_reg += s.numel;
+    } else {
+        s.off = e->P_frz;
+        e->P_frz += s.numel;
+    }
+    e->slot_index[n] = (int)e->slots.size();
+    e->slots.push_back(s);
+}
+
+static void build_registry_nb(Engine* e) {
+    const int64_t D = e->D, C = e->C, K = e->K, H = e->H, R = e->R;
+    add_slot(e, "x_mean", {1, D}, true);
+    add_slot(e, "ln_x_sd", {1, D}, true);
+    add_slot(e, "mu_bias", {1, D}, true);
+    add_slot(e, "nu_bias", {1, D}, true);
+    add_slot(e, "covar_encoding.weight", {K, C}, true);
+    add_slot(e, "covar_encoding.bias", {K}, true);
+    add_slot(e, "mu_representation_mean.weight", {K, K}, true);
+    add_slot(e, "mu_representation_mean.bias", {K}, true);
+    add_slot(e, "mu_representation_logvariance.weight", {K, K}, true);
+    add_slot(e, "mu_representation_logvariance.bias", {K}, true);
+    add_slot(e, "covar_decoding.weight", {D, C}, true);
+    add_slot(e, "covar_decoding.bias", {D}, true);
+    add_slot(e, "nu_encoding.weight", {H, D}, true);
+    add_slot(e, "nu_encoding.bias", {H}, true);
+    add_slot(e, "nu_representation_mean.weight", {R, H}, true);
+    add_slot(e, "nu_representation_mean.bias", {R}, true);
+    add_slot(e, "nu_representation_logvariance.weight", {R, H}, true);
+    add_slot(e, "nu_representation_logvariance.bias", {R}, true);
+    add_slot(e, "nu_decoding.weight", {D, R}, true);
+    add_slot(e, "nu_decoding.bias", {D}, true);
+    add_slot(e, "depth.weight", {1, D}, true);
+    add_slot(e, "depth.bias", {1}, true);
+    // frozen Sequentials (Q1: never register_module'd)
+    add_slot(e, "mu_enc.mu_encoding.weight", {K, D}, false);
+    add_slot(e, "mu_enc.mu_encoding.bias", {K}, false);
+    add_slot(e, "mu_dec.mu_decoding.weight", {D, K}, false);
+    add_slot(e, "mu_dec.mu_decoding.bias", {D}, false);
+}
+
+template <class T>
+static hipError_t dalloc(T** p, int64_t n) {
+    return hipMalloc(p, sizeof(T) * (size_t)(n > 0 ? n : 1));
+}
+
+extern "C" {
+
+void mmvae_cfg_default(mmvae_cfg* c, int32_t model) {
+    std::memset(c, 0, sizeof(*c));
+    c->model = model;
+    c->dtype = MMVAE_DTYPE_F32;
+    c->C = 1;
+    c->K = 2;   // --mean_latent / --latent default (nb.hh:59, vmf.hh:60)
+    c->H = 1;
+    c->R = 1;
+    c->max_batch = 100;  // --batch_size default (mmvae.hh:35)
+    c->lr = 1e-3f;
+    c->weight_decay = 1e-4f;
+    c->grad_clip = 1.f;
+    c->kappa_min = 0.1f;
+    c->kappa_max = 10.f;
+    c->seed = 42;
+}
+
+const char* mmvae_last_error(mmvae_h h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+
+int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
+    if (!cfg || !out) FAIL((Engine*)nullptr, MMVAE_E_ARG, "null cfg/out");
+    if (cfg->model != MMVAE_MODEL_NB) FAIL((Engine*)nullptr, MMVAE_E_ARG, "only the NB model is built in this version");
+    if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
+        cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
+    if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32 or BF16");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
+        FAIL((Engine*)nullptr, MMVAE_E_HIP, "no HIP device " + std::to_string(device));
+    mmvae_engine* e = new mmvae_engine();
+    e->cfg = *cfg;
+    e->device = device;
+    HIPCHK(e, hipSetDevice(device));
+    HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    e->D = cfg->D;
+    e->DP = (cfg->D + 63) / 64 * 64;
+    e->NT = e->DP / 64;
+    e->K = cfg->K;
+    e->KP = (cfg->K <= 32) ? 32 : 64;
+    e->C = cfg->C;
+    e->H = cfg->H;
+    e->R = cfg->R;
+    e->Bmax = cfg->max_batch;
+    e->Bpad = (cfg->max_batch + 63) / 64 * 64;
+    e->nrb_max = e->Bpad / 64;
+    build_registry_nb(e);
+
+    // gene splits: enough workgroups to fill 256 CUs twice, LDS column accumulators <= 40 KB
+    auto pick_split = [&](int nq) {
+        int ns = (int)((512 + e->nrb_max - 1) / e->nrb_max);
+        if (ns < 1) ns = 1;
+        const int tps_max = (int)(40 * 1024 / (nq * 64 * 4));
+        const int ns_min = (int)((e->NT + tps_max - 1) / tps_max);
+        if (ns < ns_min) ns = ns_min;
+        if (ns > e->NT) ns = (int)e->NT;
+        if (ns > 64) ns = 64;
+        return ns;
+    };
+    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R));
+    e->nsplit_e = pick_split((int)(2 + e->H));
+    e->n_lat_wg = (int)((e->Bpad + 31) / 32);
+    e->klp_off = e->nrb_max * e->nsplit_d;
+
+    // latent state layout
+    int64_t o = 0;
+    e->LAT_H = o; o += e->K;
+    e->LAT_MEAN = o; o += e->K;
+    e->LAT_A = o; o += e->K;
+    e->LAT_EPS = o; o += e->K;
+    e->LAT_NMEAN = o; o += e->R;
+    e->LAT_AN = o; o += e->R;
+    e->LAT_EPSN = o; o += e->R;
+    e->LAT_ZNU = o; o += e->R;
+    e->LAT_D = o; o += 1;
+    e->LAT_W = o; o += 1;
+    e->LAT_VALID = o; o += 1;
+    e->LAT_HNU = o; o += e->H + 1;  // dhnu[H], dpre
+    e->lat_stride = o;
+
+    const int64_t Bp = e->Bpad, DP = e->DP, KP = e->KP, nrb = e->nrb_max;
+    const int64_t SMALL = 2 * e->K * e->K + 2 * e->K + e->K * e->C + e->K + 2 * e->R * e->H + 2 * e->R + e->H + 1;
+    HIPCHK(e, dalloc(&e->d_params, e->P_reg));
+    HIPCHK(e, dalloc(&e->d_grads, e->P_reg));
+    HIPCHK(e, dalloc(&e->d_m, e->P_reg));
+    HIPCHK(e, dalloc(&e->d_v, e->P_reg));
+    HIPCHK(e, dalloc(&e->d_frozen, e->P_frz));
+    HIPCHK(e, hipMemset(e->d_params, 0, sizeof(float) * e->P_reg));
+    HIPCHK(e, hipMemset(e->d_grads, 0, sizeof(float) * e->P_reg));
+    HIPCHK(e, hipMemset(e->d_m, 0, sizeof(float) * e->P_reg));
+    HIPCHK(e, hipMemset(e->d_v, 0, sizeof(float) * e->P_reg));
+    HIPCHK(e, hipMemset(e->d_frozen, 0, sizeof(float) * e->P_frz));
+    HIPCHK(e, dalloc(&e->d_WeP_f, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WeP_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdP_f, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdP_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdT_f, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdT_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_cells, Bp));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, sizeof(int64_t) * Bp));
+    HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
+    HIPCHK(e, dalloc(&e->d_gene, 3 * DP));
+    HIPCHK(e, dalloc(&e->d_mvec, KP));
+    HIPCHK(e, dalloc(&e->d_rtp, Bp * (e->NT + 1)));
+    HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
+    HIPCHK(e, dalloc(&e->d_hpart, (int64_t)e->nsplit_e * Bp * KP));
+    HIPCHK(e, dalloc(&e->d_lat, Bp * e->lat_stride));
+    HIPCHK(e, dalloc(&e->d_zf, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_zb, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_d * Bp * 2));
+    HIPCHK(e, dalloc(&e->d_rowB, (int64_t)e->nsplit_d * Bp * (2 + e->R)));
+    HIPCHK(e, dalloc(&e->d_dzp, (int64_t)e->nsplit_d * Bp * 2 * KP));
+    HIPCHK(e, dalloc(&e->d_dh, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_dhT_f, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_dhT_b, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_slabB, nrb * ((1 + e->C) + 1 + e->R) * DP));
+    HIPCHK(e, dalloc(&e->d_slabC, nrb * (1 + e->C) * DP));
+    HIPCHK(e, dalloc(&e->d_slabE, nrb * (2 + e->H) * DP));
+    HIPCHK(e, dalloc(&e->d_lossp, e->klp_off + e->n_lat_wg));
+    HIPCHK(e, dalloc(&e->d_small, (int64_t)e->n_lat_wg * SMALL));
+    HIPCHK(e, dalloc(&e->d_smallg, 128));
+    HIPCHK(e, dalloc(&e->d_sumsq, 256));
+    HIPCHK(e, dalloc(&e->d_out, 4));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4));
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming));
+    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    *out = e;
+    return MMVAE_OK;
+}
+
+int mmvae_destroy(mmvae_h e) {
+    if (!e) return MMVAE_OK;
+    hipSetDevice(e->device);
+    hipStreamSynchronize(e->stream);
+    if (e->comm) ncclCommDestroy(e->comm);
+    void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
+                    e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b,
+                    e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
+                    e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
+                    e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
+                    e->d_out, e->d_tmp};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    if (e->h_cells_pin) hipHostFree(e->h_cells_pin);
+    if (e->h_eps_pin) hipHostFree(e->h_eps_pin);
+    if (e->h_out_pin) hipHostFree(e->h_out_pin);
+    for (auto ev : e->event_pool) hipEventDestroy(ev);
+    for (auto& p : e->pending) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    if (e->ev_staged) hipEventDestroy(e->ev_staged);
+    hipStreamDestroy(e->stream);
+    delete e;
+    return MMVAE_OK;
+}
+
+int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                     int64_t D, const float* covar) {
+    if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
+    if (D != e->D) FAIL(e, MMVAE_E_ARG, "upload_csr: D does not match the model's data_dim");
+    if (rowptr[0] != 0) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr[0] must be 0");
+    for (int64_t i = 0; i < N; ++i) {
+        if (rowptr[i + 1] < rowptr[i]) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr not monotone");
+        for (int64_t j = rowptr[i]; j < rowptr[i + 1]; ++j) {
+            if (col[j] < 0 || col[j] >= D) FAIL(e, MMVAE_E_ARG, "upload_csr: gene index out of range");
+            if (j > rowptr[i] && col[j] <= col[j - 1])
+                FAIL(e, MMVAE_E_ARG, "upload_csr: gene indices must be strictly increasing within a row");
+        }
+    }
+    const int64_t nnz = rowptr[N];
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    hipFree(e->d_rowptr);
+    hipFree(e->d_col);
+    hipFree(e->d_val);
+    hipFree(e->d_covar);
+    e->d_rowptr = nullptr;
+    e->d_col = nullptr;
+    e->d_val = nullptr;
+    e->d_covar = nullptr;
+    HIPCHK(e, dalloc(&e->d_rowptr, N + 1));
+    HIPCHK(e, dalloc(&e->d_col, nnz));
+    HIPCHK(e, dalloc(&e->d_val, nnz));
+    HIPCHK(e, dalloc(&e->d_covar, N * e->C));
+    HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice));
+    if (nnz > 0) {
+        HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_val, val, sizeof(float) * nnz, hipMemcpyHostToDevice));
+    }
+    if (covar) {
+        HIPCHK(e, hipMemcpy(e->d_covar, covar, sizeof(float) * N * e->C, hipMemcpyHostToDevice));
+    } else {
+        std::vector<float> ones((size_t)(N * e->C), 1.f);
+        HIPCHK(e, hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice));
+    }
+    e->N = N;
+    e->nnz = nnz;
+    return MMVAE_OK;
+}
+
+int mmvae_synth_csr(mmvae_h e, int64_t N, double lib_size, uint64_t seed, int64_t* nnz_out) {
+    if (!e || N < 1 || lib_size <= 0) FAIL(e, MMVAE_E_ARG, "synth_csr: bad arguments");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, synth_dataset(e, N, lib_size, seed, nnz_out));
+    return MMVAE_OK;
+}
+
+int mmvae_get_rows(mmvae_h e, const int64_t* rows, int64_t nrows, int64_t* rowptr_out, int32_t* col_out,
+                   float* val_out, int64_t* nnz_io) {
+    if (!e || !rows || !rowptr_out || !nnz_io) FAIL(e, MMVAE_E_ARG, "get_rows: bad arguments");
+    if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "get_rows: no dataset");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    std::vector<int64_t> rp(e->N + 1);
+    HIPCHK(e, hipMemcpy(rp.data(), e->d_rowptr, sizeof(int64_t) * (e->N + 1), hipMemcpyDeviceToHost));
+    int64_t need = 0;
+    rowptr_out[0] = 0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (rows[i] < 0 || rows[i] >= e->N) FAIL(e, MMVAE_E_ARG, "get_rows: row out of range");
+        need += rp[rows[i] + 1] - rp[rows[i]];
+        rowptr_out[i + 1] = need;
+    }
+    if (need > *nnz_io || !col_out || !val_out) {
+        *nnz_io = need;
+        return MMVAE_OK;
+    }
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t a = rp[rows[i]], n = rp[rows[i] + 1] - a;
+        if (n == 0) continue;
+        HIPCHK(e, hipMemcpy(col_out + rowptr_out[i], e->d_col + a, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(val_out + rowptr_out[i], e->d_val + a, sizeof(float) * n, hipMemcpyDeviceToHost));
+    }
+    *nnz_io = need;
+    return MMVAE_OK;
+}
+
+int mmvae_num_params(mmvae_h e, int32_t* count) {
+    if (!e || !count) FAIL(e, MMVAE_E_ARG, "num_params: null");
+    *count = (int32_t)e->slots.size();
+    return MMVAE_OK;
+}
+
+int mmvae_param_info(mmvae_h e, int32_t idx, const char** name, int64_t* numel, int32_t* registered) {
+    if (!e || idx < 0 || idx >= (int)e->slots.size()) FAIL(e, MMVAE_E_ARG, "param_info: index out of range");
+    const ParamSlot& s = e->slots[idx];
+    if (name) *name = s.name.c_str();
+    if (numel) *numel = s.numel;
+    if (registered) *registered = s.registered ? 1 : 0;
+    return MMVAE_OK;
+}
+
+static int find_slot(Engine* e, const char* name, int64_t numel, const ParamSlot** out) {
+    if (!name) FAIL(e, MMVAE_E_ARG, "null parameter name");
+    const ParamSlot* s = e->slot(name);
+    if (!s) FAIL(e, MMVAE_E_NAME, std::string("unknown parameter ") + name);
+    if (numel != s->numel)
+        FAIL(e, MMVAE_E_ARG, std::string("numel mismatch for ") + name + ": expected " + std::to_string(s->numel));
+    *out = s;
+    return MMVAE_OK;
+}
+
+int mmvae_set_param(mmvae_h e, const char* name, const float* host, int64_t numel) {
+    if (!e || !host) FAIL(e, MMVAE_E_ARG, "set_param: null");
+    const ParamSlot* s;
+    int rc = find_slot(e, name, numel, &s);
+    if (rc) return rc;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    float* dst = s->registered ? e->d_params + s->off : e->d_frozen + s->off;
+    HIPCHK(e, hipMemcpy(dst, host, sizeof(float) * numel, hipMemcpyHostToDevice));
+    if (!s->registered) e->frozen_dirty = true;
+    return MMVAE_OK;
+}
+
+int mmvae_get_param(mmvae_h e, const char* name, float* host, int64_t numel) {
+    if (!e || !host) FAIL(e, MMVAE_E_ARG, "get_param: null");
+    const ParamSlot* s;
+    int rc = find_slot(e, name, numel, &s);
+    if (rc) return rc;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const float* src = s->registered ? e->d_params + s->off : e->d_frozen + s->off;
+    HIPCHK(e, hipMemcpy(host, src, sizeof(float) * numel, hipMemcpyDeviceToHost));
+    return MMVAE_OK;
+}
+
+int mmvae_get_grad(mmvae_h e, const char* name, float* host, int64_t numel) {
+    if (!e || !host) FAIL(e, MMVAE_E_ARG, "get_grad: null");
+    const ParamSlot* s;
+    int rc = find_slot(e, name, numel, &s);
+    if (rc) return rc;
+    if (!s->registered) FAIL(e, MMVAE_E_ARG, std::string(name) + " is frozen (unregistered, Q1): no gradient");
+    if (!e->have_grads) FAIL(e, MMVAE_E_STATE, "get_grad: no update step has run");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(host, e->d_grads + s->off, sizeof(float) * numel, hipMemcpyDeviceToHost));
+    return MMVAE_OK;
+}
+
+int mmvae_init_params(mmvae_h e, uint64_t seed) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "init_params: null");
+    std::mt19937_64 rng(seed);
+    // fan_in of each weight; biases share their layer's bound (torch::nn::Linear::reset_parameters)
+    auto fan_in_of = [&](const ParamSlot& s) -> int64_t {
+        std::string base = s.name.substr(0, s.name.rfind('.'));
+        const ParamSlot* w = e->slot(base + ".weight");
+        if (!w || w->shape.size() < 2) return 1;
+        return w->shape[1];
+    };
+    for (const ParamSlot& s : e->slots) {
+        std::vector<float> v((size_t)s.numel, 0.f);
+        if (s.name == "ln_x_sd") {
+            std::fill(v.begin(), v.end(), 1.f);
+        } else if (s.name == "x_mean" || s.name == "mu_bias" || s.name == "nu_bias") {
+            // zeros (nb.hh:312-315)
+        } else {
+            const double bound = 1.0 / std::sqrt((double)fan_in_of(s));
+            std::uniform_real_distribution<float> U((float)-bound, (float)bound);
+            for (auto& x : v) x = U(rng);
+        }
+        int rc = mmvae_set_param(e, s.name.c_str(), v.data(), s.numel);
+        if (rc) return rc;
+    }
+    return mmvae_reset_optimizer(e);
+}
+
+int mmvae_reset_optimizer(mmvae_h e) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "reset_optimizer: null");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemsetAsync(e->d_m, 0, sizeof(float) * e->P_reg, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d_v, 0, sizeof(float) * e->P_reg, e->stream));
+    e->adam_step = 0;
+    return MMVAE_OK;
+}
+
+static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B) {
+    // wait until the previous step's H2D copies have consumed the pinned staging buffers
+    HIPCHK(e, hipEventSynchronize(e->ev_staged));
+    for (int64_t j = 0; j < B; ++j) {
+        int64_t r = j;
+        if (ridx) {
+            r = ridx[j];
+            if (r < 0 || r >= B) FAIL(e, MMVAE_E_ARG, "ridx out of range [0, B)");
+        }
+        const int64_t c = cell_ids[r];
+        if (c < 0 || c >= e->N) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
+        e->h_cells_pin[j] = c;
+    }
+    const int64_t Bp = (B + 63) / 64 * 64;
+    for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = -1;
+    HIPCHK(e, hipMemcpyAsync(e->d_cells, e->h_cells_pin, sizeof(int64_t) * Bp, hipMemcpyHostToDevice, e->stream));
+    return MMVAE_OK;
+}
+
+int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* total_norm_out) {
+    if (!e || !a || !a->cell_ids) FAIL(e, MMVAE_E_ARG, "run: null arguments");
+    if (a->B < 1 || a->B > e->Bmax) FAIL(e, MMVAE_E_ARG, "run: B must be in [1, max_batch]");
+    if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "run: no dataset uploaded");
+    const int64_t n_total = a->n_total > 0 ? a->n_total : a->B;
+    HIPCHK(e, hipSetDevice(e->device));
+    int rc = stage_rows(e, a->cell_ids, a->ridx, a->B);
+    if (rc) return rc;
+    if (a->eps) {
+        const int64_t ne = a->B * (e->K + e->R);
+        std::memcpy(e->h_eps_pin, a->eps, sizeof(float) * ne);
+        HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
+    }
+    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
+                                  a->row_offset));
+    if (a->update) {
+        if (e->comm && e->world > 1) {
+            ScopedTimer tm(e, "allreduce_grads");
+            if (ncclAllReduce(e->d_grads, e->d_grads, (size_t)e->P_reg, ncclFloat, ncclSum, e->comm, e->stream) !=
+                ncclSuccess)
+                FAIL(e, MMVAE_E_COMM, "ncclAllReduce failed");
+        }
+        HIPCHK(e, opt_clip_adam(e));
+        e->have_grads = true;
+    }
+    if (loss_out || total_norm_out) {
+        HIPCHK(e, hipMemcpyAsync(e->h_out_pin, e->d_out, sizeof(float) * 2, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (loss_out) *loss_out = e->h_out_pin[0];
+        if (total_norm_out) *total_norm_out = a->update ? (double)e->h_out_pin[1] : 0.0;
+    }
+    if (e->timing) timer_collect(e);
+    return MMVAE_OK;
+}
+
+int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, float* lnvar) {
+    if (!e || !cell_ids || !mean || !lnvar) FAIL(e, MMVAE_E_ARG, "encode: null arguments");
+    if (B < 1 || B > e->Bmax) FAIL(e, MMVAE_E_ARG, "encode: B must be in [1, max_batch]");
+    if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "encode: no dataset uploaded");
+    HIPCHK(e, hipSetDevice(e->device));
+    int rc = stage_rows(e, cell_ids, nullptr, B);
+    if (rc) return rc;
+    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
+    HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
+    HIPCHK(e, hipMemcpyAsync(mean, e->d_tmp, sizeof(float) * B * e->K, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(lnvar, e->d_tmp + e->Bpad * e->K, sizeof(float) * B * e->K, hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MMVAE_OK;
+}
+
+int mmvae_sync(mmvae_h e) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "sync: null");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->timing) timer_collect(e);
+    return MMVAE_OK;
+}
+
+int mmvae_comm_unique_id(void* out128) {
+    if (!out128) FAIL((Engine*)nullptr, MMVAE_E_ARG, "comm_unique_id: null");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) FAIL((Engine*)nullptr, MMVAE_E_COMM, "ncclGetUniqueId failed");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(out128, &id, 128);
+    return MMVAE_OK;
+}
+
+int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
+    if (!e || !id128 || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
+    HIPCHK(e, hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, 128);
+    if (e->comm) {
+        ncclCommDestroy(e->comm);
+        e->comm = nullptr;
+    }
+    ncclResult_t r = ncclCommInitRank(&e->comm, world, id, rank);
+    if (r != ncclSuccess) FAIL(e, MMVAE_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    e->rank = rank;
+    e->world = world;
+    return MMVAE_OK;
+}
+
+int mmvae_timing_enable(mmvae_h e, int32_t on) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "timing_enable: null");
+    if (!on) timer_collect(e);
+    e->timing = on != 0;
+    return MMVAE_OK;
+}
+
+int mmvae_timing_count(mmvae_h e, int32_t* n) {
+    if (!e || !n) FAIL(e, MMVAE_E_ARG, "timing_count: null");
+    timer_collect(e);
+    *n = (int32_t)e->timers.size();
+    return MMVAE_OK;
+}
+
+int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms, int64_t* launches) {
+    if (!e || idx < 0 || idx >= (int)e->timers.size()) FAIL(e, MMVAE_E_ARG, "timing_get: index out of range");
+    if (name) *name = e->timers[idx].name.c_str();
+    if (total_ms) *total_ms = e->timers[idx].total_ms;
+    if (launches) *launches = e->timers[idx].launches;
+    return MMVAE_OK;
+}
+
+int mmvae_timing_reset(mmvae_h e) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "timing_reset: null");
+    timer_collect(e);
+    for (auto& t : e->timers) {
+        t.total_ms = 0;
+        t.launches = 0;
+    }
+    return MMVAE_OK;
+}
+
+// ---- operators.hh scalars (host, fp32) -------------------------------------------------
+// Bit-level restatement of P. Mineiro's fasterlog / fasterlgamma (reference
+// include/utils/fastlog.h:75-85, fastgamma.h:58-60); pinned bit-exactly by tests against
+// the reference headers compiled in oracle/_ref.
+float mmvae_fasterlog(float x) {
+    uint32_t i;
+    std::memcpy(&i, &x, 4);
+    volatile float y = (float)i;
+    y = y * 8.2629582881927490e-8f;
+    return y - 87.989971088f;
+}
+
+float mmvae_fasterlgamma(float x) {
+    volatile float a = -0.0810614667f - x;
+    a = a - mmvae_fasterlog(x);
+    volatile float b = (0.5f + x) * mmvae_fasterlog(1.0f + x);
+    return a + b;
+}
+
+// operators.hh:49-101 (forward) for a scalar kappa; nu = df
+float mmvae_lbessel(float kappa, float nu) {
+    const double nud = nu;
+    const float eta = (float)((nud + 0.5) / (2. * (nud + 1.)));
+    const float lk = std::log(kappa);
+    // stuff1 = nu*log(k) + eta*k - (eta+nu)*log(2) - fasterlgamma(nu+1): ATen float ops with
+    // double scalars rounded to float
+    float s1 = (float)nud * lk;
+    s1 = s1 + eta * kappa;
+    s1 = s1 - (float)(((double)eta + nud) * std::log(2.));
+    s1 = s1 - mmvae_fasterlgamma((float)(nud + 1));
+    float s2 = kappa - 0.5f * lk;
+    s2 = s2 - (float)(0.5 * std::log(2. * M_PI));
+    return (kappa <= nu) ? s1 : s2;
+}
+
+// operators.hh:20-40: Baricz bound, independent of the upstream gradient (Q3)
+float mmvae_lbessel_grad(float kappa, float nu) {
+    const float df = nu;
+    const float lb = std::sqrt(kappa * kappa * df / (float)(df + 1.) + df * df);
+    const float ub = std::sqrt(kappa * kappa + df * df);
+    return 0.5f * (lb + ub) / kappa;
+}
+
+}  // extern "C"

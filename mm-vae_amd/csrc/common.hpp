@@ -1,0 +1,164 @@
+// Shared device helpers for the mmvae HIP engine (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MMVAE_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------------------
+// MFMA policy: both policies produce 16x16 f32 tiles with the same C/D layout
+//   col = lane & 15, row = 4 * (lane >> 4) + reg       (cdna_hip_programming.md §3)
+// A[row][k] / B[k][col]: lane supplies row/col (lane & 15) and EPL consecutive k starting
+// at KSTEP * s + EPL * (lane >> 4).
+// ---------------------------------------------------------------------------------------
+template <class T> struct MM;
+
+template <> struct MM<float> {
+    static constexpr int KSTEP = 4, EPL = 1;
+    typedef float frag;
+    static MMVAE_DEV frag load(const float* p) { return *p; }
+    static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static MMVAE_DEV frag zero() { return 0.f; }
+};
+
+template <> struct MM<__bf16> {
+    static constexpr int KSTEP = 32, EPL = 8;
+    typedef bf16x8 frag;
+    static MMVAE_DEV frag load(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+    static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static MMVAE_DEV frag zero() {
+        frag z;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
+        return z;
+    }
+};
+
+template <class T> MMVAE_DEV T to_t(float v);
+template <> MMVAE_DEV float to_t<float>(float v) { return v; }
+template <> MMVAE_DEV __bf16 to_t<__bf16>(float v) { return (__bf16)v; }
+
+// ---------------------------------------------------------------------------------------
+// Scalar math.  fast exp/log/rcp map to v_exp_f32 / v_log_f32 / v_rcp_f32 (quarter rate).
+// ---------------------------------------------------------------------------------------
+MMVAE_DEV float fexp(float x) { return __expf(x); }
+MMVAE_DEV float flog(float x) { return __logf(x); }
+MMVAE_DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// log(1 + r) for r >= 0, accurate for small r (series below 1e-2, else log(1+r): rel err <= 6e-6)
+MMVAE_DEV float log1p_pos(float r) {
+    float series = r * (1.f - r * (0.5f - r * (0.33333334f - r * (0.25f - r * 0.2f))));
+    return (r < 1e-2f) ? series : flog(1.f + r);
+}
+
+// torch softplus(beta=1, threshold=20) forward; also returns e = exp(min(u,20)) for backward.
+MMVAE_DEV float softplus_e(float u, float& e) {
+    e = fexp(fminf(u, 20.f));
+    return (u > 20.f) ? u : log1p_pos(e);
+}
+// torch softplus backward factor: u > 20 ? 1 : e / (1 + e)
+MMVAE_DEV float dsoftplus_e(float u, float e) { return (u > 20.f) ? 1.f : e * frcp(1.f + e); }
+
+// accurate torch softplus (libm log1p/exp), for per-row / per-gene scalars
+MMVAE_DEV float softplus_acc(float u) { return (u > 20.f) ? u : log1pf(expf(u)); }
+
+MMVAE_DEV float softplus(float u) {
+    float e;
+    return softplus_e(u, e);
+}
+MMVAE_DEV float dsoftplus(float u) { return (u > 20.f) ? 1.f : 1.f / (1.f + expf(-u)); }
+
+// digamma for v > 0: upward recurrence to v >= 6 then the asymptotic series
+MMVAE_DEV float digammaf_(float v) {
+    float r = 0.f;
+    while (v < 6.f) {
+        r -= 1.f / v;
+        v += 1.f;
+    }
+    float f = 1.f / (v * v);
+    float t = f * (1.f / 12 - f * (1.f / 120 - f * (1.f / 252 - f * (1.f / 240 - f * (1.f / 132)))));
+    return r + logf(v) - 0.5f / v - t;
+}
+
+// NB gamma terms for count x > 0 and overdispersion nup > 0:
+//   lgd = lgamma(nup) + lgamma(x + 1) - lgamma(nup + x)      (nb.hh:522-523)
+//   dgd = digamma(nup) - digamma(nup + x)                    (its d/d nup)
+// Integer counts up to 16 use the exact finite products/sums; other values use lgammaf.
+MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
+    if (x <= 16.f && x == floorf(x)) {
+        int n = (int)x;
+        float lsum = 0.f, rsum = 0.f, lfact = 0.f, prod = 1.f, fprod = 1.f;
+        for (int i = 0; i < n; ++i) {
+            float v = nup + (float)i;
+            rsum += 1.f / v;
+            prod *= v;
+            fprod *= (float)(i + 1);
+            if ((i & 3) == 3) {
+                lsum += logf(prod);
+                lfact += logf(fprod);
+                prod = 1.f;
+                fprod = 1.f;
+            }
+        }
+        lsum += logf(prod);
+        lfact += logf(fprod);
+        lgd = lfact - lsum;
+        dgd = -rsum;
+    } else {
+        lgd = lgammaf(nup) + lgammaf(x + 1.f) - lgammaf(nup + x);
+        dgd = digammaf_(nup) - digammaf_(nup + x);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave64 reductions
+// ---------------------------------------------------------------------------------------
+MMVAE_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+MMVAE_DEV double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 counter RNG + Box-Muller: eps(seed, step, row, k) ~ N(0,1).  Keyed by the
+// GLOBAL row so data-parallel shards draw the same noise as a single-GPU run.
+// ---------------------------------------------------------------------------------------
+MMVAE_DEV void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+MMVAE_DEV float philox_normal(uint64_t seed, uint64_t step, uint64_t row, uint32_t k) {
+    uint32_t c[4] = {(uint32_t)(k >> 1), (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)step,
+                     (uint32_t)(step >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float u1 = ((c[0] >> 8) + 1) * (1.f / 16777217.f);  // (0,1]
+    float u2 = (c[1] >> 8) * (1.f / 16777216.f);        // [0,1)
+    float r = sqrtf(-2.f * logf(u1));
+    float a = 6.2831853071795864f * u2;
+    return (k & 1) ? r * sinf(a) : r * cosf(a);
+}

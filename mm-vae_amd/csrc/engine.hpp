@@ -1,0 +1,159 @@
+// Internal state of one mmvae engine handle (one HIP device, one stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mmvae_capi.h"
+
+namespace mmvae {
+
+struct ParamSlot {
+    std::string name;
+    std::vector<int64_t> shape;
+    int64_t off = 0;     // offset into the flat registered buffer (registered) or frozen buffer
+    int64_t numel = 0;
+    bool registered = true;
+};
+
+struct TimerRec {
+    std::string name;
+    double total_ms = 0;
+    int64_t launches = 0;
+};
+
+// Device buffers are plain hipMalloc allocations owned by the engine.
+struct Engine {
+    mmvae_cfg cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // ---- shapes ----
+    int64_t D = 0, DP = 0, NT = 0;  // genes, padded to 64, #64-gene tiles
+    int64_t K = 0, KP = 0;          // latent, padded (32 or 64)
+    int64_t C = 1, H = 1, R = 1;
+    int64_t Bmax = 0, Bpad = 0;     // max rows, padded to 64
+    int64_t nrb_max = 0;            // row blocks of 64 at Bmax
+
+    // ---- dataset ----
+    int64_t N = 0, nnz = 0;
+    int64_t* d_rowptr = nullptr;
+    int32_t* d_col = nullptr;
+    float* d_val = nullptr;
+    float* d_covar = nullptr;  // [N][C]
+
+    // ---- parameters ----
+    std::vector<ParamSlot> slots;
+    std::map<std::string, int> slot_index;
+    int64_t P_reg = 0, P_frz = 0;
+    float* d_params = nullptr;  // registered, LibTorch order
+    float* d_grads = nullptr;
+    float* d_m = nullptr;
+    float* d_v = nullptr;
+    float* d_frozen = nullptr;  // frozen Sequentials (f32, reference layout)
+    int64_t adam_step = 0;
+    bool frozen_dirty = true;
+    bool have_grads = false;
+
+    // prepared frozen operand copies (rebuilt when frozen params change)
+    float* d_WeP_f = nullptr;   // [KP][DP] encoder weight, zero padded
+    __bf16* d_WeP_b = nullptr;
+    float* d_WdP_f = nullptr;   // [DP][KP] decoder weight (gene-major)
+    __bf16* d_WdP_b = nullptr;
+    float* d_WdT_f = nullptr;   // [KP][DP] decoder weight transposed
+    __bf16* d_WdT_b = nullptr;
+
+    // ---- per-step workspace ----
+    int64_t* d_cells = nullptr;      // [Bpad] gathered dataset rows (-1 = padding)
+    int64_t* h_cells_pin = nullptr;  // pinned staging
+    float* d_eps = nullptr;          // [Bpad][K] + [Bpad][R]
+    float* h_eps_pin = nullptr;
+    float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]
+    float* d_mvec = nullptr;         // [KP]
+    int32_t* d_rtp = nullptr;        // [Bpad][NT+1] row tile pointers (relative to row start)
+    float* d_rowx = nullptr;         // [Bpad][2+H]  pre_depth, lnorm2, hnu[H]
+    float* d_hpart = nullptr;        // [nsplitE][Bpad][KP]
+    float* d_lat = nullptr;          // latent state, see LAT_* offsets
+    float* d_zf = nullptr;           // [Bpad][KP]
+    __bf16* d_zb = nullptr;
+    float* d_lsep = nullptr;         // [nsplit][Bpad][2]
+    float* d_rowB = nullptr;         // [nsplit][Bpad][2+R]
+    float* d_dzp = nullptr;          // [nsplit][Bpad][2][KP]
+    float* d_dh = nullptr;           // [Bpad][KP]
+    float* d_dhT_f = nullptr;        // [KP][Bpad]
+    __bf16* d_dhT_b = nullptr;
+    float* d_slabB = nullptr;        // [nrb][nqB][DP]
+    float* d_slabC = nullptr;        // [nrb][1+C][DP]
+    float* d_slabE = nullptr;        // [nrb][2+H][DP]
+    float* d_lossp = nullptr;        // loss partials
+    float* d_small = nullptr;        // latent-bwd WG partials
+    float* d_smallg = nullptr;       // reduced small grads scratch (colsum_dh etc.)
+    double* d_sumsq = nullptr;       // sum-of-squares partials
+    float* d_out = nullptr;          // [0] loss, [1] total norm (float)
+    float* h_out_pin = nullptr;
+
+    int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder grids
+    int n_lat_wg = 1;                // latent kernels' workgroups
+    int64_t klp_off = 0;             // offset of KL partials inside d_lossp
+    hipEvent_t ev_staged = nullptr;  // last H2D copy out of the pinned staging buffers
+    float* d_tmp = nullptr;          // encode outputs
+
+    // ---- comm ----
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+
+    // ---- timing ----
+    bool timing = false;
+    std::vector<TimerRec> timers;
+    std::map<std::string, int> timer_index;
+    struct Pending { int idx; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+
+    // latent state layout (floats per row)
+    int64_t lat_stride = 0;
+    int64_t LAT_H = 0, LAT_MEAN = 0, LAT_A = 0, LAT_EPS = 0, LAT_NMEAN = 0, LAT_AN = 0,
+            LAT_EPSN = 0, LAT_ZNU = 0, LAT_D = 0, LAT_W = 0, LAT_VALID = 0, LAT_HNU = 0;
+
+    const ParamSlot* slot(const std::string& n) const {
+        auto it = slot_index.find(n);
+        return it == slot_index.end() ? nullptr : &slots[it->second];
+    }
+    float* preg(const std::string& n) const { return d_params + slot(n)->off; }
+    float* greg(const std::string& n) const { return d_grads + slot(n)->off; }
+    float* pfrz(const std::string& n) const { return d_frozen + slot(n)->off; }
+};
+
+// timing helpers (capi.hip)
+void timer_begin(Engine* e, const char* name, hipEvent_t* a);
+void timer_end(Engine* e, hipEvent_t a);
+
+struct ScopedTimer {
+    Engine* e;
+    hipEvent_t a = nullptr;
+    int idx = -1;
+    ScopedTimer(Engine* e_, const char* name) : e(e_) {
+        if (e->timing) timer_begin(e, name, &a);
+    }
+    ~ScopedTimer() {
+        if (e->timing && a) timer_end(e, a);
+    }
+};
+
+// NB launchers (nb_kernels.hip)
+hipError_t nb_prepare_frozen(Engine* e);
+hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
+                               bool use_eps, uint64_t step_id, int64_t row_offset);
+hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
+// optimiser (opt_kernels.hip)
+hipError_t opt_clip_adam(Engine* e);
+hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
+
+}  // namespace mmvae
+
+// the opaque C handle is the engine itself
+struct mmvae_engine : public mmvae::Engine {};

@@ -1,0 +1,1330 @@
+// NB-VAE ELBO step on gfx950: hand-written HIP kernels for the reference's hot path
+//   forward  nb.hh:403-508  (encode_mu, reparameterize, decode_mu, encode_nu, decode_nu, depth)
+//   loss     nb.hh:510-548  (nllik_loss, kl_loss, loss)
+//   backward (LibTorch autograd in the reference, mmvae_alg.hh:307) — hand-derived here; the
+//            algebra is restated in oracle/nb_analytic.py and proven equal to autograd there.
+//
+// Data layout in HBM: dataset = cell-major CSR (int64 rowptr, int32 gene,
+// f32 count); frozen encoder weight stored [KP][DP], frozen decoder weight stored both
+// [DP][KP] (logit GEMM operand) and [KP][DP] (dz GEMM operand), bf16 or f32.  The dense
+// [B,D] batch of the reference (mmvae_io.hh:208-245) is never materialised in HBM: every
+// kernel densifies one 16-cell x 64-gene tile at a time into LDS from the CSR.
+//
+// Kernel chain per step (one stream):
+//   k_prep        per-gene constants (softplus(ln_x_sd), bias sums), encoder mean term
+//   k_rowscan     one wave per cell row: tile pointers + raw-x sparse dots (depth, nu_enc)
+//   k_enc_fwd     densify log1p(x)/sd tiles in LDS -> MFMA with the frozen encoder
+//   k_latent_fwd  K x K heads, clamp, reparameterise (Philox or injected eps), KL
+//   k_dec<A>      logit GEMM (MFMA) + online max/sum-exp per cell        (pass A)
+//   k_dec<B>      logit GEMM + softmax + NB likelihood + every gradient term that needs only
+//                 the log-sum-exp; dz GEMM on MFMA from LDS-staged p*q, p  (pass B)
+//   k_dec<C>      logit GEMM + exp + column sums weighted by the row term E_b (pass C)
+//   k_latent_bwd  latent heads backward, KL grads, dh
+//   k_enc_bwd     dh^T x log1p(x) tiles on MFMA -> ln_x_sd grad; raw-x column sums
+//   k_grad_small / k_grad_genes   deterministic slab reductions -> flat gradient buffer
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace mmvae {
+
+static constexpr int CMAX = 8, HMAX = 8, RMAX = 8;
+
+struct NBPtrs {
+    const float *xm, *lsd, *mub, *nub, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd, *Wne, *bne, *Wnm,
+        *bnm, *Wnl, *bnl, *Wnd, *bnd, *wdp, *bdp;
+    const float *We, *be, *Wd, *bd;  // frozen (reference layouts: We [K][D], Wd [D][K])
+};
+
+struct NBGrads {
+    float *xm, *lsd, *mub, *nub, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd, *Wne, *bne, *Wnm, *bnm,
+        *Wnl, *bnl, *Wnd, *bnd, *wdp, *bdp;
+};
+
+struct Dims {
+    int D, DP, NT, K, KP, C, H, R;
+    int B, Bpad, nrb;
+    int nsE, tpsE;  // encoder splits, tiles per split
+    int nsD, tpsD;  // decoder splits
+    float inv_n, beta;
+    int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
+        LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
+    int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
+};
+
+MMVAE_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NW>
+MMVAE_DEV float block_sum(float v, float* sbuf) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sbuf[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < NW; ++i) t += sbuf[i];
+    return t;  // valid in thread 0
+}
+
+// =======================================================================================
+// k_prep — per-gene constants (nb.hh:408-410 softplus(ln_x_sd)+eps, nb.hh:440 bias terms,
+// nb.hh:458 nu_dec bias - nu_bias) and the encoder's dense mean term
+// mvec[k] = sum_g x_mean_g / (softplus(ln_x_sd_g) + 1e-4) * W_enc[k, g].
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, float* mvec) {
+    __shared__ float sbuf[8];
+    if ((int)blockIdx.x < d.KP) {
+        const int k = blockIdx.x;
+        float acc = 0.f;
+        if (k < d.K)
+            for (int g = threadIdx.x; g < d.D; g += 256)
+                acc += P.xm[g] / (softplus_acc(P.lsd[g]) + 1e-4f) * P.We[(int64_t)k * d.D + g];
+        float t = block_sum<4>(acc, sbuf);
+        if (threadIdx.x == 0) mvec[k] = t;
+        return;
+    }
+    const int g = (blockIdx.x - d.KP) * 256 + threadIdx.x;
+    if (g >= d.DP) return;
+    float inv = 0.f, bias = -INFINITY, cnu = 0.f;
+    if (g < d.D) {
+        inv = 1.f / (softplus_acc(P.lsd[g]) + 1e-4f);
+        bias = P.bd[g] + P.bcd[g] + P.mub[g];
+        cnu = P.bnd[g] - P.nub[g];
+    }
+    gene[g] = inv;
+    gene[d.DP + g] = bias;
+    gene[2 * d.DP + g] = cnu;
+}
+
+// =======================================================================================
+// k_rowscan — one wave per batch row.  Streams the row's CSR once (coalesced):
+//   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
+//   pre_b = depth(x_b) (nb.hh:498, Linear D->1 on raw x), hnu_b = nu_enc(x_b) (nb.hh:448)
+//   lnorm2_b = ||log1p(x_b)||^2 (vMF encoder normalisation, vmf.hh:255)
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cells,
+                                                 const int64_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col,
+                                                 const float* __restrict__ val, NBPtrs P, Dims d,
+                                                 int32_t* __restrict__ rtp, float* __restrict__ rowx) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= d.Bpad) return;
+    const int64_t cell = cells[b];
+    int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
+    float* rx = rowx + (int64_t)b * d.rowx_stride;
+    float pre = 0.f, ln2 = 0.f, hn[HMAX];
+#pragma unroll
+    for (int h = 0; h < HMAX; ++h) hn[h] = 0.f;
+    int n = 0;
+    int64_t s = 0;
+    if (cell >= 0) {
+        s = rowptr[cell];
+        n = (int)(rowptr[cell + 1] - s);
+    }
+    for (int j = lane; j < n; j += 64) {
+        const int g = col[s + j];
+        const float x = val[s + j];
+        pre += x * P.wdp[g];
+        const float lx = log1pf(x);
+        ln2 += lx * lx;
+#pragma unroll
+        for (int h = 0; h < HMAX; ++h)
+            if (h < d.H) hn[h] += x * P.Wne[(int64_t)h * d.D + g];
+        const int t = g >> 6;
+        const int tp = (j == 0) ? -1 : (col[s + j - 1] >> 6);
+        for (int tt = tp + 1; tt <= t; ++tt) rt[tt] = j;
+    }
+    const int tlast = (n == 0) ? -1 : (col[s + n - 1] >> 6);
+    for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
+    pre = wave_sum(pre);
+    ln2 = wave_sum(ln2);
+#pragma unroll
+    for (int h = 0; h < HMAX; ++h)
+        if (h < d.H) hn[h] = wave_sum(hn[h]);
+    if (lane == 0) {
+        rx[0] = pre + P.bdp[0];
+        rx[1] = ln2;
+        for (int h = 0; h < d.H; ++h) rx[2 + h] = hn[h] + P.bne[h];
+    }
+}
+
+// =======================================================================================
+// k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = (log1p(x)/sd) W^T - mvec, so only
+// the nonzeros are densified: each wave owns 16 cells; per 64-gene tile it zero-fills a
+// 16x64 LDS tile, scatters log1p(x)/sd from the CSR and runs the tile GEMM against the
+// frozen weight [KP][DP].  Grid = (64-cell row block) x (gene split); partial h per split.
+// =======================================================================================
+template <class T, int KP>
+__global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cells,
+                                                 const int64_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col,
+                                                 const float* __restrict__ val,
+                                                 const int32_t* __restrict__ rtp,
+                                                 const float* __restrict__ gene_inv,
+                                                 const T* __restrict__ WeP, Dims d,
+                                                 float* __restrict__ hpart) {
+    using M = MM<T>;
+    constexpr int XS = 64 + (sizeof(T) == 2 ? 8 : 4);
+    __shared__ __attribute__((aligned(16))) T xt_all[4][16 * XS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T* xt = xt_all[w];
+    const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
+    const int row0 = rb * 64 + 16 * w;
+    if (row0 >= d.Bpad) return;
+    const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
+    f32x4 acc[KP / 16];
+#pragma unroll
+    for (int lb = 0; lb < KP / 16; ++lb) acc[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int si = lane >> 2, ssub = lane & 3;
+    const int64_t cell = cells[row0 + si];
+    const int64_t rbase = cell >= 0 ? rowptr[cell] : 0;
+    const int32_t* rt = rtp + (int64_t)(row0 + si) * (d.NT + 1);
+    constexpr int ZQ = 16 * XS * (int)sizeof(T) / 16;
+    for (int t = t0; t < t1; ++t) {
+        for (int i = lane; i < ZQ; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
+        wave_sync();
+        if (cell >= 0) {
+            const int js = rt[t], je = rt[t + 1];
+            for (int j = js + ssub; j < je; j += 4) {
+                const int g = col[rbase + j];
+                xt[si * XS + (g - 64 * t)] = to_t<T>(log1pf(val[rbase + j]) * gene_inv[g]);
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int s = 0; s < 64 / M::KSTEP; ++s) {
+            const auto a = M::load(&xt[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+            for (int lb = 0; lb < KP / 16; ++lb) {
+                const auto bf = M::load(&WeP[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t +
+                                             s * M::KSTEP + (lane >> 4) * M::EPL]);
+                acc[lb] = M::mma(a, bf, acc[lb]);
+            }
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int lb = 0; lb < KP / 16; ++lb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            hpart[((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * KP + 16 * lb + (lane & 15)] =
+                acc[lb][r];
+}
+
+// =======================================================================================
+// k_latent_fwd — per cell (one wave, lane = latent k):
+//   h = mu_enc(x~) (+ frozen bias), mean = mu_repr_mean(h) + covar_enc(c) (nb.hh:412-416),
+//   lnvar = clamp(mu_repr_lnvar(h), -4, 4), z = mean + eps*exp(lnvar/2) (nb.hh:462-472),
+//   nu path (nb.hh:444-451, 489-492), depth d = softplus(pre) (nb.hh:498), KL terms (nb.hh:533-537).
+//   mode 1 = recorder encode_mu(x) (nb.hh:419-431): no covariate, writes mean/lnvar out.
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_latent_fwd(
+    NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
+    const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowx,
+    const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
+    float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
+    const int K = d.K;
+    __shared__ float sWm[64 * 65], sWl[64 * 65];
+    __shared__ float sred[4];
+    for (int i = threadIdx.x; i < K * K; i += 256) {
+        sWm[(i / K) * 65 + i % K] = P.Wm[i];
+        sWl[(i / K) * 65 + i % K] = P.Wl[i];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cpw = (d.Bpad + gridDim.x * 4 - 1) / (gridDim.x * 4);
+    float kl = 0.f;
+    for (int ci = 0; ci < cpw; ++ci) {
+        const int b = (blockIdx.x * 4 + w) * cpw + ci;
+        if (b >= d.Bpad) break;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        const bool valid = cell >= 0;
+        float* L = lat + (int64_t)b * d.lat_stride;
+        const int k = lane;
+        float h = 0.f;
+        if (k < K) {
+            for (int s = 0; s < d.nsE; ++s) h += hpart[((int64_t)s * d.Bpad + b) * d.KP + k];
+            h = h - mvec[k] + P.be[k];
+        }
+        float mean = 0.f, a = 0.f;
+        if (k < K) {
+            mean = P.bm[k];
+            a = P.bl[k];
+        }
+        for (int j = 0; j < K; ++j) {
+            const float hj = __shfl(h, j, 64);
+            if (k < K) {
+                mean += sWm[k * 65 + j] * hj;
+                a += sWl[k * 65 + j] * hj;
+            }
+        }
+        if (k < K && mode == 0) {
+            float cm = P.bce[k];
+            for (int c = 0; c < d.C; ++c) cm += P.Wce[k * d.C + c] * (valid ? covar[cell * d.C + c] : 0.f);
+            mean += cm;
+        }
+        const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
+        if (mode == 1) {
+            if (k < K && b < d.B) {
+                out_mean[(int64_t)b * K + k] = mean;
+                out_lnvar[(int64_t)b * K + k] = lnvar;
+            }
+            continue;
+        }
+        const float sig = expf(lnvar / 2.f);
+        float eps = 0.f;
+        if (k < K && b < d.B)
+            eps = eps_in ? eps_in[(int64_t)b * K + k] : philox_normal(seed, step, row_offset + b, k);
+        const float z = mean + eps * sig;
+        if (k < K) {
+            L[d.LAT_H + k] = h;
+            L[d.LAT_MEAN + k] = mean;
+            L[d.LAT_A + k] = a;
+            L[d.LAT_EPS + k] = eps;
+            if (valid) kl += 1.f + lnvar - mean * mean - expf(lnvar);
+        }
+        if (k < d.KP) {
+            const float zz = (k < K && valid) ? z : 0.f;
+            zf[(int64_t)b * d.KP + k] = zz;
+            zb[(int64_t)b * d.KP + k] = (__bf16)zz;
+        }
+        // ---- overdispersion latent (lanes r < R) ----
+        const float* rx = rowx + (int64_t)b * d.rowx_stride;
+        if (k < d.R) {
+            float nm = P.bnm[k], an = P.bnl[k];
+            for (int hh = 0; hh < d.H; ++hh) {
+                nm += P.Wnm[k * d.H + hh] * rx[2 + hh];
+                an += P.Wnl[k * d.H + hh] * rx[2 + hh];
+            }
+            const float nlv = fminf(fmaxf(an, -4.f), 4.f);
+            float en = 0.f;
+            if (b < d.B)
+                en = eps_in ? eps_in[(int64_t)d.B * K + (int64_t)b * d.R + k]
+                            : philox_normal(seed, step, row_offset + b, 4096 + k);
+            const float zn = nm + en * expf(nlv / 2.f);
+            L[d.LAT_NMEAN + k] = nm;
+            L[d.LAT_AN + k] = an;
+            L[d.LAT_EPSN + k] = en;
+            L[d.LAT_ZNU + k] = valid ? zn : 0.f;
+            if (valid) kl += 1.f + nlv - nm * nm - expf(nlv);
+        }
+        if (k == 0) {
+            const float pre = rx[0];
+            const float dd = softplus_acc(pre);
+            L[d.LAT_D] = dd;
+            L[d.LAT_W] = valid ? dd * d.inv_n : 0.f;
+            L[d.LAT_VALID] = valid ? 1.f : 0.f;
+        }
+    }
+    if (mode == 1) return;
+    kl = wave_sum(kl);
+    if (lane == 0) sred[w] = kl;
+    __syncthreads();
+    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * (sred[0] + sred[1] + sred[2] + sred[3]);
+}
+
+// =======================================================================================
+// k_dec<T, KP, PASS> — decoder + NB likelihood (nb.hh:433-442, 453-460, 510-531).
+// Each wave owns 16 cells and sweeps the 64-gene tiles of its gene split; the logit tile
+// (16 cells x 16 genes per MFMA) is never stored.  Lane l holds, per 16-gene block, gene
+// (l & 15) of cells 4(l>>4)+r, r = 0..3 (the MFMA C layout).
+//   PASS 0 (A): online max / sum-exp per cell                       -> lsep[split][cell]
+//   PASS 1 (B): softmax + NB terms; dz partials on MFMA; column sums -> rowB, dzp, slabB, loss
+//   PASS 2 (C): column sums of w_b E_b p_bg (the S_b p term of the softmax backward)
+// =======================================================================================
+struct DecPtrs {
+    const float* lat;
+    const float* zf;
+    const __bf16* zb;
+    const float* gene;  // inv, bias, cnu  [3][DP]
+    const float* Wcd;   // covar_decoding.weight [D][C]
+    const float* Wnd;   // nu_decoding.weight [D][R]
+    const float* covar;
+    const int64_t* cells;
+    const int64_t* rowptr;
+    const int32_t* col;
+    const float* val;
+    const int32_t* rtp;
+    const void* WdP;  // [DP][KP] T
+    const void* WdT;  // [KP][DP] T
+    float* lsep;      // [nsD][Bpad][2]
+    float* rowB;      // [nsD][Bpad][2+R]
+    float* dzp;       // [nsD][Bpad][2][KP]
+    float* slabB;     // [nrb][nqB][DP]
+    float* slabC;     // [nrb][1+C][DP]
+    float* lossp;     // [grid]
+};
+
+template <class T, int KP, int PASS, int CM, int RM>
+__global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
+    using M = MM<T>;
+    constexpr int KS = KP / M::KSTEP;
+    constexpr int XS = 68;                                 // f32 x tile row stride
+    constexpr int QS = 64 + (sizeof(T) == 2 ? 8 : 4);      // q tile row stride (elements)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
+    const int row0 = rb * 64 + 16 * w;
+    const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
+    const int GS = d.tpsD * 64;
+    const int C = d.C, R = d.R;
+    const int nq = (PASS == 1) ? (1 + C) + 1 + R : (1 + C);
+    // LDS carve: colacc [nq][GS] f32 | per-wave x tile [16][XS] f32 | per-wave q1,q2 [16][QS] T
+    float* sl = reinterpret_cast<float*>(smem);  // [4] loss scratch (16 B keeps alignment)
+    float* colacc = sl + 4;
+    const int ncol = (PASS == 0) ? 0 : nq * GS;
+    float* xt = colacc + ncol + w * 16 * XS;
+    T* q1 = reinterpret_cast<T*>(colacc + ncol + 4 * 16 * XS) + w * 2 * 16 * QS;
+    T* q2 = q1 + 16 * QS;
+    if (PASS != 0) {
+        for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
+        __syncthreads();
+    }
+    const bool wave_live = row0 < d.Bpad;
+    const T* Z = (sizeof(T) == 2) ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
+    const T* WdP = reinterpret_cast<const T*>(Q.WdP);
+    const T* WdT = reinterpret_cast<const T*>(Q.WdT);
+
+    float lossacc = 0.f;
+    // per-row state for my 4 rows
+    float rv[4], lse[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
+    float mrun[4], srun[4], Eacc[4], Pacc[4], dzn[4][RM], wE[4];
+    f32x4 dzA[KP / 16], dzP[KP / 16];
+    typename M::frag zfr[KS];
+    if (wave_live) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = row0 + 4 * (lane >> 4) + r;
+            const float* L = Q.lat + (int64_t)b * d.lat_stride;
+            rv[r] = L[d.LAT_VALID];
+            dv[r] = L[d.LAT_D];
+            wv[r] = L[d.LAT_W];
+            const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+#pragma unroll
+            for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+#pragma unroll
+            for (int q = 0; q < RM; ++q) {
+                znu[r][q] = (q < R) ? L[d.LAT_ZNU + q] : 0.f;
+                dzn[r][q] = 0.f;
+            }
+            mrun[r] = -INFINITY;
+            srun[r] = 0.f;
+            Eacc[r] = 0.f;
+            Pacc[r] = 0.f;
+            lse[r] = 0.f;
+            wE[r] = 0.f;
+            if (PASS != 0) {
+                float mm = -INFINITY;
+                for (int s2 = 0; s2 < d.nsD; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
+                float ss = 0.f;
+                for (int s2 = 0; s2 < d.nsD; ++s2) {
+                    const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
+                    ss += lp[1] * expf(lp[0] - mm);
+                }
+                lse[r] = mm + logf(ss);
+            }
+            if (PASS == 2) {
+                float E = 0.f;
+                for (int s2 = 0; s2 < d.nsD; ++s2) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
+                wE[r] = wv[r] * E;
+            }
+        }
+#pragma unroll
+        for (int lb = 0; lb < KP / 16; ++lb) {
+            dzA[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            dzP[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    // scatter assignment for the x tile (PASS B)
+    const int si = lane >> 2, ssub = lane & 3;
+    int64_t scell = -1, rbase = 0;
+    const int32_t* rt = nullptr;
+    if (PASS == 1 && wave_live) {
+        scell = (row0 + si < d.B) ? Q.cells[row0 + si] : -1;
+        rbase = scell >= 0 ? Q.rowptr[scell] : 0;
+        rt = Q.rtp + (int64_t)(row0 + si) * (d.NT + 1);
+    }
+
+    if (wave_live) {
+        for (int t = t0; t < t1; ++t) {
+            if (PASS == 1) {
+                for (int i = lane; i < 16 * XS / 4; i += 64)
+                    reinterpret_cast<float4*>(xt)[i] = float4{0.f, 0.f, 0.f, 0.f};
+                wave_sync();
+                if (scell >= 0) {
+                    const int js = rt[t], je = rt[t + 1];
+                    for (int j = js + ssub; j < je; j += 4)
+                        xt[si * XS + (Q.col[rbase + j] - 64 * t)] = Q.val[rbase + j];
+                }
+                wave_sync();
+            }
+#pragma unroll 1
+            for (int gb = 0; gb < 4; ++gb) {
+                const int gl = 16 * gb + (lane & 15);
+                const int gene = 64 * t + gl;
+                const bool gv = gene < d.D;
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const auto wf = M::load(&WdP[(int64_t)gene * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    acc = M::mma(zfr[s], wf, acc);
+                }
+                const float bias = Q.gene[d.DP + gene];
+                float wcd[CM];
+#pragma unroll
+                for (int c = 0; c < CM; ++c) wcd[c] = (c < C && gv) ? Q.Wcd[(int64_t)gene * C + c] : 0.f;
+                if (PASS == 0) {
+                    if (gv) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float lg = acc[r] + bias;
+#pragma unroll
+                            for (int c = 0; c < CM; ++c)
+                                if (c < C) lg += crow[r][c] * wcd[c];
+                            const float df = lg - mrun[r];
+                            const float e = fexp(-fabsf(df));
+                            srun[r] = (df > 0.f) ? fmaf(srun[r], e, 1.f) : srun[r] + e;
+                            mrun[r] = fmaxf(mrun[r], lg);
+                        }
+                    }
+                } else if (PASS == 2) {
+                    float cs[1 + CM];
+#pragma unroll
+                    for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float lg = acc[r] + bias;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c)
+                            if (c < C) lg += crow[r][c] * wcd[c];
+                        const float wp = wE[r] * fexp(lg - lse[r]);
+                        cs[0] += wp;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c)
+                            if (c < C) cs[1 + c] += wp * crow[r][c];
+                    }
+#pragma unroll
+                    for (int c = 0; c < 1 + CM; ++c) {
+                        if (c > C) break;
+                        float v = cs[c];
+                        v += __shfl_xor(v, 16, 64);
+                        v += __shfl_xor(v, 32, 64);
+                        if (lane < 16) atomicAdd(&colacc[c * GS + (t - t0) * 64 + gl], v);
+                    }
+                } else {
+                    // ---- PASS B: NB likelihood and its gradient terms ----
+                    const float cn = Q.gene[2 * d.DP + gene];
+                    float wnd[RM];
+#pragma unroll
+                    for (int q = 0; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
+                    const float gvf = gv ? 1.f : 0.f;
+                    float cs1[1 + CM], csdu = 0.f, csduz[RM];
+#pragma unroll
+                    for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
+#pragma unroll
+                    for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int rl = 4 * (lane >> 4) + r;
+                        float lg = acc[r] + bias;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c)
+                            if (c < C) lg += crow[r][c] * wcd[c];
+                        const float p = fexp(lg - lse[r]);              // nb.hh:440-441
+                        const float mu = fmaf(p, dv[r], 1e-4f);         // nb.hh:519
+                        float u = cn;
+#pragma unroll
+                        for (int q = 0; q < RM; ++q)
+                            if (q < R) u += wnd[q] * znu[r][q];
+                        float eu;
+                        const float spv = softplus_e(u, eu);            // nb.hh:458
+                        const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);  // nb.hh:459
+                        const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
+                        const float nup = nu + 1e-4f;                   // nb.hh:518
+                        const float s = mu + nup;
+                        const float rs = frcp(s);
+                        const float lgr = log1p_pos(mu * frcp(nup));    // log(s) - log(nup)
+                        float Lv = nup * lgr;                           // nb.hh:528 (x = 0 part)
+                        float q = -mu * rs;                             // n dL/dmu' - 1
+                        float dn = lgr + q;                             // n dL/dnup
+                        const float x = xt[rl * XS + gl];
+                        if (x > 0.f) {
+                            Lv += x * (flog(s) - flog(mu));             // nb.hh:527
+                            q += x * rs - x * frcp(mu);
+                            dn += x * rs;
+                            float lgd, dgd;
+                            nb_gamma_terms(nup, x, lgd, dgd);           // nb.hh:522-523
+                            Lv += lgd;
+                            dn += dgd;
+                        }
+                        const float me = rv[r] * gvf;
+                        lossacc += Lv * me;
+                        const float du = msk ? dn * dsoftplus_e(u, eu) * me : 0.f;
+                        const float pq = p * q;
+                        Eacc[r] += pq;
+                        Pacc[r] += p;
+                        const float wpq = wv[r] * pq;
+                        cs1[0] += wpq;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c)
+                            if (c < C) cs1[1 + c] += wpq * crow[r][c];
+                        csdu += du;
+#pragma unroll
+                        for (int qq = 0; qq < RM; ++qq)
+                            if (qq < R) {
+                                csduz[qq] += du * znu[r][qq];
+                                dzn[r][qq] += du * wnd[qq];
+                            }
+                        q1[rl * QS + gl] = to_t<T>(pq);
+                        q2[rl * QS + gl] = to_t<T>(p);
+                    }
+                    // column sums: reduce over the 4 lane groups, then LDS accumulate
+                    auto red = [&](float v, int slot) {
+                        v += __shfl_xor(v, 16, 64);
+                        v += __shfl_xor(v, 32, 64);
+                        if (lane < 16) atomicAdd(&colacc[slot * GS + (t - t0) * 64 + gl], v);
+                    };
+#pragma unroll
+                    for (int c = 0; c < 1 + CM; ++c)
+                        if (c <= C) red(cs1[c], c);
+                    red(csdu, 1 + C);
+#pragma unroll
+                    for (int qq = 0; qq < RM; ++qq)
+                        if (qq < R) red(csduz[qq], 2 + C + qq);
+                }
+            }
+            if (PASS == 1) {
+                // dz partial = sum_g Q[cell][g] W[g][latent] on MFMA (Q staged through LDS)
+                wave_sync();
+#pragma unroll
+                for (int s = 0; s < 64 / M::KSTEP; ++s) {
+                    const auto a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    const auto a2 = M::load(&q2[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+                    for (int lb = 0; lb < KP / 16; ++lb) {
+                        const auto bw = M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t +
+                                                     s * M::KSTEP + (lane >> 4) * M::EPL]);
+                        dzA[lb] = M::mma(a1, bw, dzA[lb]);
+                        dzP[lb] = M::mma(a2, bw, dzP[lb]);
+                    }
+                }
+                wave_sync();
+            }
+        }
+        // ---- per-row outputs ----
+        if (PASS == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float m = mrun[r], s = srun[r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+                    const float mn = fmaxf(m, m2);
+                    s = (mn == -INFINITY) ? 0.f : s * expf(m - mn) + s2 * expf(m2 - mn);
+                    m = mn;
+                }
+                if ((lane & 15) == 0) {
+                    float* lp = Q.lsep + ((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * 2;
+                    lp[0] = m;
+                    lp[1] = s;
+                }
+            }
+        }
+        if (PASS == 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float E = Eacc[r], Pp = Pacc[r];
+                float dz2[RM];
+#pragma unroll
+                for (int q = 0; q < RM; ++q) dz2[q] = dzn[r][q];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    E += __shfl_xor(E, o, 64);
+                    Pp += __shfl_xor(Pp, o, 64);
+#pragma unroll
+                    for (int q = 0; q < RM; ++q)
+                        if (q < R) dz2[q] += __shfl_xor(dz2[q], o, 64);
+                }
+                const int b = row0 + 4 * (lane >> 4) + r;
+                if ((lane & 15) == 0) {
+                    float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
+                    rp[0] = E;
+                    rp[1] = Pp;
+                    for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q];
+                }
+#pragma unroll
+                for (int lb = 0; lb < KP / 16; ++lb) {
+                    float* dp = Q.dzp + (((int64_t)sp * d.Bpad + b) * 2) * KP + 16 * lb + (lane & 15);
+                    dp[0] = dzA[lb][r];
+                    dp[KP] = dzP[lb][r];
+                }
+            }
+        }
+    }
+    if (PASS == 1) {
+        const float lw = wave_sum(lossacc);
+        if (lane == 0) sl[w] = lw;
+        __syncthreads();
+        if (threadIdx.x == 0) Q.lossp[blockIdx.x] = sl[0] + sl[1] + sl[2] + sl[3];
+    }
+    if (PASS != 0) {
+        __syncthreads();
+        float* slab = (PASS == 1) ? Q.slabB : Q.slabC;
+        const int gbase = t0 * 64;
+        const int glen = min(d.DP, t1 * 64) - gbase;
+        for (int i = threadIdx.x; i < nq * GS; i += 256) {
+            const int q = i / GS, gi = i % GS;
+            if (gi < glen) slab[((int64_t)rb * nq + q) * d.DP + gbase + gi] = colacc[i];
+        }
+    }
+}
+
+// =======================================================================================
+// k_latent_bwd — backward of reparameterisation, clamps, KL and the K x K heads
+// (autograd of nb.hh:412-416, 449-450, 462-472, 498, 533-548) per cell; per-workgroup
+// partial sums of the small-parameter gradients.
+//   dz = w_b (A''_b - E_b P_b),  w_b = d_b / n   (see oracle/nb_analytic.py)
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
+                                                    const float* __restrict__ covar,
+                                                    float* __restrict__ lat, const float* __restrict__ rowx,
+                                                    const float* __restrict__ rowB,
+                                                    const float* __restrict__ dzp, float* __restrict__ dh,
+                                                    float* __restrict__ dhT_f, __bf16* __restrict__ dhT_b,
+                                                    float* __restrict__ small) {
+    const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP;
+    __shared__ float acc_s[2 * 64 * 64 + 64 * 4 + 64 * CMAX + 4 * RMAX * HMAX + 64];
+    const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
+    for (int i = threadIdx.x; i < SMALL; i += 256) acc_s[i] = 0.f;
+    __syncthreads();
+    float* a_dWm = acc_s;
+    float* a_dWl = a_dWm + K * K;
+    float* a_dbm = a_dWl + K * K;
+    float* a_dbl = a_dbm + K;
+    float* a_dWce = a_dbl + K;
+    float* a_dhs = a_dWce + K * C;
+    float* a_dWnm = a_dhs + K;
+    float* a_dbnm = a_dWnm + R * H;
+    float* a_dWnl = a_dbnm + R;
+    float* a_dbnl = a_dWnl + R * H;
+    float* a_dbne = a_dbnl + R;
+    float* a_dbdp = a_dbne + H;
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = lane;
+    const int cpw = (d.Bpad + gridDim.x * 4 - 1) / (gridDim.x * 4);
+    float rWm[64], rWl[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        rWm[j] = 0.f;
+        rWl[j] = 0.f;
+    }
+    float rbm = 0.f, rbl = 0.f, rdhs = 0.f, rWce[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) rWce[c] = 0.f;
+    const float bn = d.beta * d.inv_n;
+    for (int ci = 0; ci < cpw; ++ci) {
+        const int b = (blockIdx.x * 4 + w) * cpw + ci;
+        if (b >= d.Bpad) break;
+        float* L = lat + (int64_t)b * d.lat_stride;
+        const bool valid = L[d.LAT_VALID] > 0.f;
+        float E = 0.f, Ps = 0.f;
+        for (int s = 0; s < d.nsD; ++s) {
+            E += rowB[((int64_t)s * d.Bpad + b) * (2 + R)];
+            Ps += rowB[((int64_t)s * d.Bpad + b) * (2 + R) + 1];
+        }
+        const float wb = L[d.LAT_W];
+        float dz = 0.f, dmean = 0.f, da = 0.f, h = 0.f;
+        if (k < K) {
+            float A2 = 0.f, Pb = 0.f;
+            for (int s = 0; s < d.nsD; ++s) {
+                const float* dp = dzp + (((int64_t)s * d.Bpad + b) * 2) * KP;
+                A2 += dp[k];
+                Pb += dp[KP + k];
+            }
+            dz = wb * (A2 - E * Pb);
+            const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
+            h = L[d.LAT_H + k];
+            const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
+            const float sig = expf(lnvar / 2.f);
+            dmean = dz + bn * mean;
+            const float dlnvar = dz * eps * sig * 0.5f + bn * 0.5f * (expf(lnvar) - 1.f);
+            da = (a >= -4.f && a <= 4.f) ? dlnvar : 0.f;
+            if (!valid) {
+                dmean = 0.f;
+                da = 0.f;
+            }
+        }
+        // dh_j = sum_k Wm[k][j] dmean_k + Wl[k][j] da_k   (lane = j)
+        float dhj = 0.f;
+        for (int kk = 0; kk < K; ++kk) {
+            const float dm = __shfl(dmean, kk, 64), dl = __shfl(da, kk, 64);
+            if (k < K) dhj += P.Wm[kk * K + k] * dm + P.Wl[kk * K + k] * dl;
+        }
+        if (k < KP) {
+            const float v = (k < K) ? dhj : 0.f;
+            dh[(int64_t)b * KP + k] = v;
+            dhT_f[(int64_t)k * d.Bpad + b] = v;
+            dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)v;
+        }
+        // weight-gradient accumulation (lane k owns row k)
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+            const float hj = __shfl(h, j, 64);
+            rWm[j] += dmean * hj;
+            rWl[j] += da * hj;
+        }
+        rbm += dmean;
+        rbl += da;
+        rdhs += (k < K) ? dhj : 0.f;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < C && cell >= 0) rWce[c] += dmean * covar[cell * C + c];
+        // ---- overdispersion path ----
+        const float* rx = rowx + (int64_t)b * d.rowx_stride;
+        float dnm = 0.f, dan = 0.f;
+        if (k < R && valid) {
+            float dzn = 0.f;
+            for (int s = 0; s < d.nsD; ++s) dzn += rowB[((int64_t)s * d.Bpad + b) * (2 + R) + 2 + k];
+            dzn *= d.inv_n;
+            const float nm = L[d.LAT_NMEAN + k], an = L[d.LAT_AN + k], en = L[d.LAT_EPSN + k];
+            const float nlv = fminf(fmaxf(an, -4.f), 4.f);
+            dnm = dzn + bn * nm;
+            const float dnl = dzn * en * expf(nlv / 2.f) * 0.5f + bn * 0.5f * (expf(nlv) - 1.f);
+            dan = (an >= -4.f && an <= 4.f) ? dnl : 0.f;
+            for (int hh = 0; hh < H; ++hh) {
+                atomicAdd(&a_dWnm[k * H + hh], dnm * rx[2 + hh]);
+                atomicAdd(&a_dWnl[k * H + hh], dan * rx[2 + hh]);
+            }
+            atomicAdd(&a_dbnm[k], dnm);
+            atomicAdd(&a_dbnl[k], dan);
+        }
+        float dhn = 0.f;
+        for (int q = 0; q < R; ++q) {
+            const float a1 = __shfl(dnm, q, 64), a2 = __shfl(dan, q, 64);
+            if (k < H) dhn += P.Wnm[q * H + k] * a1 + P.Wnl[q * H + k] * a2;
+        }
+        if (k < H) {
+            L[d.LAT_DHNU + k] = valid ? dhn : 0.f;
+            if (valid) atomicAdd(&a_dbne[k], dhn);
+        }
+        if (k == 0) {
+            const float dd = (E + Ps) * d.inv_n;   // dL/dd_b = sum_g dmu' p
+            const float pre = rx[0];
+            const float dpre = valid ? dd * dsoftplus(pre) : 0.f;
+            L[d.LAT_DPRE] = dpre;
+            if (valid) atomicAdd(a_dbdp, dpre);
+        }
+    }
+    if (k < K) {
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+            if (j < K) {
+                atomicAdd(&a_dWm[k * K + j], rWm[j]);
+                atomicAdd(&a_dWl[k * K + j], rWl[j]);
+            }
+        }
+        atomicAdd(&a_dbm[k], rbm);
+        atomicAdd(&a_dbl[k], rbl);
+        atomicAdd(&a_dhs[k], rdhs);
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < C) atomicAdd(&a_dWce[k * C + c], rWce[c]);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SMALL; i += 256) small[(int64_t)blockIdx.x * SMALL + i] = acc_s[i];
+}
+
+// =======================================================================================
+// k_enc_bwd — gradient of x_mean / ln_x_sd through the frozen encoder (autograd of
+// nb.hh:408-411) and of depth / nu_enc weights (raw x, nb.hh:448,498):
+//   Gl_g = sum_k W_enc[k,g] sum_b dh_bk log1p(x_bg)   (MFMA on densified 64x64 tiles)
+//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}     (LDS atomics during the scatter)
+// =======================================================================================
+template <class T, int KP>
+__global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cells,
+                                                 const int64_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col,
+                                                 const float* __restrict__ val,
+                                                 const int32_t* __restrict__ rtp, const float* __restrict__ lat,
+                                                 const T* __restrict__ dhT, const float* __restrict__ WeF,
+                                                 Dims d, float* __restrict__ slabE) {
+    using M = MM<T>;
+    constexpr int LS = 64 + (sizeof(T) == 2 ? 8 : 4);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
+    const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
+    const int GS = d.tpsE * 64;
+    const int nq = 2 + d.H;
+    float* colacc = reinterpret_cast<float*>(smem);
+    T* lt = reinterpret_cast<T*>(colacc + nq * GS);  // [64 genes][LS] : cells contiguous
+    for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
+    const int si = lane >> 2, ssub = lane & 3;
+    const int brow = rb * 64 + 16 * w + si;
+    const int64_t cell = (brow < d.B) ? cells[brow] : -1;
+    const int64_t rbase = cell >= 0 ? rowptr[cell] : 0;
+    const int32_t* rt = rtp + (int64_t)brow * (d.NT + 1);
+    float dpre = 0.f, dhn[HMAX];
+    if (cell >= 0) {
+        const float* L = lat + (int64_t)brow * d.lat_stride;
+        dpre = L[d.LAT_DPRE];
+#pragma unroll
+        for (int h = 0; h < HMAX; ++h) dhn[h] = (h < d.H) ? L[d.LAT_DHNU + h] : 0.f;
+    } else {
+#pragma unroll
+        for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
+    }
+    constexpr int KSB = 64 / M::KSTEP;
+    typename M::frag afr[KP / 64 > 0 ? KP / 64 : 1][KSB];
+    const int nlb = KP / 16;
+#pragma unroll
+    for (int li = 0; li < (KP / 64 > 0 ? KP / 64 : 1); ++li) {
+        const int lb = w + 4 * li;
+#pragma unroll
+        for (int s = 0; s < KSB; ++s)
+            afr[li][s] = (lb < nlb) ? M::load(&dhT[(int64_t)(16 * lb + (lane & 15)) * d.Bpad + rb * 64 +
+                                                   s * M::KSTEP + (lane >> 4) * M::EPL])
+                                    : M::zero();
+    }
+    constexpr int ZQ = 64 * LS * (int)sizeof(T) / 16;
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+        for (int i = threadIdx.x; i < ZQ; i += 256) reinterpret_cast<uint4*>(lt)[i] = uint4{0, 0, 0, 0};
+        __syncthreads();
+        if (cell >= 0) {
+            const int js = rt[t], je = rt[t + 1];
+            for (int j = js + ssub; j < je; j += 4) {
+                const int g = col[rbase + j] - 64 * t;
+                const float x = val[rbase + j];
+                lt[g * LS + 16 * w + si] = to_t<T>(log1pf(x));
+                atomicAdd(&colacc[1 * GS + (t - t0) * 64 + g], dpre * x);
+                for (int h = 0; h < d.H; ++h) atomicAdd(&colacc[(2 + h) * GS + (t - t0) * 64 + g], dhn[h] * x);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int li = 0; li < (KP / 64 > 0 ? KP / 64 : 1); ++li) {
+            const int lb = w + 4 * li;
+            if (lb >= nlb) break;
+#pragma unroll 1
+            for (int gb = 0; gb < 4; ++gb) {
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KSB; ++s) {
+                    const auto bf = M::load(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    acc = M::mma(afr[li][s], bf, acc);
+                }
+                const int gene = 64 * t + 16 * gb + (lane & 15);
+                float v = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v += WeF[(int64_t)(16 * lb + 4 * (lane >> 4) + r) * d.DP + gene] * acc[r];
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                if (lane < 16) atomicAdd(&colacc[(t - t0) * 64 + 16 * gb + (lane & 15)], v);
+            }
+        }
+        __syncthreads();
+    }
+    const int gbase = t0 * 64;
+    const int glen = min(d.DP, t1 * 64) - gbase;
+    for (int i = threadIdx.x; i < nq * GS; i += 256) {
+        const int q = i / GS, gi = i % GS;
+        if (gi < glen) slabE[((int64_t)rb * nq + q) * d.DP + gbase + gi] = colacc[i];
+    }
+}
+
+// =======================================================================================
+// Gradient assembly (deterministic, fixed-order reductions)
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restrict__ small, int nwg,
+                                                    NBGrads G, float* __restrict__ smallg,
+                                                    const float* __restrict__ lossp, int nlossp,
+                                                    const float* __restrict__ klpart, int nkl,
+                                                    float* __restrict__ out, int with_grads) {
+    const int K = d.K, C = d.C, H = d.H, R = d.R;
+    const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
+    if (blockIdx.x == 0) {
+        __shared__ float sb[8];
+        float lsum = 0.f, ksum = 0.f;
+        for (int i = threadIdx.x; i < nlossp; i += 256) lsum += lossp[i];
+        for (int i = threadIdx.x; i < nkl; i += 256) ksum += klpart[i];
+        float tl = block_sum<4>(lsum, sb);
+        float tk = block_sum<4>(ksum, sb);
+        if (threadIdx.x == 0) out[0] = (tl + tk * d.beta) * d.inv_n;
+        return;
+    }
+    if (!with_grads) return;
+    const int i = (blockIdx.x - 1) * 256 + threadIdx.x;
+    if (i >= SMALL) return;
+    float s = 0.f;
+    for (int wg = 0; wg < nwg; ++wg) s += small[(int64_t)wg * SMALL + i];
+    int o = i;
+    if (o < K * K) { G.Wm[o] = s; return; }
+    o -= K * K;
+    if (o < K * K) { G.Wl[o] = s; return; }
+    o -= K * K;
+    if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
+    o -= K;
+    if (o < K) { G.bl[o] = s; return; }
+    o -= K;
+    if (o < K * C) { G.Wce[o] = s; return; }
+    o -= K * C;
+    if (o < K) { smallg[o] = s; return; }
+    o -= K;
+    if (o < R * H) { G.Wnm[o] = s; return; }
+    o -= R * H;
+    if (o < R) { G.bnm[o] = s; return; }
+    o -= R;
+    if (o < R * H) { G.Wnl[o] = s; return; }
+    o -= R * H;
+    if (o < R) { G.bnl[o] = s; return; }
+    o -= R;
+    if (o < H) { G.bne[o] = s; return; }
+    o -= H;
+    G.bdp[0] = s;
+}
+
+__global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
+                                                    const float* __restrict__ gene,
+                                                    const float* __restrict__ slabB,
+                                                    const float* __restrict__ slabC,
+                                                    const float* __restrict__ slabE,
+                                                    const float* __restrict__ smallg, int nrb) {
+    __shared__ float cdh[128];
+    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
+    __syncthreads();
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= d.D) return;
+    const int C = d.C, R = d.R, H = d.H;
+    const int nqB = (1 + C) + 1 + R, nqC = 1 + C, nqE = 2 + H;
+    float cs1[1 + CMAX], tc[1 + CMAX], du = 0.f, duz[RMAX], gl = 0.f, raw[1 + HMAX];
+#pragma unroll
+    for (int c = 0; c < 1 + CMAX; ++c) cs1[c] = tc[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < RMAX; ++q) duz[q] = 0.f;
+#pragma unroll
+    for (int h = 0; h < 1 + HMAX; ++h) raw[h] = 0.f;
+    for (int rb = 0; rb < nrb; ++rb) {
+        const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
+        const float* sC = slabC + (int64_t)rb * nqC * d.DP + g;
+        const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
+        for (int c = 0; c <= C; ++c) {
+            cs1[c] += sB[(int64_t)c * d.DP];
+            tc[c] += sC[(int64_t)c * d.DP];
+        }
+        du += sB[(int64_t)(1 + C) * d.DP];
+        for (int q = 0; q < R; ++q) duz[q] += sB[(int64_t)(2 + C + q) * d.DP];
+        gl += sE[0];
+        for (int h = 0; h < 1 + H; ++h) raw[h] += sE[(int64_t)(1 + h) * d.DP];
+    }
+    const float inv_n = d.inv_n;
+    const float dl = cs1[0] - tc[0];
+    G.mub[g] = dl;
+    G.bcd[g] = dl;
+    for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = cs1[1 + c] - tc[1 + c];
+    G.bnd[g] = du * inv_n;
+    G.nub[g] = -du * inv_n;
+    for (int q = 0; q < R; ++q) G.Wnd[(int64_t)g * R + q] = duz[q] * inv_n;
+    // encoder normalisation params (nb.hh:408-410)
+    float gs = 0.f;
+    for (int k = 0; k < d.K; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
+    const float inv = gene[g];
+    G.xm[g] = -inv * gs;
+    const float th = P.lsd[g];
+    G.lsd[g] = -(inv * inv) * (gl - P.xm[g] * gs) * dsoftplus(th);
+    G.wdp[g] = raw[0];
+    for (int h = 0; h < H; ++h) G.Wne[(int64_t)h * d.D + g] = raw[1 + h];
+}
+
+// =======================================================================================
+// host-side launch orchestration
+// =======================================================================================
+static NBPtrs nb_ptrs(Engine* e) {
+    NBPtrs P;
+    P.xm = e->preg("x_mean");
+    P.lsd = e->preg("ln_x_sd");
+    P.mub = e->preg("mu_bias");
+    P.nub = e->preg("nu_bias");
+    P.Wce = e->preg("covar_encoding.weight");
+    P.bce = e->preg("covar_encoding.bias");
+    P.Wm = e->preg("mu_representation_mean.weight");
+    P.bm = e->preg("mu_representation_mean.bias");
+    P.Wl = e->preg("mu_representation_logvariance.weight");
+    P.bl = e->preg("mu_representation_logvariance.bias");
+    P.Wcd = e->preg("covar_decoding.weight");
+    P.bcd = e->preg("covar_decoding.bias");
+    P.Wne = e->preg("nu_encoding.weight");
+    P.bne = e->preg("nu_encoding.bias");
+    P.Wnm = e->preg("nu_representation_mean.weight");
+    P.bnm = e->preg("nu_representation_mean.bias");
+    P.Wnl = e->preg("nu_representation_logvariance.weight");
+    P.bnl = e->preg("nu_representation_logvariance.bias");
+    P.Wnd = e->preg("nu_decoding.weight");
+    P.bnd = e->preg("nu_decoding.bias");
+    P.wdp = e->preg("depth.weight");
+    P.bdp = e->preg("depth.bias");
+    P.We = e->pfrz("mu_enc.mu_encoding.weight");
+    P.be = e->pfrz("mu_enc.mu_encoding.bias");
+    P.Wd = e->pfrz("mu_dec.mu_decoding.weight");
+    P.bd = e->pfrz("mu_dec.mu_decoding.bias");
+    return P;
+}
+
+static NBGrads nb_grads(Engine* e) {
+    NBGrads G;
+    G.xm = e->greg("x_mean");
+    G.lsd = e->greg("ln_x_sd");
+    G.mub = e->greg("mu_bias");
+    G.nub = e->greg("nu_bias");
+    G.Wce = e->greg("covar_encoding.weight");
+    G.bce = e->greg("covar_encoding.bias");
+    G.Wm = e->greg("mu_representation_mean.weight");
+    G.bm = e->greg("mu_representation_mean.bias");
+    G.Wl = e->greg("mu_representation_logvariance.weight");
+    G.bl = e->greg("mu_representation_logvariance.bias");
+    G.Wcd = e->greg("covar_decoding.weight");
+    G.bcd = e->greg("covar_decoding.bias");
+    G.Wne = e->greg("nu_encoding.weight");
+    G.bne = e->greg("nu_encoding.bias");
+    G.Wnm = e->greg("nu_representation_mean.weight");
+    G.bnm = e->greg("nu_representation_mean.bias");
+    G.Wnl = e->greg("nu_representation_logvariance.weight");
+    G.bnl = e->greg("nu_representation_logvariance.bias");
+    G.Wnd = e->greg("nu_decoding.weight");
+    G.bnd = e->greg("nu_decoding.bias");
+    G.wdp = e->greg("depth.weight");
+    G.bdp = e->greg("depth.bias");
+    return G;
+}
+
+static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
+    Dims d;
+    d.D = (int)e->D;
+    d.DP = (int)e->DP;
+    d.NT = (int)e->NT;
+    d.K = (int)e->K;
+    d.KP = (int)e->KP;
+    d.C = (int)e->C;
+    d.H = (int)e->H;
+    d.R = (int)e->R;
+    d.B = (int)B;
+    d.Bpad = (int)((B + 63) / 64 * 64);
+    d.nrb = d.Bpad / 64;
+    d.nsE = e->nsplit_e;
+    d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
+    d.nsD = e->nsplit_d;
+    d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
+    d.inv_n = 1.f / (float)n_total;
+    d.beta = beta;
+    d.lat_stride = (int)e->lat_stride;
+    d.LAT_H = (int)e->LAT_H;
+    d.LAT_MEAN = (int)e->LAT_MEAN;
+    d.LAT_A = (int)e->LAT_A;
+    d.LAT_EPS = (int)e->LAT_EPS;
+    d.LAT_NMEAN = (int)e->LAT_NMEAN;
+    d.LAT_AN = (int)e->LAT_AN;
+    d.LAT_EPSN = (int)e->LAT_EPSN;
+    d.LAT_ZNU = (int)e->LAT_ZNU;
+    d.LAT_D = (int)e->LAT_D;
+    d.LAT_W = (int)e->LAT_W;
+    d.LAT_VALID = (int)e->LAT_VALID;
+    d.LAT_DHNU = (int)e->LAT_HNU;
+    d.LAT_DPRE = (int)e->LAT_HNU + (int)e->H;
+    d.rowx_stride = 2 + (int)e->H;
+    return d;
+}
+
+__global__ void k_pack_frozen(const float* We, const float* Wd, int D, int DP, int K, int KP,
+                              float* WeP_f, __bf16* WeP_b, float* WdP_f, __bf16* WdP_b, float* WdT_f,
+                              __bf16* WdT_b) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)KP * DP) return;
+    const int k = (int)(i / DP), g = (int)(i % DP);
+    const bool v = (k < K) && (g < D);
+    const float we = v ? We[(int64_t)k * D + g] : 0.f;
+    const float wd = v ? Wd[(int64_t)g * K + k] : 0.f;
+    WeP_f[i] = we;
+    WeP_b[i] = (__bf16)we;
+    WdT_f[i] = wd;
+    WdT_b[i] = (__bf16)wd;
+    WdP_f[(int64_t)g * KP + k] = wd;
+    WdP_b[(int64_t)g * KP + k] = (__bf16)wd;
+}
+
+hipError_t nb_prepare_frozen(Engine* e) {
+    const int64_t n = e->KP * e->DP;
+    ScopedTimer tm(e, "k_pack_frozen");
+    hipLaunchKernelGGL(k_pack_frozen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
+                       e->pfrz("mu_enc.mu_encoding.weight"), e->pfrz("mu_dec.mu_decoding.weight"), (int)e->D,
+                       (int)e->DP, (int)e->K, (int)e->KP, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b,
+                       e->d_WdT_f, e->d_WdT_b);
+    e->frozen_dirty = false;
+    return hipGetLastError();
+}
+
+static size_t dec_lds(const Dims& d, int pass, bool bf16) {
+    const int nq = (pass == 1) ? (1 + d.C) + 1 + d.R : (1 + d.C);
+    size_t s = 16 + ((pass == 0) ? 0 : (size_t)nq * d.tpsD * 64 * 4);
+    if (pass == 1) {
+        s += 4 * 16 * 68 * 4;                                      // x tiles
+        s += 4 * 2 * 16 * (64 + (bf16 ? 8 : 4)) * (bf16 ? 2 : 4);  // q tiles
+    }
+    return s;
+}
+
+template <class T, int KP>
+static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
+                                uint64_t step_id, int64_t row_offset) {
+    const bool bf = sizeof(T) == 2;
+    hipStream_t st = e->stream;
+    const int nrb = d.nrb;
+    float* gene = e->d_gene;
+    {
+        ScopedTimer tm(e, "k_prep");
+        hipLaunchKernelGGL(k_prep, dim3(d.KP + (d.DP + 255) / 256), dim3(256), 0, st, P, d, gene, e->d_mvec);
+    }
+    {
+        ScopedTimer tm(e, "k_rowscan");
+        hipLaunchKernelGGL(k_rowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
+                           e->d_val, P, d, e->d_rtp, e->d_rowx);
+    }
+    {
+        ScopedTimer tm(e, "k_enc_fwd");
+        hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(nrb * d.nsE), dim3(256), 0, st, e->d_cells, e->d_rowptr,
+                           e->d_col, e->d_val, e->d_rtp, gene, bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f,
+                           d, e->d_hpart);
+    }
+    {
+        ScopedTimer tm(e, "k_latent_fwd");
+        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                           e->d_hpart, e->d_mvec, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id,
+                           row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
+    }
+    DecPtrs Q;
+    Q.lat = e->d_lat;
+    Q.zf = e->d_zf;
+    Q.zb = e->d_zb;
+    Q.gene = gene;
+    Q.Wcd = P.Wcd;
+    Q.Wnd = P.Wnd;
+    Q.covar = e->d_covar;
+    Q.cells = e->d_cells;
+    Q.rowptr = e->d_rowptr;
+    Q.col = e->d_col;
+    Q.val = e->d_val;
+    Q.rtp = e->d_rtp;
+    Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
+    Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
+    Q.lsep = e->d_lsep;
+    Q.rowB = e->d_rowB;
+    Q.dzp = e->d_dzp;
+    Q.slabB = e->d_slabB;
+    Q.slabC = e->d_slabC;
+    Q.lossp = e->d_lossp;
+    const dim3 gdec(nrb * d.nsD);
+    const bool small_cr = (d.C == 1 && d.R == 1);
+    {
+        ScopedTimer tm(e, "k_dec_lse");
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 0, 1, 1>), gdec, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+    }
+    {
+        ScopedTimer tm(e, "k_dec_nb");
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 1, 1, 1>), gdec, dim3(256), dec_lds(d, 1, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 1, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 1, bf), st, Q, d);
+    }
+    NBGrads G = nb_grads(e);
+    if (!update) {
+        ScopedTimer tm(e, "k_loss");
+        hipLaunchKernelGGL(k_grad_small, dim3(1), dim3(256), 0, st, d, e->d_small, 0, G, e->d_smallg, e->d_lossp,
+                           (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
+        return hipGetLastError();
+    }
+    {
+        ScopedTimer tm(e, "k_dec_tail");
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 2, 1, 1>), gdec, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+    }
+    {
+        ScopedTimer tm(e, "k_latent_bwd");
+        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                           e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
+    }
+    {
+        ScopedTimer tm(e, "k_enc_bwd");
+        const size_t lds = (size_t)(2 + d.H) * d.tpsE * 64 * 4 + 64 * (64 + (bf ? 8 : 4)) * (bf ? 2 : 4);
+        hipLaunchKernelGGL((k_enc_bwd<T, KP>), dim3(nrb * d.nsE), dim3(256), lds, st, e->d_cells, e->d_rowptr,
+                           e->d_col, e->d_val, e->d_rtp, e->d_lat, bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f,
+                           e->d_WeP_f, d, e->d_slabE);
+    }
+    {
+        ScopedTimer tm(e, "k_grad_small");
+        const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
+        hipLaunchKernelGGL(k_grad_small, dim3(1 + (SMALL + 255) / 256), dim3(256), 0, st, d, e->d_small,
+                           e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg,
+                           e->d_out, 1);
+    }
+    {
+        ScopedTimer tm(e, "k_grad_genes");
+        hipLaunchKernelGGL(k_grad_genes, dim3((d.D + 255) / 256), dim3(256), 0, st, P, d, G, gene, e->d_slabB,
+                           e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+    }
+    return hipGetLastError();
+}
+
+hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,
+                               uint64_t step_id, int64_t row_offset) {
+    if (e->frozen_dirty) {
+        hipError_t er = nb_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = nb_dims(e, B, n_total, beta);
+    const NBPtrs P = nb_ptrs(e);
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    if (e->KP == 32) return bf ? nb_launch_all<__bf16, 32>(e, d, P, update, use_eps, step_id, row_offset)
+                               : nb_launch_all<float, 32>(e, d, P, update, use_eps, step_id, row_offset);
+    return bf ? nb_launch_all<__bf16, 64>(e, d, P, update, use_eps, step_id, row_offset)
+              : nb_launch_all<float, 64>(e, d, P, update, use_eps, step_id, row_offset);
+}
+
+template <class T, int KP>
+static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
+    const bool bf = sizeof(T) == 2;
+    hipStream_t st = e->stream;
+    hipLaunchKernelGGL(k_prep, dim3(d.KP + (d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene, e->d_mvec);
+    hipLaunchKernelGGL(k_rowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
+                       P, d, e->d_rtp, e->d_rowx);
+    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), 0, st, e->d_cells, e->d_rowptr,
+                       e->d_col, e->d_val, e->d_rtp, e->d_gene, bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f,
+                       d, e->d_hpart);
+    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                       e->d_hpart, e->d_mvec, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
+                       e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
+    return hipGetLastError();
+}
+
+hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
+    if (e->frozen_dirty) {
+        hipError_t er = nb_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = nb_dims(e, B, B, 1.f);
+    const NBPtrs P = nb_ptrs(e);
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    if (e->KP == 32) return bf ? nb_encode_t<__bf16, 32>(e, d, P, d_mean, d_lnvar)
+                               : nb_encode_t<float, 32>(e, d, P, d_mean, d_lnvar);
+    return bf ? nb_encode_t<__bf16, 64>(e, d, P, d_mean, d_lnvar) : nb_encode_t<float, 64>(e, d, P, d_mean, d_lnvar);
+}
+
+}  // namespace mmvae

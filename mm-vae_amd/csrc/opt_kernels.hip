@@ -1,0 +1,75 @@
+// clip_grad_norm_ + torch::optim::Adam (L2 weight decay) over the flat registered-parameter
+// buffer: the reference's mmvae_alg.hh:306-310 (LibTorch 2.10 clip_grad.h:54-86 and
+// optim/adam.cpp).  Two launches: per-block sum of squares, then every block folds the
+// partials, forms the clip coefficient and updates its slice (grad, wd, m, v, p in one pass).
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace mmvae {
+
+static constexpr int SUMSQ_BLOCKS = 256;
+
+__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
+    __shared__ double sb[4];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double v = g[i];
+        s += v * v;
+    }
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = sb[0] + sb[1] + sb[2] + sb[3];
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                              const double* __restrict__ part, int nparts, float max_norm,
+                                              float lr_bc1, float inv_sqrt_bc2, float b1, float b2, float wd,
+                                              float eps, float* __restrict__ out) {
+    __shared__ float s_coef;
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < nparts; ++i) t += part[i];
+        const float total = (float)sqrt(t);            // stack(norms).norm(2), fp32 tensor
+        float coef = max_norm / (total + 1e-6f);       // clip_grad.h:81
+        coef = fminf(coef, 1.f);                        // clamp(max=1), clip_grad.h:82-83
+        s_coef = coef;
+        if (blockIdx.x == 0) out[1] = total;
+    }
+    __syncthreads();
+    const float coef = s_coef;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float gi = g[i] * coef;                         // grad.mul_(clip_coef_clamped)
+        const float pi = p[i];
+        gi = gi + wd * pi;                              // grad.add(p, weight_decay)
+        const float mi = m[i] * b1 + gi * (1.f - b1);   // exp_avg.mul_(b1).add_(grad, 1-b1)
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+        const float denom = sqrtf(vi) * inv_sqrt_bc2 + eps;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi - lr_bc1 * (mi / denom);              // p.addcdiv_(exp_avg, denom, -lr/bc1)
+    }
+}
+
+hipError_t opt_clip_adam(Engine* e) {
+    e->adam_step += 1;
+    const double b1 = 0.9, b2 = 0.999;
+    const double bc1 = 1.0 - std::pow(b1, (double)e->adam_step);
+    const double bc2 = 1.0 - std::pow(b2, (double)e->adam_step);
+    const int64_t n = e->P_reg;
+    {
+        ScopedTimer tm(e, "k_sumsq");
+        hipLaunchKernelGGL(k_sumsq, dim3(SUMSQ_BLOCKS), dim3(256), 0, e->stream, e->d_grads, n, e->d_sumsq);
+    }
+    {
+        ScopedTimer tm(e, "k_adam");
+        hipLaunchKernelGGL(k_adam, dim3(SUMSQ_BLOCKS), dim3(256), 0, e->stream, e->d_params, e->d_grads, e->d_m,
+                           e->d_v, n, e->d_sumsq, SUMSQ_BLOCKS, e->cfg.grad_clip, (float)(e->cfg.lr / bc1),
+                           (float)(1.0 / std::sqrt(bc2)), (float)b1, (float)b2, e->cfg.weight_decay, 1e-8f,
+                           e->d_out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mmvae

@@ -1,0 +1,133 @@
+// Device-side synthetic single-cell dataset (bench / smoke inputs):
+//   p_g ~ Gamma(0.3, 1) normalised (host, seeded), L_c ~ LogNormal(ln lib, 0.5),
+//   x_gc ~ Poisson(L_c p_g Gamma(2, 1/2)).
+// Every (cell, gene) draw is a pure function of (seed, cell, gene) (Philox), so two passes
+// (count, fill) produce a sorted cell-major CSR without storing the dense matrix.
+#include <random>
+#include <vector>
+
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace mmvae {
+
+MMVAE_DEV float u01(uint32_t x) { return ((x >> 8) + 1) * (1.f / 16777217.f); }
+
+MMVAE_DEV int synth_count(uint64_t seed, int64_t cell, int g, float lib_c, const float* pg) {
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)cell, (uint32_t)(cell >> 32), 0x5eedu};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x9e37u);
+    // Gamma(2, 1/2) = 0.5 * (E1 + E2)
+    const float gam = -0.5f * (logf(u01(c[0])) + logf(u01(c[1])));
+    const float lam = lib_c * pg[g] * gam;
+    const float u = u01(c[2]);
+    if (lam > 30.f) {
+        const float n = sqrtf(-2.f * logf(u)) * cosf(6.2831853f * u01(c[3]));
+        return max(0, (int)rintf(lam + sqrtf(lam) * n));
+    }
+    float pk = expf(-lam), cdf = pk;
+    int k = 0;
+    while (u > cdf && k < 200) {
+        ++k;
+        pk *= lam / (float)k;
+        cdf += pk;
+    }
+    return k;
+}
+
+MMVAE_DEV float synth_lib(uint64_t seed, int64_t cell, float loglib) {
+    uint32_t c[4] = {0xffffffffu, (uint32_t)cell, (uint32_t)(cell >> 32), 0x11bu};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float n = sqrtf(-2.f * logf(u01(c[0]))) * cosf(6.2831853f * u01(c[1]));
+    return expf(loglib + 0.5f * n);
+}
+
+__global__ __launch_bounds__(256) void k_synth_count(uint64_t seed, int64_t N, int D, float loglib,
+                                                     const float* __restrict__ pg, int64_t* __restrict__ counts) {
+    __shared__ int sb[4];
+    const int64_t cell = blockIdx.x;
+    const float L = synth_lib(seed, cell, loglib);
+    int n = 0;
+    for (int g = threadIdx.x; g < D; g += 256) n += synth_count(seed, cell, g, L, pg) > 0;
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[cell] = sb[0] + sb[1] + sb[2] + sb[3];
+}
+
+__global__ __launch_bounds__(256) void k_synth_fill(uint64_t seed, int64_t N, int D, float loglib,
+                                                    const float* __restrict__ pg, const int64_t* __restrict__ rowptr,
+                                                    int32_t* __restrict__ col, float* __restrict__ val) {
+    __shared__ int wcnt[4];
+    const int64_t cell = blockIdx.x;
+    const float L = synth_lib(seed, cell, loglib);
+    int64_t base = rowptr[cell];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int g0 = 0; g0 < D; g0 += 256) {
+        const int g = g0 + threadIdx.x;
+        const int x = (g < D) ? synth_count(seed, cell, g, L, pg) : 0;
+        const uint64_t m = __ballot(x > 0);
+        const int before = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[w] = __popcll(m);
+        __syncthreads();
+        int off = 0;
+        for (int i = 0; i < w; ++i) off += wcnt[i];
+        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (x > 0) {
+            col[base + off + before] = g;
+            val[base + off + before] = (float)x;
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out) {
+    const int D = (int)e->D;
+    std::mt19937_64 rng(seed);
+    std::gamma_distribution<double> gam(0.3, 1.0);
+    std::vector<float> pg(D);
+    double tot = 0;
+    std::vector<double> tmp(D);
+    for (int g = 0; g < D; ++g) tot += (tmp[g] = gam(rng));
+    for (int g = 0; g < D; ++g) pg[g] = (float)(tmp[g] / tot);
+    float* d_pg = nullptr;
+    int64_t* d_cnt = nullptr;
+    hipError_t er;
+    if ((er = hipMalloc(&d_pg, sizeof(float) * D)) != hipSuccess) return er;
+    if ((er = hipMalloc(&d_cnt, sizeof(int64_t) * N)) != hipSuccess) return er;
+    hipMemcpy(d_pg, pg.data(), sizeof(float) * D, hipMemcpyHostToDevice);
+    const float loglib = (float)std::log(lib);
+    hipLaunchKernelGGL(k_synth_count, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg, d_cnt);
+    std::vector<int64_t> cnt(N), rp(N + 1, 0);
+    if ((er = hipMemcpyAsync(cnt.data(), d_cnt, sizeof(int64_t) * N, hipMemcpyDeviceToHost, e->stream)) != hipSuccess)
+        return er;
+    if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;
+    for (int64_t i = 0; i < N; ++i) rp[i + 1] = rp[i] + cnt[i];
+    const int64_t nnz = rp[N];
+    hipFree(e->d_rowptr);
+    hipFree(e->d_col);
+    hipFree(e->d_val);
+    hipFree(e->d_covar);
+    e->d_rowptr = nullptr;
+    e->d_col = nullptr;
+    e->d_val = nullptr;
+    e->d_covar = nullptr;
+    if ((er = hipMalloc(&e->d_rowptr, sizeof(int64_t) * (N + 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_col, sizeof(int32_t) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_val, sizeof(float) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_covar, sizeof(float) * N * e->C)) != hipSuccess) return er;
+    hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice);
+    std::vector<float> ones((size_t)N * e->C, 1.f);
+    hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg,
+                       e->d_rowptr, e->d_col, e->d_val);
+    if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;
+    hipFree(d_pg);
+    hipFree(d_cnt);
+    e->N = N;
+    e->nnz = nnz;
+    if (nnz_out) *nnz_out = nnz;
+    return hipGetLastError();
+}
+
+}  // namespace mmvae

@@ -1,0 +1,158 @@
+"""vMF-VAE oracle: the reference's op sequence on ATen CPU fp32 (test infrastructure only).
+
+Restates ``include/models/vmf.hh:250-440``, the Angular layer
+(``include/modules/angular.hh:34-70``) and the custom ``lbessel`` autograd op
+(``include/operators.hh:13-101``).  As in the reference the *latent* is Gaussian; the
+von Mises-Fisher distribution is the likelihood of the L2-normalised log1p data.
+Quirks: Q3 (lbessel backward ignores the upstream gradient), Q4 (ln_kappa starts just below
+kappa_min so the strict clamp mask zeroes its gradient), Q5 (fasterlog/fasterlgamma).
+"""
+from collections import OrderedDict
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .adam import LibTorchAdam, clip_grad_norm_
+from .fastmath import fasterlgamma, fasterlog
+from .nb_oracle import _linear_init
+
+F32 = torch.float32
+
+
+class _LBessel(torch.autograd.Function):
+    """operators.hh:49-101 forward, operators.hh:20-40 backward."""
+
+    @staticmethod
+    def forward(ctx, kappa, nu):
+        ctx.save_for_backward(kappa)
+        ctx.nu = float(nu)
+        nu = float(nu)
+        eta = float(np.float32((nu + 0.5) / (2.0 * (nu + 1.0))))           # const float eta
+        stuff1 = nu * torch.log(kappa) + eta * kappa - (eta + nu) * math.log(2.0) \
+            - float(fasterlgamma(np.float32(nu + 1)))
+        stuff2 = kappa - 0.5 * torch.log(kappa) - 0.5 * math.log(2.0 * math.pi)
+        return torch.le(kappa, nu).type_as(kappa).mul(stuff1) + torch.gt(kappa, nu).type_as(kappa).mul(stuff2)
+
+    @staticmethod
+    def backward(ctx, grad):
+        (x,) = ctx.saved_tensors
+        df = ctx.nu
+        lb = torch.sqrt(x * x * df / (df + 1.0) + df * df)
+        ub = torch.sqrt(x * x + df * df)
+        return 0.5 * (lb + ub) / x, None   # Q3: grad (the upstream) is not used
+
+
+def lbessel_op(kappa, nu):
+    return _LBessel.apply(kappa, nu)
+
+
+def param_names():
+    """vmf_vae_tImpl registration order (vmf.hh:325-388)."""
+    return ["x_mean", "ln_x_sd", "ln_kappa", "covar_encoding.weight", "covar_encoding.bias",
+            "representation_mean.weight", "representation_mean.bias",
+            "representation_logvariance.weight", "representation_logvariance.bias",
+            "covar_decoding_.weight", "covar_decoding_.bias"]
+
+
+def init_params(D, C=1, Z=2, kappa_min=0.1, seed=0):
+    """vmf_vae_tImpl::vmf_vae_tImpl (vmf.hh:307-389), default architecture (no hidden layers)."""
+    g = torch.Generator().manual_seed(seed)
+    p = OrderedDict()
+    p["x_mean"] = torch.zeros((1, D), dtype=F32)
+    p["ln_x_sd"] = torch.ones((1, D), dtype=F32)
+    p["ln_kappa"] = torch.ones((1,), dtype=F32) * float(np.log(np.float32(kappa_min)))  # vmf.hh:323
+    fr = OrderedDict()
+    bound = 1.0 / math.sqrt(D)   # Angular: kaiming_uniform_(a = sqrt 5), angular.hh:62
+    fr["z_enc.0.weight"] = (torch.rand((Z, D), generator=g, dtype=F32) * 2 - 1) * bound
+    p["covar_encoding.weight"], p["covar_encoding.bias"] = _linear_init(g, Z, C)
+    p["representation_mean.weight"], p["representation_mean.bias"] = _linear_init(g, Z, Z)
+    p["representation_logvariance.weight"], p["representation_logvariance.bias"] = _linear_init(g, Z, Z)
+    fr["z_dec.decoding.weight"], fr["z_dec.decoding.bias"] = _linear_init(g, D, Z)
+    p["covar_decoding_.weight"], p["covar_decoding_.bias"] = _linear_init(g, D, C)
+    assert list(p.keys()) == param_names()
+    return p, fr
+
+
+class VMFModel:
+    def __init__(self, params, frozen, kappa_min=0.1, kappa_max=10.0):
+        self.p = OrderedDict((k, v.clone().requires_grad_(True)) for k, v in params.items())
+        self.fr = OrderedDict((k, v.clone()) for k, v in frozen.items())
+        self.kmin, self.kmax = float(np.float32(kappa_min)), float(np.float32(kappa_max))
+
+    def lin(self, name, x):
+        return F.linear(x, self.p[name + ".weight"], self.p[name + ".bias"])
+
+    def angular(self, x):
+        """angular.hh:34-42: W~ = normalize(relu(W) + 1e-4, dim=1); x W~^T (no bias)."""
+        ww = F.normalize(F.relu(self.fr["z_enc.0.weight"]) + 1e-4, p=2.0, dim=1)
+        return F.linear(x, ww)
+
+    def encode(self, x, c=None):
+        """vmf.hh:250-265 (with covariate) / vmf.hh:267-281 (recorder)."""
+        eps = 1e-2 / float(np.float32(x.size(1)))
+        xn = F.normalize(x.log1p(), p=2.0, dim=1)
+        xn_std = torch.div(torch.sub(xn, self.p["x_mean"]), F.softplus(self.p["ln_x_sd"]) + eps)
+        h = self.angular(xn_std)
+        lnvar = torch.clamp(self.lin("representation_logvariance", h), -4.0, 4.0)
+        mean = self.lin("representation_mean", h)
+        if c is not None:
+            mean = mean + self.lin("covar_encoding", c)
+        return mean, lnvar
+
+    def decode(self, z, c):
+        """vmf.hh:283-290."""
+        h = torch.exp(F.linear(z, self.fr["z_dec.decoding.weight"], self.fr["z_dec.decoding.bias"]))
+        hc = self.lin("covar_decoding_", c)
+        return F.normalize(h + hc, p=2.0, dim=1)
+
+    def forward(self, x, c, eps, training=True):
+        """vmf.hh:292-304 (Gaussian reparameterisation vmf.hh:394-404)."""
+        mean, lnvar = self.encode(x, c)
+        z = mean + eps.mul(lnvar.div(2.0).exp()) if training else mean
+        recon = self.decode(z, c)
+        kappa = torch.clamp(torch.exp(self.p["ln_kappa"]), self.kmin, self.kmax)
+        return dict(recon=recon, mean=mean, lnvar=lnvar, kappa=kappa)
+
+
+def vmf_vae_loss(x, y, kl_weight):
+    """vmf.hh:419-440."""
+    eps = 1e-2 / float(np.float32(x.size(1)))
+    yobs = F.normalize(F.relu(x).log1p() + eps, p=2.0, dim=1)
+    n = float(yobs.size(0))
+    dd = float(yobs.size(1))
+    df = float(np.float32(max(0.5 * dd - 1.0, 0.0)))
+    kl = -0.5 * torch.sum(1 + y["lnvar"] - y["mean"].pow(2) - y["lnvar"].exp())
+    llik = torch.sum(yobs * y["recon"], 1) * y["kappa"]
+    llik = llik + (df * torch.log(y["kappa"]) - lbessel_op(y["kappa"], df))
+    llik = llik - 0.5 * dd * float(fasterlog(np.float32(2.0 * math.pi)))
+    return kl / n * kl_weight - llik.sum() / n
+
+
+class VMFTrainer:
+    def __init__(self, params, frozen, lr=1e-3, kappa_min=0.1, kappa_max=10.0, grad_clip=1.0):
+        self.m = VMFModel(params, frozen, kappa_min, kappa_max)
+        self.adam = LibTorchAdam(list(self.m.p.values()), lr=lr, weight_decay=1e-4)
+        self.grad_clip = grad_clip
+
+    def step(self, x, c, eps, beta):
+        y = self.m.forward(x, c, eps, True)
+        L = vmf_vae_loss(x, y, beta)
+        self.adam.zero_grad()
+        L.backward()
+        grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.m.p.items())
+        total = clip_grad_norm_([v.grad for v in self.m.p.values()], self.grad_clip)
+        self.adam.step()
+        return dict(loss=float(L.detach()), grads=grads, total_norm=total)
+
+    @torch.no_grad()
+    def eval_loss(self, x, c, eps, beta):
+        return float(vmf_vae_loss(x, self.m.forward(x, c, eps, True), beta))
+
+    @torch.no_grad()
+    def encode(self, x):
+        return self.m.encode(x, None)
+
+    def params(self):
+        return OrderedDict((k, v.detach().clone()) for k, v in self.m.p.items())

@@ -1,0 +1,92 @@
+"""Generate the golden NB/vMF fixtures from the oracle (run in the build container only).
+
+    python tests/golden/make_golden.py
+
+Each fixture is a small .npz: the dataset CSR, per-step cell ids / covariates / noise /
+beta, the initial registered and frozen parameters (LibTorch names), and per step the
+oracle's loss, pre-clip gradients, clip total-norm and post-Adam parameters, plus one
+eval-forward loss (Q12).  The oracle runs the reference's own call sequence on ATen 2.10
+CPU fp32 (see oracle/__init__.py for why this pins parity).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import nb_oracle, synth  # noqa: E402
+
+NB_CASES = [
+    # name, N, D, K, C, H, R, B, steps, lib, seed
+    ("nb_small", 40, 50, 8, 1, 1, 1, 16, 3, 200.0, 1),
+    ("nb_mid", 300, 500, 16, 1, 1, 1, 64, 3, 300.0, 2),
+    ("nb_generic", 60, 70, 5, 2, 2, 2, 32, 3, 150.0, 3),
+    ("nb_k1", 20, 30, 1, 1, 1, 1, 8, 2, 100.0, 4),
+    ("nb_dups", 10, 40, 8, 1, 1, 1, 24, 2, 120.0, 5),
+    ("nb_k64", 128, 256, 64, 1, 1, 1, 128, 2, 500.0, 6),
+]
+
+
+def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed):
+    rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    if C == 1:
+        covar = np.ones((N, 1), dtype=np.float32)  # nb_vae_main.cc:68-73 auto ones covariate
+    else:
+        covar = rng.standard_normal((N, C)).astype(np.float32)
+    params, frozen = nb_oracle.init_params(D, C=C, K=K, H=H, R=R, seed=seed)
+    tr = nb_oracle.NBTrainer(params, frozen)
+    out = dict(N=N, D=D, K=K, C=C, H=H, R=R, B=B, steps=steps,
+               rowptr=rowptr, col=col, val=val, covar=covar)
+    for k, v in params.items():
+        out["init/" + k] = v.numpy()
+    for k, v in frozen.items():
+        out["frozen/" + k] = v.numpy()
+    nbatch = (N + B - 1) // B
+    for t in range(steps):
+        b = t % nbatch
+        batch = (b * B + np.arange(B)) % N            # mmvae_alg.hh:264-266
+        ridx = rng.integers(0, B, size=B)             # mmvae_alg.hh:292-293
+        cells = batch[ridx]                           # index_select (mmvae_alg.hh:300-301)
+        x = torch.from_numpy(synth.densify(rowptr, col, val, cells, D))
+        c = torch.from_numpy(covar[cells])
+        eps_mu = torch.from_numpy(rng.standard_normal((B, K)).astype(np.float32))
+        eps_nu = torch.from_numpy(rng.standard_normal((B, R)).astype(np.float32))
+        beta = nb_oracle.kl_beta(t)
+        r = tr.step(x, c, eps_mu, eps_nu, beta)
+        out[f"s{t}/cells"] = cells.astype(np.int64)
+        out[f"s{t}/eps_mu"] = eps_mu.numpy()
+        out[f"s{t}/eps_nu"] = eps_nu.numpy()
+        out[f"s{t}/beta"] = np.float32(beta)
+        out[f"s{t}/loss"] = np.float32(r["loss"])
+        out[f"s{t}/total_norm"] = np.float64(r["total_norm"])
+        for k, v in r["grads"].items():
+            out[f"s{t}/grad/" + k] = v.numpy()
+        for k, v in tr.params().items():
+            out[f"s{t}/param/" + k] = v.numpy()
+    # one eval forward (Q12) after the last step, on the first batch
+    cells = (np.arange(B) % N).astype(np.int64)
+    x = torch.from_numpy(synth.densify(rowptr, col, val, cells, D))
+    c = torch.from_numpy(covar[cells])
+    eps_mu = torch.from_numpy(rng.standard_normal((B, K)).astype(np.float32))
+    eps_nu = torch.from_numpy(rng.standard_normal((B, R)).astype(np.float32))
+    out["eval/cells"] = cells
+    out["eval/eps_mu"] = eps_mu.numpy()
+    out["eval/eps_nu"] = eps_nu.numpy()
+    out["eval/beta"] = np.float32(0.5)
+    out["eval/loss"] = np.float32(tr.eval_loss(x, c, eps_mu, eps_nu, 0.5))
+    m, lv = tr.encode(x)
+    out["eval/enc_mean"] = m.numpy()
+    out["eval/enc_lnvar"] = lv.numpy()
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(name, "loss", [float(out[f"s{t}/loss"]) for t in range(steps)], os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(1)
+    for case in NB_CASES:
+        make_nb(*case)

@@ -1,0 +1,70 @@
+"""Shared helpers for the parity tests (fixture loading, engine setup, comparisons)."""
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden_files(prefix="nb_"):
+    return sorted(glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+
+
+def load(path):
+    z = np.load(path)  # allow_pickle defaults to False
+    return {k: z[k] for k in z.files}
+
+
+def dims(z):
+    return {k: int(z[k]) for k in ("N", "D", "K", "C", "H", "R", "B")}
+
+
+def params_of(z, prefix):
+    return {k[len(prefix):]: z[k] for k in z if k.startswith(prefix)}
+
+
+def eps_of(z, tag):
+    return np.concatenate([z[f"{tag}/eps_mu"].ravel(), z[f"{tag}/eps_nu"].ravel()]).astype(np.float32)
+
+
+def engine_from_fixture(z, dtype="f32"):
+    from mmvae_amd import Engine
+    d = dims(z)
+    eng = Engine(D=d["D"], K=d["K"], C=d["C"], H=d["H"], R=d["R"], max_batch=max(d["B"], 64), dtype=dtype)
+    eng.upload_csr(z["rowptr"], z["col"], z["val"], covar=z["covar"])
+    eng.set_params(params_of(z, "init/"))
+    eng.set_params(params_of(z, "frozen/"))
+    return eng
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+def assert_grads_close(got, want, rtol, ctx=""):
+    """Norm-relative: max|got - want| <= rtol * max|want| per tensor."""
+    bad = []
+    for k, w in want.items():
+        e = rel_err(got[k], w)
+        if e > rtol:
+            bad.append((k, e))
+    assert not bad, f"{ctx} gradient mismatch (rtol {rtol}): {bad}"
+
+
+def assert_adam_close(got, want, grads, lr=1e-3, atol=2e-5, ctx=""):
+    """Post-Adam params.  Adam's first steps move every coordinate by ~lr*sign(g): a
+    coordinate whose gradient is at the fp32 noise floor may flip sign, so those are
+    allowed an lr-sized difference; all others must agree to atol."""
+    bad = []
+    for k, w in want.items():
+        g = np.abs(np.asarray(grads[k], np.float64).ravel())
+        d = np.abs(np.asarray(got[k], np.float64).ravel() - np.asarray(w, np.float64).ravel())
+        noisy = g <= 1e-4 * (g.max() + 1e-30)
+        lim = np.where(noisy, 2.5 * lr, atol)
+        if np.any(d > lim):
+            i = int(np.argmax(d - lim))
+            bad.append((k, float(d[i]), float(g[i])))
+    assert not bad, f"{ctx} parameter mismatch after Adam: {bad}"
