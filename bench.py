@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--cells", type=int, default=100000)
     ap.add_argument("--latent", type=int, default=64)
     ap.add_argument("--lib-size", type=float, default=2000.0)
-    ap.add_argument("--cpu-sample", type=int, default=256)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=1024)
+    ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=5)
     return ap.parse_args()
