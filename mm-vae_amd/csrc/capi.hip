@@ -1,5 +1,6 @@
 // C-ABI implementation (include/mmvae_capi.h): handle lifecycle, parameter registry,
 // dataset upload, step orchestration, RCCL gradient all-reduce, kernel timing.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -193,8 +194,10 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         return ns;
     };
     e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R));
+    // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
+    e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split((int)(2 + e->H));
-    e->n_lat_wg = (int)((e->Bpad + 31) / 32);
+    e->n_lat_wg = (int)((e->Bpad + 15) / 16);
     e->klp_off = e->nrb_max * e->nsplit_d;
 
     // latent state layout
@@ -235,7 +238,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, sizeof(int64_t) * Bp));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
-    HIPCHK(e, dalloc(&e->d_gene, 3 * DP));
+    HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
     HIPCHK(e, dalloc(&e->d_mvec, KP));
     HIPCHK(e, dalloc(&e->d_rtp, Bp * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
@@ -243,7 +246,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_lat, Bp * e->lat_stride));
     HIPCHK(e, dalloc(&e->d_zf, Bp * KP));
     HIPCHK(e, dalloc(&e->d_zb, Bp * KP));
-    HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_d * Bp * 2));
+    HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_a * Bp * 2));
     HIPCHK(e, dalloc(&e->d_rowB, (int64_t)e->nsplit_d * Bp * (2 + e->R)));
     HIPCHK(e, dalloc(&e->d_dzp, (int64_t)e->nsplit_d * Bp * 2 * KP));
     HIPCHK(e, dalloc(&e->d_dh, Bp * KP));

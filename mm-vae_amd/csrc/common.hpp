@@ -24,6 +24,7 @@ template <> struct MM<float> {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
     }
     static MMVAE_DEV frag zero() { return 0.f; }
+    static MMVAE_DEV frag load_f32(const float* p) { return *p; }
 };
 
 template <> struct MM<__bf16> {
@@ -32,6 +33,15 @@ template <> struct MM<__bf16> {
     static MMVAE_DEV frag load(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
     static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    // 8 consecutive f32 (16-byte aligned) -> one bf16 fragment (v_cvt_pk_bf16_f32)
+    static MMVAE_DEV frag load_f32(const float* p) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        frag f;
+        f[0] = (__bf16)a.x; f[1] = (__bf16)a.y; f[2] = (__bf16)a.z; f[3] = (__bf16)a.w;
+        f[4] = (__bf16)b.x; f[5] = (__bf16)b.y; f[6] = (__bf16)b.z; f[7] = (__bf16)b.w;
+        return f;
     }
     static MMVAE_DEV frag zero() {
         frag z;
@@ -48,71 +58,88 @@ template <> MMVAE_DEV __bf16 to_t<__bf16>(float v) { return (__bf16)v; }
 // ---------------------------------------------------------------------------------------
 // Scalar math.  fast exp/log/rcp map to v_exp_f32 / v_log_f32 / v_rcp_f32 (quarter rate).
 // ---------------------------------------------------------------------------------------
-MMVAE_DEV float fexp(float x) { return __expf(x); }
-MMVAE_DEV float flog(float x) { return __logf(x); }
+// Raw v_exp_f32 / v_log_f32 (base 2) — no denormal range fix-ups: every call site feeds
+// normal inputs (log args >= 1e-4) or tolerates a flushed tiny exp result.
+MMVAE_DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+MMVAE_DEV float flog2(float x) { return __builtin_amdgcn_logf(x); }
+MMVAE_DEV float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+MMVAE_DEV float flog(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 MMVAE_DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // log(1 + r) for r >= 0, accurate for small r (series below 1e-2, else log(1+r): rel err <= 6e-6)
+// Both candidates are pinned with an empty asm so the compiler emits v_cndmask instead of
+// an exec-masked if/else around the v_log (which costs two divergent paths per element).
 MMVAE_DEV float log1p_pos(float r) {
     float series = r * (1.f - r * (0.5f - r * (0.33333334f - r * (0.25f - r * 0.2f))));
-    return (r < 1e-2f) ? series : flog(1.f + r);
+    float lg = flog(1.f + r);
+    asm volatile("" : "+v"(series), "+v"(lg));
+    return (r < 1e-2f) ? series : lg;
 }
 
-// torch softplus(beta=1, threshold=20) forward; also returns e = exp(min(u,20)) for backward.
-MMVAE_DEV float softplus_e(float u, float& e) {
-    e = fexp(fminf(u, 20.f));
-    return (u > 20.f) ? u : log1p_pos(e);
+// torch softplus(beta=1, threshold=20) and its backward factor, branch free:
+//   sp = max(u, 0) + log1p(exp(-|u|))    (== u in fp32 for u > 20, the threshold branch)
+//   sig = 1 / (1 + exp(-u))             (== 1 in fp32 for u > 20)
+MMVAE_DEV float softplus_sig(float u, float& sig) {
+    const float e = fexp(-fabsf(u));
+    const float r = frcp(1.f + e);
+    sig = (u >= 0.f) ? r : e * r;
+    return fmaxf(u, 0.f) + log1p_pos(e);
 }
-// torch softplus backward factor: u > 20 ? 1 : e / (1 + e)
-MMVAE_DEV float dsoftplus_e(float u, float e) { return (u > 20.f) ? 1.f : e * frcp(1.f + e); }
 
 // accurate torch softplus (libm log1p/exp), for per-row / per-gene scalars
 MMVAE_DEV float softplus_acc(float u) { return (u > 20.f) ? u : log1pf(expf(u)); }
 
-MMVAE_DEV float softplus(float u) {
-    float e;
-    return softplus_e(u, e);
-}
 MMVAE_DEV float dsoftplus(float u) { return (u > 20.f) ? 1.f : 1.f / (1.f + expf(-u)); }
+
+// log Gamma(v), v > 0: shift to v >= 8 (one log of the product), then Stirling's series
+// (truncation error < 1e-9 relative at v >= 8).  Compact: few registers, no tables.
+MMVAE_DEV float lgamma_pos(float v) {
+    float prod = 1.f;
+    while (v < 8.f) {
+        prod *= v;
+        v += 1.f;
+    }
+    const float r = frcp(v), r2 = r * r;
+    const float series = r * (0.083333333f - r2 * (0.0027777778f - r2 * (0.00079365079f - r2 * 0.00059523810f)));
+    return (v - 0.5f) * flog(v) - v + 0.91893853320467274f + series - flog(prod);
+}
 
 // digamma for v > 0: upward recurrence to v >= 6 then the asymptotic series
 MMVAE_DEV float digammaf_(float v) {
     float r = 0.f;
     while (v < 6.f) {
-        r -= 1.f / v;
+        r -= frcp(v);
         v += 1.f;
     }
-    float f = 1.f / (v * v);
-    float t = f * (1.f / 12 - f * (1.f / 120 - f * (1.f / 252 - f * (1.f / 240 - f * (1.f / 132)))));
-    return r + logf(v) - 0.5f / v - t;
+    const float f = frcp(v * v);
+    const float t = f * (1.f / 12 - f * (1.f / 120 - f * (1.f / 252 - f * (1.f / 240 - f * (1.f / 132)))));
+    return r + flog(v) - 0.5f * frcp(v) - t;
 }
 
 // NB gamma terms for count x > 0 and overdispersion nup > 0:
 //   lgd = lgamma(nup) + lgamma(x + 1) - lgamma(nup + x)      (nb.hh:522-523)
 //   dgd = digamma(nup) - digamma(nup + x)                    (its d/d nup)
-// Integer counts up to 16 use the exact finite products/sums; other values use lgammaf.
+// Integer counts up to 64 use the exact finite products/sums (4 factors per log);
+// other values use the compact lgamma / digamma above.
 MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
-    if (x <= 16.f && x == floorf(x)) {
-        int n = (int)x;
-        float lsum = 0.f, rsum = 0.f, lfact = 0.f, prod = 1.f, fprod = 1.f;
+    if (x <= 64.f && x == floorf(x)) {
+        const int n = (int)x;
+        float lsum = 0.f, rsum = 0.f, prod = 1.f, fprod = 1.f;
         for (int i = 0; i < n; ++i) {
-            float v = nup + (float)i;
-            rsum += 1.f / v;
+            const float v = nup + (float)i;
+            rsum += frcp(v);
             prod *= v;
             fprod *= (float)(i + 1);
             if ((i & 3) == 3) {
-                lsum += logf(prod);
-                lfact += logf(fprod);
+                lsum += flog(prod) - flog(fprod);
                 prod = 1.f;
                 fprod = 1.f;
             }
         }
-        lsum += logf(prod);
-        lfact += logf(fprod);
-        lgd = lfact - lsum;
+        lgd = -(lsum + flog(prod) - flog(fprod));
         dgd = -rsum;
     } else {
-        lgd = lgammaf(nup) + lgammaf(x + 1.f) - lgammaf(nup + x);
+        lgd = lgamma_pos(nup) + lgamma_pos(x + 1.f) - lgamma_pos(nup + x);
         dgd = digammaf_(nup) - digammaf_(nup + x);
     }
 }

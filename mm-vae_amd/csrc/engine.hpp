@@ -96,7 +96,8 @@ struct Engine {
     float* d_out = nullptr;          // [0] loss, [1] total norm (float)
     float* h_out_pin = nullptr;
 
-    int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder grids
+    int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder pass-B grids
+    int nsplit_a = 1;                // D-split of decoder passes A / C
     int n_lat_wg = 1;                // latent kernels' workgroups
     int64_t klp_off = 0;             // offset of KL partials inside d_lossp
     hipEvent_t ev_staged = nullptr;  // last H2D copy out of the pinned staging buffers

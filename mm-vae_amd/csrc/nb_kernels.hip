@@ -44,11 +44,13 @@ struct Dims {
     int D, DP, NT, K, KP, C, H, R;
     int B, Bpad, nrb;
     int nsE, tpsE;  // encoder splits, tiles per split
-    int nsD, tpsD;  // decoder splits
+    int nsD, tpsD;  // decoder pass-B splits
+    int nsA, tpsA;  // decoder passes A / C splits
     float inv_n, beta;
     int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
         LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
     int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
+    int four;         // == 4, opaque to the compiler (keeps pass B's gene-block loop rolled)
 };
 
 MMVAE_DEV void wave_sync() {
@@ -75,29 +77,39 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
 // nb.hh:458 nu_dec bias - nu_bias) and the encoder's dense mean term
 // mvec[k] = sum_g x_mean_g / (softplus(ln_x_sd_g) + 1e-4) * W_enc[k, g].
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, float* mvec) {
-    __shared__ float sbuf[8];
-    if ((int)blockIdx.x < d.KP) {
-        const int k = blockIdx.x;
-        float acc = 0.f;
-        if (k < d.K)
-            for (int g = threadIdx.x; g < d.D; g += 256)
-                acc += P.xm[g] / (softplus_acc(P.lsd[g]) + 1e-4f) * P.We[(int64_t)k * d.D + g];
-        float t = block_sum<4>(acc, sbuf);
-        if (threadIdx.x == 0) mvec[k] = t;
-        return;
-    }
-    const int g = (blockIdx.x - d.KP) * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= d.DP) return;
-    float inv = 0.f, bias = -INFINITY, cnu = 0.f;
+    float inv = 0.f, bias = -INFINITY, cnu = 0.f, xmi = 0.f;
     if (g < d.D) {
         inv = 1.f / (softplus_acc(P.lsd[g]) + 1e-4f);
         bias = P.bd[g] + P.bcd[g] + P.mub[g];
         cnu = P.bnd[g] - P.nub[g];
+        xmi = P.xm[g] * inv;
     }
     gene[g] = inv;
     gene[d.DP + g] = bias;
     gene[2 * d.DP + g] = cnu;
+    gene[3 * d.DP + g] = xmi;
+    // packed decoder record (bias, cn, Wcd[g][0], Wnd[g][0]) read once per 16-gene block
+    const bool v = g < d.D;
+    reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
+        float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
+}
+
+// mvec[k] = sum_g x_mean_g / sd_g * W_enc[k, g]  (the dense part of the encoder input)
+__global__ __launch_bounds__(256) void k_mvec(NBPtrs P, Dims d, const float* __restrict__ gene, float* mvec) {
+    __shared__ float sbuf[8];
+    const int k = blockIdx.x;
+    const float* xmi = gene + 3 * d.DP;
+    float acc = 0.f;
+    if (k < d.K) {
+        const float* wr = P.We + (int64_t)k * d.D;
+#pragma unroll 4
+        for (int g = threadIdx.x; g < d.D; g += 256) acc += xmi[g] * wr[g];
+    }
+    const float t = block_sum<4>(acc, sbuf);
+    if (threadIdx.x == 0) mvec[k] = t;
 }
 
 // =======================================================================================
@@ -114,7 +126,7 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= d.Bpad) return;
-    const int64_t cell = cells[b];
+    const int64_t cell = (b < d.B) ? cells[b] : -1;
     int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
     float* rx = rowx + (int64_t)b * d.rowx_stride;
     float pre = 0.f, ln2 = 0.f, hn[HMAX];
@@ -126,20 +138,35 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
         s = rowptr[cell];
         n = (int)(rowptr[cell + 1] - s);
     }
-    for (int j = lane; j < n; j += 64) {
-        const int g = col[s + j];
-        const float x = val[s + j];
-        pre += x * P.wdp[g];
-        const float lx = log1pf(x);
-        ln2 += lx * lx;
+    const int32_t* cr = col + s;
+    const float* vr = val + s;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        int g[4], gp[4];
+        float x[4];
 #pragma unroll
-        for (int h = 0; h < HMAX; ++h)
-            if (h < d.H) hn[h] += x * P.Wne[(int64_t)h * d.D + g];
-        const int t = g >> 6;
-        const int tp = (j == 0) ? -1 : (col[s + j - 1] >> 6);
-        for (int tt = tp + 1; tt <= t; ++tt) rt[tt] = j;
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + lane + 64 * u;
+            const bool ok = j < n;
+            g[u] = ok ? cr[j] : 0;
+            x[u] = ok ? vr[j] : 0.f;
+            gp[u] = (ok && j > 0) ? cr[j - 1] : -64;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + lane + 64 * u;
+            if (j < n) {
+                pre += x[u] * P.wdp[g[u]];
+                const float lx = log1pf(x[u]);
+                ln2 += lx * lx;
+#pragma unroll
+                for (int h = 0; h < HMAX; ++h)
+                    if (h < d.H) hn[h] += x[u] * P.Wne[(int64_t)h * d.D + g[u]];
+                const int t = g[u] >> 6;
+                for (int tt = (gp[u] >> 6) + 1; tt <= t; ++tt) rt[tt] = j;
+            }
+        }
     }
-    const int tlast = (n == 0) ? -1 : (col[s + n - 1] >> 6);
+    const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
     for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
     pre = wave_sum(pre);
     ln2 = wave_sum(ln2);
@@ -335,8 +362,11 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
 // (16 cells x 16 genes per MFMA) is never stored.  Lane l holds, per 16-gene block, gene
 // (l & 15) of cells 4(l>>4)+r, r = 0..3 (the MFMA C layout).
 //   PASS 0 (A): online max / sum-exp per cell                       -> lsep[split][cell]
-//   PASS 1 (B): softmax + NB terms; dz partials on MFMA; column sums -> rowB, dzp, slabB, loss
+//   PASS 1 (B): softmax + NB terms with x = 0 for every element (branch free), then a
+//               compacted pass over the tile's nonzeros adds the x-dependent terms
+//               (x log(s/mu), lgamma/digamma); dz partials on MFMA; column sums
 //   PASS 2 (C): column sums of w_b E_b p_bg (the S_b p term of the softmax backward)
+// The frozen decoder rows of the next tile are prefetched into registers one tile ahead.
 // =======================================================================================
 struct DecPtrs {
     const float* lat;
@@ -361,42 +391,88 @@ struct DecPtrs {
     float* lossp;     // [grid]
 };
 
+// Per-wave CSR entries of 16 rows inside one gene tile, flattened over the wave's lanes.
+// tile_rows() runs with the whole wave active and publishes the rows' inclusive prefix
+// counts to per-wave LDS (rinc[16]); tile_entry_row() then only reads LDS, so it is safe
+// inside divergent code (a cross-lane shuffle there would read inactive lanes as 0).
+MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
+    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(inc, o, 16);
+        if ((lane & 15) >= o) inc += v;
+    }
+    if (lane < 16) rinc[lane] = inc;
+    const int total = __shfl(inc, 15, 64);
+    wave_sync();
+    return total;
+}
+
+// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
+MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) r += (rinc[i] <= e) ? 1 : 0;
+    within = e - (r > 0 ? rinc[r - 1] : 0);
+    return r;
+}
+
 template <class T, int KP, int PASS, int CM, int RM>
-__global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
+__global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
     using M = MM<T>;
-    constexpr int KS = KP / M::KSTEP;
-    constexpr int XS = 68;                                 // f32 x tile row stride
-    constexpr int QS = 64 + (sizeof(T) == 2 ? 8 : 4);      // q tile row stride (elements)
+    using Fr = typename M::frag;
+    constexpr int KS = KP / M::KSTEP;   // k-steps of the logit GEMM
+    constexpr int GK = 64 / M::KSTEP;   // k-steps of the dz GEMM over a 64-gene tile
+    constexpr bool BF = sizeof(T) == 2;
+    constexpr int QS = 64 + (BF ? 8 : 4);  // q1 tile row stride (elements)
+    constexpr int PS = 68;                 // f32 p tile row stride
+    constexpr int NRS = 3 + RM + CM;       // row scalars: d, w, valid, znu[R], c[C]
+    constexpr bool GEN = (CM > 1) || (RM > 1);  // general covariate / overdispersion widths
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
+    const int nsp = (PASS == 1) ? d.nsD : d.nsA;
+    const int tps = (PASS == 1) ? d.tpsD : d.tpsA;
+    const int sp = blockIdx.x % nsp, rb = blockIdx.x / nsp;
     const int row0 = rb * 64 + 16 * w;
-    const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
-    const int GS = d.tpsD * 64;
+    const int t0 = sp * tps, t1 = min(d.NT, t0 + tps);
+    const int ntl = t1 - t0;
+    const int GS = tps * 64;
     const int C = d.C, R = d.R;
     const int nq = (PASS == 1) ? (1 + C) + 1 + R : (1 + C);
-    // LDS carve: colacc [nq][GS] f32 | per-wave x tile [16][XS] f32 | per-wave q1,q2 [16][QS] T
-    float* sl = reinterpret_cast<float*>(smem);  // [4] loss scratch (16 B keeps alignment)
-    float* colacc = sl + 4;
-    const int ncol = (PASS == 0) ? 0 : nq * GS;
-    float* xt = colacc + ncol + w * 16 * XS;
-    T* q1 = reinterpret_cast<T*>(colacc + ncol + 4 * 16 * XS) + w * 2 * 16 * QS;
-    T* q2 = q1 + 16 * QS;
+    const int S = tps + 1;  // rt row stride in LDS
+    // ---- LDS carve (16-byte aligned pieces) ----
+    float* sl = reinterpret_cast<float*>(smem);  // [4]
+    float* colacc = sl + 4;                      // [nq][GS]       (B, C)
+    char* wbase = reinterpret_cast<char*>(colacc + ((PASS == 0) ? 0 : nq * GS));
+    const int wbytes = (PASS == 1) ? (16 * QS * (int)sizeof(T) + 16 * PS * 4 + ((16 * S * 4 + 15) / 16) * 16 +
+                                      16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64)
+                                   : 0;
+    char* wp = wbase + w * wbytes;
+    T* q1 = reinterpret_cast<T*>(wp);
+    float* q2 = reinterpret_cast<float*>(q1 + 16 * QS);
+    int32_t* rtl = reinterpret_cast<int32_t*>(q2 + 16 * PS);
+    int64_t* rbl = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(rtl) + ((16 * S * 4 + 15) / 16) * 16);
+    float* rsc = reinterpret_cast<float*>(rbl + 16);
+    float* rcorr = rsc + 16 * NRS;
+    int32_t* rinc = reinterpret_cast<int32_t*>(rcorr + ((16 * (1 + RM) + 3) / 4) * 4);
+
     if (PASS != 0) {
         for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
         __syncthreads();
     }
     const bool wave_live = row0 < d.Bpad;
-    const T* Z = (sizeof(T) == 2) ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
+    const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
     const T* WdP = reinterpret_cast<const T*>(Q.WdP);
     const T* WdT = reinterpret_cast<const T*>(Q.WdT);
+    const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);  // (bias, cn, Wcd0, Wnd0)
 
     float lossacc = 0.f;
-    // per-row state for my 4 rows
-    float rv[4], lse[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
+    float rv[4], lse2[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
     float mrun[4], srun[4], Eacc[4], Pacc[4], dzn[4][RM], wE[4];
     f32x4 dzA[KP / 16], dzP[KP / 16];
-    typename M::frag zfr[KS];
+    Fr zfr[KS];
+    constexpr float L2E = 1.4426950408889634f;
     if (wave_live) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -416,21 +492,22 @@ __global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
                 znu[r][q] = (q < R) ? L[d.LAT_ZNU + q] : 0.f;
                 dzn[r][q] = 0.f;
             }
-            mrun[r] = -INFINITY;
+            mrun[r] = -1e30f;
             srun[r] = 0.f;
             Eacc[r] = 0.f;
             Pacc[r] = 0.f;
-            lse[r] = 0.f;
+            lse2[r] = 0.f;
             wE[r] = 0.f;
             if (PASS != 0) {
+                // combine the per-split (max, sum-exp) of pass A; kept in log2 units
                 float mm = -INFINITY;
-                for (int s2 = 0; s2 < d.nsD; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
+                for (int s2 = 0; s2 < d.nsA; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
                 float ss = 0.f;
-                for (int s2 = 0; s2 < d.nsD; ++s2) {
+                for (int s2 = 0; s2 < d.nsA; ++s2) {
                     const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
                     ss += lp[1] * expf(lp[0] - mm);
                 }
-                lse[r] = mm + logf(ss);
+                lse2[r] = (mm + logf(ss)) * L2E;
             }
             if (PASS == 2) {
                 float E = 0.f;
@@ -443,184 +520,311 @@ __global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
             dzA[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
             dzP[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-    }
-    // scatter assignment for the x tile (PASS B)
-    const int si = lane >> 2, ssub = lane & 3;
-    int64_t scell = -1, rbase = 0;
-    const int32_t* rt = nullptr;
-    if (PASS == 1 && wave_live) {
-        scell = (row0 + si < d.B) ? Q.cells[row0 + si] : -1;
-        rbase = scell >= 0 ? Q.rowptr[scell] : 0;
-        rt = Q.rtp + (int64_t)(row0 + si) * (d.NT + 1);
+        if (PASS == 1) {
+            // per-wave row data for the sparse pass: tile pointers, CSR bases, row scalars
+            for (int i = lane; i < 16 * S; i += 64) {
+                const int rr = i / S, tt = i % S;
+                rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
+            }
+            if (lane < 16) {
+                const int b = row0 + lane;
+                const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+                rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
+                const float* L = Q.lat + (int64_t)b * d.lat_stride;
+                float* rs = rsc + lane * NRS;
+                rs[0] = L[d.LAT_D];
+                rs[1] = L[d.LAT_W];
+                rs[2] = L[d.LAT_VALID];
+                for (int q = 0; q < RM; ++q) rs[3 + q] = (q < R) ? L[d.LAT_ZNU + q] : 0.f;
+                for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+                for (int q = 0; q < 1 + RM; ++q) rcorr[lane * (1 + RM) + q] = 0.f;
+            }
+            wave_sync();
+        }
     }
 
-    if (wave_live) {
-        for (int t = t0; t < t1; ++t) {
-            if (PASS == 1) {
-                for (int i = lane; i < 16 * XS / 4; i += 64)
-                    reinterpret_cast<float4*>(xt)[i] = float4{0.f, 0.f, 0.f, 0.f};
-                wave_sync();
-                if (scell >= 0) {
-                    const int js = rt[t], je = rt[t + 1];
-                    for (int j = js + ssub; j < je; j += 4)
-                        xt[si * XS + (Q.col[rbase + j] - 64 * t)] = Q.val[rbase + j];
-                }
-                wave_sync();
-            }
-#pragma unroll 1
+    // ---- tile loop.  Decoder rows + per-gene records are prefetched into registers: a whole
+    // tile ahead in the light passes (A, C); a 2-block ring (half a tile ahead) in pass B,
+    // whose long epilogue hides the latency and whose register budget is tight.
+    constexpr bool PF_TILE = PASS != 1;
+    constexpr int NBUF = PF_TILE ? 4 : 2;
+    Fr wc[NBUF][KS], wn[PF_TILE ? 4 : 1][KS];
+    float4 gc[NBUF], gn[PF_TILE ? 4 : 1];
+    auto load_blk = [&](int t, int gb, Fr (&wf)[KS], float4& gr) {
+        const int gene = 64 * t + 16 * gb + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            wf[s] = M::load(&WdP[(int64_t)gene * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+        gr = grec[gene];
+    };
+    if (wave_live && ntl > 0) {
+        if (PF_TILE) {
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) load_blk(t0, gb, wn[PF_TILE ? gb : 0], gn[PF_TILE ? gb : 0]);
+        } else {
+            load_blk(t0, 0, wc[0], gc[0]);
+            load_blk(t0, 1, wc[1], gc[1]);
+        }
+    }
+    for (int t = t0; wave_live && t < t1; ++t) {
+        if (PF_TILE) {
+#pragma unroll
             for (int gb = 0; gb < 4; ++gb) {
-                const int gl = 16 * gb + (lane & 15);
-                const int gene = 64 * t + gl;
-                const bool gv = gene < d.D;
-                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                gc[PF_TILE ? gb : 0] = gn[PF_TILE ? gb : 0];
 #pragma unroll
-                for (int s = 0; s < KS; ++s) {
-                    const auto wf = M::load(&WdP[(int64_t)gene * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
-                    acc = M::mma(zfr[s], wf, acc);
+                for (int s = 0; s < KS; ++s) wc[PF_TILE ? gb : 0][s] = wn[PF_TILE ? gb : 0][s];
+            }
+            if (t + 1 < t1) {
+#pragma unroll
+                for (int gb = 0; gb < 4; ++gb) load_blk(t + 1, gb, wn[PF_TILE ? gb : 0], gn[PF_TILE ? gb : 0]);
+            }
+        }
+        const int tl = t - t0;
+        // sparse-pass entries of this tile: issue the CSR loads now, consume after the epilogue
+        int total = 0;
+        int e_row[2] = {0, 0}, e_gl[2] = {0, 0};
+        float e_x[2] = {0.f, 0.f};
+        if (PASS == 1) {
+            total = tile_rows(rtl, S, tl, lane, rinc);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int e = lane + 64 * k;
+                if (e < total) {
+                    int within;
+                    const int r = tile_entry_row(rinc, e, within);
+                    const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+                    e_row[k] = r;
+                    e_gl[k] = Q.col[gi] - 64 * t;
+                    e_x[k] = Q.val[gi];
                 }
-                const float bias = Q.gene[d.DP + gene];
-                float wcd[CM];
+            }
+        }
+        // 16-gene block body.  Pass B keeps the blocks as a rolled loop: unrolling its long
+        // epilogue 4x multiplies live temporaries past 2 waves/SIMD.  A/C unroll fully.
+        auto gb_body = [&](const int gb) {
+            const int gl = 16 * gb + (lane & 15);
+            const int gene = 64 * t + gl;
+            const bool gv = gene < d.D;
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            float4 g4;
+            if (PF_TILE) {
 #pragma unroll
-                for (int c = 0; c < CM; ++c) wcd[c] = (c < C && gv) ? Q.Wcd[(int64_t)gene * C + c] : 0.f;
-                if (PASS == 0) {
-                    if (gv) {
+                for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[PF_TILE ? gb : 0][s], acc);
+                g4 = gc[PF_TILE ? gb : 0];
+            } else {
+                // two named slots: even blocks use slot 0, odd blocks slot 1; each slot is
+                // refilled with the block two ahead right after its MFMAs consume it
+                constexpr int SL = 0;
+                const int sl = gb & 1;  // resolved statically: gb_body is called with literal parity
+                (void)SL;
+                if (sl == 0) {
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float lg = acc[r] + bias;
+                    for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[0][s], acc);
+                    g4 = gc[0];
+                    if (gb < 2) load_blk(t, gb + 2, wc[0], gc[0]);
+                    else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[0], gc[0]);
+                } else {
 #pragma unroll
-                            for (int c = 0; c < CM; ++c)
-                                if (c < C) lg += crow[r][c] * wcd[c];
-                            const float df = lg - mrun[r];
-                            const float e = fexp(-fabsf(df));
-                            srun[r] = (df > 0.f) ? fmaf(srun[r], e, 1.f) : srun[r] + e;
-                            mrun[r] = fmaxf(mrun[r], lg);
-                        }
-                    }
-                } else if (PASS == 2) {
-                    float cs[1 + CM];
+                    for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[NBUF - 1][s], acc);
+                    g4 = gc[NBUF - 1];
+                    if (gb < 2) load_blk(t, gb + 2, wc[NBUF - 1], gc[NBUF - 1]);
+                    else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[NBUF - 1], gc[NBUF - 1]);
+                }
+            }
+            const float bias = g4.x;
+            float wcd[CM];
+            wcd[0] = g4.z;
 #pragma unroll
-                    for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
+            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && gv) ? Q.Wcd[(int64_t)gene * C + c] : 0.f;
+            if (PASS == 0) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float lg = acc[r] + bias;
+                for (int r = 0; r < 4; ++r) {
+                    float lg = acc[r] + bias;
 #pragma unroll
-                        for (int c = 0; c < CM; ++c)
-                            if (c < C) lg += crow[r][c] * wcd[c];
-                        const float wp = wE[r] * fexp(lg - lse[r]);
-                        cs[0] += wp;
+                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
+                    // online max / sum-exp, branch free.  Padded genes carry bias = -inf, so
+                    // df = -inf, e = 0: they add nothing (mrun starts finite, never NaN).
+                    const float df = lg - mrun[r];
+                    const float e = fexp(-fabsf(df));
+                    const bool up = df > 0.f;
+                    srun[r] = fmaf(srun[r], up ? e : 1.f, up ? 1.f : e);
+                    mrun[r] = fmaxf(mrun[r], lg);
+                }
+            } else if (PASS == 2) {
+                float cs[1 + CM];
 #pragma unroll
-                        for (int c = 0; c < CM; ++c)
-                            if (c < C) cs[1 + c] += wp * crow[r][c];
-                    }
+                for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
 #pragma unroll
-                    for (int c = 0; c < 1 + CM; ++c) {
-                        if (c > C) break;
+                for (int r = 0; r < 4; ++r) {
+                    float lg = acc[r] + bias;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
+                    const float wp = wE[r] * fexp2(fmaf(lg, L2E, -lse2[r]));
+                    cs[0] += wp;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[r][c], cs[1 + c]);
+                }
+#pragma unroll
+                for (int c = 0; c < 1 + CM; ++c) {
+                    if (c <= C) {
                         float v = cs[c];
                         v += __shfl_xor(v, 16, 64);
                         v += __shfl_xor(v, 32, 64);
-                        if (lane < 16) atomicAdd(&colacc[c * GS + (t - t0) * 64 + gl], v);
-                    }
-                } else {
-                    // ---- PASS B: NB likelihood and its gradient terms ----
-                    const float cn = Q.gene[2 * d.DP + gene];
-                    float wnd[RM];
-#pragma unroll
-                    for (int q = 0; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
-                    const float gvf = gv ? 1.f : 0.f;
-                    float cs1[1 + CM], csdu = 0.f, csduz[RM];
-#pragma unroll
-                    for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
-#pragma unroll
-                    for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int rl = 4 * (lane >> 4) + r;
-                        float lg = acc[r] + bias;
-#pragma unroll
-                        for (int c = 0; c < CM; ++c)
-                            if (c < C) lg += crow[r][c] * wcd[c];
-                        const float p = fexp(lg - lse[r]);              // nb.hh:440-441
-                        const float mu = fmaf(p, dv[r], 1e-4f);         // nb.hh:519
-                        float u = cn;
-#pragma unroll
-                        for (int q = 0; q < RM; ++q)
-                            if (q < R) u += wnd[q] * znu[r][q];
-                        float eu;
-                        const float spv = softplus_e(u, eu);            // nb.hh:458
-                        const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);  // nb.hh:459
-                        const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
-                        const float nup = nu + 1e-4f;                   // nb.hh:518
-                        const float s = mu + nup;
-                        const float rs = frcp(s);
-                        const float lgr = log1p_pos(mu * frcp(nup));    // log(s) - log(nup)
-                        float Lv = nup * lgr;                           // nb.hh:528 (x = 0 part)
-                        float q = -mu * rs;                             // n dL/dmu' - 1
-                        float dn = lgr + q;                             // n dL/dnup
-                        const float x = xt[rl * XS + gl];
-                        if (x > 0.f) {
-                            Lv += x * (flog(s) - flog(mu));             // nb.hh:527
-                            q += x * rs - x * frcp(mu);
-                            dn += x * rs;
-                            float lgd, dgd;
-                            nb_gamma_terms(nup, x, lgd, dgd);           // nb.hh:522-523
-                            Lv += lgd;
-                            dn += dgd;
-                        }
-                        const float me = rv[r] * gvf;
-                        lossacc += Lv * me;
-                        const float du = msk ? dn * dsoftplus_e(u, eu) * me : 0.f;
-                        const float pq = p * q;
-                        Eacc[r] += pq;
-                        Pacc[r] += p;
-                        const float wpq = wv[r] * pq;
-                        cs1[0] += wpq;
-#pragma unroll
-                        for (int c = 0; c < CM; ++c)
-                            if (c < C) cs1[1 + c] += wpq * crow[r][c];
-                        csdu += du;
-#pragma unroll
-                        for (int qq = 0; qq < RM; ++qq)
-                            if (qq < R) {
-                                csduz[qq] += du * znu[r][qq];
-                                dzn[r][qq] += du * wnd[qq];
-                            }
-                        q1[rl * QS + gl] = to_t<T>(pq);
-                        q2[rl * QS + gl] = to_t<T>(p);
-                    }
-                    // column sums: reduce over the 4 lane groups, then LDS accumulate
-                    auto red = [&](float v, int slot) {
-                        v += __shfl_xor(v, 16, 64);
-                        v += __shfl_xor(v, 32, 64);
-                        if (lane < 16) atomicAdd(&colacc[slot * GS + (t - t0) * 64 + gl], v);
-                    };
-#pragma unroll
-                    for (int c = 0; c < 1 + CM; ++c)
-                        if (c <= C) red(cs1[c], c);
-                    red(csdu, 1 + C);
-#pragma unroll
-                    for (int qq = 0; qq < RM; ++qq)
-                        if (qq < R) red(csduz[qq], 2 + C + qq);
-                }
-            }
-            if (PASS == 1) {
-                // dz partial = sum_g Q[cell][g] W[g][latent] on MFMA (Q staged through LDS)
-                wave_sync();
-#pragma unroll
-                for (int s = 0; s < 64 / M::KSTEP; ++s) {
-                    const auto a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-                    const auto a2 = M::load(&q2[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-#pragma unroll
-                    for (int lb = 0; lb < KP / 16; ++lb) {
-                        const auto bw = M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t +
-                                                     s * M::KSTEP + (lane >> 4) * M::EPL]);
-                        dzA[lb] = M::mma(a1, bw, dzA[lb]);
-                        dzP[lb] = M::mma(a2, bw, dzP[lb]);
+                        if (lane < 16) atomicAdd(&colacc[c * GS + tl * 64 + gl], v);
                     }
                 }
-                wave_sync();
+            } else {
+                // ---- PASS B dense epilogue: every element as if x = 0 ----
+                const float cn = g4.y;
+                float wnd[RM];
+                wnd[0] = g4.w;
+#pragma unroll
+                for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
+                const float gvf = gv ? 1.f : 0.f;
+                float cs1[1 + CM], csdu = 0.f, csduz[RM];
+#pragma unroll
+                for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
+#pragma unroll
+                for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = 4 * (lane >> 4) + r;
+                    float lg = acc[r] + bias;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
+                    const float p = fexp2(fmaf(lg, L2E, -lse2[r]));      // nb.hh:440-441
+                    const float mu = fmaf(p, dv[r], 1e-4f);              // nb.hh:519
+                    float u = cn;
+#pragma unroll
+                    for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], znu[r][q], u);
+                    float sig;
+                    const float spv = softplus_sig(u, sig);              // nb.hh:458
+                    const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);     // nb.hh:459
+                    const float mskf = ((spv >= 1e-4f) && (spv <= 1e4f)) ? 1.f : 0.f;
+                    const float nup = nu + 1e-4f;                        // nb.hh:518
+                    const float s = mu + nup;
+                    const float rs = frcp(s);
+                    const float lgr = log1p_pos(mu * frcp(nup));         // log(s) - log(nup)
+                    const float me = rv[r] * gvf;
+                    lossacc = fmaf(nup * lgr, me, lossacc);              // nb.hh:528, x = 0
+                    const float q = -mu * rs;                            // n dL/dmu' - 1
+                    const float du = (lgr + q) * sig * (mskf * me);
+                    const float pq = p * q;
+                    Eacc[r] += pq;
+                    Pacc[r] += p;
+                    const float wpq = wv[r] * pq;
+                    cs1[0] += wpq;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) cs1[1 + c] = fmaf(wpq, crow[r][c], cs1[1 + c]);
+                    csdu += du;
+#pragma unroll
+                    for (int qq = 0; qq < RM; ++qq) {
+                        csduz[qq] = fmaf(du, znu[r][qq], csduz[qq]);
+                        dzn[r][qq] = fmaf(du, wnd[qq], dzn[r][qq]);
+                    }
+                    q1[rl * QS + gl] = to_t<T>(pq);
+                    q2[rl * PS + gl] = p;
+                }
+                auto red = [&](float v, int slot) {
+                    v += __shfl_xor(v, 16, 64);
+                    v += __shfl_xor(v, 32, 64);
+                    if (lane < 16) atomicAdd(&colacc[slot * GS + tl * 64 + gl], v);
+                };
+#pragma unroll
+                for (int c = 0; c < 1 + CM; ++c)
+                    if (c <= C) red(cs1[c], c);
+                red(csdu, 1 + C);
+#pragma unroll
+                for (int qq = 0; qq < RM; ++qq)
+                    if (qq < R) red(csduz[qq], 2 + C + qq);
             }
+        };
+        if constexpr (PASS == 1) {
+#pragma unroll 1
+            for (int gp = 0; gp < 4; gp += 2) {
+                gb_body(gp);       // even block: slot 0
+                gb_body(gp + 1);   // odd block: slot 1
+            }
+        } else {
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) gb_body(gb);
         }
-        // ---- per-row outputs ----
+        if (PASS == 1) {
+            wave_sync();
+            // ---- sparse pass: x-dependent terms for the tile's nonzeros only ----
+            auto correct = [&](int r, int gl, float x) {
+                const float* rs_ = rsc + r * NRS;
+                const float p = q2[r * PS + gl];
+                const int gene = 64 * t + gl;
+                const float mu = fmaf(p, rs_[0], 1e-4f);
+                const float4 g4 = grec[gene];
+                float u = g4.y;
+                float wnd[RM];
+                wnd[0] = g4.w;
+#pragma unroll
+                for (int q = 1; q < RM; ++q) wnd[q] = (q < R) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
+#pragma unroll
+                for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], rs_[3 + q], u);
+                float sig;
+                const float spv = softplus_sig(u, sig);
+                const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);
+                const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
+                const float nup = nu + 1e-4f;
+                const float s = mu + nup;
+                const float rs = frcp(s);
+                float lgd, dgd;
+                nb_gamma_terms(nup, x, lgd, dgd);                   // nb.hh:522-523
+                lossacc += x * (flog(s) - flog(mu)) + lgd;          // nb.hh:527
+                const float dq = x * rs - x * frcp(mu);
+                const float pdq = p * dq;
+                q1[r * QS + gl] = to_t<T>(p * (dq - mu * rs));      // p * q with the x terms
+                atomicAdd(&rcorr[r * (1 + RM)], pdq);
+                const float wpdq = rs_[1] * pdq;
+                atomicAdd(&colacc[0 * GS + tl * 64 + gl], wpdq);
+                for (int c = 0; c < C; ++c) atomicAdd(&colacc[(1 + c) * GS + tl * 64 + gl], wpdq * rs_[3 + RM + c]);
+                const float ddu = msk ? (x * rs + dgd) * sig : 0.f;
+                atomicAdd(&colacc[(1 + C) * GS + tl * 64 + gl], ddu);
+                for (int q = 0; q < R; ++q) {
+                    atomicAdd(&colacc[(2 + C + q) * GS + tl * 64 + gl], ddu * rs_[3 + q]);
+                    atomicAdd(&rcorr[r * (1 + RM) + 1 + q], ddu * wnd[q]);
+                }
+            };
+#pragma unroll 1
+            for (int e = lane, k = 0; e < total; e += 64, ++k) {
+                int r, gl;
+                float x;
+                if (k < 2) {
+                    r = k == 0 ? e_row[0] : e_row[1];
+                    gl = k == 0 ? e_gl[0] : e_gl[1];
+                    x = k == 0 ? e_x[0] : e_x[1];
+                } else {
+                    int within;
+                    r = tile_entry_row(rinc, e, within);
+                    const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+                    gl = Q.col[gi] - 64 * t;
+                    x = Q.val[gi];
+                }
+                correct(r, gl, x);
+            }
+            wave_sync();
+            // ---- dz partial = sum_g Q[cell][g] W[g][latent] on MFMA (Q staged through LDS) ----
+#pragma unroll
+            for (int s = 0; s < GK; ++s) {
+                const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+                for (int lb = 0; lb < KP / 16; ++lb) {
+                    const Fr bw = M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t + s * M::KSTEP +
+                                               (lane >> 4) * M::EPL]);
+                    dzA[lb] = M::mma(a1, bw, dzA[lb]);
+                    dzP[lb] = M::mma(a2, bw, dzP[lb]);
+                }
+            }
+            wave_sync();
+        }
+    }
+    // ---- per-row outputs ----
+    if (wave_live) {
         if (PASS == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -629,7 +833,7 @@ __global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
                 for (int o = 1; o < 16; o <<= 1) {
                     const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
                     const float mn = fmaxf(m, m2);
-                    s = (mn == -INFINITY) ? 0.f : s * expf(m - mn) + s2 * expf(m2 - mn);
+                    s = s * expf(m - mn) + s2 * expf(m2 - mn);
                     m = mn;
                 }
                 if ((lane & 15) == 0) {
@@ -651,15 +855,15 @@ __global__ __launch_bounds__(256) void k_dec(DecPtrs Q, Dims d) {
                     E += __shfl_xor(E, o, 64);
                     Pp += __shfl_xor(Pp, o, 64);
 #pragma unroll
-                    for (int q = 0; q < RM; ++q)
-                        if (q < R) dz2[q] += __shfl_xor(dz2[q], o, 64);
+                    for (int q = 0; q < RM; ++q) dz2[q] += __shfl_xor(dz2[q], o, 64);
                 }
-                const int b = row0 + 4 * (lane >> 4) + r;
+                const int rl = 4 * (lane >> 4) + r;
+                const int b = row0 + rl;
                 if ((lane & 15) == 0) {
                     float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
-                    rp[0] = E;
+                    rp[0] = E + rcorr[rl * (1 + RM)];
                     rp[1] = Pp;
-                    for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q];
+                    for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q] + rcorr[rl * (1 + RM) + 1 + q];
                 }
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
@@ -702,8 +906,16 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                                                     float* __restrict__ dhT_f, __bf16* __restrict__ dhT_b,
                                                     float* __restrict__ small) {
     const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP;
-    __shared__ float acc_s[2 * 64 * 64 + 64 * 4 + 64 * CMAX + 4 * RMAX * HMAX + 64];
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
     const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
+    const int KS1 = K + 1;
+    float* sWm = lsm;
+    float* sWl = sWm + K * KS1;
+    float* acc_s = sWl + K * KS1;
+    for (int i = threadIdx.x; i < K * K; i += 256) {
+        sWm[(i / K) * KS1 + i % K] = P.Wm[i];
+        sWl[(i / K) * KS1 + i % K] = P.Wl[i];
+    }
     for (int i = threadIdx.x; i < SMALL; i += 256) acc_s[i] = 0.f;
     __syncthreads();
     float* a_dWm = acc_s;
@@ -768,7 +980,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         float dhj = 0.f;
         for (int kk = 0; kk < K; ++kk) {
             const float dm = __shfl(dmean, kk, 64), dl = __shfl(da, kk, 64);
-            if (k < K) dhj += P.Wm[kk * K + k] * dm + P.Wl[kk * K + k] * dl;
+            if (k < K) dhj += sWm[kk * KS1 + k] * dm + sWl[kk * KS1 + k] * dl;
         }
         if (k < KP) {
             const float v = (k < K) ? dhj : 0.f;
@@ -1001,33 +1213,44 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ slabC,
                                                     const float* __restrict__ slabE,
                                                     const float* __restrict__ smallg, int nrb) {
-    __shared__ float cdh[128];
-    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
-    __syncthreads();
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= d.D) return;
+    constexpr int NQMAX = (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
+    __shared__ float cdh[64];
+    __shared__ float red[3][64][NQMAX + 1];
     const int C = d.C, R = d.R, H = d.H;
     const int nqB = (1 + C) + 1 + R, nqC = 1 + C, nqE = 2 + H;
-    float cs1[1 + CMAX], tc[1 + CMAX], du = 0.f, duz[RMAX], gl = 0.f, raw[1 + HMAX];
+    const int nq = nqB + nqC + nqE;
+    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
+    const int gi = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const int g = blockIdx.x * 64 + gi;
+    float acc[NQMAX];
 #pragma unroll
-    for (int c = 0; c < 1 + CMAX; ++c) cs1[c] = tc[c] = 0.f;
+    for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
+    if (g < d.D) {
+        for (int rb = part; rb < nrb; rb += 4) {
+            const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
+            const float* sC = slabC + (int64_t)rb * nqC * d.DP + g;
+            const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
 #pragma unroll
-    for (int q = 0; q < RMAX; ++q) duz[q] = 0.f;
-#pragma unroll
-    for (int h = 0; h < 1 + HMAX; ++h) raw[h] = 0.f;
-    for (int rb = 0; rb < nrb; ++rb) {
-        const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
-        const float* sC = slabC + (int64_t)rb * nqC * d.DP + g;
-        const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
-        for (int c = 0; c <= C; ++c) {
-            cs1[c] += sB[(int64_t)c * d.DP];
-            tc[c] += sC[(int64_t)c * d.DP];
+            for (int q = 0; q < NQMAX; ++q) {
+                if (q < nqB) acc[q] += sB[(int64_t)q * d.DP];
+                else if (q < nqB + nqC) acc[q] += sC[(int64_t)(q - nqB) * d.DP];
+                else if (q < nq) acc[q] += sE[(int64_t)(q - nqB - nqC) * d.DP];
+            }
         }
-        du += sB[(int64_t)(1 + C) * d.DP];
-        for (int q = 0; q < R; ++q) duz[q] += sB[(int64_t)(2 + C + q) * d.DP];
-        gl += sE[0];
-        for (int h = 0; h < 1 + H; ++h) raw[h] += sE[(int64_t)(1 + h) * d.DP];
     }
+    if (part > 0)
+#pragma unroll
+        for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
+    __syncthreads();
+    if (part != 0 || g >= d.D) return;
+#pragma unroll
+    for (int q = 0; q < NQMAX; ++q) acc[q] += red[0][gi][q] + red[1][gi][q] + red[2][gi][q];
+    const float* cs1 = acc;               // [1+C]
+    const float du = acc[1 + C];
+    const float* duz = acc + 2 + C;       // [R]
+    const float* tc = acc + nqB;          // [1+C]
+    const float gl = acc[nqB + nqC];
+    const float* raw = acc + nqB + nqC + 1;  // depth, nu_enc[H]
     const float inv_n = d.inv_n;
     const float dl = cs1[0] - tc[0];
     G.mub[g] = dl;
@@ -1125,6 +1348,8 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
     d.nsD = e->nsplit_d;
     d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
+    d.nsA = e->nsplit_a;
+    d.tpsA = (int)((e->NT + d.nsA - 1) / d.nsA);
     d.inv_n = 1.f / (float)n_total;
     d.beta = beta;
     d.lat_stride = (int)e->lat_stride;
@@ -1142,6 +1367,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_DHNU = (int)e->LAT_HNU;
     d.LAT_DPRE = (int)e->LAT_HNU + (int)e->H;
     d.rowx_stride = 2 + (int)e->H;
+    d.four = 4;
     return d;
 }
 
@@ -1173,12 +1399,15 @@ hipError_t nb_prepare_frozen(Engine* e) {
     return hipGetLastError();
 }
 
-static size_t dec_lds(const Dims& d, int pass, bool bf16) {
+static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
     const int nq = (pass == 1) ? (1 + d.C) + 1 + d.R : (1 + d.C);
-    size_t s = 16 + ((pass == 0) ? 0 : (size_t)nq * d.tpsD * 64 * 4);
+    const int tps = (pass == 1) ? d.tpsD : d.tpsA;
+    size_t s = 16 + ((pass == 0) ? 0 : (size_t)nq * tps * 64 * 4);
     if (pass == 1) {
-        s += 4 * 16 * 68 * 4;                                      // x tiles
-        s += 4 * 2 * 16 * (64 + (bf16 ? 8 : 4)) * (bf16 ? 2 : 4);  // q tiles
+        const int QS = 64 + (bf16 ? 8 : 4), S = d.tpsD + 1, NRS = 3 + RM + CM;
+        const size_t per = 16 * QS * (bf16 ? 2 : 4) + 16 * 68 * 4 + ((16 * S * 4 + 15) / 16) * 16 +
+                           16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64;
+        s += 4 * per;
     }
     return s;
 }
@@ -1192,7 +1421,11 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     float* gene = e->d_gene;
     {
         ScopedTimer tm(e, "k_prep");
-        hipLaunchKernelGGL(k_prep, dim3(d.KP + (d.DP + 255) / 256), dim3(256), 0, st, P, d, gene, e->d_mvec);
+        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, gene);
+    }
+    {
+        ScopedTimer tm(e, "k_mvec");
+        hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(256), 0, st, P, d, gene, e->d_mvec);
     }
     {
         ScopedTimer tm(e, "k_rowscan");
@@ -1233,16 +1466,17 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     Q.slabC = e->d_slabC;
     Q.lossp = e->d_lossp;
     const dim3 gdec(nrb * d.nsD);
+    const dim3 gdecA(nrb * d.nsA);
     const bool small_cr = (d.C == 1 && d.R == 1);
     {
         ScopedTimer tm(e, "k_dec_lse");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 0, 1, 1>), gdec, dim3(256), dec_lds(d, 0, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 0, 1, 1>), gdecA, dim3(256), dec_lds(d, 0, bf, 1, 1), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX, RMAX>), gdecA, dim3(256), dec_lds(d, 0, bf, CMAX, RMAX), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_dec_nb");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 1, 1, 1>), gdec, dim3(256), dec_lds(d, 1, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 1, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 1, bf), st, Q, d);
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 1, 1, 1>), gdec, dim3(256), dec_lds(d, 1, bf, 1, 1), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 1, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 1, bf, CMAX, RMAX), st, Q, d);
     }
     NBGrads G = nb_grads(e);
     if (!update) {
@@ -1253,12 +1487,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 2, 1, 1>), gdec, dim3(256), dec_lds(d, 2, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 2, 1, 1>), gdecA, dim3(256), dec_lds(d, 2, bf, 1, 1), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX, RMAX>), gdecA, dim3(256), dec_lds(d, 2, bf, CMAX, RMAX), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");
-        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+        const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
+        const size_t lds = (size_t)(2 * d.K * (d.K + 1) + SMALL) * 4;
+        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
                            e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     {
@@ -1277,7 +1513,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_grad_genes");
-        hipLaunchKernelGGL(k_grad_genes, dim3((d.D + 255) / 256), dim3(256), 0, st, P, d, G, gene, e->d_slabB,
+        hipLaunchKernelGGL(k_grad_genes, dim3((d.D + 63) / 64), dim3(256), 0, st, P, d, G, gene, e->d_slabB,
                            e->d_slabC, e->d_slabE, e->d_smallg, nrb);
     }
     return hipGetLastError();
@@ -1302,7 +1538,8 @@ template <class T, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
-    hipLaunchKernelGGL(k_prep, dim3(d.KP + (d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene, e->d_mvec);
+    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene);
+    hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(256), 0, st, P, d, e->d_gene, e->d_mvec);
     hipLaunchKernelGGL(k_rowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
                        P, d, e->d_rtp, e->d_rowx);
     hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), 0, st, e->d_cells, e->d_rowptr,
