@@ -22,6 +22,8 @@
 //   k_latent_bwd  latent heads backward, KL grads, dh
 //   k_enc_bwd     dh^T x log1p(x) tiles on MFMA -> ln_x_sd grad; raw-x column sums
 //   k_grad_small / k_grad_genes   deterministic slab reductions -> flat gradient buffer
+#include <cstdlib>
+
 #include "common.hpp"
 #include "engine.hpp"
 
@@ -50,7 +52,7 @@ struct Dims {
     int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
         LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
     int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
-    int four;         // == 4, opaque to the compiler (keeps pass B's gene-block loop rolled)
+    int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
 };
 
 MMVAE_DEV void wave_sync() {
@@ -586,6 +588,7 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
         float e_x[2] = {0.f, 0.f};
         if (PASS == 1) {
             total = tile_rows(rtl, S, tl, lane, rinc);
+            if (d.dbg & 1) total = 0;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int e = lane + 64 * k;
@@ -621,13 +624,15 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
 #pragma unroll
                     for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[0][s], acc);
                     g4 = gc[0];
-                    if (gb < 2) load_blk(t, gb + 2, wc[0], gc[0]);
+                    if (d.dbg & 8) {
+                    } else if (gb < 2) load_blk(t, gb + 2, wc[0], gc[0]);
                     else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[0], gc[0]);
                 } else {
 #pragma unroll
                     for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[NBUF - 1][s], acc);
                     g4 = gc[NBUF - 1];
-                    if (gb < 2) load_blk(t, gb + 2, wc[NBUF - 1], gc[NBUF - 1]);
+                    if (d.dbg & 8) {
+                    } else if (gb < 2) load_blk(t, gb + 2, wc[NBUF - 1], gc[NBUF - 1]);
                     else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[NBUF - 1], gc[NBUF - 1]);
                 }
             }
@@ -726,6 +731,7 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
                     q2[rl * PS + gl] = p;
                 }
                 auto red = [&](float v, int slot) {
+                    if (d.dbg & 4) { lossacc += v; return; }
                     v += __shfl_xor(v, 16, 64);
                     v += __shfl_xor(v, 32, 64);
                     if (lane < 16) atomicAdd(&colacc[slot * GS + tl * 64 + gl], v);
@@ -773,11 +779,13 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
                 const float s = mu + nup;
                 const float rs = frcp(s);
                 float lgd, dgd;
+                if (d.dbg & 32) { lgd = x * nup; dgd = x + nup; } else
                 nb_gamma_terms(nup, x, lgd, dgd);                   // nb.hh:522-523
                 lossacc += x * (flog(s) - flog(mu)) + lgd;          // nb.hh:527
                 const float dq = x * rs - x * frcp(mu);
                 const float pdq = p * dq;
                 q1[r * QS + gl] = to_t<T>(p * (dq - mu * rs));      // p * q with the x terms
+                if (d.dbg & 64) { lossacc += pdq + ((msk ? (x * rs + dgd) * sig : 0.f)); } else {
                 atomicAdd(&rcorr[r * (1 + RM)], pdq);
                 const float wpdq = rs_[1] * pdq;
                 atomicAdd(&colacc[0 * GS + tl * 64 + gl], wpdq);
@@ -787,6 +795,7 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
                 for (int q = 0; q < R; ++q) {
                     atomicAdd(&colacc[(2 + C + q) * GS + tl * 64 + gl], ddu * rs_[3 + q]);
                     atomicAdd(&rcorr[r * (1 + RM) + 1 + q], ddu * wnd[q]);
+                }
                 }
             };
 #pragma unroll 1
@@ -809,12 +818,12 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             wave_sync();
             // ---- dz partial = sum_g Q[cell][g] W[g][latent] on MFMA (Q staged through LDS) ----
 #pragma unroll
-            for (int s = 0; s < GK; ++s) {
+            for (int s = 0; s < ((d.dbg & 2) ? 0 : GK); ++s) {
                 const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
                 const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t + s * M::KSTEP +
+                    const Fr bw = (d.dbg & 16) ? a1 : M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t + s * M::KSTEP +
                                                (lane >> 4) * M::EPL]);
                     dzA[lb] = M::mma(a1, bw, dzA[lb]);
                     dzP[lb] = M::mma(a2, bw, dzP[lb]);
@@ -1367,7 +1376,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_DHNU = (int)e->LAT_HNU;
     d.LAT_DPRE = (int)e->LAT_HNU + (int)e->H;
     d.rowx_stride = 2 + (int)e->H;
-    d.four = 4;
+    { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
     return d;
 }
 
