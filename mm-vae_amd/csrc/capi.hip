@@ -248,6 +248,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_zb, Bp * KP));
     HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_a * Bp * 2));
     HIPCHK(e, dalloc(&e->d_rowB, (int64_t)e->nsplit_d * Bp * (2 + e->R)));
+    HIPCHK(e, dalloc(&e->d_rowfin, Bp * 2));
     HIPCHK(e, dalloc(&e->d_dzp, (int64_t)e->nsplit_d * Bp * 2 * KP));
     HIPCHK(e, dalloc(&e->d_dh, Bp * KP));
     HIPCHK(e, dalloc(&e->d_dhT_f, Bp * KP));
@@ -276,7 +277,7 @@ int mmvae_destroy(mmvae_h e) {
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b,
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
-                    e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
+                    e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
                     e->d_out, e->d_tmp};
     for (void* b : bufs)

@@ -51,6 +51,24 @@ template <> struct MM<__bf16> {
     }
 };
 
+// ---------------------------------------------------------------------------------------
+// LDS-DMA staging (global_load_lds_dwordx4): the LDS destination is wave-uniform base +
+// 16 * lane, so tiles are staged lane-linear and the bank swizzle is applied on the SOURCE
+// address.  Image of a [rows][RB-byte] tile: 16-byte chunk c of row r lives at chunk
+// c ^ ((r >> 1) & (RB/16 - 1)) — conflict-free for the 16-row MFMA fragment reads
+// (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+MMVAE_DEV void glds16(const void* g, void* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+MMVAE_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
+    constexpr int NCH = RB / 16;
+    return row * RB + ((((byte >> 4) ^ ((row >> 1) & (NCH - 1)))) << 4) + (byte & 15);
+}
+
 template <class T> MMVAE_DEV T to_t(float v);
 template <> MMVAE_DEV float to_t<float>(float v) { return v; }
 template <> MMVAE_DEV __bf16 to_t<__bf16>(float v) { return (__bf16)v; }

@@ -82,6 +82,7 @@ struct Engine {
     __bf16* d_zb = nullptr;
     float* d_lsep = nullptr;         // [nsplit][Bpad][2]
     float* d_rowB = nullptr;         // [nsplit][Bpad][2+R]
+    float* d_rowfin = nullptr;       // [Bpad][2]: lse2, w E
     float* d_dzp = nullptr;          // [nsplit][Bpad][2][KP]
     float* d_dh = nullptr;           // [Bpad][KP]
     float* d_dhT_f = nullptr;        // [KP][Bpad]

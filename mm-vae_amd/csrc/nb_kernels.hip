@@ -385,7 +385,8 @@ struct DecPtrs {
     const int32_t* rtp;
     const void* WdP;  // [DP][KP] T
     const void* WdT;  // [KP][DP] T
-    float* lsep;      // [nsD][Bpad][2]
+    float* lsep;      // [nsA][Bpad][2]
+    float* rowfin;    // [Bpad][2]: lse (log2 units) after pass A, w_b E_b after pass B
     float* rowB;      // [nsD][Bpad][2+R]
     float* dzp;       // [nsD][Bpad][2][KP]
     float* slabB;     // [nrb][nqB][DP]
@@ -500,22 +501,8 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             Pacc[r] = 0.f;
             lse2[r] = 0.f;
             wE[r] = 0.f;
-            if (PASS != 0) {
-                // combine the per-split (max, sum-exp) of pass A; kept in log2 units
-                float mm = -INFINITY;
-                for (int s2 = 0; s2 < d.nsA; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
-                float ss = 0.f;
-                for (int s2 = 0; s2 < d.nsA; ++s2) {
-                    const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
-                    ss += lp[1] * expf(lp[0] - mm);
-                }
-                lse2[r] = (mm + logf(ss)) * L2E;
-            }
-            if (PASS == 2) {
-                float E = 0.f;
-                for (int s2 = 0; s2 < d.nsD; ++s2) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
-                wE[r] = wv[r] * E;
-            }
+            if (PASS != 0) lse2[r] = Q.rowfin[2 * b];        // k_rowfin<0>
+            if (PASS == 2) wE[r] = Q.rowfin[2 * b + 1];      // k_rowfin<1>
         }
 #pragma unroll
         for (int lb = 0; lb < KP / 16; ++lb) {
@@ -545,13 +532,36 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
         }
     }
 
-    // ---- tile loop.  Decoder rows + per-gene records are prefetched into registers: a whole
-    // tile ahead in the light passes (A, C); a 2-block ring (half a tile ahead) in pass B,
-    // whose long epilogue hides the latency and whose register budget is tight.
-    constexpr bool PF_TILE = PASS != 1;
-    constexpr int NBUF = PF_TILE ? 4 : 2;
-    Fr wc[NBUF][KS], wn[PF_TILE ? 4 : 1][KS];
-    float4 gc[NBUF], gn[PF_TILE ? 4 : 1];
+    // ---- tile loop.  Passes A and C stage each tile's decoder rows + per-gene records once
+    // per workgroup into LDS by LDS-DMA (double-buffered, swizzled image, swz_off), so the four
+    // waves share one L2->CU transfer; pass B (VALU-bound, loads hidden behind its epilogue)
+    // keeps a 2-block register ring half a tile ahead.
+    constexpr bool STG = PASS != 1;
+    constexpr int RB = KP * (int)sizeof(T);  // bytes per staged gene row
+    constexpr int NCH = RB / 16;
+    constexpr int STB = 64 * RB + 1024;      // one stage buffer: W tile + grec tile
+    char* stg = wbase;
+    auto stage = [&](int t, int buf) {
+        char* sb = stg + buf * STB;
+        const char* Wt = reinterpret_cast<const char*>(WdP) + (int64_t)64 * t * RB;
+        for (int pc = w; pc <= NCH; pc += 4) {
+            if (pc < NCH) {
+                const int pos = pc * 1024 + lane * 16;
+                const int g = pos / RB, cp = (pos % RB) >> 4;
+                glds16(Wt + g * RB + ((cp ^ ((g >> 1) & (NCH - 1))) << 4), sb + pc * 1024);
+            } else {
+                glds16(grec + 64 * t + lane, sb + 64 * RB);
+            }
+        }
+    };
+    auto wfrag = [&](int buf, int gb, int s) -> Fr {
+        const int g = 16 * gb + (lane & 15);
+        const int off = (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T);
+        return *reinterpret_cast<const Fr*>(stg + buf * STB + swz_off<RB>(g, off));
+    };
+    constexpr int NBUF = 2;
+    Fr wc[NBUF][KS];
+    float4 gc[NBUF];
     auto load_blk = [&](int t, int gb, Fr (&wf)[KS], float4& gr) {
         const int gene = 64 * t + 16 * gb + (lane & 15);
 #pragma unroll
@@ -559,28 +569,17 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             wf[s] = M::load(&WdP[(int64_t)gene * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
         gr = grec[gene];
     };
-    if (wave_live && ntl > 0) {
-        if (PF_TILE) {
-#pragma unroll
-            for (int gb = 0; gb < 4; ++gb) load_blk(t0, gb, wn[PF_TILE ? gb : 0], gn[PF_TILE ? gb : 0]);
-        } else {
-            load_blk(t0, 0, wc[0], gc[0]);
-            load_blk(t0, 1, wc[1], gc[1]);
-        }
+    if (STG) {
+        if (ntl > 0) stage(t0, 0);
+        vm_wait_all();
+        __syncthreads();
+    } else if (wave_live && ntl > 0) {
+        load_blk(t0, 0, wc[0], gc[0]);
+        load_blk(t0, 1, wc[1], gc[1]);
     }
-    for (int t = t0; wave_live && t < t1; ++t) {
-        if (PF_TILE) {
-#pragma unroll
-            for (int gb = 0; gb < 4; ++gb) {
-                gc[PF_TILE ? gb : 0] = gn[PF_TILE ? gb : 0];
-#pragma unroll
-                for (int s = 0; s < KS; ++s) wc[PF_TILE ? gb : 0][s] = wn[PF_TILE ? gb : 0][s];
-            }
-            if (t + 1 < t1) {
-#pragma unroll
-                for (int gb = 0; gb < 4; ++gb) load_blk(t + 1, gb, wn[PF_TILE ? gb : 0], gn[PF_TILE ? gb : 0]);
-            }
-        }
+    for (int t = t0; (STG || wave_live) && t < t1; ++t) {
+        const int buf = (t - t0) & 1;
+        if (STG && t + 1 < t1) stage(t + 1, buf ^ 1);
         const int tl = t - t0;
         // sparse-pass entries of this tile: issue the CSR loads now, consume after the epilogue
         int total = 0;
@@ -610,10 +609,10 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             const bool gv = gene < d.D;
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
             float4 g4;
-            if (PF_TILE) {
+            if (STG) {
 #pragma unroll
-                for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[PF_TILE ? gb : 0][s], acc);
-                g4 = gc[PF_TILE ? gb : 0];
+                for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wfrag(buf, gb, s), acc);
+                g4 = reinterpret_cast<const float4*>(stg + buf * STB + 64 * RB)[gl];
             } else {
                 // two named slots: even blocks use slot 0, odd blocks slot 1; each slot is
                 // refilled with the block two ahead right after its MFMAs consume it
@@ -831,6 +830,7 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             }
             wave_sync();
         }
+        if (STG) __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
     }
     // ---- per-row outputs ----
     if (wave_live) {
@@ -1408,6 +1408,29 @@ hipError_t nb_prepare_frozen(Engine* e) {
     return hipGetLastError();
 }
 
+// Per-row finalisation between decoder passes (one thread per row):
+//   MODE 0: combine pass A's per-split (max, sum-exp) -> log-sum-exp in log2 units
+//   MODE 1: E_b = sum over pass-B splits, stored as w_b E_b for pass C
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rowfin(DecPtrs Q, Dims d) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= d.Bpad) return;
+    if (MODE == 0) {
+        float mm = -INFINITY;
+        for (int s2 = 0; s2 < d.nsA; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
+        float ss = 0.f;
+        for (int s2 = 0; s2 < d.nsA; ++s2) {
+            const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
+            ss += lp[1] * expf(lp[0] - mm);
+        }
+        Q.rowfin[2 * b] = (mm + logf(ss)) * 1.4426950408889634f;
+    } else {
+        float E = 0.f;
+        for (int s2 = 0; s2 < d.nsD; ++s2) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + d.R)];
+        Q.rowfin[2 * b + 1] = Q.lat[(int64_t)b * d.lat_stride + d.LAT_W] * E;
+    }
+}
+
 static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
     const int nq = (pass == 1) ? (1 + d.C) + 1 + d.R : (1 + d.C);
     const int tps = (pass == 1) ? d.tpsD : d.tpsA;
@@ -1417,6 +1440,8 @@ static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
         const size_t per = 16 * QS * (bf16 ? 2 : 4) + 16 * 68 * 4 + ((16 * S * 4 + 15) / 16) * 16 +
                            16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64;
         s += 4 * per;
+    } else {
+        s += 2 * ((size_t)64 * d.KP * (bf16 ? 2 : 4) + 1024);  // double-buffered W + grec stage
     }
     return s;
 }
@@ -1469,6 +1494,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
     Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
     Q.lsep = e->d_lsep;
+    Q.rowfin = e->d_rowfin;
     Q.rowB = e->d_rowB;
     Q.dzp = e->d_dzp;
     Q.slabB = e->d_slabB;
@@ -1483,6 +1509,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX, RMAX>), gdecA, dim3(256), dec_lds(d, 0, bf, CMAX, RMAX), st, Q, d);
     }
     {
+        ScopedTimer tm(e, "k_rowfin");
+        hipLaunchKernelGGL(k_rowfin<0>, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, Q, d);
+    }
+    {
         ScopedTimer tm(e, "k_dec_nb");
         if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 1, 1, 1>), gdec, dim3(256), dec_lds(d, 1, bf, 1, 1), st, Q, d);
         else hipLaunchKernelGGL((k_dec<T, KP, 1, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 1, bf, CMAX, RMAX), st, Q, d);
@@ -1493,6 +1523,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         hipLaunchKernelGGL(k_grad_small, dim3(1), dim3(256), 0, st, d, e->d_small, 0, G, e->d_smallg, e->d_lossp,
                            (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
         return hipGetLastError();
+    }
+    {
+        ScopedTimer tm(e, "k_rowfin");
+        hipLaunchKernelGGL(k_rowfin<1>, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
