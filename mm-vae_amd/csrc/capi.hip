@@ -234,6 +234,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_WdP_b, KP * DP));
     HIPCHK(e, dalloc(&e->d_WdT_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WdT_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WeS_f, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WeS_b, KP * DP));
     HIPCHK(e, dalloc(&e->d_cells, Bp));
     HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, sizeof(int64_t) * Bp));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
@@ -275,7 +277,7 @@ int mmvae_destroy(mmvae_h e) {
     hipStreamSynchronize(e->stream);
     if (e->comm) ncclCommDestroy(e->comm);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
-                    e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b,
+                    e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,

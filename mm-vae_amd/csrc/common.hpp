@@ -7,6 +7,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MMVAE_DEV __device__ __forceinline__
+#define MMVAE_HOSTDEV __host__ __device__ __forceinline__
 
 // ---------------------------------------------------------------------------------------
 // MFMA policy: both policies produce 16x16 f32 tiles with the same C/D layout
@@ -64,6 +65,10 @@ MMVAE_DEV void glds16(const void* g, void* lds_wave_base) {
     __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 MMVAE_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Workgroup barrier that completes this wave's LDS traffic but leaves global loads in flight
+// (a __syncthreads() would drain vmcnt(0), exposing the latency of prefetches issued before it).
+// Any LDS-DMA that the next phase reads must be retired (vm_wait_all) before calling it.
+MMVAE_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
     constexpr int NCH = RB / 16;
     return row * RB + ((((byte >> 4) ^ ((row >> 1) & (NCH - 1)))) << 4) + (byte & 15);

@@ -82,6 +82,8 @@ struct Engine {
     __bf16* d_zb = nullptr;
     float* d_lsep = nullptr;         // [nsplit][Bpad][2]
     float* d_rowB = nullptr;         // [nsplit][Bpad][2+R]
+    float* d_WeS_f = nullptr;        // [KP][DP] encoder weight / sd (per step)
+    __bf16* d_WeS_b = nullptr;
     float* d_rowfin = nullptr;       // [Bpad][2]: lse2, w E
     float* d_dzp = nullptr;          // [nsplit][Bpad][2][KP]
     float* d_dh = nullptr;           // [Bpad][KP]

@@ -79,7 +79,8 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
 // nb.hh:458 nu_dec bias - nu_bias) and the encoder's dense mean term
 // mvec[k] = sum_g x_mean_g / (softplus(ln_x_sd_g) + 1e-4) * W_enc[k, g].
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene) {
+__global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, const float* __restrict__ WeP_f,
+                                              float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= d.DP) return;
     float inv = 0.f, bias = -INFINITY, cnu = 0.f, xmi = 0.f;
@@ -97,6 +98,12 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene) {
     const bool v = g < d.D;
     reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
         float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
+    // encoder weight pre-scaled by 1/(softplus(ln_x_sd)+1e-4): x~ W^T = log1p(x) (W inv)^T - mvec
+    for (int k = 0; k < d.KP; ++k) {
+        const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
+        if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+        else WeS_f[(int64_t)k * d.DP + g] = ws;
+    }
 }
 
 // mvec[k] = sum_g x_mean_g / sd_g * W_enc[k, g]  (the dense part of the encoder input)
@@ -115,11 +122,13 @@ __global__ __launch_bounds__(256) void k_mvec(NBPtrs P, Dims d, const float* __r
 }
 
 // =======================================================================================
-// k_rowscan — one wave per batch row.  Streams the row's CSR once (coalesced):
+// k_rowscan — one wave per batch row.  Streams the row's CSR once (coalesced, 4 chunks of
+// 64 entries in flight per lane):
 //   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
 //   pre_b = depth(x_b) (nb.hh:498, Linear D->1 on raw x), hnu_b = nu_enc(x_b) (nb.hh:448)
-//   lnorm2_b = ||log1p(x_b)||^2 (vMF encoder normalisation, vmf.hh:255)
+// H1: the default overdispersion encoding width H = 1 (nb.hh:60).
 // =======================================================================================
+template <bool H1>
 __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cells,
                                                  const int64_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col,
@@ -131,9 +140,10 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
     const int64_t cell = (b < d.B) ? cells[b] : -1;
     int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
     float* rx = rowx + (int64_t)b * d.rowx_stride;
-    float pre = 0.f, ln2 = 0.f, hn[HMAX];
+    constexpr int HN = H1 ? 1 : HMAX;
+    float pre = 0.f, hn[HN];
 #pragma unroll
-    for (int h = 0; h < HMAX; ++h) hn[h] = 0.f;
+    for (int h = 0; h < HN; ++h) hn[h] = 0.f;
     int n = 0;
     int64_t s = 0;
     if (cell >= 0) {
@@ -142,51 +152,202 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
     }
     const int32_t* cr = col + s;
     const float* vr = val + s;
-    for (int j0 = 0; j0 < n; j0 += 256) {
-        int g[4], gp[4];
-        float x[4];
+    const float* wdp = P.wdp;
+    const float* wne = P.Wne;
+    const int H = H1 ? 1 : d.H;
+    // chunk j0 = 256 entries (4 per lane); the next chunk's loads are issued after this
+    // chunk's table gathers, so waiting for the gathers leaves the prefetch in flight
+    int g[4], gp[4];
+    float x[4];
+    auto load_chunk = [&](int j0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int j = j0 + lane + 64 * u;
+            const int j = j0 + 64 * u + lane;
             const bool ok = j < n;
             g[u] = ok ? cr[j] : 0;
             x[u] = ok ? vr[j] : 0.f;
             gp[u] = (ok && j > 0) ? cr[j - 1] : -64;
         }
+    };
+    if (n > 0) load_chunk(0);
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        int gc[4], gpc[4];
+        float xc[4], wa[4], wb[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int j = j0 + lane + 64 * u;
-            if (j < n) {
-                pre += x[u] * P.wdp[g[u]];
-                const float lx = log1pf(x[u]);
-                ln2 += lx * lx;
+            gc[u] = g[u];
+            gpc[u] = gp[u];
+            xc[u] = x[u];
+            wa[u] = wdp[gc[u]];
+            wb[u] = H1 ? wne[gc[u]] : 0.f;
+        }
+        if (j0 + 256 < n) load_chunk(j0 + 256);
 #pragma unroll
-                for (int h = 0; h < HMAX; ++h)
-                    if (h < d.H) hn[h] += x[u] * P.Wne[(int64_t)h * d.D + g[u]];
-                const int t = g[u] >> 6;
-                for (int tt = (gp[u] >> 6) + 1; tt <= t; ++tt) rt[tt] = j;
+        for (int u = 0; u < 4; ++u) {
+            pre = fmaf(xc[u], wa[u], pre);   // x = 0 on padding lanes
+            if (H1) {
+                hn[0] = fmaf(xc[u], wb[u], hn[0]);
+            } else {
+                for (int h = 0; h < H; ++h)
+                    hn[h < HN ? h : 0] = fmaf(xc[u], wne[(int64_t)h * d.D + gc[u]], hn[h < HN ? h : 0]);
             }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u + lane;
+            if (j < n)
+                for (int tt = (gpc[u] >> 6) + 1; tt <= (gc[u] >> 6); ++tt) rt[tt] = j;
         }
     }
     const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
     for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
     pre = wave_sum(pre);
-    ln2 = wave_sum(ln2);
-#pragma unroll
-    for (int h = 0; h < HMAX; ++h)
-        if (h < d.H) hn[h] = wave_sum(hn[h]);
+    if (H1) {
+        hn[0] = wave_sum(hn[0]);
+    } else {
+        for (int h = 0; h < H; ++h) hn[h < HN ? h : 0] = wave_sum(hn[h < HN ? h : 0]);
+    }
     if (lane == 0) {
         rx[0] = pre + P.bdp[0];
-        rx[1] = ln2;
-        for (int h = 0; h < d.H; ++h) rx[2 + h] = hn[h] + P.bne[h];
+        rx[1] = 0.f;
+        for (int h = 0; h < H; ++h) rx[2 + h] = hn[h < HN ? h : 0] + P.bne[h];
     }
 }
 
 // =======================================================================================
-// k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = (log1p(x)/sd) W^T - mvec, so only
-// the nonzeros are densified: each wave owns 16 cells; per 64-gene tile it zero-fills a
-// 16x64 LDS tile, scatters log1p(x)/sd from the CSR and runs the tile GEMM against the
-// frozen weight [KP][DP].  Grid = (64-cell row block) x (gene split); partial h per split.
+// Per-wave CSR entry streams over 64-gene tiles (a wave owns 16 rows).  A tile's entries are
+// flattened over the rows (row-major, genes ascending) and spread over the lanes: lane l
+// takes entries l and l + 64 (the common case, prefetched a tile ahead into registers);
+// entries past 128 are fetched on the spot.  tile_rows() runs with the whole wave active
+// and publishes the rows' inclusive prefix counts to per-wave LDS (rinc[16]);
+// tile_entry_row() then only reads LDS, so it is safe inside divergent code.
+// rtl = the wave's tile pointers [16][S] (from k_rowscan), rbl = the rows' CSR bases [16].
+// =======================================================================================
+MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
+    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(inc, o, 16);
+        if ((lane & 15) >= o) inc += v;
+    }
+    if (lane < 16) rinc[lane] = inc;
+    const int total = __shfl(inc, 15, 64);
+    wave_sync();
+    return total;
+}
+
+// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
+MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
+    const int4* r4 = reinterpret_cast<const int4*>(rinc);
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int4 v = r4[i];
+        r += (v.x <= e) + (v.y <= e) + (v.z <= e) + (i < 3 ? (v.w <= e) : 0);
+    }
+    within = e - (r > 0 ? rinc[r - 1] : 0);
+    return r;
+}
+
+struct TileEntries {
+    int total;
+    int row[2], gl[2];
+    float x[2];
+};
+
+MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane, int32_t* rinc,
+                          const int64_t* rbl, const int32_t* __restrict__ col, const float* __restrict__ val) {
+    te.total = tile_rows(rtl, S, tl, lane, rinc);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = lane + 64 * k;
+        te.row[k] = -1;
+        te.gl[k] = 0;
+        te.x[k] = 0.f;
+        if (e < te.total) {
+            int within;
+            const int r = tile_entry_row(rinc, e, within);
+            const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+            te.row[k] = r;
+            te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
+            te.x[k] = val[gi];
+        }
+    }
+}
+
+// visit every entry of the fetched tile: f(row, gene-in-tile, x)
+template <class F>
+MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane,
+                          const int32_t* rinc, const int64_t* rbl, const int32_t* __restrict__ col,
+                          const float* __restrict__ val, F&& f) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (te.row[k] >= 0) f(te.row[k], te.gl[k] - 64 * t, te.x[k]);
+    for (int e = 128 + lane; e < te.total; e += 64) {
+        int within;
+        const int r = tile_entry_row(rinc, e, within);
+        const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+        f(r, col[gi] - 64 * t, val[gi]);
+    }
+}
+
+// log1p of a count: exact libm form in the f32 parity mode, fast form for bf16 tiles
+template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : log1p_pos(x); }
+
+// LDS carve shared by the two encoder kernels (host computes the same size)
+struct EncLds {
+    int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;
+    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre) {
+        const int stb = KP * 64 * esz;
+        o_x = pre + 2 * stb;
+        o_rtl = o_x + 4 * xbytes_per_wave;
+        o_rbl = o_rtl + ((4 * 16 * S * 4 + 15) / 16) * 16;
+        o_rinc = o_rbl + 4 * 16 * 8;
+        o_rsc = o_rinc + 4 * 16 * 4;
+        bytes = o_rsc + 4 * 16 * (1 + HMAX) * 4;
+    }
+};
+
+// Register-staged copy of a [NR rows][RB bytes] tile (row stride `ld` bytes in HBM) into the
+// swizzled LDS image read by swz_off<RB>: loads issued early, ds_write_b128 late, so the
+// copy overlaps a compute phase without an LDS-DMA in flight (hipcc drains vmcnt(0) before
+// LDS reads while a DMA is outstanding).
+template <int NR, int RB>
+struct RegStage {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    static constexpr int NC = NR * RB / 16 / 256;  // 16-byte chunks per thread (1, 2 or 4)
+    static_assert(NC >= 1 && NC <= 4, "RegStage: 1..4 chunks per thread");
+    u32x4 v0, v1, v2, v3;
+    MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
+        const int c = (int)threadIdx.x + 256 * i;
+        return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
+    }
+    MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
+        const int c = (int)threadIdx.x + 256 * i;
+        *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
+    }
+    MMVAE_DEV void load(const char* src, int64_t ld) {
+        v0 = ld1(src, ld, 0);
+        if constexpr (NC > 1) v1 = ld1(src, ld, 1);
+        if constexpr (NC > 2) v2 = ld1(src, ld, 2);
+        if constexpr (NC > 3) v3 = ld1(src, ld, 3);
+    }
+    MMVAE_DEV void store(char* dst) const {
+        st1(dst, 0, v0);
+        if constexpr (NC > 1) st1(dst, 1, v1);
+        if constexpr (NC > 2) st1(dst, 2, v2);
+        if constexpr (NC > 3) st1(dst, 3, v3);
+    }
+};
+
+// =======================================================================================
+// k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = log1p(x) (W/sd)^T - mvec, so only
+// the nonzeros are densified.  Workgroup = 64 cells x one gene split; per 64-gene tile the
+// frozen weight tile (pre-scaled by 1/sd in k_prep, [KP][DP]) is staged ONCE per workgroup
+// into LDS by LDS-DMA (double-buffered, swizzled), while each wave scatters its 16 cells'
+// log1p(x) for the NEXT tile into a wave-private 16x64 LDS tile (entries prefetched two
+// tiles ahead).  Partial h per gene split -> hpart.
 // =======================================================================================
 template <class T, int KP>
 __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cells,
@@ -194,55 +355,90 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
                                                  const int32_t* __restrict__ col,
                                                  const float* __restrict__ val,
                                                  const int32_t* __restrict__ rtp,
-                                                 const float* __restrict__ gene_inv,
-                                                 const T* __restrict__ WeP, Dims d,
+                                                 const T* __restrict__ WeS, Dims d,
                                                  float* __restrict__ hpart) {
     using M = MM<T>;
-    constexpr int XS = 64 + (sizeof(T) == 2 ? 8 : 4);
-    __shared__ __attribute__((aligned(16))) T xt_all[4][16 * XS];
+    using Fr = typename M::frag;
+    constexpr int XS = sizeof(T) == 2 ? 80 : 68;   // x tile row stride (elements): conflict-free
+    constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
+    constexpr int NCH = RB / 16;
+    constexpr int STB = KP * RB;
+    constexpr int XB = 2 * 16 * XS * (int)sizeof(T);  // per wave: two x tiles
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    T* xt = xt_all[w];
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
     const int row0 = rb * 64 + 16 * w;
-    if (row0 >= d.Bpad) return;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
+    const int S = d.tpsE + 1;
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0);
+    char* wst = smem;
+    T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
+    int32_t* rtl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
+    int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
+    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16;
+
+    for (int i = lane; i < 16 * S; i += 64) {
+        const int rr = i / S, tt = i % S;
+        rtl[i] = (t0 + tt <= d.NT) ? rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
+    }
+    if (lane < 16) {
+        const int b = row0 + lane;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
+    }
+    for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
+    wave_sync();
+
+    RegStage<KP, RB> wreg;
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
+    (void)NCH;
+    auto scatter = [&](const TileEntries& te, T* dst, int tl, int t) {
+        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val,
+                   [&](int r, int gl, float x) { dst[r * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
+    };
+
     f32x4 acc[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) acc[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int si = lane >> 2, ssub = lane & 3;
-    const int64_t cell = cells[row0 + si];
-    const int64_t rbase = cell >= 0 ? rowptr[cell] : 0;
-    const int32_t* rt = rtp + (int64_t)(row0 + si) * (d.NT + 1);
-    constexpr int ZQ = 16 * XS * (int)sizeof(T) / 16;
+    TileEntries pend;
+    if (t0 < t1) {
+        wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
+        wreg.store(wst);
+        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, col, val);
+        scatter(pend, xt, 0, t0);
+        if (t0 + 1 < t1) tile_fetch(pend, rtl, S, 1, t0 + 1, lane, rinc, rbl, col, val);
+    }
+    vm_wait_all();
+    __syncthreads();
     for (int t = t0; t < t1; ++t) {
-        for (int i = lane; i < ZQ; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
-        wave_sync();
-        if (cell >= 0) {
-            const int js = rt[t], je = rt[t + 1];
-            for (int j = js + ssub; j < je; j += 4) {
-                const int g = col[rbase + j];
-                xt[si * XS + (g - 64 * t)] = to_t<T>(log1pf(val[rbase + j]) * gene_inv[g]);
-            }
-        }
-        wave_sync();
+        const int tl = t - t0, buf = tl & 1;
+        if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
+        const T* xb = xt + buf * 16 * XS;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
-            const auto a = M::load(&xt[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+            const Fr a = *reinterpret_cast<const Fr*>(&xb[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
             for (int lb = 0; lb < KP / 16; ++lb) {
-                const auto bf = M::load(&WeP[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t +
-                                             s * M::KSTEP + (lane >> 4) * M::EPL]);
-                acc[lb] = M::mma(a, bf, acc[lb]);
+                const Fr bw = *reinterpret_cast<const Fr*>(
+                    wst + buf * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                acc[lb] = M::mma(a, bw, acc[lb]);
             }
         }
-        wave_sync();
+        if (t + 1 < t1) {
+            T* xn = xt + (buf ^ 1) * 16 * XS;
+            for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xn)[i] = uint4{0, 0, 0, 0};
+            scatter(pend, xn, tl + 1, t + 1);
+            wreg.store(wst + (buf ^ 1) * STB);
+        }
+        // the entry prefetch below stays in flight across the barrier
+        if (t + 2 < t1) tile_fetch(pend, rtl, S, tl + 2, t + 2, lane, rinc, rbl, col, val);
+        lds_barrier();
     }
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            hpart[((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * KP + 16 * lb + (lane & 15)] =
-                acc[lb][r];
+            hpart[((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * KP + 16 * lb + (lane & 15)] = acc[lb][r];
 }
 
 // =======================================================================================
@@ -393,33 +589,6 @@ struct DecPtrs {
     float* slabC;     // [nrb][1+C][DP]
     float* lossp;     // [grid]
 };
-
-// Per-wave CSR entries of 16 rows inside one gene tile, flattened over the wave's lanes.
-// tile_rows() runs with the whole wave active and publishes the rows' inclusive prefix
-// counts to per-wave LDS (rinc[16]); tile_entry_row() then only reads LDS, so it is safe
-// inside divergent code (a cross-lane shuffle there would read inactive lanes as 0).
-MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
-    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
-    int inc = cnt;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const int v = __shfl_up(inc, o, 16);
-        if ((lane & 15) >= o) inc += v;
-    }
-    if (lane < 16) rinc[lane] = inc;
-    const int total = __shfl(inc, 15, 64);
-    wave_sync();
-    return total;
-}
-
-// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
-MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < 15; ++i) r += (rinc[i] <= e) ? 1 : 0;
-    within = e - (r > 0 ? rinc[r - 1] : 0);
-    return r;
-}
 
 template <class T, int KP, int PASS, int CM, int RM>
 __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
@@ -902,6 +1071,380 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
 }
 
 // =======================================================================================
+// k_dec_nb<T, KP, CM, RM> — decoder pass B: softmax + NB likelihood + every gradient term
+// that needs only the row log-sum-exp (nb.hh:433-442, 453-460, 510-531 and their autograd).
+// Workgroup = 64 cells (4 waves x 16) x one gene split.  Per 64-gene tile:
+//   1. logits on MFMA against the decoder tile staged once per workgroup in LDS, p = softmax
+//      (kept in registers in the MFMA C layout, also written to the wave's LDS p tile)
+//   2. sparse pass over the tile's nonzeros (flattened over the wave's lanes): the
+//      x-dependent terms (x log(s/mu), lgamma/digamma) -> loss, and the two per-element
+//      corrections (p dq, d du) PLAIN-stored into the wave's correction tile (positions
+//      are unique, so no atomics)
+//   3. dense epilogue in the owner lanes (every element as if x = 0, plus its correction):
+//      row sums in registers, column sums reduced across the wave's 16 rows with
+//      permlane swaps and written as per-wave partials
+//   4. dz partials on MFMA from the LDS-staged p*q and p tiles
+//   5. barrier; the four waves' column partials are summed in a fixed order and stored to
+//      this row block's slab in HBM (deterministic, no LDS or global atomics)
+// The next tile's decoder rows, WdT rows and gene records are register-staged during the
+// tile (loads early, ds_write after the barrier); CSR entries are prefetched a tile ahead.
+// =======================================================================================
+template <class T> struct CorrPair;
+template <> struct CorrPair<float> {
+    typedef float2 type;
+    static MMVAE_DEV type pack(float a, float b) { return float2{a, b}; }
+    static MMVAE_DEV void unpack(type v, float& a, float& b) { a = v.x; b = v.y; }
+};
+template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to bf16
+    typedef uint32_t type;
+    static MMVAE_DEV type pack(float a, float b) {
+        const __bf16 x = (__bf16)a, y = (__bf16)b;
+        return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+    }
+    static MMVAE_DEV void unpack(type v, float& a, float& b) {
+        a = __uint_as_float(v << 16);
+        b = __uint_as_float(v & 0xffff0000u);
+    }
+};
+
+// sum over the four 16-lane row groups (lanes l, l^16, l^32, l^48), result in every lane
+MMVAE_DEV float sum_rowgroups(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+struct DecNBLds {
+    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_rtl, o_rbl, o_rsc, o_rinc, bytes;
+    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz) {
+        const int wtile = 64 * KP * esz;
+        o_gst = wtile;
+        o_tst = o_gst + 1024;
+        o_part = o_tst + KP * 64 * esz;
+        o_wave = o_part + ((4 * nq * 64 * 4 + 15) / 16) * 16;
+        const int QS = 64 + (esz == 2 ? 8 : 4);
+        o_q2 = 16 * QS * esz;
+        o_cc = o_q2 + 16 * 68 * 4;
+        o_rtl = o_cc + 16 * 64 * csz;
+        o_rbl = o_rtl + ((16 * S * 4 + 15) / 16) * 16;
+        o_rsc = o_rbl + 16 * 8;
+        o_rinc = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
+        wave_bytes = o_rinc + 64;
+        bytes = o_wave + 4 * wave_bytes;
+    }
+};
+
+template <class T, int KP, int CM, int RM>
+__global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
+    using M = MM<T>;
+    using Fr = typename M::frag;
+    using CP = CorrPair<T>;
+    typedef typename CP::type CT;
+    constexpr int KS = KP / M::KSTEP;   // k-steps of the logit GEMM
+    constexpr int GK = 64 / M::KSTEP;   // k-steps of the dz GEMM over a 64-gene tile
+    constexpr bool BF = sizeof(T) == 2;
+    constexpr int QS = 64 + (BF ? 8 : 4);
+    constexpr int PS = 68;
+    constexpr int NRS = 3 + RM + CM;    // row scalars: d, w, valid, znu[R], c[C]
+    constexpr int RBW = KP * (int)sizeof(T);  // staged decoder row (one gene)
+    constexpr int RBT = 64 * (int)sizeof(T);  // staged WdT row (one latent, 64 genes)
+    constexpr float L2E = 1.4426950408889634f;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
+    const int row0 = rb * 64 + 16 * w;
+    const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
+    const int S = d.tpsD + 1;
+    const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
+    const int nq = (1 + C) + 1 + R;
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT));
+    char* wst = smem;
+    const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
+    char* tst = smem + L.o_tst;
+    float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][nq][64]
+    char* wp = smem + L.o_wave + w * L.wave_bytes;
+    T* q1 = reinterpret_cast<T*>(wp);
+    float* q2 = reinterpret_cast<float*>(wp + L.o_q2);
+    CT* cc = reinterpret_cast<CT*>(wp + L.o_cc);
+    int32_t* rtl = reinterpret_cast<int32_t*>(wp + L.o_rtl);
+    int64_t* rbl = reinterpret_cast<int64_t*>(wp + L.o_rbl);
+    float* rsc = reinterpret_cast<float*>(wp + L.o_rsc);
+    int32_t* rinc = reinterpret_cast<int32_t*>(wp + L.o_rinc);
+    const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
+    const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
+    const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
+    const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);  // (bias, cn, Wcd0, Wnd0)
+
+    // ---- per-row state (lane holds rows 4(lane>>4)+r of the wave's 16) ----
+    Fr zfr[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    float rv[4], lse2[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
+    float Eacc[4], Pacc[4], dzn[4][RM];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = row0 + 4 * (lane >> 4) + r;
+        const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
+        rv[r] = Lr[d.LAT_VALID];
+        dv[r] = Lr[d.LAT_D];
+        wv[r] = Lr[d.LAT_W];
+        lse2[r] = Q.rowfin[2 * b];
+        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+#pragma unroll
+        for (int q = 0; q < RM; ++q) {
+            znu[r][q] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
+            dzn[r][q] = 0.f;
+        }
+        Eacc[r] = 0.f;
+        Pacc[r] = 0.f;
+    }
+    f32x4 dzA[KP / 16], dzP[KP / 16];
+#pragma unroll
+    for (int lb = 0; lb < KP / 16; ++lb) {
+        dzA[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dzP[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float lossacc = 0.f;
+    // ---- per-wave row data for the sparse pass ----
+    for (int i = lane; i < 16 * S; i += 64) {
+        const int rr = i / S, tt = i % S;
+        rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
+    }
+    if (lane < 16) {
+        const int b = row0 + lane;
+        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+        rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
+        const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
+        float* rs = rsc + lane * NRS;
+        rs[0] = Lr[d.LAT_D];
+        rs[1] = Lr[d.LAT_W];
+        rs[2] = Lr[d.LAT_VALID];
+        for (int q = 0; q < RM; ++q) rs[3 + q] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
+        for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+    }
+    for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+
+    // ---- staging of the decoder tile, its gene records and the WdT tile ----
+    RegStage<64, RBW> wreg;
+    RegStage<KP, RBT> treg;
+    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    auto stage_load = [&](int t) {
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
+        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
+    };
+    auto stage_store = [&]() {
+        wreg.store(wst);
+        treg.store(tst);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[threadIdx.x] = greg;
+    };
+    TileEntries pend;
+    if (t0 < t1) {
+        stage_load(t0);
+        stage_store();
+        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+    }
+    __syncthreads();
+
+    for (int t = t0; t < t1; ++t) {
+        const int tl = t - t0;
+        if (t + 1 < t1) stage_load(t + 1);
+        // ---- 1. logits -> p ----
+        float pv[4][4];
+#pragma unroll
+        for (int gb = 0; gb < 4; ++gb) {
+            const int gl = 16 * gb + (lane & 15);
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+            const float4 g4 = gst[gl];
+            float wcd[CM];
+            wcd[0] = g4.z;
+#pragma unroll
+            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float lg = acc[r] + g4.x;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
+                pv[gb][r] = fexp2(fmaf(lg, L2E, -lse2[r]));           // nb.hh:440-441
+                q2[(4 * (lane >> 4) + r) * PS + gl] = pv[gb][r];
+            }
+        }
+        wave_sync();
+        // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
+        tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val, [&](int r, int gl, float x) {
+            const float* rs_ = rsc + r * NRS;
+            const float p = q2[r * PS + gl];
+            const float mu = fmaf(p, rs_[0], 1e-4f);
+            const float4 g4 = gst[gl];
+            float wnd[RM];
+            wnd[0] = g4.w;
+#pragma unroll
+            for (int q = 1; q < RM; ++q) wnd[q] = (q < R) ? Q.Wnd[(int64_t)(64 * t + gl) * R + q] : 0.f;
+            float u = g4.y;
+#pragma unroll
+            for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], rs_[3 + q], u);
+            float sig;
+            const float spv = softplus_sig(u, sig);
+            const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);
+            const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
+            const float nup = nu + 1e-4f;
+            const float sv = mu + nup;
+            const float rsv = frcp(sv);
+            float lgd, dgd;
+            nb_gamma_terms(nup, x, lgd, dgd);                           // nb.hh:522-523
+            lossacc += x * (flog(sv) - flog(mu)) + lgd;                 // nb.hh:527
+            const float dq = x * rsv - x * frcp(mu);
+            const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
+            cc[r * 64 + gl] = CP::pack(p * dq, ddu);
+        });
+        wave_sync();
+        // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
+        if (t + 1 < t1) tile_fetch(pend, rtl, S, tl + 1, t + 1, lane, rinc, rbl, Q.col, Q.val);
+        // ---- 3. dense epilogue in the owner lanes ----
+#pragma unroll 1
+        for (int gb = 0; gb < 4; ++gb) {
+            const int gl = 16 * gb + (lane & 15);
+            const int gene = 64 * t + gl;
+            const bool gv = gene < d.D;
+            const float4 g4 = gst[gl];
+            const float cn = g4.y;
+            float wnd[RM];
+            wnd[0] = g4.w;
+#pragma unroll
+            for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
+            const float gvf = gv ? 1.f : 0.f;
+            float cs1[1 + CM], csdu = 0.f, csduz[RM];
+#pragma unroll
+            for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
+#pragma unroll
+            for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
+            float pg[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pg[r] = (gb == 0) ? pv[0][r] : (gb == 1) ? pv[1][r] : (gb == 2) ? pv[2][r] : pv[3][r];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = 4 * (lane >> 4) + r;
+                const float p = pg[r];
+                const float mu = fmaf(p, dv[r], 1e-4f);              // nb.hh:519
+                float u = cn;
+#pragma unroll
+                for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], znu[r][q], u);
+                float sig;
+                const float spv = softplus_sig(u, sig);              // nb.hh:458
+                const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);     // nb.hh:459
+                const float mskf = ((spv >= 1e-4f) && (spv <= 1e4f)) ? 1.f : 0.f;
+                const float nup = nu + 1e-4f;                        // nb.hh:518
+                const float sv = mu + nup;
+                const float rsv = frcp(sv);
+                const float lgr = log1p_pos(mu * frcp(nup));         // log(s) - log(nup)
+                const float me = rv[r] * gvf;
+                lossacc = fmaf(nup * lgr, me, lossacc);              // nb.hh:528, x = 0 part
+                const float q = -mu * rsv;                           // n dL/dmu' - 1 at x = 0
+                float cpq, cdu;
+                CP::unpack(cc[rl * 64 + gl], cpq, cdu);
+                const float pq = fmaf(p, q, cpq);
+                const float du = fmaf((lgr + q) * sig, mskf * me, cdu);
+                Eacc[r] += pq;
+                Pacc[r] += p;
+                const float wpq = wv[r] * pq;
+                cs1[0] += wpq;
+#pragma unroll
+                for (int c = 0; c < CM; ++c) cs1[1 + c] = fmaf(wpq, crow[r][c], cs1[1 + c]);
+                csdu += du;
+#pragma unroll
+                for (int qq = 0; qq < RM; ++qq) {
+                    csduz[qq] = fmaf(du, znu[r][qq], csduz[qq]);
+                    dzn[r][qq] = fmaf(du, wnd[qq], dzn[r][qq]);
+                }
+                q1[rl * QS + gl] = to_t<T>(pq);
+            }
+            float* pw = part + w * nq * 64 + gl;
+#pragma unroll
+            for (int c = 0; c < 1 + CM; ++c)
+                if (c <= C) {
+                    const float v = sum_rowgroups(cs1[c]);
+                    if (lane < 16) pw[c * 64] = v;
+                }
+            {
+                const float v = sum_rowgroups(csdu);
+                if (lane < 16) pw[(1 + C) * 64] = v;
+            }
+#pragma unroll
+            for (int qq = 0; qq < RM; ++qq)
+                if (qq < R) {
+                    const float v = sum_rowgroups(csduz[qq]);
+                    if (lane < 16) pw[(2 + C + qq) * 64] = v;
+                }
+        }
+        wave_sync();
+        for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
+#pragma unroll
+        for (int s = 0; s < GK; ++s) {
+            const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+            const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+            for (int lb = 0; lb < KP / 16; ++lb) {
+                const Fr bw = *reinterpret_cast<const Fr*>(
+                    tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                dzA[lb] = M::mma(a1, bw, dzA[lb]);
+                dzP[lb] = M::mma(a2, bw, dzP[lb]);
+            }
+        }
+        // ---- 5. combine the waves' column partials -> slab (fixed order) ----
+        lds_barrier();
+        for (int i = threadIdx.x; i < nq * 64; i += 256) {
+            const int q = i >> 6, g = i & 63;
+            const float v = part[(0 * nq + q) * 64 + g] + part[(1 * nq + q) * 64 + g] + part[(2 * nq + q) * 64 + g] +
+                            part[(3 * nq + q) * 64 + g];
+            Q.slabB[((int64_t)rb * nq + q) * d.DP + 64 * t + g] = v;
+        }
+        if (t + 1 < t1) stage_store();
+        lds_barrier();
+    }
+    // ---- per-row outputs ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float E = Eacc[r], Pp = Pacc[r];
+        float dz2[RM];
+#pragma unroll
+        for (int q = 0; q < RM; ++q) dz2[q] = dzn[r][q];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            E += __shfl_xor(E, o, 64);
+            Pp += __shfl_xor(Pp, o, 64);
+#pragma unroll
+            for (int q = 0; q < RM; ++q) dz2[q] += __shfl_xor(dz2[q], o, 64);
+        }
+        const int b = row0 + 4 * (lane >> 4) + r;
+        if ((lane & 15) == 0) {
+            float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
+            rp[0] = E;
+            rp[1] = Pp;
+            for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q < RM ? q : 0];
+        }
+#pragma unroll
+        for (int lb = 0; lb < KP / 16; ++lb) {
+            float* dp = Q.dzp + (((int64_t)sp * d.Bpad + b) * 2) * KP + 16 * lb + (lane & 15);
+            dp[0] = dzA[lb][r];
+            dp[KP] = dzP[lb][r];
+        }
+    }
+    const float lw = wave_sum(lossacc);
+    __syncthreads();
+    if (lane == 0) part[w] = lw;
+    __syncthreads();
+    if (threadIdx.x == 0) Q.lossp[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// =======================================================================================
 // k_latent_bwd — backward of reparameterisation, clamps, KL and the K x K heads
 // (autograd of nb.hh:412-416, 449-450, 462-472, 498, 533-548) per cell; per-workgroup
 // partial sums of the small-parameter gradients.
@@ -1069,94 +1612,142 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
 // =======================================================================================
 // k_enc_bwd — gradient of x_mean / ln_x_sd through the frozen encoder (autograd of
 // nb.hh:408-411) and of depth / nu_enc weights (raw x, nb.hh:448,498):
-//   Gl_g = sum_k W_enc[k,g] sum_b dh_bk log1p(x_bg)   (MFMA on densified 64x64 tiles)
-//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}     (LDS atomics during the scatter)
+//   Gl_g = sum_k W_enc[k,g] M[k,g],  M = dh^T log1p(x)   (MFMA on densified 64x64 tiles)
+//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}       (LDS atomics during the scatter)
+// Workgroup = 64 cells x one gene split.  The x tile [64 genes][64 cells] is shared by the
+// four waves (each wave owns one 16-latent block of M and scatters its own 16 cells into the
+// tile's cell columns); the W_enc tile for the epilogue is staged by LDS-DMA.  Both are
+// double-buffered with one barrier per tile.
 // =======================================================================================
-template <class T, int KP>
+template <class T, int KP, bool H1>
 __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cells,
                                                  const int64_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col,
                                                  const float* __restrict__ val,
                                                  const int32_t* __restrict__ rtp, const float* __restrict__ lat,
-                                                 const T* __restrict__ dhT, const float* __restrict__ WeF,
+                                                 const T* __restrict__ dhT, const T* __restrict__ WeP,
                                                  Dims d, float* __restrict__ slabE) {
     using M = MM<T>;
-    constexpr int LS = 64 + (sizeof(T) == 2 ? 8 : 4);
+    using Fr = typename M::frag;
+    constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // x tile row (gene) stride in elements
+    constexpr int RB = 64 * (int)sizeof(T);
+    constexpr int NCH = RB / 16;
+    constexpr int STB = KP * RB;
+    constexpr int XT = 64 * LS * (int)sizeof(T);   // one shared x tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
+    const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
+    const int S = d.tpsE + 1;
     const int GS = d.tpsE * 64;
-    const int nq = 2 + d.H;
+    const int H = H1 ? 1 : d.H;
+    const int nq = 2 + H;
+    constexpr int HN = H1 ? 1 : HMAX;
+    const int pre = ((nq * GS * 4 + 15) / 16) * 16;
+    // carve: colacc | W stage x2 | x tiles x2 (shared, in the per-wave x region) | per-wave rows
+    const EncLds L(KP, (int)sizeof(T), S, XT / 2, pre);
     float* colacc = reinterpret_cast<float*>(smem);
-    T* lt = reinterpret_cast<T*>(colacc + nq * GS);  // [64 genes][LS] : cells contiguous
+    char* wst = smem + pre;
+    T* lt = reinterpret_cast<T*>(smem + L.o_x);  // [2][64 genes][LS]
+    int32_t* rtl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
+    int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
+    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16;
+    float* rsc = reinterpret_cast<float*>(smem + L.o_rsc) + w * 16 * (1 + HMAX);
+
     for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
-    const int si = lane >> 2, ssub = lane & 3;
-    const int brow = rb * 64 + 16 * w + si;
-    const int64_t cell = (brow < d.B) ? cells[brow] : -1;
-    const int64_t rbase = cell >= 0 ? rowptr[cell] : 0;
-    const int32_t* rt = rtp + (int64_t)brow * (d.NT + 1);
-    float dpre = 0.f, dhn[HMAX];
-    if (cell >= 0) {
-        const float* L = lat + (int64_t)brow * d.lat_stride;
-        dpre = L[d.LAT_DPRE];
-#pragma unroll
-        for (int h = 0; h < HMAX; ++h) dhn[h] = (h < d.H) ? L[d.LAT_DHNU + h] : 0.f;
-    } else {
-#pragma unroll
-        for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
+    for (int i = lane; i < 16 * S; i += 64) {
+        const int rr = i / S, tt = i % S;
+        rtl[i] = (t0 + tt <= d.NT) ? rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
     }
+    if (lane < 16) {
+        const int b = row0 + lane;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
+        const float* Lr = lat + (int64_t)b * d.lat_stride;
+        rsc[lane * (1 + HMAX)] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
+        for (int h = 0; h < H; ++h) rsc[lane * (1 + HMAX) + 1 + h] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
+    }
+    // this wave's 16 cell columns of a tile: 64 genes x 32 bytes (bf16) / 64 bytes (f32)
+    auto zero_cols = [&](T* tile) {
+        constexpr int CB = 16 * (int)sizeof(T) / 16;  // uint4 per gene row
+#pragma unroll
+        for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(tile + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+    };
+    zero_cols(lt);
+    zero_cols(lt + 64 * LS);
+    // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
+    const int lb = w;
     constexpr int KSB = 64 / M::KSTEP;
-    typename M::frag afr[KP / 64 > 0 ? KP / 64 : 1][KSB];
-    const int nlb = KP / 16;
+    Fr afr[KSB];
 #pragma unroll
-    for (int li = 0; li < (KP / 64 > 0 ? KP / 64 : 1); ++li) {
-        const int lb = w + 4 * li;
-#pragma unroll
-        for (int s = 0; s < KSB; ++s)
-            afr[li][s] = (lb < nlb) ? M::load(&dhT[(int64_t)(16 * lb + (lane & 15)) * d.Bpad + rb * 64 +
-                                                   s * M::KSTEP + (lane >> 4) * M::EPL])
-                                    : M::zero();
+    for (int s = 0; s < KSB; ++s)
+        afr[s] = (lb < KP / 16) ? M::load(&dhT[(int64_t)(16 * lb + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
+                                               (lane >> 4) * M::EPL])
+                                : M::zero();
+    wave_sync();
+
+    RegStage<KP, RB> wreg;
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
+    (void)NCH;
+    auto scatter = [&](const TileEntries& te, T* tile, int tl, int t) {
+        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val, [&](int r, int gl, float x) {
+            tile[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
+            const float* rs = rsc + r * (1 + HMAX);
+            atomicAdd(&colacc[1 * GS + tl * 64 + gl], rs[0] * x);
+            for (int h = 0; h < H; ++h) atomicAdd(&colacc[(2 + h) * GS + tl * 64 + gl], rs[1 + h] * x);
+        });
+    };
+    (void)HN;
+
+    TileEntries pend;
+    if (t0 < t1) {
+        wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
+        wreg.store(wst);
+        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, col, val);
+        __syncthreads();  // colacc zeroed before the scatter's atomics
+        scatter(pend, lt, 0, t0);
+        if (t0 + 1 < t1) tile_fetch(pend, rtl, S, 1, t0 + 1, lane, rinc, rbl, col, val);
     }
-    constexpr int ZQ = 64 * LS * (int)sizeof(T) / 16;
+    vm_wait_all();
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
-        for (int i = threadIdx.x; i < ZQ; i += 256) reinterpret_cast<uint4*>(lt)[i] = uint4{0, 0, 0, 0};
-        __syncthreads();
-        if (cell >= 0) {
-            const int js = rt[t], je = rt[t + 1];
-            for (int j = js + ssub; j < je; j += 4) {
-                const int g = col[rbase + j] - 64 * t;
-                const float x = val[rbase + j];
-                lt[g * LS + 16 * w + si] = to_t<T>(log1pf(x));
-                atomicAdd(&colacc[1 * GS + (t - t0) * 64 + g], dpre * x);
-                for (int h = 0; h < d.H; ++h) atomicAdd(&colacc[(2 + h) * GS + (t - t0) * 64 + g], dhn[h] * x);
-            }
-        }
-        __syncthreads();
+        const int tl = t - t0, buf = tl & 1;
+        if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
+        const T* xb = lt + buf * 64 * LS;
+        const char* wb = wst + buf * STB;
+        if (lb < KP / 16) {
 #pragma unroll
-        for (int li = 0; li < (KP / 64 > 0 ? KP / 64 : 1); ++li) {
-            const int lb = w + 4 * li;
-            if (lb >= nlb) break;
-#pragma unroll 1
             for (int gb = 0; gb < 4; ++gb) {
                 f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KSB; ++s) {
-                    const auto bf = M::load(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-                    acc = M::mma(afr[li][s], bf, acc);
+                    const Fr bx = *reinterpret_cast<const Fr*>(&xb[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    acc = M::mma(afr[s], bx, acc);
                 }
-                const int gene = 64 * t + 16 * gb + (lane & 15);
+                const int gl = 16 * gb + (lane & 15);
                 float v = 0.f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v += WeF[(int64_t)(16 * lb + 4 * (lane >> 4) + r) * d.DP + gene] * acc[r];
+                for (int r = 0; r < 4; ++r) {
+                    const int k = 16 * lb + 4 * (lane >> 4) + r;
+                    v = fmaf(static_cast<float>(*reinterpret_cast<const T*>(wb + swz_off<RB>(k, gl * (int)sizeof(T)))), acc[r], v);
+                }
                 v += __shfl_xor(v, 16, 64);
                 v += __shfl_xor(v, 32, 64);
-                if (lane < 16) atomicAdd(&colacc[(t - t0) * 64 + 16 * gb + (lane & 15)], v);
+                if (lane < 16) atomicAdd(&colacc[tl * 64 + gl], v);
             }
         }
-        __syncthreads();
+        if (t + 1 < t1) {
+            T* xn = lt + (buf ^ 1) * 64 * LS;
+            zero_cols(xn);
+            scatter(pend, xn, tl + 1, t + 1);
+            wreg.store(wst + (buf ^ 1) * STB);
+        }
+        // the entry prefetch below stays in flight across the barrier
+        if (t + 2 < t1) tile_fetch(pend, rtl, S, tl + 2, t + 2, lane, rinc, rbl, col, val);
+        lds_barrier();
     }
+    __syncthreads();
     const int gbase = t0 * 64;
     const int glen = min(d.DP, t1 * 64) - gbase;
     for (int i = threadIdx.x; i < nq * GS; i += 256) {
@@ -1216,26 +1807,32 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
     G.bdp[0] = s;
 }
 
+// Per-gene gradients from the per-row-block column slabs of passes B, C and k_enc_bwd,
+// summed in a fixed order (deterministic).  32 genes x 8 row-block partitions per workgroup.
+// SMALL: the default widths C = R = H = 1 (9 slab rows per gene, all compile-time).
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ gene,
                                                     const float* __restrict__ slabB,
                                                     const float* __restrict__ slabC,
                                                     const float* __restrict__ slabE,
                                                     const float* __restrict__ smallg, int nrb) {
-    constexpr int NQMAX = (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
+    constexpr int NQMAX = SMALL ? 9 : (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
+    constexpr int NPART = 8;
     __shared__ float cdh[64];
-    __shared__ float red[3][64][NQMAX + 1];
-    const int C = d.C, R = d.R, H = d.H;
+    __shared__ float red[NPART - 1][32][NQMAX + 1];
+    const int C = SMALL ? 1 : d.C, R = SMALL ? 1 : d.R, H = SMALL ? 1 : d.H;
     const int nqB = (1 + C) + 1 + R, nqC = 1 + C, nqE = 2 + H;
     const int nq = nqB + nqC + nqE;
     for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
-    const int gi = threadIdx.x & 63, part = threadIdx.x >> 6;
-    const int g = blockIdx.x * 64 + gi;
+    const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
+    const int g = blockIdx.x * 32 + gi;
     float acc[NQMAX];
 #pragma unroll
     for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
     if (g < d.D) {
-        for (int rb = part; rb < nrb; rb += 4) {
+#pragma unroll 2
+        for (int rb = part; rb < nrb; rb += NPART) {
             const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
             const float* sC = slabC + (int64_t)rb * nqC * d.DP + g;
             const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
@@ -1253,7 +1850,9 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     __syncthreads();
     if (part != 0 || g >= d.D) return;
 #pragma unroll
-    for (int q = 0; q < NQMAX; ++q) acc[q] += red[0][gi][q] + red[1][gi][q] + red[2][gi][q];
+    for (int pp = 0; pp < NPART - 1; ++pp)
+#pragma unroll
+        for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
     const float* cs1 = acc;               // [1+C]
     const float du = acc[1 + C];
     const float* duz = acc + 2 + C;       // [R]
@@ -1270,6 +1869,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     for (int q = 0; q < R; ++q) G.Wnd[(int64_t)g * R + q] = duz[q] * inv_n;
     // encoder normalisation params (nb.hh:408-410)
     float gs = 0.f;
+#pragma unroll 8
     for (int k = 0; k < d.K; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
     const float inv = gene[g];
     G.xm[g] = -inv * gs;
@@ -1447,6 +2047,18 @@ static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
 }
 
 template <class T, int KP>
+static size_t enc_fwd_lds(const Dims& d) {
+    constexpr int XS = sizeof(T) == 2 ? 80 : 68;
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes;
+}
+template <class T, int KP>
+static size_t enc_bwd_lds(const Dims& d) {
+    constexpr int LS = sizeof(T) == 2 ? 80 : 68;
+    const int pre = (((2 + d.H) * d.tpsE * 64 * 4 + 15) / 16) * 16;
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 64 * LS * (int)sizeof(T) / 2, pre).bytes;
+}
+
+template <class T, int KP>
 static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
                                 uint64_t step_id, int64_t row_offset) {
     const bool bf = sizeof(T) == 2;
@@ -1455,7 +2067,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     float* gene = e->d_gene;
     {
         ScopedTimer tm(e, "k_prep");
-        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, gene);
+        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, gene, e->d_WeP_f, e->d_WeS_f,
+                           bf ? e->d_WeS_b : nullptr);
     }
     {
         ScopedTimer tm(e, "k_mvec");
@@ -1463,14 +2076,18 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_rowscan");
-        hipLaunchKernelGGL(k_rowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
-                           e->d_val, P, d, e->d_rtp, e->d_rowx);
+        if (d.H == 1)
+            hipLaunchKernelGGL(k_rowscan<true>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr,
+                               e->d_col, e->d_val, P, d, e->d_rtp, e->d_rowx);
+        else
+            hipLaunchKernelGGL(k_rowscan<false>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr,
+                               e->d_col, e->d_val, P, d, e->d_rtp, e->d_rowx);
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
-        hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(nrb * d.nsE), dim3(256), 0, st, e->d_cells, e->d_rowptr,
-                           e->d_col, e->d_val, e->d_rtp, gene, bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f,
-                           d, e->d_hpart);
+        hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_cells,
+                           e->d_rowptr, e->d_col, e->d_val, e->d_rtp, bf ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d,
+                           e->d_hpart);
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
@@ -1514,8 +2131,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_nb");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 1, 1, 1>), gdec, dim3(256), dec_lds(d, 1, bf, 1, 1), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 1, CMAX, RMAX>), gdec, dim3(256), dec_lds(d, 1, bf, CMAX, RMAX), st, Q, d);
+        const int nqB = (1 + d.C) + 1 + d.R;
+        const int csz = bf ? 4 : 8;
+        if (small_cr)
+            hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1>), gdec, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz).bytes, st, Q, d);
+        else
+            hipLaunchKernelGGL((k_dec_nb<T, KP, CMAX, RMAX>), gdec, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz).bytes, st, Q, d);
     }
     NBGrads G = nb_grads(e);
     if (!update) {
@@ -1542,10 +2165,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_enc_bwd");
-        const size_t lds = (size_t)(2 + d.H) * d.tpsE * 64 * 4 + 64 * (64 + (bf ? 8 : 4)) * (bf ? 2 : 4);
-        hipLaunchKernelGGL((k_enc_bwd<T, KP>), dim3(nrb * d.nsE), dim3(256), lds, st, e->d_cells, e->d_rowptr,
-                           e->d_col, e->d_val, e->d_rtp, e->d_lat, bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f,
-                           e->d_WeP_f, d, e->d_slabE);
+        const T* WeT = bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f;
+        const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
+        if (d.H == 1)
+            hipLaunchKernelGGL((k_enc_bwd<T, KP, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+                               e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
+        else
+            hipLaunchKernelGGL((k_enc_bwd<T, KP, false>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+                               e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
     }
     {
         ScopedTimer tm(e, "k_grad_small");
@@ -1556,8 +2183,12 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_grad_genes");
-        hipLaunchKernelGGL(k_grad_genes, dim3((d.D + 63) / 64), dim3(256), 0, st, P, d, G, gene, e->d_slabB,
-                           e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        if (d.C == 1 && d.R == 1 && d.H == 1)
+            hipLaunchKernelGGL(k_grad_genes<true>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        else
+            hipLaunchKernelGGL(k_grad_genes<false>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
     }
     return hipGetLastError();
 }
@@ -1581,13 +2212,18 @@ template <class T, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
-    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene);
+    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
+                       bf ? e->d_WeS_b : nullptr);
     hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(256), 0, st, P, d, e->d_gene, e->d_mvec);
-    hipLaunchKernelGGL(k_rowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
-                       P, d, e->d_rtp, e->d_rowx);
-    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), 0, st, e->d_cells, e->d_rowptr,
-                       e->d_col, e->d_val, e->d_rtp, e->d_gene, bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f,
-                       d, e->d_hpart);
+    if (d.H == 1)
+        hipLaunchKernelGGL(k_rowscan<true>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
+                           e->d_val, P, d, e->d_rtp, e->d_rowx);
+    else
+        hipLaunchKernelGGL(k_rowscan<false>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
+                           e->d_val, P, d, e->d_rtp, e->d_rowx);
+    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_cells,
+                           e->d_rowptr, e->d_col, e->d_val, e->d_rtp, bf ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d,
+                           e->d_hpart);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
                        e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
