@@ -197,7 +197,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split((int)(2 + e->H));
-    e->n_lat_wg = (int)((e->Bpad + 15) / 16);
+    e->n_lat_wg = (int)(e->Bpad / 64);  // latent kernels: 64 cells per workgroup
     e->klp_off = e->nrb_max * e->nsplit_d;
 
     // latent state layout

@@ -442,13 +442,16 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
 }
 
 // =======================================================================================
-// k_latent_fwd — per cell (one wave, lane = latent k):
+// k_latent_fwd — the K x K heads and the reparameterisation for 64 cells per workgroup
+// (wave w owns cells 16w..16w+15, lane = latent k):
 //   h = mu_enc(x~) (+ frozen bias), mean = mu_repr_mean(h) + covar_enc(c) (nb.hh:412-416),
 //   lnvar = clamp(mu_repr_lnvar(h), -4, 4), z = mean + eps*exp(lnvar/2) (nb.hh:462-472),
 //   nu path (nb.hh:444-451, 489-492), depth d = softplus(pre) (nb.hh:498), KL terms (nb.hh:533-537).
+// The heads are [64 cells x K] x [K x K] products: W rows from LDS (lane-distinct), h from an
+// LDS [cell][k] image read as wave-uniform broadcasts.
 //   mode 1 = recorder encode_mu(x) (nb.hh:419-431): no covariate, writes mean/lnvar out.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_latent_fwd(
+__global__ __launch_bounds__(1024) void k_latent_fwd(
     NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowx,
     const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
@@ -456,48 +459,62 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
-    __shared__ float sred[4];
-    for (int i = threadIdx.x; i < K * K; i += 256) {
+    __shared__ __attribute__((aligned(16))) float sH[64 * 68];  // [cell][k]
+    __shared__ float sred[16];
+    for (int i = threadIdx.x; i < K * K; i += 1024) {
         sWm[(i / K) * 65 + i % K] = P.Wm[i];
         sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
-    __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int cpw = (d.Bpad + gridDim.x * 4 - 1) / (gridDim.x * 4);
+    const int k = lane;
+    const int bw = blockIdx.x * 64 + 4 * w;  // first cell of this wave (4 cells per wave)
+    // h = sum of the encoder's gene-split partials - mvec + bias
+    const float hb = (k < K) ? P.be[k] - mvec[k] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        float h = 0.f;
+        if (k < K && b < d.Bpad) {
+            h = hb;
+            for (int s2 = 0; s2 < d.nsE; ++s2) h += hpart[((int64_t)s2 * d.Bpad + b) * d.KP + k];
+        }
+        sH[(4 * w + c) * 68 + k] = h;
+    }
+    __syncthreads();
+    float mean[4], av[4];
+    const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        mean[c] = bm;
+        av[c] = bl;
+    }
+    const int kk = (k < K) ? k : 0;
+    for (int jj = 0; jj < K; ++jj) {
+        const float wm = sWm[kk * 65 + jj], wl = sWl[kk * 65 + jj];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float hj = sH[(4 * w + c) * 68 + jj];
+            mean[c] = fmaf(wm, hj, mean[c]);
+            av[c] = fmaf(wl, hj, av[c]);
+        }
+    }
     float kl = 0.f;
-    for (int ci = 0; ci < cpw; ++ci) {
-        const int b = (blockIdx.x * 4 + w) * cpw + ci;
-        if (b >= d.Bpad) break;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
         const int64_t cell = (b < d.B) ? cells[b] : -1;
         const bool valid = cell >= 0;
         float* L = lat + (int64_t)b * d.lat_stride;
-        const int k = lane;
-        float h = 0.f;
-        if (k < K) {
-            for (int s = 0; s < d.nsE; ++s) h += hpart[((int64_t)s * d.Bpad + b) * d.KP + k];
-            h = h - mvec[k] + P.be[k];
-        }
-        float mean = 0.f, a = 0.f;
-        if (k < K) {
-            mean = P.bm[k];
-            a = P.bl[k];
-        }
-        for (int j = 0; j < K; ++j) {
-            const float hj = __shfl(h, j, 64);
-            if (k < K) {
-                mean += sWm[k * 65 + j] * hj;
-                a += sWl[k * 65 + j] * hj;
-            }
-        }
+        const float h = sH[(4 * w + c) * 68 + k];
+        float mn = mean[c], a = av[c];
         if (k < K && mode == 0) {
             float cm = P.bce[k];
-            for (int c = 0; c < d.C; ++c) cm += P.Wce[k * d.C + c] * (valid ? covar[cell * d.C + c] : 0.f);
-            mean += cm;
+            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * (valid ? covar[cell * d.C + q] : 0.f);
+            mn += cm;
         }
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
         if (mode == 1) {
             if (k < K && b < d.B) {
-                out_mean[(int64_t)b * K + k] = mean;
+                out_mean[(int64_t)b * K + k] = mn;
                 out_lnvar[(int64_t)b * K + k] = lnvar;
             }
             continue;
@@ -506,13 +523,13 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         float eps = 0.f;
         if (k < K && b < d.B)
             eps = eps_in ? eps_in[(int64_t)b * K + k] : philox_normal(seed, step, row_offset + b, k);
-        const float z = mean + eps * sig;
+        const float z = mn + eps * sig;
         if (k < K) {
             L[d.LAT_H + k] = h;
-            L[d.LAT_MEAN + k] = mean;
+            L[d.LAT_MEAN + k] = mn;
             L[d.LAT_A + k] = a;
             L[d.LAT_EPS + k] = eps;
-            if (valid) kl += 1.f + lnvar - mean * mean - expf(lnvar);
+            if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
         }
         if (k < d.KP) {
             const float zz = (k < K && valid) ? z : 0.f;
@@ -551,7 +568,11 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
-    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * (sred[0] + sred[1] + sred[2] + sred[3]);
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int q = 0; q < 16; ++q) t += sred[q];
+        klpart[blockIdx.x] = -0.5f * t;
+    }
 }
 
 // =======================================================================================
@@ -1446,11 +1467,14 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 
 // =======================================================================================
 // k_latent_bwd — backward of reparameterisation, clamps, KL and the K x K heads
-// (autograd of nb.hh:412-416, 449-450, 462-472, 498, 533-548) per cell; per-workgroup
-// partial sums of the small-parameter gradients.
+// (autograd of nb.hh:412-416, 449-450, 462-472, 498, 533-548) for 64 cells per workgroup:
 //   dz = w_b (A''_b - E_b P_b),  w_b = d_b / n   (see oracle/nb_analytic.py)
+// Per cell (lane = latent): dmean, dlnvar through the clamp; then the three small products
+//   dh = dmean Wm + da Wl,  dWm += dmean^T h,  dWl += da^T h
+// from LDS images with wave-uniform broadcast reads.  Every per-workgroup partial is a plain
+// store (fixed-order sums, no atomics); k_grad_small reduces the partials.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
+__global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
                                                     const float* __restrict__ covar,
                                                     float* __restrict__ lat, const float* __restrict__ rowx,
                                                     const float* __restrict__ rowB,
@@ -1458,64 +1482,64 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                                                     float* __restrict__ dhT_f, __bf16* __restrict__ dhT_b,
                                                     float* __restrict__ small) {
     const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP;
-    extern __shared__ __attribute__((aligned(16))) float lsm[];
     const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
-    const int KS1 = K + 1;
-    float* sWm = lsm;
-    float* sWl = sWm + K * KS1;
-    float* acc_s = sWl + K * KS1;
-    for (int i = threadIdx.x; i < K * K; i += 256) {
-        sWm[(i / K) * KS1 + i % K] = P.Wm[i];
-        sWl[(i / K) * KS1 + i % K] = P.Wl[i];
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sWm = lsm;                 // [K][65]
+    float* sWl = sWm + 64 * 65;       // [K][65]
+    float* sDM = sWl + 64 * 65;       // [cell][68] dmean
+    float* sDA = sDM + 64 * 68;       // [cell][68] dlnvar-pre-clamp (a)
+    float* sH = sDA + 64 * 68;        // [cell][68] h
+    float* wpart = sH + 64 * 68;      // [16][NSM] per-wave small partials
+    const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
+    for (int i = threadIdx.x; i < K * K; i += 1024) {
+        sWm[(i / K) * 65 + i % K] = P.Wm[i];
+        sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
-    for (int i = threadIdx.x; i < SMALL; i += 256) acc_s[i] = 0.f;
-    __syncthreads();
-    float* a_dWm = acc_s;
-    float* a_dWl = a_dWm + K * K;
-    float* a_dbm = a_dWl + K * K;
-    float* a_dbl = a_dbm + K;
-    float* a_dWce = a_dbl + K;
-    float* a_dhs = a_dWce + K * C;
-    float* a_dWnm = a_dhs + K;
-    float* a_dbnm = a_dWnm + R * H;
-    float* a_dWnl = a_dbnm + R;
-    float* a_dbnl = a_dWnl + R * H;
-    float* a_dbne = a_dbnl + R;
-    float* a_dbdp = a_dbne + H;
-
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int cpw = (d.Bpad + gridDim.x * 4 - 1) / (gridDim.x * 4);
-    float rWm[64], rWl[64];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        rWm[j] = 0.f;
-        rWl[j] = 0.f;
-    }
-    float rbm = 0.f, rbl = 0.f, rdhs = 0.f, rWce[CMAX];
+    const int bw = blockIdx.x * 64 + 4 * w;  // 4 cells per wave
+    float* wp = wpart + w * NSM;
+    float* p_dbm = wp;                 // [64]
+    float* p_dbl = p_dbm + 64;         // [64]
+    float* p_dhs = p_dbl + 64;         // [64]
+    float* p_dWce = p_dhs + 64;        // [64][CMAX]
+    float* p_dWnm = p_dWce + 64 * CMAX;  // [R][H]
+    float* p_dWnl = p_dWnm + RMAX * HMAX;
+    float* p_dbnm = p_dWnl + RMAX * HMAX;
+    float* p_dbnl = p_dbnm + RMAX;
+    float* p_dbne = p_dbnl + RMAX;
+    float* p_dbdp = p_dbne + HMAX;
+    for (int i = lane; i < NSM; i += 64) wp[i] = 0.f;
+    const float bn = d.beta * d.inv_n;
+    float rbm = 0.f, rbl = 0.f, rWce[CMAX];
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) rWce[c] = 0.f;
-    const float bn = d.beta * d.inv_n;
-    for (int ci = 0; ci < cpw; ++ci) {
-        const int b = (blockIdx.x * 4 + w) * cpw + ci;
-        if (b >= d.Bpad) break;
+    float rdnm[HMAX], rdnl[HMAX], rbnm = 0.f, rbnl = 0.f, rbne = 0.f, rbdp = 0.f;
+#pragma unroll
+    for (int h = 0; h < HMAX; ++h) {
+        rdnm[h] = 0.f;
+        rdnl[h] = 0.f;
+    }
+    // ---- per cell: dmean, da (lane = k) ----
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
         float* L = lat + (int64_t)b * d.lat_stride;
-        const bool valid = L[d.LAT_VALID] > 0.f;
+        const bool valid = (b < d.Bpad) && L[d.LAT_VALID] > 0.f;
         float E = 0.f, Ps = 0.f;
-        for (int s = 0; s < d.nsD; ++s) {
-            E += rowB[((int64_t)s * d.Bpad + b) * (2 + R)];
-            Ps += rowB[((int64_t)s * d.Bpad + b) * (2 + R) + 1];
+        for (int s2 = 0; s2 < d.nsD; ++s2) {
+            E += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
+            Ps += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R) + 1];
         }
         const float wb = L[d.LAT_W];
-        float dz = 0.f, dmean = 0.f, da = 0.f, h = 0.f;
+        float dmean = 0.f, da = 0.f, h = 0.f;
         if (k < K) {
             float A2 = 0.f, Pb = 0.f;
-            for (int s = 0; s < d.nsD; ++s) {
-                const float* dp = dzp + (((int64_t)s * d.Bpad + b) * 2) * KP;
+            for (int s2 = 0; s2 < d.nsD; ++s2) {
+                const float* dp = dzp + (((int64_t)s2 * d.Bpad + b) * 2) * KP;
                 A2 += dp[k];
                 Pb += dp[KP + k];
             }
-            dz = wb * (A2 - E * Pb);
+            const float dz = wb * (A2 - E * Pb);
             const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
             h = L[d.LAT_H + k];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
@@ -1528,85 +1552,154 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                 da = 0.f;
             }
         }
-        // dh_j = sum_k Wm[k][j] dmean_k + Wl[k][j] da_k   (lane = j)
-        float dhj = 0.f;
-        for (int kk = 0; kk < K; ++kk) {
-            const float dm = __shfl(dmean, kk, 64), dl = __shfl(da, kk, 64);
-            if (k < K) dhj += sWm[kk * KS1 + k] * dm + sWl[kk * KS1 + k] * dl;
-        }
-        if (k < KP) {
-            const float v = (k < K) ? dhj : 0.f;
-            dh[(int64_t)b * KP + k] = v;
-            dhT_f[(int64_t)k * d.Bpad + b] = v;
-            dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)v;
-        }
-        // weight-gradient accumulation (lane k owns row k)
-#pragma unroll
-        for (int j = 0; j < 64; ++j) {
-            const float hj = __shfl(h, j, 64);
-            rWm[j] += dmean * hj;
-            rWl[j] += da * hj;
-        }
+        sDM[(4 * w + c) * 68 + k] = dmean;
+        sDA[(4 * w + c) * 68 + k] = da;
+        sH[(4 * w + c) * 68 + k] = h;
         rbm += dmean;
         rbl += da;
-        rdhs += (k < K) ? dhj : 0.f;
         const int64_t cell = (b < d.B) ? cells[b] : -1;
 #pragma unroll
-        for (int c = 0; c < CMAX; ++c)
-            if (c < C && cell >= 0) rWce[c] += dmean * covar[cell * C + c];
-        // ---- overdispersion path ----
+        for (int q = 0; q < CMAX; ++q)
+            if (q < C && cell >= 0) rWce[q] += dmean * covar[cell * C + q];
+        // ---- overdispersion path (lanes < R) and depth (lane 0) ----
         const float* rx = rowx + (int64_t)b * d.rowx_stride;
         float dnm = 0.f, dan = 0.f;
         if (k < R && valid) {
             float dzn = 0.f;
-            for (int s = 0; s < d.nsD; ++s) dzn += rowB[((int64_t)s * d.Bpad + b) * (2 + R) + 2 + k];
+            for (int s2 = 0; s2 < d.nsD; ++s2) dzn += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R) + 2 + k];
             dzn *= d.inv_n;
             const float nm = L[d.LAT_NMEAN + k], an = L[d.LAT_AN + k], en = L[d.LAT_EPSN + k];
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             dnm = dzn + bn * nm;
             const float dnl = dzn * en * expf(nlv / 2.f) * 0.5f + bn * 0.5f * (expf(nlv) - 1.f);
             dan = (an >= -4.f && an <= 4.f) ? dnl : 0.f;
-            for (int hh = 0; hh < H; ++hh) {
-                atomicAdd(&a_dWnm[k * H + hh], dnm * rx[2 + hh]);
-                atomicAdd(&a_dWnl[k * H + hh], dan * rx[2 + hh]);
-            }
-            atomicAdd(&a_dbnm[k], dnm);
-            atomicAdd(&a_dbnl[k], dan);
+#pragma unroll
+            for (int hh = 0; hh < HMAX; ++hh)
+                if (hh < H) {
+                    rdnm[hh] += dnm * rx[2 + hh];
+                    rdnl[hh] += dan * rx[2 + hh];
+                }
+            rbnm += dnm;
+            rbnl += dan;
         }
         float dhn = 0.f;
         for (int q = 0; q < R; ++q) {
             const float a1 = __shfl(dnm, q, 64), a2 = __shfl(dan, q, 64);
             if (k < H) dhn += P.Wnm[q * H + k] * a1 + P.Wnl[q * H + k] * a2;
         }
-        if (k < H) {
+        if (k < H && b < d.Bpad) {
             L[d.LAT_DHNU + k] = valid ? dhn : 0.f;
-            if (valid) atomicAdd(&a_dbne[k], dhn);
+            if (valid) rbne += dhn;
         }
-        if (k == 0) {
+        if (k == 0 && b < d.Bpad) {
             const float dd = (E + Ps) * d.inv_n;   // dL/dd_b = sum_g dmu' p
             const float pre = rx[0];
             const float dpre = valid ? dd * dsoftplus(pre) : 0.f;
             L[d.LAT_DPRE] = dpre;
-            if (valid) atomicAdd(a_dbdp, dpre);
+            rbdp += dpre;
         }
-    }
-    if (k < K) {
-#pragma unroll
-        for (int j = 0; j < 64; ++j) {
-            if (j < K) {
-                atomicAdd(&a_dWm[k * K + j], rWm[j]);
-                atomicAdd(&a_dWl[k * K + j], rWl[j]);
-            }
-        }
-        atomicAdd(&a_dbm[k], rbm);
-        atomicAdd(&a_dbl[k], rbl);
-        atomicAdd(&a_dhs[k], rdhs);
-#pragma unroll
-        for (int c = 0; c < CMAX; ++c)
-            if (c < C) atomicAdd(&a_dWce[k * C + c], rWce[c]);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < SMALL; i += 256) small[(int64_t)blockIdx.x * SMALL + i] = acc_s[i];
+    // ---- dh for the wave's 4 cells (lane = j): 4 latents per step via 16-byte broadcasts ----
+    {
+        const int jj = (k < K) ? k : 0;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k4 = 0; k4 < K; k4 += 4) {
+            float wm[4], wl[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                wm[u] = (k4 + u < K) ? sWm[(k4 + u) * 65 + jj] : 0.f;
+                wl[u] = (k4 + u < K) ? sWl[(k4 + u) * 65 + jj] : 0.f;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 dm = *reinterpret_cast<const float4*>(&sDM[(4 * w + c) * 68 + k4]);
+                const float4 dl = *reinterpret_cast<const float4*>(&sDA[(4 * w + c) * 68 + k4]);
+                acc[c] = fmaf(dm.x, wm[0], fmaf(dm.y, wm[1], fmaf(dm.z, wm[2], fmaf(dm.w, wm[3], acc[c]))));
+                acc[c] = fmaf(dl.x, wl[0], fmaf(dl.y, wl[1], fmaf(dl.z, wl[2], fmaf(dl.w, wl[3], acc[c]))));
+            }
+        }
+        float rdhs = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            if (k < KP) {
+                const float v = (k < K) ? acc[c] : 0.f;
+                dh[(int64_t)b * KP + k] = v;
+                dhT_f[(int64_t)k * d.Bpad + b] = v;
+                dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)v;
+                rdhs += v;
+            }
+        }
+        p_dhs[k] = rdhs;
+    }
+    p_dbm[k] = rbm;
+    p_dbl[k] = rbl;
+#pragma unroll
+    for (int q = 0; q < CMAX; ++q) p_dWce[k * CMAX + q] = rWce[q];
+    if (k < R) {
+        for (int hh = 0; hh < H; ++hh) {
+            p_dWnm[k * HMAX + hh] = rdnm[hh < HMAX ? hh : 0];
+            p_dWnl[k * HMAX + hh] = rdnl[hh < HMAX ? hh : 0];
+        }
+        p_dbnm[k] = rbnm;
+        p_dbnl[k] = rbnl;
+    }
+    if (k < H) p_dbne[k] = rbne;
+    if (k == 0) p_dbdp[0] = rbdp;
+    // ---- dWm, dWl = [dmean | da]^T h over the workgroup's 64 cells (lane = k, wave w: j = 4w..4w+3) ----
+    float* out = small + (int64_t)blockIdx.x * SMALL;
+    {
+        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gl[4] = {0.f, 0.f, 0.f, 0.f};
+        const int kk = (k < K) ? k : 0;
+        for (int b = 0; b < 64; ++b) {
+            const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
+            const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 4 * w]);
+            gm[0] = fmaf(dm, h4.x, gm[0]); gm[1] = fmaf(dm, h4.y, gm[1]);
+            gm[2] = fmaf(dm, h4.z, gm[2]); gm[3] = fmaf(dm, h4.w, gm[3]);
+            gl[0] = fmaf(dl, h4.x, gl[0]); gl[1] = fmaf(dl, h4.y, gl[1]);
+            gl[2] = fmaf(dl, h4.z, gl[2]); gl[3] = fmaf(dl, h4.w, gl[3]);
+        }
+        if (k < K) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j2 = 4 * w + q;
+                if (j2 < K) {
+                    out[k * K + j2] = gm[q];
+                    out[K * K + k * K + j2] = gl[q];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- the small vectors: fixed-order sum of the four waves' partials ----
+    const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + K,
+              o_bnm = o_nm + R * H, o_nl = o_bnm + R, o_bnl = o_nl + R * H, o_bne = o_bnl + R, o_bdp = o_bne + H;
+    auto wsum = [&](int off) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += wpart[q * NSM + off];
+        return t;
+    };
+    for (int i = threadIdx.x; i < K; i += 1024) {
+        out[o_bm + i] = wsum(i);
+        out[o_bl + i] = wsum(64 + i);
+        out[o_dhs + i] = wsum(128 + i);
+        for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
+    }
+    const int b_nm = 192 + 64 * CMAX, b_nl = b_nm + RMAX * HMAX, b_bnm = b_nl + RMAX * HMAX, b_bnl = b_bnm + RMAX,
+              b_bne = b_bnl + RMAX, b_bdp = b_bne + HMAX;
+    for (int i = threadIdx.x; i < R * H; i += 1024) {
+        const int r2 = i / H, h2 = i % H;
+        out[o_nm + i] = wsum(b_nm + r2 * HMAX + h2);
+        out[o_nl + i] = wsum(b_nl + r2 * HMAX + h2);
+    }
+    for (int i = threadIdx.x; i < R; i += 1024) {
+        out[o_bnm + i] = wsum(b_bnm + i);
+        out[o_bnl + i] = wsum(b_bnl + i);
+    }
+    for (int i = threadIdx.x; i < H; i += 1024) out[o_bne + i] = wsum(b_bne + i);
+    if (threadIdx.x == 0) out[o_bdp] = wsum(b_bdp);
 }
 
 // =======================================================================================
@@ -2091,7 +2184,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
-        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar,
                            e->d_hpart, e->d_mvec, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id,
                            row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
     }
@@ -2158,9 +2251,9 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");
-        const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
-        const size_t lds = (size_t)(2 * d.K * (d.K + 1) + SMALL) * 4;
-        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
+        const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
+        const size_t lds = (size_t)(2 * 64 * 65 + 3 * 64 * 68 + 16 * NSM) * 4;
+        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(1024), lds, st, P, d, e->d_cells, e->d_covar,
                            e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     {
@@ -2224,7 +2317,7 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_cells,
                            e->d_rowptr, e->d_col, e->d_val, e->d_rtp, bf ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d,
                            e->d_hpart);
-    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
                        e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
     return hipGetLastError();
