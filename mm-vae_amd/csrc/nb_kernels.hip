@@ -1705,13 +1705,26 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
 // =======================================================================================
 // k_enc_bwd — gradient of x_mean / ln_x_sd through the frozen encoder (autograd of
 // nb.hh:408-411) and of depth / nu_enc weights (raw x, nb.hh:448,498):
-//   Gl_g = sum_k W_enc[k,g] M[k,g],  M = dh^T log1p(x)   (MFMA on densified 64x64 tiles)
-//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}       (LDS atomics during the scatter)
-// Workgroup = 64 cells x one gene split.  The x tile [64 genes][64 cells] is shared by the
-// four waves (each wave owns one 16-latent block of M and scatters its own 16 cells into the
-// tile's cell columns); the W_enc tile for the epilogue is staged by LDS-DMA.  Both are
-// double-buffered with one barrier per tile.
+//   Gl_g  = sum_k W_enc[k,g] M[k,g],  M = dh^T log1p(x)   (MFMA on densified 64x64 tiles)
+//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}        (gene-owner lanes over an f32 tile)
+// Workgroup = 64 cells x one gene split.  The log1p(x) tile [64 genes][64 cells] and the raw
+// count tile are shared by the four waves (each wave scatters its own 16 cells); wave w owns
+// M's latent block w and the raw sums of gene block w.  Everything is written straight to the
+// row block's slab in a fixed order — no atomics.  Single-buffered tiles, two barriers per tile.
 // =======================================================================================
+struct EncBwdLds {
+    int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, bytes;
+    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc) {
+        o_lt = KP * 64 * esz;
+        o_raw = o_lt + 64 * LS * esz;
+        o_part = o_raw + 64 * 68 * 4;
+        o_scal = o_part + 4 * 64 * 4;
+        o_wave = o_scal + nsc * 64 * 4;
+        wave_bytes = ((16 * S * 4 + 15) / 16) * 16 + 16 * 8 + 64;
+        bytes = o_wave + 4 * wave_bytes;
+    }
+};
+
 template <class T, int KP, bool H1>
 __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cells,
                                                  const int64_t* __restrict__ rowptr,
@@ -1722,33 +1735,28 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
                                                  Dims d, float* __restrict__ slabE) {
     using M = MM<T>;
     using Fr = typename M::frag;
-    constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // x tile row (gene) stride in elements
-    constexpr int RB = 64 * (int)sizeof(T);
-    constexpr int NCH = RB / 16;
-    constexpr int STB = KP * RB;
-    constexpr int XT = 64 * LS * (int)sizeof(T);   // one shared x tile
+    constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // log1p tile row (gene) stride, elements
+    constexpr int RB = 64 * (int)sizeof(T);        // staged W_enc row (one latent, 64 genes)
+    constexpr int HN = H1 ? 1 : HMAX;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const int GS = d.tpsE * 64;
     const int H = H1 ? 1 : d.H;
     const int nq = 2 + H;
-    constexpr int HN = H1 ? 1 : HMAX;
-    const int pre = ((nq * GS * 4 + 15) / 16) * 16;
-    // carve: colacc | W stage x2 | x tiles x2 (shared, in the per-wave x region) | per-wave rows
-    const EncLds L(KP, (int)sizeof(T), S, XT / 2, pre);
-    float* colacc = reinterpret_cast<float*>(smem);
-    char* wst = smem + pre;
-    T* lt = reinterpret_cast<T*>(smem + L.o_x);  // [2][64 genes][LS]
-    int32_t* rtl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
-    int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
-    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16;
-    float* rsc = reinterpret_cast<float*>(smem + L.o_rsc) + w * 16 * (1 + HMAX);
+    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN);
+    char* wst = smem;
+    T* lt = reinterpret_cast<T*>(smem + L.o_lt);          // [64 genes][LS]  log1p(x)
+    float* raw = reinterpret_cast<float*>(smem + L.o_raw);  // [64 genes][68] x
+    float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][64]
+    float* scal = reinterpret_cast<float*>(smem + L.o_scal);  // [1+H][64 cells]: dpre, dhnu_h
+    char* wpb = smem + L.o_wave + w * L.wave_bytes;
+    int32_t* rtl = reinterpret_cast<int32_t*>(wpb);
+    int64_t* rbl = reinterpret_cast<int64_t*>(wpb + ((16 * S * 4 + 15) / 16) * 16);
+    int32_t* rinc = reinterpret_cast<int32_t*>(rbl + 16);
 
-    for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
     for (int i = lane; i < 16 * S; i += 64) {
         const int rr = i / S, tt = i % S;
         rtl[i] = (t0 + tt <= d.NT) ? rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
@@ -1758,17 +1766,23 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         const int64_t cell = (b < d.B) ? cells[b] : -1;
         rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
         const float* Lr = lat + (int64_t)b * d.lat_stride;
-        rsc[lane * (1 + HMAX)] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
-        for (int h = 0; h < H; ++h) rsc[lane * (1 + HMAX) + 1 + h] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
+        scal[16 * w + lane] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
+        for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
     }
-    // this wave's 16 cell columns of a tile: 64 genes x 32 bytes (bf16) / 64 bytes (f32)
-    auto zero_cols = [&](T* tile) {
-        constexpr int CB = 16 * (int)sizeof(T) / 16;  // uint4 per gene row
+    // this wave's 16 cell columns of both tiles
+    auto zero_cols = [&]() {
+        constexpr int CB = 16 * (int)sizeof(T) / 16;
 #pragma unroll
-        for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(tile + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+        for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(lt + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
     };
-    zero_cols(lt);
-    zero_cols(lt + 64 * LS);
+    auto scatter = [&](const TileEntries& te, int tl, int t) {
+        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val, [&](int r, int gl, float x) {
+            lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
+            raw[gl * 68 + 16 * w + r] = x;
+        });
+    };
     // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
     const int lb = w;
     constexpr int KSB = 64 / M::KSTEP;
@@ -1778,44 +1792,49 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         afr[s] = (lb < KP / 16) ? M::load(&dhT[(int64_t)(16 * lb + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
                                                (lane >> 4) * M::EPL])
                                 : M::zero();
-    wave_sync();
-
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
-    (void)NCH;
-    auto scatter = [&](const TileEntries& te, T* tile, int tl, int t) {
-        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val, [&](int r, int gl, float x) {
-            tile[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
-            const float* rs = rsc + r * (1 + HMAX);
-            atomicAdd(&colacc[1 * GS + tl * 64 + gl], rs[0] * x);
-            for (int h = 0; h < H; ++h) atomicAdd(&colacc[(2 + h) * GS + tl * 64 + gl], rs[1 + h] * x);
-        });
-    };
-    (void)HN;
 
     TileEntries pend;
     if (t0 < t1) {
         wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
         wreg.store(wst);
+        zero_cols();
         tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, col, val);
-        __syncthreads();  // colacc zeroed before the scatter's atomics
-        scatter(pend, lt, 0, t0);
+        scatter(pend, 0, t0);
         if (t0 + 1 < t1) tile_fetch(pend, rtl, S, 1, t0 + 1, lane, rinc, rbl, col, val);
     }
-    vm_wait_all();
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
-        const int tl = t - t0, buf = tl & 1;
+        const int tl = t - t0;
         if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
-        const T* xb = lt + buf * 64 * LS;
-        const char* wb = wst + buf * STB;
+        // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
+        {
+            const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
+            const float4* xr = reinterpret_cast<const float4*>(raw + gl * 68 + 16 * q4);
+            float4 xv[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xv[c] = xr[c];
+            for (int h = 0; h < 1 + H; ++h) {
+                const float4* sc = reinterpret_cast<const float4*>(scal + h * 64 + 16 * q4);
+                float v = 0.f;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 a = sc[c];
+                    v = fmaf(xv[c].x, a.x, fmaf(xv[c].y, a.y, fmaf(xv[c].z, a.z, fmaf(xv[c].w, a.w, v))));
+                }
+                v = sum_rowgroups(v);
+                if (lane < 16) slabE[((int64_t)rb * nq + 1 + h) * d.DP + 64 * t + gl] = v;
+            }
+        }
+        // ---- M block w on MFMA, then Gl partial = sum over the block's latents of W M ----
         if (lb < KP / 16) {
 #pragma unroll
             for (int gb = 0; gb < 4; ++gb) {
                 f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KSB; ++s) {
-                    const Fr bx = *reinterpret_cast<const Fr*>(&xb[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    const Fr bx = *reinterpret_cast<const Fr*>(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
                     acc = M::mma(afr[s], bx, acc);
                 }
                 const int gl = 16 * gb + (lane & 15);
@@ -1823,29 +1842,27 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * lb + 4 * (lane >> 4) + r;
-                    v = fmaf(static_cast<float>(*reinterpret_cast<const T*>(wb + swz_off<RB>(k, gl * (int)sizeof(T)))), acc[r], v);
+                    v = fmaf(static_cast<float>(*reinterpret_cast<const T*>(wst + swz_off<RB>(k, gl * (int)sizeof(T)))), acc[r], v);
                 }
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
-                if (lane < 16) atomicAdd(&colacc[tl * 64 + gl], v);
+                v = sum_rowgroups(v);
+                if (lane < 16) part[w * 64 + gl] = v;
             }
+        } else if (lane < 16) {
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) part[w * 64 + 16 * gb + lane] = 0.f;
+        }
+        lds_barrier();
+        if (threadIdx.x < 64) {
+            const int g = threadIdx.x;
+            slabE[((int64_t)rb * nq) * d.DP + 64 * t + g] = part[g] + part[64 + g] + part[128 + g] + part[192 + g];
         }
         if (t + 1 < t1) {
-            T* xn = lt + (buf ^ 1) * 64 * LS;
-            zero_cols(xn);
-            scatter(pend, xn, tl + 1, t + 1);
-            wreg.store(wst + (buf ^ 1) * STB);
+            zero_cols();
+            scatter(pend, tl + 1, t + 1);
+            wreg.store(wst);
         }
-        // the entry prefetch below stays in flight across the barrier
         if (t + 2 < t1) tile_fetch(pend, rtl, S, tl + 2, t + 2, lane, rinc, rbl, col, val);
         lds_barrier();
-    }
-    __syncthreads();
-    const int gbase = t0 * 64;
-    const int glen = min(d.DP, t1 * 64) - gbase;
-    for (int i = threadIdx.x; i < nq * GS; i += 256) {
-        const int q = i / GS, gi = i % GS;
-        if (gi < glen) slabE[((int64_t)rb * nq + q) * d.DP + gbase + gi] = colacc[i];
     }
 }
 
@@ -2147,8 +2164,7 @@ static size_t enc_fwd_lds(const Dims& d) {
 template <class T, int KP>
 static size_t enc_bwd_lds(const Dims& d) {
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;
-    const int pre = (((2 + d.H) * d.tpsE * 64 * 4 + 15) / 16) * 16;
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 64 * LS * (int)sizeof(T) / 2, pre).bytes;
+    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX)).bytes;
 }
 
 template <class T, int KP>
