@@ -170,6 +170,14 @@ MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
 // ---------------------------------------------------------------------------------------
 // Wave64 reductions
 // ---------------------------------------------------------------------------------------
+// sum over the four 16-lane row groups (lanes l, l^16, l^32, l^48), result in every lane
+MMVAE_DEV float sum_rowgroups(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 MMVAE_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -81,25 +81,31 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, const float* __restrict__ WeP_f,
                                               float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b) {
+    // grid (genes / 256, KP / 8): every y-slice packs 8 latent rows of the scaled encoder weight
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= d.DP) return;
-    float inv = 0.f, bias = -INFINITY, cnu = 0.f, xmi = 0.f;
-    if (g < d.D) {
-        inv = 1.f / (softplus_acc(P.lsd[g]) + 1e-4f);
-        bias = P.bd[g] + P.bcd[g] + P.mub[g];
-        cnu = P.bnd[g] - P.nub[g];
-        xmi = P.xm[g] * inv;
+    float inv = 0.f;
+    if (g < d.D) inv = 1.f / (softplus_acc(P.lsd[g]) + 1e-4f);
+    if (blockIdx.y == 0) {
+        float bias = -INFINITY, cnu = 0.f, xmi = 0.f;
+        if (g < d.D) {
+            bias = P.bd[g] + P.bcd[g] + P.mub[g];
+            cnu = P.bnd[g] - P.nub[g];
+            xmi = P.xm[g] * inv;
+        }
+        gene[g] = inv;
+        gene[d.DP + g] = bias;
+        gene[2 * d.DP + g] = cnu;
+        gene[3 * d.DP + g] = xmi;
+        // packed decoder record (bias, cn, Wcd[g][0], Wnd[g][0])
+        const bool v = g < d.D;
+        reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
+            float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
     }
-    gene[g] = inv;
-    gene[d.DP + g] = bias;
-    gene[2 * d.DP + g] = cnu;
-    gene[3 * d.DP + g] = xmi;
-    // packed decoder record (bias, cn, Wcd[g][0], Wnd[g][0]) read once per 16-gene block
-    const bool v = g < d.D;
-    reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
-        float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
     // encoder weight pre-scaled by 1/(softplus(ln_x_sd)+1e-4): x~ W^T = log1p(x) (W inv)^T - mvec
-    for (int k = 0; k < d.KP; ++k) {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const int k = blockIdx.y * 8 + kk;
         const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
         if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
         else WeS_f[(int64_t)k * d.DP + g] = ws;
@@ -107,18 +113,24 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 }
 
 // mvec[k] = sum_g x_mean_g / sd_g * W_enc[k, g]  (the dense part of the encoder input)
-__global__ __launch_bounds__(256) void k_mvec(NBPtrs P, Dims d, const float* __restrict__ gene, float* mvec) {
-    __shared__ float sbuf[8];
+__global__ __launch_bounds__(1024) void k_mvec(NBPtrs P, Dims d, const float* __restrict__ gene, float* mvec) {
+    __shared__ float sbuf[16];
     const int k = blockIdx.x;
     const float* xmi = gene + 3 * d.DP;
     float acc = 0.f;
     if (k < d.K) {
         const float* wr = P.We + (int64_t)k * d.D;
 #pragma unroll 4
-        for (int g = threadIdx.x; g < d.D; g += 256) acc += xmi[g] * wr[g];
+        for (int g = threadIdx.x; g < d.D; g += 1024) acc += xmi[g] * wr[g];
     }
-    const float t = block_sum<4>(acc, sbuf);
-    if (threadIdx.x == 0) mvec[k] = t;
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) sbuf[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int q = 0; q < 16; ++q) t += sbuf[q];
+        mvec[k] = t;
+    }
 }
 
 // =======================================================================================
@@ -636,8 +648,8 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
     const int S = tps + 1;  // rt row stride in LDS
     // ---- LDS carve (16-byte aligned pieces) ----
     float* sl = reinterpret_cast<float*>(smem);  // [4]
-    float* colacc = sl + 4;                      // [nq][GS]       (B, C)
-    char* wbase = reinterpret_cast<char*>(colacc + ((PASS == 0) ? 0 : nq * GS));
+    float* colacc = sl + 4;                      // B: [nq][GS];  C: per-wave partials [2][4][nq][64]
+    char* wbase = reinterpret_cast<char*>(colacc + ((PASS == 0) ? 0 : (PASS == 1) ? nq * GS : 2 * 4 * nq * 64));
     const int wbytes = (PASS == 1) ? (16 * QS * (int)sizeof(T) + 16 * PS * 4 + ((16 * S * 4 + 15) / 16) * 16 +
                                       16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64)
                                    : 0;
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
     float* rcorr = rsc + 16 * NRS;
     int32_t* rinc = reinterpret_cast<int32_t*>(rcorr + ((16 * (1 + RM) + 3) / 4) * 4);
 
-    if (PASS != 0) {
+    if (PASS == 1) {
         for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
         __syncthreads();
     }
@@ -858,13 +870,13 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
 #pragma unroll
                     for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[r][c], cs[1 + c]);
                 }
+                // per-wave partial of this tile (fixed-order combine after the tile barrier)
+                float* pw = colacc + ((((t - t0) & 1) * 4 + w) * nq) * 64 + gl;
 #pragma unroll
                 for (int c = 0; c < 1 + CM; ++c) {
                     if (c <= C) {
-                        float v = cs[c];
-                        v += __shfl_xor(v, 16, 64);
-                        v += __shfl_xor(v, 32, 64);
-                        if (lane < 16) atomicAdd(&colacc[c * GS + tl * 64 + gl], v);
+                        const float v = sum_rowgroups(cs[c]);
+                        if (lane < 16) pw[c * 64] = v;
                     }
                 }
             } else {
@@ -1021,6 +1033,14 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             wave_sync();
         }
         if (STG) __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
+        if (PASS == 2) {
+            const float* pb = colacc + (((t - t0) & 1) * 4 * nq) * 64;
+            for (int i = threadIdx.x; i < nq * 64; i += 256) {
+                const int q = i >> 6, g = i & 63;
+                Q.slabC[((int64_t)rb * nq + q) * d.DP + 64 * t + g] =
+                    pb[(0 * nq + q) * 64 + g] + pb[(1 * nq + q) * 64 + g] + pb[(2 * nq + q) * 64 + g] + pb[(3 * nq + q) * 64 + g];
+            }
+        }
     }
     // ---- per-row outputs ----
     if (wave_live) {
@@ -1079,9 +1099,9 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
         __syncthreads();
         if (threadIdx.x == 0) Q.lossp[blockIdx.x] = sl[0] + sl[1] + sl[2] + sl[3];
     }
-    if (PASS != 0) {
+    if (PASS == 1) {
         __syncthreads();
-        float* slab = (PASS == 1) ? Q.slabB : Q.slabC;
+        float* slab = Q.slabB;
         const int gbase = t0 * 64;
         const int glen = min(d.DP, t1 * 64) - gbase;
         for (int i = threadIdx.x; i < nq * GS; i += 256) {
@@ -1127,14 +1147,6 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
         b = __uint_as_float(v & 0xffff0000u);
     }
 };
-
-// sum over the four 16-lane row groups (lanes l, l^16, l^32, l^48), result in every lane
-MMVAE_DEV float sum_rowgroups(float v) {
-    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
 
 struct DecNBLds {
     int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_rtl, o_rbl, o_rsc, o_rinc, bytes;
@@ -2144,7 +2156,7 @@ __global__ __launch_bounds__(256) void k_rowfin(DecPtrs Q, Dims d) {
 static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
     const int nq = (pass == 1) ? (1 + d.C) + 1 + d.R : (1 + d.C);
     const int tps = (pass == 1) ? d.tpsD : d.tpsA;
-    size_t s = 16 + ((pass == 0) ? 0 : (size_t)nq * tps * 64 * 4);
+    size_t s = 16 + ((pass == 0) ? 0 : (pass == 1) ? (size_t)nq * tps * 64 * 4 : (size_t)2 * 4 * nq * 64 * 4);
     if (pass == 1) {
         const int QS = 64 + (bf16 ? 8 : 4), S = d.tpsD + 1, NRS = 3 + RM + CM;
         const size_t per = 16 * QS * (bf16 ? 2 : 4) + 16 * 68 * 4 + ((16 * S * 4 + 15) / 16) * 16 +
@@ -2176,12 +2188,12 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     float* gene = e->d_gene;
     {
         ScopedTimer tm(e, "k_prep");
-        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, gene, e->d_WeP_f, e->d_WeS_f,
+        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, gene, e->d_WeP_f, e->d_WeS_f,
                            bf ? e->d_WeS_b : nullptr);
     }
     {
         ScopedTimer tm(e, "k_mvec");
-        hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(256), 0, st, P, d, gene, e->d_mvec);
+        hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, gene, e->d_mvec);
     }
     {
         ScopedTimer tm(e, "k_rowscan");
@@ -2321,9 +2333,9 @@ template <class T, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
-    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
+    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
                        bf ? e->d_WeS_b : nullptr);
-    hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(256), 0, st, P, d, e->d_gene, e->d_mvec);
+    hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, e->d_gene, e->d_mvec);
     if (d.H == 1)
         hipLaunchKernelGGL(k_rowscan<true>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
                            e->d_val, P, d, e->d_rtp, e->d_rowx);

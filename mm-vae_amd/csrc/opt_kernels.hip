@@ -28,9 +28,14 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
                                               float lr_bc1, float inv_sqrt_bc2, float b1, float b2, float wd,
                                               float eps, float* __restrict__ out) {
     __shared__ float s_coef;
+    __shared__ double sb[4];
+    double tp = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += 256) tp += part[i];  // fixed order per block
+    tp = wave_sum_d(tp);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = tp;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int i = 0; i < nparts; ++i) t += part[i];
+        const double t = (sb[0] + sb[1]) + (sb[2] + sb[3]);
         const float total = (float)sqrt(t);            // stack(norms).norm(2), fp32 tensor
         float coef = max_norm / (total + 1e-6f);       // clip_grad.h:81
         coef = fminf(coef, 1.f);                        // clamp(max=1), clip_grad.h:82-83
