@@ -109,61 +109,68 @@ MMVAE_DEV float softplus_sig(float u, float& sig) {
     return fmaxf(u, 0.f) + log1p_pos(e);
 }
 
+// clamp(sp, 1e-4, 1e4) as one v_med3_f32 (nb.hh:459)
+MMVAE_DEV float clamp_nu(float sp) { return __builtin_amdgcn_fmed3f(sp, 1e-4f, 1e4f); }
+
 // accurate torch softplus (libm log1p/exp), for per-row / per-gene scalars
 MMVAE_DEV float softplus_acc(float u) { return (u > 20.f) ? u : log1pf(expf(u)); }
 
 MMVAE_DEV float dsoftplus(float u) { return (u > 20.f) ? 1.f : 1.f / (1.f + expf(-u)); }
 
-// log Gamma(v), v > 0: shift to v >= 8 (one log of the product), then Stirling's series
-// (truncation error < 1e-9 relative at v >= 8).  Compact: few registers, no tables.
-MMVAE_DEV float lgamma_pos(float v) {
-    float prod = 1.f;
-    while (v < 8.f) {
-        prod *= v;
-        v += 1.f;
-    }
-    const float r = frcp(v), r2 = r * r;
-    const float series = r * (0.083333333f - r2 * (0.0027777778f - r2 * (0.00079365079f - r2 * 0.00059523810f)));
-    return (v - 0.5f) * flog(v) - v + 0.91893853320467274f + series - flog(prod);
-}
-
-// digamma for v > 0: upward recurrence to v >= 6 then the asymptotic series
-MMVAE_DEV float digammaf_(float v) {
-    float r = 0.f;
-    while (v < 6.f) {
-        r -= frcp(v);
-        v += 1.f;
-    }
-    const float f = frcp(v * v);
-    const float t = f * (1.f / 12 - f * (1.f / 120 - f * (1.f / 252 - f * (1.f / 240 - f * (1.f / 132)))));
-    return r + flog(v) - 0.5f * frcp(v) - t;
-}
-
-// NB gamma terms for count x > 0 and overdispersion nup > 0:
+// ---------------------------------------------------------------------------------------
+// Gamma-function terms of the NB likelihood for a count x > 0 and overdispersion nup > 0:
 //   lgd = lgamma(nup) + lgamma(x + 1) - lgamma(nup + x)      (nb.hh:522-523)
 //   dgd = digamma(nup) - digamma(nup + x)                    (its d/d nup)
-// Integer counts up to 64 use the exact finite products/sums (4 factors per log);
-// other values use the compact lgamma / digamma above.
+// Counts 1..4 (the bulk of single-cell data) use the exact finite product / sum with one log
+// and one reciprocal.  Everything else shifts each argument below 8 up by 8 (branch free:
+// P = v(v+1)..(v+7) and S = P'/P = sum 1/(v+i) by the product rule) and evaluates Stirling's
+// series and the digamma asymptotic series at z >= 8 (truncation < 1e-9 relative), sharing
+// log z and 1/z between the two.
+// ---------------------------------------------------------------------------------------
+struct GammaAt {
+    float lg, dg;  // lgamma(v), digamma(v)
+};
+MMVAE_DEV GammaAt gamma_at(float v, bool need_dg) {
+    float P = v, Pd = 1.f;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+        const float a = v + (float)i;
+        Pd = fmaf(Pd, a, P);
+        P *= a;
+    }
+    const bool sh = v < 8.f;
+    const float z = sh ? v + 8.f : v;
+    const float lz = flog(z), r = frcp(z), r2 = r * r;
+    const float lP = sh ? flog(P) : 0.f;
+    GammaAt o;
+    o.lg = (z - 0.5f) * lz - z + 0.91893853320467274f +
+           r * (0.083333333f - r2 * (0.0027777778f - r2 * 0.00079365079f)) - lP;
+    o.dg = 0.f;
+    if (need_dg) {
+        const float S = sh ? Pd * frcp(P) : 0.f;
+        o.dg = lz - 0.5f * r - r2 * (0.083333333f - r2 * (0.0083333333f - r2 * 0.0039682540f)) - S;
+    }
+    return o;
+}
+
 MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
-    if (x <= 64.f && x == floorf(x)) {
-        const int n = (int)x;
-        float lsum = 0.f, rsum = 0.f, prod = 1.f, fprod = 1.f;
-        for (int i = 0; i < n; ++i) {
-            const float v = nup + (float)i;
-            rsum += frcp(v);
-            prod *= v;
-            fprod *= (float)(i + 1);
-            if ((i & 3) == 3) {
-                lsum += flog(prod) - flog(fprod);
-                prod = 1.f;
-                fprod = 1.f;
-            }
+    if (x <= 4.f && x == floorf(x)) {
+        float P = 1.f, Pd = 0.f, F = 1.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool on = (float)i < x;
+            const float a = on ? nup + (float)i : 1.f;
+            Pd = on ? fmaf(Pd, a, P) : Pd;
+            P *= a;
+            F *= on ? (float)(i + 1) : 1.f;
         }
-        lgd = -(lsum + flog(prod) - flog(fprod));
-        dgd = -rsum;
+        const float rP = frcp(P);
+        lgd = flog(F * rP);     // log(x!) - log(nup (nup+1) .. (nup+x-1))
+        dgd = -Pd * rP;         // -sum 1/(nup+i)
     } else {
-        lgd = lgamma_pos(nup) + lgamma_pos(x + 1.f) - lgamma_pos(nup + x);
-        dgd = digammaf_(nup) - digammaf_(nup + x);
+        const GammaAt a = gamma_at(nup, true), b = gamma_at(nup + x, true), c = gamma_at(x + 1.f, false);
+        lgd = a.lg + c.lg - b.lg;
+        dgd = a.dg - b.dg;
     }
 }
 

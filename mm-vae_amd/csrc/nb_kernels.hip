@@ -588,16 +588,13 @@ __global__ __launch_bounds__(1024) void k_latent_fwd(
 }
 
 // =======================================================================================
-// k_dec<T, KP, PASS> — decoder + NB likelihood (nb.hh:433-442, 453-460, 510-531).
-// Each wave owns 16 cells and sweeps the 64-gene tiles of its gene split; the logit tile
-// (16 cells x 16 genes per MFMA) is never stored.  Lane l holds, per 16-gene block, gene
-// (l & 15) of cells 4(l>>4)+r, r = 0..3 (the MFMA C layout).
-//   PASS 0 (A): online max / sum-exp per cell                       -> lsep[split][cell]
-//   PASS 1 (B): softmax + NB terms with x = 0 for every element (branch free), then a
-//               compacted pass over the tile's nonzeros adds the x-dependent terms
-//               (x log(s/mu), lgamma/digamma); dz partials on MFMA; column sums
-//   PASS 2 (C): column sums of w_b E_b p_bg (the S_b p term of the softmax backward)
-// The frozen decoder rows of the next tile are prefetched into registers one tile ahead.
+// Decoder (nb.hh:433-442, 453-460, 510-531).  Three passes over the [B, D] logit matrix,
+// which is never stored: the softmax backward needs the row sum E_b = sum_g P q, which is
+// known only after a full sweep of the row.
+//   k_dec<PASS 0> (A): online max / sum-exp per cell                      -> lsep[split][cell]
+//   k_dec_nb     (B): softmax + NB terms + dz GEMM + column sums          (see below)
+//   k_dec<PASS 2> (C): column sums of w_b E_b p_bg (the E_b P term of the softmax backward)
+// Lane l holds, per 16-gene block, gene (l & 15) of cells 4(l>>4)+r, r = 0..3 (MFMA C layout).
 // =======================================================================================
 struct DecPtrs {
     const float* lat;
@@ -623,129 +620,50 @@ struct DecPtrs {
     float* lossp;     // [grid]
 };
 
-template <class T, int KP, int PASS, int CM, int RM>
+// Passes A and C: each tile's decoder rows + gene records are staged ONCE per workgroup into
+// LDS by LDS-DMA (double-buffered, swizzled image), shared by the four waves.
+template <class T, int KP, int PASS, int CM>
 __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
     using M = MM<T>;
     using Fr = typename M::frag;
-    constexpr int KS = KP / M::KSTEP;   // k-steps of the logit GEMM
-    constexpr int GK = 64 / M::KSTEP;   // k-steps of the dz GEMM over a 64-gene tile
+    constexpr int KS = KP / M::KSTEP;
     constexpr bool BF = sizeof(T) == 2;
-    constexpr int QS = 64 + (BF ? 8 : 4);  // q1 tile row stride (elements)
-    constexpr int PS = 68;                 // f32 p tile row stride
-    constexpr int NRS = 3 + RM + CM;       // row scalars: d, w, valid, znu[R], c[C]
-    constexpr bool GEN = (CM > 1) || (RM > 1);  // general covariate / overdispersion widths
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nsp = (PASS == 1) ? d.nsD : d.nsA;
-    const int tps = (PASS == 1) ? d.tpsD : d.tpsA;
-    const int sp = blockIdx.x % nsp, rb = blockIdx.x / nsp;
-    const int row0 = rb * 64 + 16 * w;
-    const int t0 = sp * tps, t1 = min(d.NT, t0 + tps);
-    const int ntl = t1 - t0;
-    const int GS = tps * 64;
-    const int C = d.C, R = d.R;
-    const int nq = (PASS == 1) ? (1 + C) + 1 + R : (1 + C);
-    const int S = tps + 1;  // rt row stride in LDS
-    // ---- LDS carve (16-byte aligned pieces) ----
-    float* sl = reinterpret_cast<float*>(smem);  // [4]
-    float* colacc = sl + 4;                      // B: [nq][GS];  C: per-wave partials [2][4][nq][64]
-    char* wbase = reinterpret_cast<char*>(colacc + ((PASS == 0) ? 0 : (PASS == 1) ? nq * GS : 2 * 4 * nq * 64));
-    const int wbytes = (PASS == 1) ? (16 * QS * (int)sizeof(T) + 16 * PS * 4 + ((16 * S * 4 + 15) / 16) * 16 +
-                                      16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64)
-                                   : 0;
-    char* wp = wbase + w * wbytes;
-    T* q1 = reinterpret_cast<T*>(wp);
-    float* q2 = reinterpret_cast<float*>(q1 + 16 * QS);
-    int32_t* rtl = reinterpret_cast<int32_t*>(q2 + 16 * PS);
-    int64_t* rbl = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(rtl) + ((16 * S * 4 + 15) / 16) * 16);
-    float* rsc = reinterpret_cast<float*>(rbl + 16);
-    float* rcorr = rsc + 16 * NRS;
-    int32_t* rinc = reinterpret_cast<int32_t*>(rcorr + ((16 * (1 + RM) + 3) / 4) * 4);
-
-    if (PASS == 1) {
-        for (int i = threadIdx.x; i < nq * GS; i += 256) colacc[i] = 0.f;
-        __syncthreads();
-    }
-    const bool wave_live = row0 < d.Bpad;
-    const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
-    const T* WdP = reinterpret_cast<const T*>(Q.WdP);
-    const T* WdT = reinterpret_cast<const T*>(Q.WdT);
-    const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);  // (bias, cn, Wcd0, Wnd0)
-
-    float lossacc = 0.f;
-    float rv[4], lse2[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
-    float mrun[4], srun[4], Eacc[4], Pacc[4], dzn[4][RM], wE[4];
-    f32x4 dzA[KP / 16], dzP[KP / 16];
-    Fr zfr[KS];
-    constexpr float L2E = 1.4426950408889634f;
-    if (wave_live) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int b = row0 + 4 * (lane >> 4) + r;
-            const float* L = Q.lat + (int64_t)b * d.lat_stride;
-            rv[r] = L[d.LAT_VALID];
-            dv[r] = L[d.LAT_D];
-            wv[r] = L[d.LAT_W];
-            const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
-#pragma unroll
-            for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
-#pragma unroll
-            for (int q = 0; q < RM; ++q) {
-                znu[r][q] = (q < R) ? L[d.LAT_ZNU + q] : 0.f;
-                dzn[r][q] = 0.f;
-            }
-            mrun[r] = -1e30f;
-            srun[r] = 0.f;
-            Eacc[r] = 0.f;
-            Pacc[r] = 0.f;
-            lse2[r] = 0.f;
-            wE[r] = 0.f;
-            if (PASS != 0) lse2[r] = Q.rowfin[2 * b];        // k_rowfin<0>
-            if (PASS == 2) wE[r] = Q.rowfin[2 * b + 1];      // k_rowfin<1>
-        }
-#pragma unroll
-        for (int lb = 0; lb < KP / 16; ++lb) {
-            dzA[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            dzP[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        if (PASS == 1) {
-            // per-wave row data for the sparse pass: tile pointers, CSR bases, row scalars
-            for (int i = lane; i < 16 * S; i += 64) {
-                const int rr = i / S, tt = i % S;
-                rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
-            }
-            if (lane < 16) {
-                const int b = row0 + lane;
-                const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
-                rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
-                const float* L = Q.lat + (int64_t)b * d.lat_stride;
-                float* rs = rsc + lane * NRS;
-                rs[0] = L[d.LAT_D];
-                rs[1] = L[d.LAT_W];
-                rs[2] = L[d.LAT_VALID];
-                for (int q = 0; q < RM; ++q) rs[3 + q] = (q < R) ? L[d.LAT_ZNU + q] : 0.f;
-                for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
-                for (int q = 0; q < 1 + RM; ++q) rcorr[lane * (1 + RM) + q] = 0.f;
-            }
-            wave_sync();
-        }
-    }
-
-    // ---- tile loop.  Passes A and C stage each tile's decoder rows + per-gene records once
-    // per workgroup into LDS by LDS-DMA (double-buffered, swizzled image, swz_off), so the four
-    // waves share one L2->CU transfer; pass B (VALU-bound, loads hidden behind its epilogue)
-    // keeps a 2-block register ring half a tile ahead.
-    constexpr bool STG = PASS != 1;
     constexpr int RB = KP * (int)sizeof(T);  // bytes per staged gene row
     constexpr int NCH = RB / 16;
     constexpr int STB = 64 * RB + 1024;      // one stage buffer: W tile + grec tile
-    char* stg = wbase;
+    constexpr float L2E = 1.4426950408889634f;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = blockIdx.x % d.nsA, rb = blockIdx.x / d.nsA;
+    const int row0 = rb * 64 + 16 * w;
+    const int t0 = sp * d.tpsA, t1 = min(d.NT, t0 + d.tpsA);
+    const int C = (CM == 1) ? 1 : d.C;
+    const int nq = 1 + C;
+    char* stg = smem;
+    float* part = reinterpret_cast<float*>(smem + 2 * STB);  // C: [2][4][nq][64]
+    const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
+    const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
+    const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
+
+    Fr zfr[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    float lse2[4], wE[4], crow[4][CM], mrun[4], srun[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = row0 + 4 * (lane >> 4) + r;
+        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        lse2[r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;      // k_rowfin<0>
+        wE[r] = (PASS == 2) ? Q.rowfin[2 * b + 1] : 0.f;    // k_rowfin<1>
+        mrun[r] = -1e30f;
+        srun[r] = 0.f;
+    }
     auto stage = [&](int t, int buf) {
         char* sb = stg + buf * STB;
-        const char* Wt = reinterpret_cast<const char*>(WdP) + (int64_t)64 * t * RB;
+        const char* Wt = WdPc + (int64_t)64 * t * RB;
         for (int pc = w; pc <= NCH; pc += 4) {
             if (pc < NCH) {
                 const int pos = pc * 1024 + lane * 16;
@@ -756,96 +674,29 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             }
         }
     };
-    auto wfrag = [&](int buf, int gb, int s) -> Fr {
-        const int g = 16 * gb + (lane & 15);
-        const int off = (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T);
-        return *reinterpret_cast<const Fr*>(stg + buf * STB + swz_off<RB>(g, off));
-    };
-    constexpr int NBUF = 2;
-    Fr wc[NBUF][KS];
-    float4 gc[NBUF];
-    auto load_blk = [&](int t, int gb, Fr (&wf)[KS], float4& gr) {
-        const int gene = 64 * t + 16 * gb + (lane & 15);
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            wf[s] = M::load(&WdP[(int64_t)gene * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
-        gr = grec[gene];
-    };
-    if (STG) {
-        if (ntl > 0) stage(t0, 0);
-        vm_wait_all();
-        __syncthreads();
-    } else if (wave_live && ntl > 0) {
-        load_blk(t0, 0, wc[0], gc[0]);
-        load_blk(t0, 1, wc[1], gc[1]);
-    }
-    for (int t = t0; (STG || wave_live) && t < t1; ++t) {
+    if (t0 < t1) stage(t0, 0);
+    vm_wait_all();
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
         const int buf = (t - t0) & 1;
-        if (STG && t + 1 < t1) stage(t + 1, buf ^ 1);
-        const int tl = t - t0;
-        // sparse-pass entries of this tile: issue the CSR loads now, consume after the epilogue
-        int total = 0;
-        int e_row[2] = {0, 0}, e_gl[2] = {0, 0};
-        float e_x[2] = {0.f, 0.f};
-        if (PASS == 1) {
-            total = tile_rows(rtl, S, tl, lane, rinc);
-            if (d.dbg & 1) total = 0;
+        if (t + 1 < t1) stage(t + 1, buf ^ 1);
+        const char* sb = stg + buf * STB;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int e = lane + 64 * k;
-                if (e < total) {
-                    int within;
-                    const int r = tile_entry_row(rinc, e, within);
-                    const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-                    e_row[k] = r;
-                    e_gl[k] = Q.col[gi] - 64 * t;
-                    e_x[k] = Q.val[gi];
-                }
-            }
-        }
-        // 16-gene block body.  Pass B keeps the blocks as a rolled loop: unrolling its long
-        // epilogue 4x multiplies live temporaries past 2 waves/SIMD.  A/C unroll fully.
-        auto gb_body = [&](const int gb) {
+        for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
-            const int gene = 64 * t + gl;
-            const bool gv = gene < d.D;
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            float4 g4;
-            if (STG) {
 #pragma unroll
-                for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wfrag(buf, gb, s), acc);
-                g4 = reinterpret_cast<const float4*>(stg + buf * STB + 64 * RB)[gl];
-            } else {
-                // two named slots: even blocks use slot 0, odd blocks slot 1; each slot is
-                // refilled with the block two ahead right after its MFMAs consume it
-                constexpr int SL = 0;
-                const int sl = gb & 1;  // resolved statically: gb_body is called with literal parity
-                (void)SL;
-                if (sl == 0) {
-#pragma unroll
-                    for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[0][s], acc);
-                    g4 = gc[0];
-                    if (d.dbg & 8) {
-                    } else if (gb < 2) load_blk(t, gb + 2, wc[0], gc[0]);
-                    else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[0], gc[0]);
-                } else {
-#pragma unroll
-                    for (int s = 0; s < KS; ++s) acc = M::mma(zfr[s], wc[NBUF - 1][s], acc);
-                    g4 = gc[NBUF - 1];
-                    if (d.dbg & 8) {
-                    } else if (gb < 2) load_blk(t, gb + 2, wc[NBUF - 1], gc[NBUF - 1]);
-                    else if (t + 1 < t1) load_blk(t + 1, gb - 2, wc[NBUF - 1], gc[NBUF - 1]);
-                }
-            }
-            const float bias = g4.x;
+            for (int s = 0; s < KS; ++s)
+                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+            const float4 g4 = reinterpret_cast<const float4*>(sb + 64 * RB)[gl];
             float wcd[CM];
             wcd[0] = g4.z;
 #pragma unroll
-            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && gv) ? Q.Wcd[(int64_t)gene * C + c] : 0.f;
+            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
             if (PASS == 0) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float lg = acc[r] + bias;
+                    float lg = acc[r] + g4.x;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
                     // online max / sum-exp, branch free.  Padded genes carry bias = -inf, so
@@ -856,13 +707,13 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
                     srun[r] = fmaf(srun[r], up ? e : 1.f, up ? 1.f : e);
                     mrun[r] = fmaxf(mrun[r], lg);
                 }
-            } else if (PASS == 2) {
+            } else {
                 float cs[1 + CM];
 #pragma unroll
                 for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float lg = acc[r] + bias;
+                    float lg = acc[r] + g4.x;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
                     const float wp = wE[r] * fexp2(fmaf(lg, L2E, -lse2[r]));
@@ -871,170 +722,18 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
                     for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[r][c], cs[1 + c]);
                 }
                 // per-wave partial of this tile (fixed-order combine after the tile barrier)
-                float* pw = colacc + ((((t - t0) & 1) * 4 + w) * nq) * 64 + gl;
+                float* pw = part + ((buf * 4 + w) * nq) * 64 + gl;
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) {
+                for (int c = 0; c < 1 + CM; ++c)
                     if (c <= C) {
                         const float v = sum_rowgroups(cs[c]);
                         if (lane < 16) pw[c * 64] = v;
                     }
-                }
-            } else {
-                // ---- PASS B dense epilogue: every element as if x = 0 ----
-                const float cn = g4.y;
-                float wnd[RM];
-                wnd[0] = g4.w;
-#pragma unroll
-                for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
-                const float gvf = gv ? 1.f : 0.f;
-                float cs1[1 + CM], csdu = 0.f, csduz[RM];
-#pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
-#pragma unroll
-                for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rl = 4 * (lane >> 4) + r;
-                    float lg = acc[r] + bias;
-#pragma unroll
-                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
-                    const float p = fexp2(fmaf(lg, L2E, -lse2[r]));      // nb.hh:440-441
-                    const float mu = fmaf(p, dv[r], 1e-4f);              // nb.hh:519
-                    float u = cn;
-#pragma unroll
-                    for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], znu[r][q], u);
-                    float sig;
-                    const float spv = softplus_sig(u, sig);              // nb.hh:458
-                    const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);     // nb.hh:459
-                    const float mskf = ((spv >= 1e-4f) && (spv <= 1e4f)) ? 1.f : 0.f;
-                    const float nup = nu + 1e-4f;                        // nb.hh:518
-                    const float s = mu + nup;
-                    const float rs = frcp(s);
-                    const float lgr = log1p_pos(mu * frcp(nup));         // log(s) - log(nup)
-                    const float me = rv[r] * gvf;
-                    lossacc = fmaf(nup * lgr, me, lossacc);              // nb.hh:528, x = 0
-                    const float q = -mu * rs;                            // n dL/dmu' - 1
-                    const float du = (lgr + q) * sig * (mskf * me);
-                    const float pq = p * q;
-                    Eacc[r] += pq;
-                    Pacc[r] += p;
-                    const float wpq = wv[r] * pq;
-                    cs1[0] += wpq;
-#pragma unroll
-                    for (int c = 0; c < CM; ++c) cs1[1 + c] = fmaf(wpq, crow[r][c], cs1[1 + c]);
-                    csdu += du;
-#pragma unroll
-                    for (int qq = 0; qq < RM; ++qq) {
-                        csduz[qq] = fmaf(du, znu[r][qq], csduz[qq]);
-                        dzn[r][qq] = fmaf(du, wnd[qq], dzn[r][qq]);
-                    }
-                    q1[rl * QS + gl] = to_t<T>(pq);
-                    q2[rl * PS + gl] = p;
-                }
-                auto red = [&](float v, int slot) {
-                    if (d.dbg & 4) { lossacc += v; return; }
-                    v += __shfl_xor(v, 16, 64);
-                    v += __shfl_xor(v, 32, 64);
-                    if (lane < 16) atomicAdd(&colacc[slot * GS + tl * 64 + gl], v);
-                };
-#pragma unroll
-                for (int c = 0; c < 1 + CM; ++c)
-                    if (c <= C) red(cs1[c], c);
-                red(csdu, 1 + C);
-#pragma unroll
-                for (int qq = 0; qq < RM; ++qq)
-                    if (qq < R) red(csduz[qq], 2 + C + qq);
             }
-        };
-        if constexpr (PASS == 1) {
-#pragma unroll 1
-            for (int gp = 0; gp < 4; gp += 2) {
-                gb_body(gp);       // even block: slot 0
-                gb_body(gp + 1);   // odd block: slot 1
-            }
-        } else {
-#pragma unroll
-            for (int gb = 0; gb < 4; ++gb) gb_body(gb);
         }
-        if (PASS == 1) {
-            wave_sync();
-            // ---- sparse pass: x-dependent terms for the tile's nonzeros only ----
-            auto correct = [&](int r, int gl, float x) {
-                const float* rs_ = rsc + r * NRS;
-                const float p = q2[r * PS + gl];
-                const int gene = 64 * t + gl;
-                const float mu = fmaf(p, rs_[0], 1e-4f);
-                const float4 g4 = grec[gene];
-                float u = g4.y;
-                float wnd[RM];
-                wnd[0] = g4.w;
-#pragma unroll
-                for (int q = 1; q < RM; ++q) wnd[q] = (q < R) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
-#pragma unroll
-                for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], rs_[3 + q], u);
-                float sig;
-                const float spv = softplus_sig(u, sig);
-                const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);
-                const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
-                const float nup = nu + 1e-4f;
-                const float s = mu + nup;
-                const float rs = frcp(s);
-                float lgd, dgd;
-                if (d.dbg & 32) { lgd = x * nup; dgd = x + nup; } else
-                nb_gamma_terms(nup, x, lgd, dgd);                   // nb.hh:522-523
-                lossacc += x * (flog(s) - flog(mu)) + lgd;          // nb.hh:527
-                const float dq = x * rs - x * frcp(mu);
-                const float pdq = p * dq;
-                q1[r * QS + gl] = to_t<T>(p * (dq - mu * rs));      // p * q with the x terms
-                if (d.dbg & 64) { lossacc += pdq + ((msk ? (x * rs + dgd) * sig : 0.f)); } else {
-                atomicAdd(&rcorr[r * (1 + RM)], pdq);
-                const float wpdq = rs_[1] * pdq;
-                atomicAdd(&colacc[0 * GS + tl * 64 + gl], wpdq);
-                for (int c = 0; c < C; ++c) atomicAdd(&colacc[(1 + c) * GS + tl * 64 + gl], wpdq * rs_[3 + RM + c]);
-                const float ddu = msk ? (x * rs + dgd) * sig : 0.f;
-                atomicAdd(&colacc[(1 + C) * GS + tl * 64 + gl], ddu);
-                for (int q = 0; q < R; ++q) {
-                    atomicAdd(&colacc[(2 + C + q) * GS + tl * 64 + gl], ddu * rs_[3 + q]);
-                    atomicAdd(&rcorr[r * (1 + RM) + 1 + q], ddu * wnd[q]);
-                }
-                }
-            };
-#pragma unroll 1
-            for (int e = lane, k = 0; e < total; e += 64, ++k) {
-                int r, gl;
-                float x;
-                if (k < 2) {
-                    r = k == 0 ? e_row[0] : e_row[1];
-                    gl = k == 0 ? e_gl[0] : e_gl[1];
-                    x = k == 0 ? e_x[0] : e_x[1];
-                } else {
-                    int within;
-                    r = tile_entry_row(rinc, e, within);
-                    const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-                    gl = Q.col[gi] - 64 * t;
-                    x = Q.val[gi];
-                }
-                correct(r, gl, x);
-            }
-            wave_sync();
-            // ---- dz partial = sum_g Q[cell][g] W[g][latent] on MFMA (Q staged through LDS) ----
-#pragma unroll
-            for (int s = 0; s < ((d.dbg & 2) ? 0 : GK); ++s) {
-                const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-                const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-#pragma unroll
-                for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = (d.dbg & 16) ? a1 : M::load(&WdT[(int64_t)(16 * lb + (lane & 15)) * d.DP + 64 * t + s * M::KSTEP +
-                                               (lane >> 4) * M::EPL]);
-                    dzA[lb] = M::mma(a1, bw, dzA[lb]);
-                    dzP[lb] = M::mma(a2, bw, dzP[lb]);
-                }
-            }
-            wave_sync();
-        }
-        if (STG) __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
+        __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
         if (PASS == 2) {
-            const float* pb = colacc + (((t - t0) & 1) * 4 * nq) * 64;
+            const float* pb = part + (buf * 4 * nq) * 64;
             for (int i = threadIdx.x; i < nq * 64; i += 256) {
                 const int q = i >> 6, g = i & 63;
                 Q.slabC[((int64_t)rb * nq + q) * d.DP + 64 * t + g] =
@@ -1042,71 +741,22 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
             }
         }
     }
-    // ---- per-row outputs ----
-    if (wave_live) {
-        if (PASS == 0) {
+    if (PASS == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float m = mrun[r], s = srun[r];
+        for (int r = 0; r < 4; ++r) {
+            float m = mrun[r], s = srun[r];
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
-                    const float mn = fmaxf(m, m2);
-                    s = s * expf(m - mn) + s2 * expf(m2 - mn);
-                    m = mn;
-                }
-                if ((lane & 15) == 0) {
-                    float* lp = Q.lsep + ((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * 2;
-                    lp[0] = m;
-                    lp[1] = s;
-                }
+            for (int o = 1; o < 16; o <<= 1) {
+                const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+                const float mn = fmaxf(m, m2);
+                s = s * expf(m - mn) + s2 * expf(m2 - mn);
+                m = mn;
             }
-        }
-        if (PASS == 1) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float E = Eacc[r], Pp = Pacc[r];
-                float dz2[RM];
-#pragma unroll
-                for (int q = 0; q < RM; ++q) dz2[q] = dzn[r][q];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    E += __shfl_xor(E, o, 64);
-                    Pp += __shfl_xor(Pp, o, 64);
-#pragma unroll
-                    for (int q = 0; q < RM; ++q) dz2[q] += __shfl_xor(dz2[q], o, 64);
-                }
-                const int rl = 4 * (lane >> 4) + r;
-                const int b = row0 + rl;
-                if ((lane & 15) == 0) {
-                    float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
-                    rp[0] = E + rcorr[rl * (1 + RM)];
-                    rp[1] = Pp;
-                    for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q] + rcorr[rl * (1 + RM) + 1 + q];
-                }
-#pragma unroll
-                for (int lb = 0; lb < KP / 16; ++lb) {
-                    float* dp = Q.dzp + (((int64_t)sp * d.Bpad + b) * 2) * KP + 16 * lb + (lane & 15);
-                    dp[0] = dzA[lb][r];
-                    dp[KP] = dzP[lb][r];
-                }
+            if ((lane & 15) == 0) {
+                float* lp = Q.lsep + ((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * 2;
+                lp[0] = m;
+                lp[1] = s;
             }
-        }
-    }
-    if (PASS == 1) {
-        const float lw = wave_sum(lossacc);
-        if (lane == 0) sl[w] = lw;
-        __syncthreads();
-        if (threadIdx.x == 0) Q.lossp[blockIdx.x] = sl[0] + sl[1] + sl[2] + sl[3];
-    }
-    if (PASS == 1) {
-        __syncthreads();
-        float* slab = Q.slabB;
-        const int gbase = t0 * 64;
-        const int glen = min(d.DP, t1 * 64) - gbase;
-        for (int i = threadIdx.x; i < nq * GS; i += 256) {
-            const int q = i / GS, gi = i % GS;
-            if (gi < glen) slab[((int64_t)rb * nq + q) * d.DP + gbase + gi] = colacc[i];
         }
     }
 }
@@ -1325,8 +975,8 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], rs_[3 + q], u);
             float sig;
             const float spv = softplus_sig(u, sig);
-            const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);
-            const bool msk = (spv >= 1e-4f) && (spv <= 1e4f);
+            const float nu = clamp_nu(spv);
+            const bool msk = nu == spv;                                 // clamp passes the gradient
             const float nup = nu + 1e-4f;
             const float sv = mu + nup;
             const float rsv = frcp(sv);
@@ -1371,8 +1021,8 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                 for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], znu[r][q], u);
                 float sig;
                 const float spv = softplus_sig(u, sig);              // nb.hh:458
-                const float nu = fminf(fmaxf(spv, 1e-4f), 1e4f);     // nb.hh:459
-                const float mskf = ((spv >= 1e-4f) && (spv <= 1e4f)) ? 1.f : 0.f;
+                const float nu = clamp_nu(spv);                      // nb.hh:459
+                const float sgm = (nu == spv) ? sig : 0.f;           // clamp mask folded into sig
                 const float nup = nu + 1e-4f;                        // nb.hh:518
                 const float sv = mu + nup;
                 const float rsv = frcp(sv);
@@ -1383,7 +1033,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                 float cpq, cdu;
                 CP::unpack(cc[rl * 64 + gl], cpq, cdu);
                 const float pq = fmaf(p, q, cpq);
-                const float du = fmaf((lgr + q) * sig, mskf * me, cdu);
+                const float du = fmaf((lgr + q) * sgm, me, cdu);
                 Eacc[r] += pq;
                 Pacc[r] += p;
                 const float wpq = wv[r] * pq;
@@ -2153,18 +1803,10 @@ __global__ __launch_bounds__(256) void k_rowfin(DecPtrs Q, Dims d) {
     }
 }
 
-static size_t dec_lds(const Dims& d, int pass, bool bf16, int CM, int RM) {
-    const int nq = (pass == 1) ? (1 + d.C) + 1 + d.R : (1 + d.C);
-    const int tps = (pass == 1) ? d.tpsD : d.tpsA;
-    size_t s = 16 + ((pass == 0) ? 0 : (pass == 1) ? (size_t)nq * tps * 64 * 4 : (size_t)2 * 4 * nq * 64 * 4);
-    if (pass == 1) {
-        const int QS = 64 + (bf16 ? 8 : 4), S = d.tpsD + 1, NRS = 3 + RM + CM;
-        const size_t per = 16 * QS * (bf16 ? 2 : 4) + 16 * 68 * 4 + ((16 * S * 4 + 15) / 16) * 16 +
-                           16 * 8 + 16 * NRS * 4 + ((16 * (1 + RM) * 4 + 15) / 16) * 16 + 64;
-        s += 4 * per;
-    } else {
-        s += 2 * ((size_t)64 * d.KP * (bf16 ? 2 : 4) + 1024);  // double-buffered W + grec stage
-    }
+static size_t dec_lds(const Dims& d, int pass, bool bf16) {
+    const int nq = 1 + d.C;
+    size_t s = 2 * ((size_t)64 * d.KP * (bf16 ? 2 : 4) + 1024);  // double-buffered W + grec stage
+    if (pass == 2) s += (size_t)2 * 4 * nq * 64 * 4;
     return s;
 }
 
@@ -2243,8 +1885,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const bool small_cr = (d.C == 1 && d.R == 1);
     {
         ScopedTimer tm(e, "k_dec_lse");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 0, 1, 1>), gdecA, dim3(256), dec_lds(d, 0, bf, 1, 1), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX, RMAX>), gdecA, dim3(256), dec_lds(d, 0, bf, CMAX, RMAX), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec<T, KP, 0, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_rowfin");
@@ -2274,8 +1916,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
-        if (small_cr) hipLaunchKernelGGL((k_dec<T, KP, 2, 1, 1>), gdecA, dim3(256), dec_lds(d, 2, bf, 1, 1), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX, RMAX>), gdecA, dim3(256), dec_lds(d, 2, bf, CMAX, RMAX), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec<T, KP, 2, 1>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");
