@@ -105,11 +105,8 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(rank, world, obj[0])
 
-    def cells_for(step):
-        base = ((step * world + rank) * B) % Ncells
-        return (base + np.arange(B)) % Ncells
-
-    batches = [cells_for(s) for s in range(args.warmup + args.steps)]
+    # weak scaling: B cells per rank, global batch B * world (mmvae_amd.shard_batch)
+    batches = [mmvae_amd.shard_batch(s, B * world, Ncells, rank, world)[0] for s in range(args.warmup + args.steps)]
     beta = 1.0
     n_total = B * world
 

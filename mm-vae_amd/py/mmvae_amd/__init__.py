@@ -290,6 +290,20 @@ class Engine:
 
 
 # ---- operators.hh scalars ----
+def shard_batch(batch, B_global, N, rank, world):
+    """Data-parallel batch selection (host logic, no GPU).
+
+    The reference draws batch ``batch`` as the contiguous dataset rows (batch*B + j) % N,
+    j < B (mmvae_alg.hh:264-266).  Under DP the global batch of B_global rows is split into
+    ``world`` equal contiguous slices; rank r takes rows [r B/W, (r+1) B/W) of it.
+    Returns (cell_ids int64 [B_global/world], row_offset = global index of the first row)."""
+    if B_global % world:
+        raise ValueError("global batch must divide evenly across ranks")
+    b = B_global // world
+    base = batch * B_global + rank * b
+    return (base + np.arange(b, dtype=np.int64)) % N, rank * b
+
+
 def lbessel(kappa, nu):
     return lib().mmvae_lbessel(kappa, nu)
 

@@ -186,10 +186,13 @@ def kl_loss(mean, lnvar):
     return -0.5 * torch.sum(1 + lnvar - mean.pow(2) - lnvar.exp())
 
 
-def loss(x, y, kl_weight=1.0):
-    """nb.hh:539-548: (NLL + w*KL_mu + w*KL_nu) / n."""
+def loss(x, y, kl_weight=1.0, n_total=None):
+    """nb.hh:539-548: (NLL + w*KL_mu + w*KL_nu) / n.
+
+    n_total (data-parallel restatement only): the divisor is the GLOBAL batch, so the
+    per-rank losses and gradients sum to the single-process ones."""
     recon = nllik_loss(x, y)
-    n = float(x.size(0))
+    n = float(x.size(0)) if n_total is None else float(n_total)
     ret = recon
     ret = ret + kl_loss(y["mu_mean"], y["mu_lnvar"]) * kl_weight
     ret = ret + kl_loss(y["nu_mean"], y["nu_lnvar"]) * kl_weight
@@ -221,6 +224,22 @@ class NBTrainer:
         L.backward()
         grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.m.p.items())
         total = clip_grad_norm_([v.grad for v in self.m.p.values()], self.grad_clip)
+        self.adam.step()
+        return dict(loss=float(L.detach()), grads=grads, total_norm=total)
+
+    def step_dp(self, x, c, eps_mu, eps_nu, beta, n_total, allreduce):
+        """The engine's data-parallel step (mm-vae_amd/csrc/capi.hip mmvae_run): this rank's
+        rows with the loss divided by the global batch n_total, backward, SUM all-reduce of
+        the registered gradients (``allreduce(list_of_tensors)`` sums in place across ranks),
+        then clip_grad_norm_ + Adam on the identical summed gradients of every rank."""
+        y = self.m.forward(x, c, eps_mu, eps_nu, True)
+        L = loss(x, y, beta, n_total=n_total)
+        self.adam.zero_grad()
+        L.backward()
+        gl = [v.grad for v in self.m.p.values()]
+        allreduce(gl)
+        grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.m.p.items())
+        total = clip_grad_norm_(gl, self.grad_clip)
         self.adam.step()
         return dict(loss=float(L.detach()), grads=grads, total_norm=total)
 
