@@ -96,6 +96,26 @@ static void add_slot(Engine* e, const std::string& n, std::vector<int64_t> shape
     e->slots.push_back(s);
 }
 
+// vmf_vae_tImpl registration order (vmf.hh:318-388); the Angular encoder and the decoder
+// Sequential are never register_module'd (Q1) and stay frozen.
+static void build_registry_vmf(Engine* e) {
+    const int64_t D = e->D, C = e->C, K = e->K;
+    add_slot(e, "x_mean", {1, D}, true);
+    add_slot(e, "ln_x_sd", {1, D}, true);
+    add_slot(e, "ln_kappa", {1}, true);
+    add_slot(e, "covar_encoding.weight", {K, C}, true);
+    add_slot(e, "covar_encoding.bias", {K}, true);
+    add_slot(e, "representation_mean.weight", {K, K}, true);
+    add_slot(e, "representation_mean.bias", {K}, true);
+    add_slot(e, "representation_logvariance.weight", {K, K}, true);
+    add_slot(e, "representation_logvariance.bias", {K}, true);
+    add_slot(e, "covar_decoding_.weight", {D, C}, true);
+    add_slot(e, "covar_decoding_.bias", {D}, true);
+    add_slot(e, "z_enc.0.weight", {K, D}, false);
+    add_slot(e, "z_dec.decoding.weight", {D, K}, false);
+    add_slot(e, "z_dec.decoding.bias", {D}, false);
+}
+
 static void build_registry_nb(Engine* e) {
     const int64_t D = e->D, C = e->C, K = e->K, H = e->H, R = e->R;
     add_slot(e, "x_mean", {1, D}, true);
@@ -155,7 +175,10 @@ const char* mmvae_last_error(mmvae_h h) { return h ? h->err.c_str() : g_last_err
 
 int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (!cfg || !out) FAIL((Engine*)nullptr, MMVAE_E_ARG, "null cfg/out");
-    if (cfg->model != MMVAE_MODEL_NB) FAIL((Engine*)nullptr, MMVAE_E_ARG, "only the NB model is built in this version");
+    if (cfg->model != MMVAE_MODEL_NB && cfg->model != MMVAE_MODEL_VMF)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "model must be MMVAE_MODEL_NB or MMVAE_MODEL_VMF");
+    if (cfg->model == MMVAE_MODEL_VMF && !(cfg->kappa_min > 0.f && cfg->kappa_max >= cfg->kappa_min))
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "vMF needs 0 < kappa_min <= kappa_max");
     if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
         cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
@@ -180,7 +203,12 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->Bmax = cfg->max_batch;
     e->Bpad = (cfg->max_batch + 63) / 64 * 64;
     e->nrb_max = e->Bpad / 64;
-    build_registry_nb(e);
+    if (cfg->model == MMVAE_MODEL_VMF) {
+        e->H = e->R = 1;  // unused by the vMF model
+        build_registry_vmf(e);
+    } else {
+        build_registry_nb(e);
+    }
 
     // gene splits: enough workgroups to fill 256 CUs twice, LDS column accumulators <= 40 KB
     auto pick_split = [&](int nq) {
@@ -263,6 +291,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_smallg, 128));
     HIPCHK(e, dalloc(&e->d_sumsq, 256));
     HIPCHK(e, dalloc(&e->d_out, 4));
+    HIPCHK(e, dalloc(&e->d_rowv, Bp));
+    HIPCHK(e, dalloc(&e->d_vk, 8));
     HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4));
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming));
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
@@ -281,7 +311,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_out, e->d_tmp};
+                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (e->h_cells_pin) hipHostFree(e->h_cells_pin);
@@ -455,6 +485,8 @@ int mmvae_init_params(mmvae_h e, uint64_t seed) {
         std::vector<float> v((size_t)s.numel, 0.f);
         if (s.name == "ln_x_sd") {
             std::fill(v.begin(), v.end(), 1.f);
+        } else if (s.name == "ln_kappa") {
+            std::fill(v.begin(), v.end(), std::log(e->cfg.kappa_min));  // vmf.hh:323 (float log, Q4)
         } else if (s.name == "x_mean" || s.name == "mu_bias" || s.name == "nu_bias") {
             // zeros (nb.hh:312-315)
         } else {
@@ -504,14 +536,19 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, a->cell_ids, a->ridx, a->B);
     if (rc) return rc;
+    const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
     if (a->eps) {
-        const int64_t ne = a->B * (e->K + e->R);
+        const int64_t ne = a->B * (e->K + (vmf ? 0 : e->R));
         std::memcpy(e->h_eps_pin, a->eps, sizeof(float) * ne);
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
-    HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
-                                  a->row_offset));
+    if (vmf)
+        HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
+                                       a->row_offset));
+    else
+        HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
+                                      a->row_offset));
     if (a->update) {
         if (e->comm && e->world > 1) {
             ScopedTimer tm(e, "allreduce_grads");
@@ -541,7 +578,8 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
-    HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
+    if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
+    else HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
     HIPCHK(e, hipMemcpyAsync(mean, e->d_tmp, sizeof(float) * B * e->K, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(lnvar, e->d_tmp + e->Bpad * e->K, sizeof(float) * B * e->K, hipMemcpyDeviceToHost,
                              e->stream));

@@ -97,6 +97,8 @@ struct Engine {
     float* d_smallg = nullptr;       // reduced small grads scratch (colsum_dh etc.)
     double* d_sumsq = nullptr;       // sum-of-squares partials
     float* d_out = nullptr;          // [0] loss, [1] total norm (float)
+    float* d_rowv = nullptr;         // vMF: [Bpad] cos_b = <y_b, r_b>
+    float* d_vk = nullptr;           // vMF: kappa scalars (k_vkappa)
     float* h_out_pin = nullptr;
 
     int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder pass-B grids
@@ -153,6 +155,15 @@ hipError_t nb_prepare_frozen(Engine* e);
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
                                bool use_eps, uint64_t step_id, int64_t row_offset);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
+// vMF launchers (vmf_kernels.hip)
+hipError_t vmf_prepare_frozen(Engine* e);
+hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
+                                bool use_eps, uint64_t step_id, int64_t row_offset);
+hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
+// encoder kernels shared by both models (nb_kernels.hip)
+struct Dims;
+hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart);
+hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab);
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);

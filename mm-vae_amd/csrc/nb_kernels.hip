@@ -26,10 +26,9 @@
 
 #include "common.hpp"
 #include "engine.hpp"
+#include "tiles.hpp"
 
 namespace mmvae {
-
-static constexpr int CMAX = 8, HMAX = 8, RMAX = 8;
 
 struct NBPtrs {
     const float *xm, *lsd, *mub, *nub, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd, *Wne, *bne, *Wnm,
@@ -42,37 +41,6 @@ struct NBGrads {
         *Wnl, *bnl, *Wnd, *bnd, *wdp, *bdp;
 };
 
-struct Dims {
-    int D, DP, NT, K, KP, C, H, R;
-    int B, Bpad, nrb;
-    int nsE, tpsE;  // encoder splits, tiles per split
-    int nsD, tpsD;  // decoder pass-B splits
-    int nsA, tpsA;  // decoder passes A / C splits
-    float inv_n, beta;
-    int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
-        LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
-    int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
-    int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
-};
-
-MMVAE_DEV void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int NW>
-MMVAE_DEV float block_sum(float v, float* sbuf) {
-    v = wave_sum(v);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    __syncthreads();
-    if (lane == 0) sbuf[w] = v;
-    __syncthreads();
-    float t = 0.f;
-    if (threadIdx.x == 0)
-        for (int i = 0; i < NW; ++i) t += sbuf[i];
-    return t;  // valid in thread 0
-}
 
 // =======================================================================================
 // k_prep — per-gene constants (nb.hh:408-410 softplus(ln_x_sd)+eps, nb.hh:440 bias terms,
@@ -226,132 +194,6 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
     }
 }
 
-// =======================================================================================
-// Per-wave CSR entry streams over 64-gene tiles (a wave owns 16 rows).  A tile's entries are
-// flattened over the rows (row-major, genes ascending) and spread over the lanes: lane l
-// takes entries l and l + 64 (the common case, prefetched a tile ahead into registers);
-// entries past 128 are fetched on the spot.  tile_rows() runs with the whole wave active
-// and publishes the rows' inclusive prefix counts to per-wave LDS (rinc[16]);
-// tile_entry_row() then only reads LDS, so it is safe inside divergent code.
-// rtl = the wave's tile pointers [16][S] (from k_rowscan), rbl = the rows' CSR bases [16].
-// =======================================================================================
-MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
-    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
-    int inc = cnt;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const int v = __shfl_up(inc, o, 16);
-        if ((lane & 15) >= o) inc += v;
-    }
-    if (lane < 16) rinc[lane] = inc;
-    const int total = __shfl(inc, 15, 64);
-    wave_sync();
-    return total;
-}
-
-// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
-MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
-    const int4* r4 = reinterpret_cast<const int4*>(rinc);
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int4 v = r4[i];
-        r += (v.x <= e) + (v.y <= e) + (v.z <= e) + (i < 3 ? (v.w <= e) : 0);
-    }
-    within = e - (r > 0 ? rinc[r - 1] : 0);
-    return r;
-}
-
-struct TileEntries {
-    int total;
-    int row[2], gl[2];
-    float x[2];
-};
-
-MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane, int32_t* rinc,
-                          const int64_t* rbl, const int32_t* __restrict__ col, const float* __restrict__ val) {
-    te.total = tile_rows(rtl, S, tl, lane, rinc);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int e = lane + 64 * k;
-        te.row[k] = -1;
-        te.gl[k] = 0;
-        te.x[k] = 0.f;
-        if (e < te.total) {
-            int within;
-            const int r = tile_entry_row(rinc, e, within);
-            const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-            te.row[k] = r;
-            te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
-            te.x[k] = val[gi];
-        }
-    }
-}
-
-// visit every entry of the fetched tile: f(row, gene-in-tile, x)
-template <class F>
-MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane,
-                          const int32_t* rinc, const int64_t* rbl, const int32_t* __restrict__ col,
-                          const float* __restrict__ val, F&& f) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (te.row[k] >= 0) f(te.row[k], te.gl[k] - 64 * t, te.x[k]);
-    for (int e = 128 + lane; e < te.total; e += 64) {
-        int within;
-        const int r = tile_entry_row(rinc, e, within);
-        const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-        f(r, col[gi] - 64 * t, val[gi]);
-    }
-}
-
-// log1p of a count: exact libm form in the f32 parity mode, fast form for bf16 tiles
-template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : log1p_pos(x); }
-
-// LDS carve shared by the two encoder kernels (host computes the same size)
-struct EncLds {
-    int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;
-    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre) {
-        const int stb = KP * 64 * esz;
-        o_x = pre + 2 * stb;
-        o_rtl = o_x + 4 * xbytes_per_wave;
-        o_rbl = o_rtl + ((4 * 16 * S * 4 + 15) / 16) * 16;
-        o_rinc = o_rbl + 4 * 16 * 8;
-        o_rsc = o_rinc + 4 * 16 * 4;
-        bytes = o_rsc + 4 * 16 * (1 + HMAX) * 4;
-    }
-};
-
-// Register-staged copy of a [NR rows][RB bytes] tile (row stride `ld` bytes in HBM) into the
-// swizzled LDS image read by swz_off<RB>: loads issued early, ds_write_b128 late, so the
-// copy overlaps a compute phase without an LDS-DMA in flight (hipcc drains vmcnt(0) before
-// LDS reads while a DMA is outstanding).
-template <int NR, int RB>
-struct RegStage {
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    static constexpr int NC = NR * RB / 16 / 256;  // 16-byte chunks per thread (1, 2 or 4)
-    static_assert(NC >= 1 && NC <= 4, "RegStage: 1..4 chunks per thread");
-    u32x4 v0, v1, v2, v3;
-    MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
-        const int c = (int)threadIdx.x + 256 * i;
-        return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
-    }
-    MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
-        const int c = (int)threadIdx.x + 256 * i;
-        *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
-    }
-    MMVAE_DEV void load(const char* src, int64_t ld) {
-        v0 = ld1(src, ld, 0);
-        if constexpr (NC > 1) v1 = ld1(src, ld, 1);
-        if constexpr (NC > 2) v2 = ld1(src, ld, 2);
-        if constexpr (NC > 3) v3 = ld1(src, ld, 3);
-    }
-    MMVAE_DEV void store(char* dst) const {
-        st1(dst, 0, v0);
-        if constexpr (NC > 1) st1(dst, 1, v1);
-        if constexpr (NC > 2) st1(dst, 2, v2);
-        if constexpr (NC > 3) st1(dst, 3, v3);
-    }
-};
 
 // =======================================================================================
 // k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = log1p(x) (W/sd)^T - mvec, so only
@@ -1387,7 +1229,7 @@ struct EncBwdLds {
     }
 };
 
-template <class T, int KP, bool H1>
+template <class T, int KP, bool H1, bool RAW>
 __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cells,
                                                  const int64_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col,
@@ -1407,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
     const int H = H1 ? 1 : d.H;
-    const int nq = 2 + H;
+    const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
     const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN);
     char* wst = smem;
     T* lt = reinterpret_cast<T*>(smem + L.o_lt);          // [64 genes][LS]  log1p(x)
@@ -1427,22 +1269,25 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         const int b = row0 + lane;
         const int64_t cell = (b < d.B) ? cells[b] : -1;
         rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
-        const float* Lr = lat + (int64_t)b * d.lat_stride;
-        scal[16 * w + lane] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
-        for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
+        if (RAW) {
+            const float* Lr = lat + (int64_t)b * d.lat_stride;
+            scal[16 * w + lane] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
+            for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
+        }
     }
     // this wave's 16 cell columns of both tiles
     auto zero_cols = [&]() {
         constexpr int CB = 16 * (int)sizeof(T) / 16;
 #pragma unroll
         for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(lt + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+        if (RAW)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
+            for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
     };
     auto scatter = [&](const TileEntries& te, int tl, int t) {
         tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val, [&](int r, int gl, float x) {
             lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
-            raw[gl * 68 + 16 * w + r] = x;
+            if (RAW) raw[gl * 68 + 16 * w + r] = x;
         });
     };
     // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
@@ -1471,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         const int tl = t - t0;
         if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
         // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
-        {
+        if (RAW) {
             const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
             const float4* xr = reinterpret_cast<const float4*>(raw + gl * 68 + 16 * q4);
             float4 xv[4];
@@ -1931,10 +1776,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         const T* WeT = bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f;
         const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
         if (d.H == 1)
-            hipLaunchKernelGGL((k_enc_bwd<T, KP, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+            hipLaunchKernelGGL((k_enc_bwd<T, KP, true, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
                                e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
         else
-            hipLaunchKernelGGL((k_enc_bwd<T, KP, false>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+            hipLaunchKernelGGL((k_enc_bwd<T, KP, false, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
                                e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
     }
     {
@@ -2004,6 +1849,33 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
     if (e->KP == 32) return bf ? nb_encode_t<__bf16, 32>(e, d, P, d_mean, d_lnvar)
                                : nb_encode_t<float, 32>(e, d, P, d_mean, d_lnvar);
     return bf ? nb_encode_t<__bf16, 64>(e, d, P, d_mean, d_lnvar) : nb_encode_t<float, 64>(e, d, P, d_mean, d_lnvar);
+}
+
+// ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
+template <class T, int KP>
+static void enc_fwd_go(Engine* e, const Dims& d, const void* WeS, float* hpart) {
+    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), e->stream,
+                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, (const T*)WeS, d, hpart);
+}
+template <class T, int KP>
+static void enc_bwd_go(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
+    hipLaunchKernelGGL((k_enc_bwd<T, KP, true, false>), dim3(d.nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)),
+                       e->stream, e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, (const T*)dhT,
+                       (const T*)WeP, d, slab);
+}
+
+hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart) {
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    if (e->KP == 32) bf ? enc_fwd_go<__bf16, 32>(e, d, WeS, hpart) : enc_fwd_go<float, 32>(e, d, WeS, hpart);
+    else bf ? enc_fwd_go<__bf16, 64>(e, d, WeS, hpart) : enc_fwd_go<float, 64>(e, d, WeS, hpart);
+    return hipGetLastError();
+}
+
+hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    if (e->KP == 32) bf ? enc_bwd_go<__bf16, 32>(e, d, dhT, WeP, slab) : enc_bwd_go<float, 32>(e, d, dhT, WeP, slab);
+    else bf ? enc_bwd_go<__bf16, 64>(e, d, dhT, WeP, slab) : enc_bwd_go<float, 64>(e, d, dhT, WeP, slab);
+    return hipGetLastError();
 }
 
 }  // namespace mmvae

@@ -1,0 +1,171 @@
+// Shared device-side pieces of the NB and vMF engines: launch dimensions, wave helpers,
+// CSR tile streaming (cell-major rows densified 16 cells x 64 genes at a time) and the
+// register-staged LDS tile copy.  Device-inline only: every __global__ kernel lives in
+// exactly one translation unit (nb_kernels.hip / vmf_kernels.hip).
+#pragma once
+#include "common.hpp"
+
+namespace mmvae {
+
+static constexpr int CMAX = 8, HMAX = 8, RMAX = 8;
+
+struct Dims {
+    int D, DP, NT, K, KP, C, H, R;
+    int B, Bpad, nrb;
+    int nsE, tpsE;  // encoder splits, tiles per split
+    int nsD, tpsD;  // decoder pass-B splits
+    int nsA, tpsA;  // decoder passes A / C splits
+    float inv_n, beta;
+    int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
+        LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
+    int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
+    int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
+};
+
+MMVAE_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NW>
+MMVAE_DEV float block_sum(float v, float* sbuf) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sbuf[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < NW; ++i) t += sbuf[i];
+    return t;  // valid in thread 0
+}
+
+// =======================================================================================
+// Per-wave CSR entry streams over 64-gene tiles (a wave owns 16 rows).  A tile's entries are
+// flattened over the rows (row-major, genes ascending) and spread over the lanes: lane l
+// takes entries l and l + 64 (the common case, prefetched a tile ahead into registers);
+// entries past 128 are fetched on the spot.  tile_rows() runs with the whole wave active
+// and publishes the rows' inclusive prefix counts to per-wave LDS (rinc[16]);
+// tile_entry_row() then only reads LDS, so it is safe inside divergent code.
+// rtl = the wave's tile pointers [16][S] (from k_rowscan), rbl = the rows' CSR bases [16].
+// =======================================================================================
+MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
+    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(inc, o, 16);
+        if ((lane & 15) >= o) inc += v;
+    }
+    if (lane < 16) rinc[lane] = inc;
+    const int total = __shfl(inc, 15, 64);
+    wave_sync();
+    return total;
+}
+
+// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
+MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
+    const int4* r4 = reinterpret_cast<const int4*>(rinc);
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int4 v = r4[i];
+        r += (v.x <= e) + (v.y <= e) + (v.z <= e) + (i < 3 ? (v.w <= e) : 0);
+    }
+    within = e - (r > 0 ? rinc[r - 1] : 0);
+    return r;
+}
+
+struct TileEntries {
+    int total;
+    int row[2], gl[2];
+    float x[2];
+};
+
+MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane, int32_t* rinc,
+                          const int64_t* rbl, const int32_t* __restrict__ col, const float* __restrict__ val) {
+    te.total = tile_rows(rtl, S, tl, lane, rinc);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = lane + 64 * k;
+        te.row[k] = -1;
+        te.gl[k] = 0;
+        te.x[k] = 0.f;
+        if (e < te.total) {
+            int within;
+            const int r = tile_entry_row(rinc, e, within);
+            const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+            te.row[k] = r;
+            te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
+            te.x[k] = val[gi];
+        }
+    }
+}
+
+// visit every entry of the fetched tile: f(row, gene-in-tile, x)
+template <class F>
+MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane,
+                          const int32_t* rinc, const int64_t* rbl, const int32_t* __restrict__ col,
+                          const float* __restrict__ val, F&& f) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (te.row[k] >= 0) f(te.row[k], te.gl[k] - 64 * t, te.x[k]);
+    for (int e = 128 + lane; e < te.total; e += 64) {
+        int within;
+        const int r = tile_entry_row(rinc, e, within);
+        const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
+        f(r, col[gi] - 64 * t, val[gi]);
+    }
+}
+
+// log1p of a count: exact libm form in the f32 parity mode, fast form for bf16 tiles
+template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : log1p_pos(x); }
+
+// LDS carve shared by the two encoder kernels (host computes the same size)
+struct EncLds {
+    int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;
+    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre) {
+        const int stb = KP * 64 * esz;
+        o_x = pre + 2 * stb;
+        o_rtl = o_x + 4 * xbytes_per_wave;
+        o_rbl = o_rtl + ((4 * 16 * S * 4 + 15) / 16) * 16;
+        o_rinc = o_rbl + 4 * 16 * 8;
+        o_rsc = o_rinc + 4 * 16 * 4;
+        bytes = o_rsc + 4 * 16 * (1 + HMAX) * 4;
+    }
+};
+
+// Register-staged copy of a [NR rows][RB bytes] tile (row stride `ld` bytes in HBM) into the
+// swizzled LDS image read by swz_off<RB>: loads issued early, ds_write_b128 late, so the
+// copy overlaps a compute phase without an LDS-DMA in flight (hipcc drains vmcnt(0) before
+// LDS reads while a DMA is outstanding).
+template <int NR, int RB>
+struct RegStage {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    static constexpr int NC = NR * RB / 16 / 256;  // 16-byte chunks per thread (1, 2 or 4)
+    static_assert(NC >= 1 && NC <= 4, "RegStage: 1..4 chunks per thread");
+    u32x4 v0, v1, v2, v3;
+    MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
+        const int c = (int)threadIdx.x + 256 * i;
+        return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
+    }
+    MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
+        const int c = (int)threadIdx.x + 256 * i;
+        *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
+    }
+    MMVAE_DEV void load(const char* src, int64_t ld) {
+        v0 = ld1(src, ld, 0);
+        if constexpr (NC > 1) v1 = ld1(src, ld, 1);
+        if constexpr (NC > 2) v2 = ld1(src, ld, 2);
+        if constexpr (NC > 3) v3 = ld1(src, ld, 3);
+    }
+    MMVAE_DEV void store(char* dst) const {
+        st1(dst, 0, v0);
+        if constexpr (NC > 1) st1(dst, 1, v1);
+        if constexpr (NC > 2) st1(dst, 2, v2);
+        if constexpr (NC > 3) st1(dst, 3, v3);
+    }
+};
+
+}  // namespace mmvae

@@ -1,0 +1,1104 @@
+// vMF-VAE ELBO step on gfx950: hand-written HIP kernels for the reference's second model
+//   forward  vmf.hh:250-304      (encode: normalised log1p + Angular encoder; Gaussian latent;
+//                                 decode: exp(z_dec(z)) + covar_dec(c), L2-normalised)
+//            angular.hh:34-42    (W~ = normalize(relu(W) + 1e-4), frozen: precomputed once)
+//   loss     vmf.hh:410-440      (kappa <y, r> + df log kappa - lbessel(kappa, df) - D/2 log 2pi)
+//            operators.hh:13-101 (lbessel forward; backward = Baricz bound, ignores upstream, Q3)
+//   backward hand-derived; the algebra is restated in oracle/vmf_analytic.py and proven equal
+//            to LibTorch autograd there.
+//
+// Kernel chain per step (one stream), sharing the CSR tile machinery of tiles.hpp and the
+// encoder GEMM kernels of nb_kernels.hip (enc_forward_launch / enc_backward_launch):
+//   k_vprep        per-gene 1/(softplus(ln_x_sd)+eps), decoder gene records, W~/s
+//   k_vmvec        dense encoder term mvec = (x_mean/s) W~^T
+//   k_vrowscan     one wave per cell: tile pointers, sum l^2, sum (l+eps)^2 - D eps^2
+//   k_enc_fwd      sum_nnz l (W~/s)  on MFMA                    (shared with NB)
+//   k_vlatent_fwd  h = that / ||l|| - mvec, heads, clamp, reparameterise, KL
+//   k_vkappa       kappa = clamp(exp(ln_kappa)), lbessel terms (one thread)
+//   k_vdec<0>      logits on MFMA, u = exp, v = u + hc: row sums |v|^2, sum v, sum l v
+//   k_vrowfin      cos_b = <y_b, r_b>, per-row backward coefficients alpha_b, beta_b
+//   k_vdec<1>      dv = alpha (l + eps) + beta v, da = dv u: column sums + dz GEMM on MFMA
+//   k_vlatent_bwd  heads backward, KL grads, dh (scaled by 1/||l|| for the encoder)
+//   k_enc_bwd      sum_k W~ (dh/||l||)^T log1p(x)                (shared with NB)
+//   k_vgrad_small / k_vgrad_genes   fixed-order reductions into the flat gradient
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "common.hpp"
+#include "engine.hpp"
+#include "tiles.hpp"
+
+namespace mmvae {
+
+struct VPtrs {
+    const float *xm, *lsd, *lk, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd;
+    const float *We, *Wd, *bd;  // frozen (reference layouts: Angular W [Z][D], z_dec W [D][Z], b [D])
+};
+
+struct VGrads {
+    float *xm, *lsd, *lk, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd;
+};
+
+// Model scalars fixed by D (vmf.hh:252,421,427,435; operators.hh:75-76)
+struct VScal {
+    float epsD;    // 1e-2 / D
+    float df;      // max(D/2 - 1, 0)
+    float kmin, kmax;
+    float lg_df1;  // fasterlgamma(df + 1)
+    float c2;      // 0.5 D fasterlog(2 pi)
+    int rank0;     // this rank adds the lbessel backward term (once per global batch)
+};
+
+// d_vk: kappa scalars written by k_vkappa
+enum { VK_KAPPA = 0, VK_EXP = 1, VK_MASK = 2, VK_T = 3, VK_BARICZ = 4 };
+
+// =======================================================================================
+// Frozen operand preparation (once per set_param of a frozen tensor)
+//   W~ = normalize(relu(W) + 1e-4, dim 1)  (angular.hh:37-39)  -> packed [KP][DP] f32 / bf16
+//   z_dec weight -> [DP][KP] (logit GEMM B operand) and [KP][DP] (dz GEMM B operand)
+// =======================================================================================
+__global__ __launch_bounds__(1024) void k_vnorm_enc(const float* __restrict__ W, int D, int DP, int K,
+                                                    float* __restrict__ WeP_f, __bf16* __restrict__ WeP_b) {
+    __shared__ float sb[16];
+    const int k = blockIdx.x;
+    float ss = 0.f;
+    if (k < K)
+        for (int g = threadIdx.x; g < D; g += 1024) {
+            const float r = fmaxf(W[(int64_t)k * D + g], 0.f) + 1e-4f;
+            ss = fmaf(r, r, ss);
+        }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += sb[q];
+    const float nrm = fmaxf(sqrtf(t), 1e-12f);  // F::normalize: x / max(||x||, eps)
+    for (int g = threadIdx.x; g < DP; g += 1024) {
+        float v = 0.f;
+        if (k < K && g < D) v = (fmaxf(W[(int64_t)k * D + g], 0.f) + 1e-4f) / nrm;
+        WeP_f[(int64_t)k * DP + g] = v;
+        WeP_b[(int64_t)k * DP + g] = (__bf16)v;
+    }
+}
+
+__global__ void k_vpack_dec(const float* Wd, int D, int DP, int K, int KP, float* WdP_f, __bf16* WdP_b, float* WdT_f,
+                            __bf16* WdT_b) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)KP * DP) return;
+    const int k = (int)(i / DP), g = (int)(i % DP);
+    const float wd = (k < K && g < D) ? Wd[(int64_t)g * K + k] : 0.f;
+    WdT_f[i] = wd;
+    WdT_b[i] = (__bf16)wd;
+    WdP_f[(int64_t)g * KP + k] = wd;
+    WdP_b[(int64_t)g * KP + k] = (__bf16)wd;
+}
+
+// =======================================================================================
+// k_vprep — per-gene constants of the step:
+//   inv_g = 1 / (softplus(ln_x_sd_g) + eps)       (vmf.hh:255-256)
+//   xmi_g = x_mean_g inv_g                         (dense part of the encoder input)
+//   grec_g = (b_dec_g, b_cd_g, W_cd[g][0], valid)  (vmf.hh:285-287)
+//   WeS[k][g] = inv_g W~[k][g]                     (encoder B operand, bf16 or f32)
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, float* __restrict__ gene,
+                                               const float* __restrict__ WeP_f, float* __restrict__ WeS_f,
+                                               __bf16* __restrict__ WeS_b) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= d.DP) return;
+    const bool v = g < d.D;
+    const float inv = v ? 1.f / (softplus_acc(P.lsd[g]) + epsD) : 0.f;
+    if (blockIdx.y == 0) {
+        gene[g] = inv;
+        gene[3 * d.DP + g] = v ? P.xm[g] * inv : 0.f;
+        reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
+            float4{v ? P.bd[g] : 0.f, v ? P.bcd[g] : 0.f, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? 1.f : 0.f};
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const int k = blockIdx.y * 8 + kk;
+        const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
+        if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+        else WeS_f[(int64_t)k * d.DP + g] = ws;
+    }
+}
+
+// mvec[k] = sum_g xmi_g W~[k][g]
+__global__ __launch_bounds__(1024) void k_vmvec(Dims d, const float* __restrict__ gene, const float* __restrict__ WeP_f,
+                                                float* __restrict__ mvec) {
+    __shared__ float sb[16];
+    const int k = blockIdx.x;
+    const float* xmi = gene + 3 * d.DP;
+    const float* wr = WeP_f + (int64_t)k * d.DP;
+    float acc = 0.f;
+#pragma unroll 4
+    for (int g = threadIdx.x; g < d.D; g += 1024) acc = fmaf(xmi[g], wr[g], acc);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int q = 0; q < 16; ++q) t += sb[q];
+        mvec[k] = t;
+    }
+}
+
+// =======================================================================================
+// k_vrowscan — one wave per batch row, one coalesced sweep of the row's CSR:
+//   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
+//   rowx[b] = (sum l^2, sum (l^2 + 2 eps l))  with l = log1p(x) (vmf.hh:253, 422-423)
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_vrowscan(const int64_t* __restrict__ cells, const int64_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const float* __restrict__ val, Dims d,
+                                                  float epsD, int32_t* __restrict__ rtp, float* __restrict__ rowx) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= d.Bpad) return;
+    const int64_t cell = (b < d.B) ? cells[b] : -1;
+    int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
+    int n = 0;
+    int64_t s = 0;
+    if (cell >= 0) {
+        s = rowptr[cell];
+        n = (int)(rowptr[cell + 1] - s);
+    }
+    const int32_t* cr = col + s;
+    const float* vr = val + s;
+    float sl2 = 0.f, sy = 0.f;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        int g[4], gp[4];
+        float x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u + lane;
+            const bool ok = j < n;
+            g[u] = ok ? cr[j] : 0;
+            x[u] = ok ? vr[j] : 0.f;
+            gp[u] = (ok && j > 0) ? cr[j - 1] : -64;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float l = log1pf(x[u]);
+            const float ly = log1pf(fmaxf(x[u], 0.f));
+            sl2 = fmaf(l, l, sl2);
+            sy = fmaf(ly, ly + 2.f * epsD, sy);
+            const int j = j0 + 64 * u + lane;
+            if (j < n)
+                for (int tt = (gp[u] >> 6) + 1; tt <= (g[u] >> 6); ++tt) rt[tt] = j;
+        }
+    }
+    const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
+    for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
+    sl2 = wave_sum(sl2);
+    sy = wave_sum(sy);
+    if (lane == 0) {
+        rowx[(int64_t)b * d.rowx_stride] = sl2;
+        rowx[(int64_t)b * d.rowx_stride + 1] = sy;
+    }
+}
+
+// =======================================================================================
+// k_vlatent_fwd — encoder head + Gaussian reparameterisation for 64 cells per workgroup
+// (wave w owns cells 4w..4w+3, lane = latent k):
+//   h = (sum_nnz l W~/s) / ||l|| - mvec              (vmf.hh:253-258, Angular has no bias)
+//   mean = repr_mean(h) + covar_enc(c), lnvar = clamp(repr_lnvar(h), -4, 4)   (vmf.hh:259-264)
+//   z = mean + eps exp(lnvar/2)                       (vmf.hh:394-404), KL (vmf.hh:410-414)
+//   mode 1 = recorder encode(x) (vmf.hh:267-281): no covariate, writes mean/lnvar out.
+// Per-row state kept for the backward: h, mean, pre-clamp a, eps, 1/||l|| (LAT_D), valid.
+// =======================================================================================
+__global__ __launch_bounds__(1024) void k_vlatent_fwd(
+    VPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
+    const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowx,
+    const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
+    float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
+    const int K = d.K;
+    __shared__ float sWm[64 * 65], sWl[64 * 65];
+    __shared__ __attribute__((aligned(16))) float sH[64 * 68];
+    __shared__ float sred[16];
+    for (int i = threadIdx.x; i < K * K; i += 1024) {
+        sWm[(i / K) * 65 + i % K] = P.Wm[i];
+        sWl[(i / K) * 65 + i % K] = P.Wl[i];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = lane;
+    const int bw = blockIdx.x * 64 + 4 * w;
+    const float mk = (k < K) ? mvec[k] : 0.f;
+    float inx[4];
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        inx[c] = 1.f / fmaxf(sqrtf(rowx[(int64_t)b * d.rowx_stride]), 1e-12f);  // F::normalize
+        float h = 0.f;
+        if (k < K) {
+            float s = 0.f;
+            for (int s2 = 0; s2 < d.nsE; ++s2) s += hpart[((int64_t)s2 * d.Bpad + b) * d.KP + k];
+            h = s * inx[c] - mk;
+        }
+        sH[(4 * w + c) * 68 + k] = h;
+    }
+    __syncthreads();
+    float mean[4], av[4];
+    const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        mean[c] = bm;
+        av[c] = bl;
+    }
+    const int kk = (k < K) ? k : 0;
+    for (int jj = 0; jj < K; ++jj) {
+        const float wm = sWm[kk * 65 + jj], wl = sWl[kk * 65 + jj];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float hj = sH[(4 * w + c) * 68 + jj];
+            mean[c] = fmaf(wm, hj, mean[c]);
+            av[c] = fmaf(wl, hj, av[c]);
+        }
+    }
+    float kl = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        const bool valid = cell >= 0;
+        float* L = lat + (int64_t)b * d.lat_stride;
+        const float h = sH[(4 * w + c) * 68 + k];
+        float mn = mean[c];
+        const float a = av[c];
+        if (k < K && mode == 0) {
+            float cm = P.bce[k];
+            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * (valid ? covar[cell * d.C + q] : 0.f);
+            mn += cm;
+        }
+        const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
+        if (mode == 1) {
+            if (k < K && b < d.B) {
+                out_mean[(int64_t)b * K + k] = mn;
+                out_lnvar[(int64_t)b * K + k] = lnvar;
+            }
+            continue;
+        }
+        const float sig = expf(lnvar / 2.f);
+        float eps = 0.f;
+        if (k < K && b < d.B)
+            eps = eps_in ? eps_in[(int64_t)b * K + k] : philox_normal(seed, step, row_offset + b, k);
+        const float z = mn + eps * sig;
+        if (k < K) {
+            L[d.LAT_H + k] = h;
+            L[d.LAT_MEAN + k] = mn;
+            L[d.LAT_A + k] = a;
+            L[d.LAT_EPS + k] = eps;
+            if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
+        }
+        if (k < d.KP) {
+            const float zz = (k < K && valid) ? z : 0.f;
+            zf[(int64_t)b * d.KP + k] = zz;
+            zb[(int64_t)b * d.KP + k] = (__bf16)zz;
+        }
+        if (k == 0) {
+            L[d.LAT_D] = inx[c];
+            L[d.LAT_VALID] = valid ? 1.f : 0.f;
+        }
+    }
+    if (mode == 1) return;
+    kl = wave_sum(kl);
+    if (lane == 0) sred[w] = kl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int q = 0; q < 16; ++q) t += sred[q];
+        klpart[blockIdx.x] = -0.5f * t;
+    }
+}
+
+// =======================================================================================
+// k_vkappa — kappa = clamp(exp(ln_kappa), kappa_min, kappa_max) (vmf.hh:301) and the scalar
+// loss terms T = df log kappa - lbessel(kappa, df) (vmf.hh:433, operators.hh:65-81) in the
+// reference's fp32 operation order; the lbessel backward (Baricz bound, operators.hh:34-37).
+// exp/log are evaluated in double and rounded once (correctly rounded fp32), so the clamp
+// mask agrees with ATen's at the initial ln_kappa = log(kappa_min) (Q4).
+// =======================================================================================
+__global__ void k_vkappa(VPtrs P, VScal s, float* __restrict__ vk) {
+    if (threadIdx.x != 0) return;
+    const float lk = P.lk[0];
+    const float e = (float)exp((double)lk);
+    const float kap = fminf(fmaxf(e, s.kmin), s.kmax);
+    const float lkap = (float)log((double)kap);
+    const double nu = s.df;
+    const float eta = (float)((nu + 0.5) / (2. * (nu + 1.)));
+    float s1 = s.df * lkap;
+    s1 = s1 + eta * kap;
+    s1 = s1 - (float)(((double)eta + nu) * log(2.));
+    s1 = s1 - s.lg_df1;
+    float s2 = kap - 0.5f * lkap;
+    s2 = s2 - (float)(0.5 * log(2. * M_PI));
+    const float lb = (kap <= s.df) ? s1 : s2;
+    const float T = s.df * lkap - lb;
+    const float x2 = kap * kap;
+    const float lo = sqrtf(x2 * s.df / (s.df + 1.f) + s.df * s.df);
+    const float up = sqrtf(x2 + s.df * s.df);
+    vk[VK_KAPPA] = kap;
+    vk[VK_EXP] = e;
+    vk[VK_MASK] = (e >= s.kmin && e <= s.kmax) ? 1.f : 0.f;  // clamp backward mask (inclusive)
+    vk[VK_T] = T;
+    vk[VK_BARICZ] = 0.5f * (lo + up) / kap;
+}
+
+// =======================================================================================
+// Decoder passes (vmf.hh:283-289, 419-440).  The [B, D] reconstruction is never stored:
+//   k_vdec<0>: u = exp(z W_d^T + b_d), v = u + hc       -> per row |v|^2, sum v, sum_nnz l v
+//   k_vdec<1>: dv = alpha_b (l + eps) + beta_b v, da = dv u
+//              -> column sums of dv, dv c (covar_decoding_ grads) and dz = da W_d on MFMA
+// Workgroup = 64 cells (4 waves x 16) x one gene split.  Per 64-gene tile the decoder rows
+// (and in pass 1 the [KP][64] transposed tile) are register-staged once per workgroup into
+// LDS; each wave densifies its 16 cells' log1p(x) into a wave-private 16x64 tile from the
+// CSR (entries prefetched a tile ahead).  Lane l holds gene (l & 15) of cells 4(l>>4)+r.
+// =======================================================================================
+struct VDecPtrs {
+    const float* lat;
+    const float* zf;
+    const __bf16* zb;
+    const float* gene;
+    const float* Wcd;
+    const float* covar;
+    const int64_t* cells;
+    const int64_t* rowptr;
+    const int32_t* col;
+    const float* val;
+    const int32_t* rtp;
+    const void* WdP;       // [DP][KP] T
+    const void* WdT;       // [KP][DP] T
+    const float* rowfin;   // [Bpad][2]: alpha, beta
+    float* rowB;           // [nsD][Bpad][3]: |v|^2, sum v, sum l v
+    float* dzp;            // [nsD][Bpad][KP]
+    float* slabB;          // [nrb][1+C][DP]
+};
+
+struct VDecLds {
+    int o_g, o_t, o_part, o_wave, o_q1, o_rtl, o_rbl, o_rinc, wave_bytes, bytes;
+    MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass) {
+        o_g = 64 * KP * esz;
+        o_t = o_g + 1024;
+        o_part = o_t + (pass ? KP * 64 * esz : 0);
+        o_wave = o_part + (pass ? 4 * nq * 64 * 4 : 0);
+        const int QS = 64 + (esz == 2 ? 8 : 4);
+        o_q1 = 16 * 68 * 4;                                   // after the l tile
+        o_rtl = o_q1 + (pass ? ((16 * QS * esz + 15) / 16) * 16 : 0);
+        o_rbl = o_rtl + ((16 * S * 4 + 15) / 16) * 16;
+        o_rinc = o_rbl + 16 * 8;
+        wave_bytes = o_rinc + 64;
+        bytes = o_wave + 4 * wave_bytes;
+    }
+};
+
+template <class T, int KP, int PASS, int CM>
+__global__ __launch_bounds__(256, 2) void k_vdec(VDecPtrs Q, Dims d, float epsD) {
+    using M = MM<T>;
+    using Fr = typename M::frag;
+    constexpr int KS = KP / M::KSTEP;
+    constexpr int GK = 64 / M::KSTEP;
+    constexpr bool BF = sizeof(T) == 2;
+    constexpr int QS = 64 + (BF ? 8 : 4);
+    constexpr int LS = 68;
+    constexpr int RBW = KP * (int)sizeof(T);
+    constexpr int RBT = 64 * (int)sizeof(T);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
+    const int row0 = rb * 64 + 16 * w;
+    const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
+    const int S = d.tpsD + 1;
+    const int C = (CM == 1) ? 1 : d.C;
+    const int nq = 1 + C;
+    const VDecLds L(KP, (int)sizeof(T), S, nq, PASS);
+    char* wst = smem;
+    const float4* gst = reinterpret_cast<const float4*>(smem + L.o_g);
+    char* tst = smem + L.o_t;
+    float* part = reinterpret_cast<float*>(smem + L.o_part);
+    char* wp = smem + L.o_wave + w * L.wave_bytes;
+    float* lt = reinterpret_cast<float*>(wp);
+    T* q1 = reinterpret_cast<T*>(wp + L.o_q1);
+    int32_t* rtl = reinterpret_cast<int32_t*>(wp + L.o_rtl);
+    int64_t* rbl = reinterpret_cast<int64_t*>(wp + L.o_rbl);
+    int32_t* rinc = reinterpret_cast<int32_t*>(wp + L.o_rinc);
+    const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
+    const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
+    const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
+    const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
+
+    Fr zfr[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    float crow[4][CM], ra[4], rbt[4], svv[4], sv[4], slv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = row0 + 4 * (lane >> 4) + r;
+        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        ra[r] = PASS ? Q.rowfin[2 * b] : 0.f;
+        rbt[r] = PASS ? Q.rowfin[2 * b + 1] : 0.f;
+        svv[r] = 0.f;
+        sv[r] = 0.f;
+        slv[r] = 0.f;
+    }
+    f32x4 dz[KP / 16];
+#pragma unroll
+    for (int lb = 0; lb < KP / 16; ++lb) dz[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = lane; i < 16 * S; i += 64) {
+        const int rr = i / S, tt = i % S;
+        rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
+    }
+    if (lane < 16) {
+        const int b = row0 + lane;
+        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+        rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
+    }
+
+    RegStage<64, RBW> wreg;
+    RegStage<KP, RBT> treg;
+    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    auto stage_load = [&](int t) {
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
+        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
+    };
+    auto stage_store = [&]() {
+        wreg.store(wst);
+        if (PASS) treg.store(tst);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
+    };
+    TileEntries pend;
+    if (t0 < t1) {
+        stage_load(t0);
+        stage_store();
+        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+    }
+    __syncthreads();
+
+    for (int t = t0; t < t1; ++t) {
+        const int tl = t - t0;
+        if (t + 1 < t1) stage_load(t + 1);
+        // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
+        for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
+        wave_sync();
+        tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val,
+                   [&](int r, int gl, float x) { lt[r * LS + gl] = log1pf(fmaxf(x, 0.f)); });
+        wave_sync();
+        if (t + 1 < t1) tile_fetch(pend, rtl, S, tl + 1, t + 1, lane, rinc, rbl, Q.col, Q.val);
+#pragma unroll
+        for (int gb = 0; gb < 4; ++gb) {
+            const int gl = 16 * gb + (lane & 15);
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+            const float4 g4 = gst[gl];
+            float wcd[CM];
+            wcd[0] = g4.z;
+#pragma unroll
+            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
+            float cs[1 + CM];
+#pragma unroll
+            for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = 4 * (lane >> 4) + r;
+                const float u = fexp(acc[r] + g4.x);             // exp(z_dec(z))   vmf.hh:285
+                float hc = g4.y;                                 // covar_dec(c)    vmf.hh:286
+#pragma unroll
+                for (int c = 0; c < CM; ++c) hc = fmaf(crow[r][c], wcd[c], hc);
+                const float v = (u + hc) * g4.w;                 // padded genes: 0
+                const float l = lt[rl * LS + gl];
+                if (PASS == 0) {
+                    svv[r] = fmaf(v, v, svv[r]);
+                    sv[r] += v;
+                    slv[r] = fmaf(l, v, slv[r]);
+                } else {
+                    const float dv = fmaf(ra[r], (l + epsD) * g4.w, rbt[r] * v);
+                    cs[0] += dv;
+#pragma unroll
+                    for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(dv, crow[r][c], cs[1 + c]);
+                    q1[rl * QS + gl] = to_t<T>(dv * u);
+                }
+            }
+            if (PASS) {
+                float* pw = part + w * nq * 64 + gl;
+#pragma unroll
+                for (int c = 0; c < 1 + CM; ++c)
+                    if (c <= C) {
+                        const float s = sum_rowgroups(cs[c]);
+                        if (lane < 16) pw[c * 64] = s;
+                    }
+            }
+        }
+        if (PASS) {
+            wave_sync();
+            // dz[cell][latent] += sum_g da[cell][g] W_d[g][latent]
+#pragma unroll
+            for (int s = 0; s < GK; ++s) {
+                const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+#pragma unroll
+                for (int lb = 0; lb < KP / 16; ++lb) {
+                    const Fr bw = *reinterpret_cast<const Fr*>(
+                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                    dz[lb] = M::mma(a1, bw, dz[lb]);
+                }
+            }
+        }
+        lds_barrier();
+        if (PASS) {
+            for (int i = threadIdx.x; i < nq * 64; i += 256) {
+                const int q = i >> 6, g = i & 63;
+                Q.slabB[((int64_t)rb * nq + q) * d.DP + 64 * t + g] =
+                    part[(0 * nq + q) * 64 + g] + part[(1 * nq + q) * 64 + g] + part[(2 * nq + q) * 64 + g] +
+                    part[(3 * nq + q) * 64 + g];
+            }
+        }
+        if (t + 1 < t1) stage_store();
+        lds_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int b = row0 + 4 * (lane >> 4) + r;
+        if (PASS == 0) {
+            float a = svv[r], s1 = sv[r], s2 = slv[r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                a += __shfl_xor(a, o, 64);
+                s1 += __shfl_xor(s1, o, 64);
+                s2 += __shfl_xor(s2, o, 64);
+            }
+            if ((lane & 15) == 0) {
+                float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * 3;
+                rp[0] = a;
+                rp[1] = s1;
+                rp[2] = s2;
+            }
+        } else {
+#pragma unroll
+            for (int lb = 0; lb < KP / 16; ++lb)
+                Q.dzp[((int64_t)sp * d.Bpad + b) * KP + 16 * lb + (lane & 15)] = dz[lb][r];
+        }
+    }
+}
+
+// =======================================================================================
+// k_vrowfin — per row (one thread): combine pass-0 splits, cos_b = <y_b, r_b>
+// (vmf.hh:422-432) and the decoder backward coefficients (see oracle/vmf_analytic.py):
+//   alpha_b = -(kappa/n) / (nv ny),  beta_b = (kappa/n) cos_b / nv^2
+// (below the normalize eps, r = v / eps and the clamp passes no gradient: beta = 0).
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_vrowfin(Dims d, float epsD, const float* __restrict__ lat,
+                                                 const float* __restrict__ rowx, const float* __restrict__ rowB,
+                                                 const float* __restrict__ vk, float* __restrict__ rowfin,
+                                                 float* __restrict__ rowcos) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= d.Bpad) return;
+    float Svv = 0.f, Sv = 0.f, Slv = 0.f;
+    for (int s = 0; s < d.nsD; ++s) {
+        const float* rp = rowB + ((int64_t)s * d.Bpad + b) * 3;
+        Svv += rp[0];
+        Sv += rp[1];
+        Slv += rp[2];
+    }
+    const bool valid = lat[(int64_t)b * d.lat_stride + d.LAT_VALID] > 0.f;
+    const float nvr = sqrtf(Svv);
+    const float nv = fmaxf(nvr, 1e-12f);
+    const float ny = fmaxf(sqrtf(rowx[(int64_t)b * d.rowx_stride + 1] + (float)d.D * epsD * epsD), 1e-12f);
+    const float cosb = (Slv + epsD * Sv) / (ny * nv);
+    const float kn = vk[VK_KAPPA] * d.inv_n;
+    float al = -kn / (nv * ny), be = kn * cosb / (nv * nv);
+    if (!(nvr >= 1e-12f)) {
+        al = -kn / (1e-12f * ny);
+        be = 0.f;
+    }
+    rowfin[2 * b] = valid ? al : 0.f;
+    rowfin[2 * b + 1] = valid ? be : 0.f;
+    rowcos[b] = valid ? cosb : 0.f;
+}
+
+// =======================================================================================
+// k_vlatent_bwd — backward of the reparameterisation, clamp, KL and the Z x Z heads for 64
+// cells per workgroup (lane = latent):  dz = sum over decoder splits,
+//   dmean = dz + (beta/n) mean,  da = [dz eps e^{lnvar/2}/2 + (beta/n)(e^{lnvar} - 1)/2] mask
+//   dh = dmean Wm + da Wl;  dWm += dmean^T h, dWl += da^T h (per-workgroup partials)
+// dhT (encoder backward operand) = dh / ||l||; the x_mean gradient needs the unscaled sum.
+// =======================================================================================
+__global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int64_t* __restrict__ cells,
+                                                     const float* __restrict__ covar, const float* __restrict__ lat,
+                                                     const float* __restrict__ dzp, float* __restrict__ dhT_f,
+                                                     __bf16* __restrict__ dhT_b, float* __restrict__ small) {
+    const int K = d.K, C = d.C, KP = d.KP;
+    const int SMALL = 2 * K * K + 2 * K + K * C + K;
+    constexpr int NSM = 3 * 64 + 64 * CMAX;
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sWm = lsm;               // [K][65]
+    float* sWl = sWm + 64 * 65;     // [K][65]
+    float* sDM = sWl + 64 * 65;     // [cell][68] dmean
+    float* sDA = sDM + 64 * 68;     // [cell][68] d(pre-clamp lnvar)
+    float* sH = sDA + 64 * 68;      // [cell][68] h
+    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + 64 * 68);  // [16][NSM]
+    for (int i = threadIdx.x; i < K * K; i += 1024) {
+        sWm[(i / K) * 65 + i % K] = P.Wm[i];
+        sWl[(i / K) * 65 + i % K] = P.Wl[i];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = lane;
+    const int bw = blockIdx.x * 64 + 4 * w;
+    const float bn = d.beta * d.inv_n;
+    float rbm = 0.f, rbl = 0.f, rWce[CMAX], inx[4];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) rWce[c] = 0.f;
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        const float* L = lat + (int64_t)b * d.lat_stride;
+        const bool valid = L[d.LAT_VALID] > 0.f;
+        inx[c] = L[d.LAT_D];
+        float dmean = 0.f, da = 0.f, h = 0.f;
+        if (k < K) {
+            float dz = 0.f;
+            for (int s2 = 0; s2 < d.nsD; ++s2) dz += dzp[((int64_t)s2 * d.Bpad + b) * KP + k];
+            const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
+            h = L[d.LAT_H + k];
+            const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
+            const float sig = expf(lnvar / 2.f);
+            dmean = dz + bn * mean;
+            const float dlnvar = dz * eps * sig * 0.5f + bn * 0.5f * (expf(lnvar) - 1.f);
+            da = (a >= -4.f && a <= 4.f) ? dlnvar : 0.f;
+            if (!valid) {
+                dmean = 0.f;
+                da = 0.f;
+            }
+        }
+        sDM[(4 * w + c) * 68 + k] = dmean;
+        sDA[(4 * w + c) * 68 + k] = da;
+        sH[(4 * w + c) * 68 + k] = h;
+        rbm += dmean;
+        rbl += da;
+        const int64_t cell = (b < d.B) ? cells[b] : -1;
+#pragma unroll
+        for (int q = 0; q < CMAX; ++q)
+            if (q < C && cell >= 0) rWce[q] += dmean * covar[cell * C + q];
+    }
+    __syncthreads();
+    float* wp = wpart[w];
+    {
+        const int jj = (k < K) ? k : 0;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k4 = 0; k4 < K; k4 += 4) {
+            float wm[4], wl[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                wm[u] = (k4 + u < K) ? sWm[(k4 + u) * 65 + jj] : 0.f;
+                wl[u] = (k4 + u < K) ? sWl[(k4 + u) * 65 + jj] : 0.f;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 dm = *reinterpret_cast<const float4*>(&sDM[(4 * w + c) * 68 + k4]);
+                const float4 dl = *reinterpret_cast<const float4*>(&sDA[(4 * w + c) * 68 + k4]);
+                acc[c] = fmaf(dm.x, wm[0], fmaf(dm.y, wm[1], fmaf(dm.z, wm[2], fmaf(dm.w, wm[3], acc[c]))));
+                acc[c] = fmaf(dl.x, wl[0], fmaf(dl.y, wl[1], fmaf(dl.z, wl[2], fmaf(dl.w, wl[3], acc[c]))));
+            }
+        }
+        float rdhs = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            if (k < KP) {
+                const float v = (k < K) ? acc[c] : 0.f;
+                const float vs = v * inx[c];
+                dhT_f[(int64_t)k * d.Bpad + b] = vs;
+                dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)vs;
+                rdhs += v;
+            }
+        }
+        wp[128 + k] = rdhs;
+    }
+    wp[k] = rbm;
+    wp[64 + k] = rbl;
+#pragma unroll
+    for (int q = 0; q < CMAX; ++q) wp[192 + k * CMAX + q] = rWce[q];
+    float* out = small + (int64_t)blockIdx.x * SMALL;
+    {
+        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gl[4] = {0.f, 0.f, 0.f, 0.f};
+        const int kk = (k < K) ? k : 0;
+        for (int b = 0; b < 64; ++b) {
+            const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
+            const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 4 * w]);
+            gm[0] = fmaf(dm, h4.x, gm[0]); gm[1] = fmaf(dm, h4.y, gm[1]);
+            gm[2] = fmaf(dm, h4.z, gm[2]); gm[3] = fmaf(dm, h4.w, gm[3]);
+            gl[0] = fmaf(dl, h4.x, gl[0]); gl[1] = fmaf(dl, h4.y, gl[1]);
+            gl[2] = fmaf(dl, h4.z, gl[2]); gl[3] = fmaf(dl, h4.w, gl[3]);
+        }
+        if (k < K) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j2 = 4 * w + q;
+                if (j2 < K) {
+                    out[k * K + j2] = gm[q];
+                    out[K * K + k * K + j2] = gl[q];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
+    auto wsum = [&](int off) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += wpart[q][off];
+        return t;
+    };
+    for (int i = threadIdx.x; i < K; i += 1024) {
+        out[o_bm + i] = wsum(i);
+        out[o_bl + i] = wsum(64 + i);
+        out[o_dhs + i] = wsum(128 + i);
+        for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
+    }
+}
+static constexpr size_t VLAT_BWD_LDS = (size_t)(2 * 64 * 65 + 3 * 64 * 68 + 16 * (3 * 64 + 64 * CMAX)) * 4;
+
+// =======================================================================================
+// k_vgrad_small — block 0: the loss (vmf.hh:429-439) and the ln_kappa gradient
+//   L = beta KL / n - (kappa sum_b cos_b + B (T - c2)) / n
+//   dkappa = -sum_b cos_b / n + df (-B/n) / kappa + [rank 0] Baricz(kappa)   (Q3: the lbessel
+//   backward ignores its upstream gradient, so under DP only one rank adds it)
+//   dln_kappa = dkappa exp(ln_kappa) [kappa_min <= exp(ln_kappa) <= kappa_max]
+// other blocks: fixed-order reduction of k_vlatent_bwd's per-workgroup partials.
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const float* __restrict__ small, int nwg,
+                                                     VGrads G, float* __restrict__ smallg,
+                                                     const float* __restrict__ rowcos, const float* __restrict__ klpart,
+                                                     int nkl, const float* __restrict__ vk, float* __restrict__ out,
+                                                     int with_grads) {
+    const int K = d.K, C = d.C;
+    const int SMALL = 2 * K * K + 2 * K + K * C + K;
+    if (blockIdx.x == 0) {
+        __shared__ float sb[8];
+        float cs = 0.f, ks = 0.f;
+        for (int i = threadIdx.x; i < d.Bpad; i += 256) cs += rowcos[i];
+        for (int i = threadIdx.x; i < nkl; i += 256) ks += klpart[i];
+        const float tc = block_sum<4>(cs, sb);
+        const float tk = block_sum<4>(ks, sb);
+        if (threadIdx.x == 0) {
+            const float kap = vk[VK_KAPPA];
+            const float Bn = (float)d.B * d.inv_n;
+            const float llik_sum = fmaf(kap, tc, (float)d.B * (vk[VK_T] - sc.c2));
+            out[0] = tk * d.beta * d.inv_n - llik_sum * d.inv_n;
+            if (with_grads) {
+                float dk = -tc * d.inv_n;
+                dk += (sc.df * -Bn) / kap;
+                if (sc.rank0) dk += vk[VK_BARICZ];
+                G.lk[0] = (vk[VK_MASK] > 0.f) ? dk * vk[VK_EXP] : 0.f;
+            }
+        }
+        return;
+    }
+    if (!with_grads) return;
+    const int i = (blockIdx.x - 1) * 256 + threadIdx.x;
+    if (i >= SMALL) return;
+    float s = 0.f;
+    for (int wg = 0; wg < nwg; ++wg) s += small[(int64_t)wg * SMALL + i];
+    int o = i;
+    if (o < K * K) { G.Wm[o] = s; return; }
+    o -= K * K;
+    if (o < K * K) { G.Wl[o] = s; return; }
+    o -= K * K;
+    if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
+    o -= K;
+    if (o < K) { G.bl[o] = s; return; }
+    o -= K;
+    if (o < K * C) { G.Wce[o] = s; return; }
+    o -= K * C;
+    smallg[o] = s;  // cdh = sum_b dh_b
+}
+
+// Per-gene gradients from the row-block slabs (fixed order): covar_decoding_ (decoder pass 1)
+// and x_mean / ln_x_sd through the Angular encoder (k_enc_bwd's sum_k W~ M term).
+__global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, const float* __restrict__ gene,
+                                                     const float* __restrict__ WeP_f, const float* __restrict__ slabB,
+                                                     const float* __restrict__ slabE, const float* __restrict__ smallg,
+                                                     int nrb) {
+    constexpr int NQMAX = 1 + CMAX + 1;
+    constexpr int NPART = 8;
+    __shared__ float cdh[64];
+    __shared__ float red[NPART - 1][32][NQMAX + 1];
+    const int C = d.C, nqB = 1 + C, nq = nqB + 1;
+    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
+    const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
+    const int g = blockIdx.x * 32 + gi;
+    float acc[NQMAX];
+#pragma unroll
+    for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
+    if (g < d.D) {
+        for (int rb = part; rb < nrb; rb += NPART) {
+            const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
+#pragma unroll
+            for (int q = 0; q < NQMAX; ++q) {
+                if (q < nqB) acc[q] += sB[(int64_t)q * d.DP];
+                else if (q < nq) acc[q] += slabE[(int64_t)rb * d.DP + g];
+            }
+        }
+    }
+    if (part > 0)
+#pragma unroll
+        for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
+    __syncthreads();
+    if (part != 0 || g >= d.D) return;
+#pragma unroll
+    for (int pp = 0; pp < NPART - 1; ++pp)
+#pragma unroll
+        for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
+    G.bcd[g] = acc[0];
+    for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = acc[1 + c];
+    const float Gl = acc[nqB];
+    float gs = 0.f;
+    for (int k = 0; k < d.K; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
+    const float inv = gene[g];
+    G.xm[g] = -inv * gs;
+    G.lsd[g] = -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]);
+}
+
+// =======================================================================================
+// host-side launch orchestration
+// =======================================================================================
+static VPtrs vmf_ptrs(Engine* e) {
+    VPtrs P;
+    P.xm = e->preg("x_mean");
+    P.lsd = e->preg("ln_x_sd");
+    P.lk = e->preg("ln_kappa");
+    P.Wce = e->preg("covar_encoding.weight");
+    P.bce = e->preg("covar_encoding.bias");
+    P.Wm = e->preg("representation_mean.weight");
+    P.bm = e->preg("representation_mean.bias");
+    P.Wl = e->preg("representation_logvariance.weight");
+    P.bl = e->preg("representation_logvariance.bias");
+    P.Wcd = e->preg("covar_decoding_.weight");
+    P.bcd = e->preg("covar_decoding_.bias");
+    P.We = e->pfrz("z_enc.0.weight");
+    P.Wd = e->pfrz("z_dec.decoding.weight");
+    P.bd = e->pfrz("z_dec.decoding.bias");
+    return P;
+}
+
+static VGrads vmf_grads(Engine* e) {
+    VGrads G;
+    G.xm = e->greg("x_mean");
+    G.lsd = e->greg("ln_x_sd");
+    G.lk = e->greg("ln_kappa");
+    G.Wce = e->greg("covar_encoding.weight");
+    G.bce = e->greg("covar_encoding.bias");
+    G.Wm = e->greg("representation_mean.weight");
+    G.bm = e->greg("representation_mean.bias");
+    G.Wl = e->greg("representation_logvariance.weight");
+    G.bl = e->greg("representation_logvariance.bias");
+    G.Wcd = e->greg("covar_decoding_.weight");
+    G.bcd = e->greg("covar_decoding_.bias");
+    return G;
+}
+
+static float host_fasterlog(float x) {
+    uint32_t i;
+    std::memcpy(&i, &x, 4);
+    volatile float y = (float)i;
+    y = y * 8.2629582881927490e-8f;
+    return y - 87.989971088f;
+}
+
+static VScal vmf_scal(Engine* e) {
+    VScal s;
+    const int64_t D = e->D;
+    s.epsD = (float)(1e-2 / (double)(float)D);
+    s.df = (float)std::max(0.5 * (double)(float)D - 1., 0.);
+    s.kmin = e->cfg.kappa_min;
+    s.kmax = e->cfg.kappa_max;
+    s.lg_df1 = mmvae_fasterlgamma((float)((double)s.df + 1));
+    s.c2 = (float)(0.5 * (double)(float)D * (double)host_fasterlog((float)(2. * M_PI)));
+    s.rank0 = e->rank == 0 ? 1 : 0;
+    return s;
+}
+
+hipError_t vmf_prepare_frozen(Engine* e) {
+    ScopedTimer tm(e, "k_vpack_frozen");
+    hipLaunchKernelGGL(k_vnorm_enc, dim3((unsigned)e->KP), dim3(1024), 0, e->stream, e->pfrz("z_enc.0.weight"),
+                       (int)e->D, (int)e->DP, (int)e->K, e->d_WeP_f, e->d_WeP_b);
+    const int64_t n = e->KP * e->DP;
+    hipLaunchKernelGGL(k_vpack_dec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
+                       e->pfrz("z_dec.decoding.weight"), (int)e->D, (int)e->DP, (int)e->K, (int)e->KP, e->d_WdP_f,
+                       e->d_WdP_b, e->d_WdT_f, e->d_WdT_b);
+    e->frozen_dirty = false;
+    return hipGetLastError();
+}
+
+static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
+    Dims d{};
+    d.D = (int)e->D;
+    d.DP = (int)e->DP;
+    d.NT = (int)e->NT;
+    d.K = (int)e->K;
+    d.KP = (int)e->KP;
+    d.C = (int)e->C;
+    d.H = 1;
+    d.R = 1;
+    d.B = (int)B;
+    d.Bpad = (int)((B + 63) / 64 * 64);
+    d.nrb = d.Bpad / 64;
+    d.nsE = e->nsplit_e;
+    d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
+    d.nsD = e->nsplit_d;
+    d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
+    d.nsA = e->nsplit_a;
+    d.tpsA = (int)((e->NT + d.nsA - 1) / d.nsA);
+    d.inv_n = 1.f / (float)n_total;
+    d.beta = beta;
+    d.lat_stride = (int)e->lat_stride;
+    d.LAT_H = (int)e->LAT_H;
+    d.LAT_MEAN = (int)e->LAT_MEAN;
+    d.LAT_A = (int)e->LAT_A;
+    d.LAT_EPS = (int)e->LAT_EPS;
+    d.LAT_D = (int)e->LAT_D;  // vMF: 1 / ||log1p x||
+    d.LAT_VALID = (int)e->LAT_VALID;
+    d.rowx_stride = 2 + (int)e->H;
+    d.dbg = 0;
+    return d;
+}
+
+template <class T, int KP>
+static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const VScal& sc, bool update,
+                                 bool use_eps, uint64_t step_id, int64_t row_offset, int mode, float* out_mean,
+                                 float* out_lnvar) {
+    const bool bf = sizeof(T) == 2;
+    hipStream_t st = e->stream;
+    const int nrb = d.nrb;
+    float* gene = e->d_gene;
+    {
+        ScopedTimer tm(e, "k_vprep");
+        hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, sc.epsD, gene,
+                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr);
+    }
+    {
+        ScopedTimer tm(e, "k_vmvec");
+        hipLaunchKernelGGL(k_vmvec, dim3(d.KP), dim3(1024), 0, st, d, gene, e->d_WeP_f, e->d_mvec);
+    }
+    {
+        ScopedTimer tm(e, "k_vrowscan");
+        hipLaunchKernelGGL(k_vrowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
+                           d, sc.epsD, e->d_rtp, e->d_rowx);
+    }
+    {
+        ScopedTimer tm(e, "k_enc_fwd");
+        hipError_t er = enc_forward_launch(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart);
+        if (er != hipSuccess) return er;
+    }
+    {
+        ScopedTimer tm(e, "k_vlatent_fwd");
+        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
+                           e->d_mvec, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id, row_offset,
+                           e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
+    }
+    if (mode == 1) return hipGetLastError();
+    {
+        ScopedTimer tm(e, "k_vkappa");
+        hipLaunchKernelGGL(k_vkappa, dim3(1), dim3(64), 0, st, P, sc, e->d_vk);
+    }
+    VDecPtrs Q;
+    Q.lat = e->d_lat;
+    Q.zf = e->d_zf;
+    Q.zb = e->d_zb;
+    Q.gene = gene;
+    Q.Wcd = P.Wcd;
+    Q.covar = e->d_covar;
+    Q.cells = e->d_cells;
+    Q.rowptr = e->d_rowptr;
+    Q.col = e->d_col;
+    Q.val = e->d_val;
+    Q.rtp = e->d_rtp;
+    Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
+    Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
+    Q.rowfin = e->d_rowfin;
+    Q.rowB = e->d_rowB;
+    Q.dzp = e->d_dzp;
+    Q.slabB = e->d_slabB;
+    const dim3 gdec(nrb * d.nsD);
+    const int nq = 1 + d.C;
+    const int S = d.tpsD + 1;
+    {
+        ScopedTimer tm(e, "k_vdec_fwd");
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0).bytes;
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec<T, KP, 0, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec<T, KP, 0, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+    }
+    {
+        ScopedTimer tm(e, "k_vrowfin");
+        hipLaunchKernelGGL(k_vrowfin, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, d, sc.epsD, e->d_lat, e->d_rowx,
+                           e->d_rowB, e->d_vk, e->d_rowfin, e->d_rowv);
+    }
+    VGrads G = vmf_grads(e);
+    const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K;
+    if (!update) {
+        ScopedTimer tm(e, "k_loss");
+        hipLaunchKernelGGL(k_vgrad_small, dim3(1), dim3(256), 0, st, d, sc, e->d_small, 0, G, e->d_smallg, e->d_rowv,
+                           e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 0);
+        return hipGetLastError();
+    }
+    {
+        ScopedTimer tm(e, "k_vdec_bwd");
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 1).bytes;
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec<T, KP, 1, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec<T, KP, 1, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+    }
+    {
+        ScopedTimer tm(e, "k_vlatent_bwd");
+        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(1024), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
+                           e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
+    }
+    {
+        ScopedTimer tm(e, "k_enc_bwd");
+        hipError_t er = enc_backward_launch(e, d, bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f,
+                                            bf ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f, e->d_slabE);
+        if (er != hipSuccess) return er;
+    }
+    {
+        ScopedTimer tm(e, "k_vgrad_small");
+        hipLaunchKernelGGL(k_vgrad_small, dim3(1 + (SMALL + 255) / 256), dim3(256), 0, st, d, sc, e->d_small,
+                           e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 1);
+    }
+    {
+        ScopedTimer tm(e, "k_vgrad_genes");
+        hipLaunchKernelGGL(k_vgrad_genes, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                           e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+    }
+    return hipGetLastError();
+}
+
+template <class... A>
+static hipError_t vmf_dispatch(Engine* e, A... a) {
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    if (e->KP == 32) return bf ? vmf_launch_all<__bf16, 32>(e, a...) : vmf_launch_all<float, 32>(e, a...);
+    return bf ? vmf_launch_all<__bf16, 64>(e, a...) : vmf_launch_all<float, 64>(e, a...);
+}
+
+hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,
+                                uint64_t step_id, int64_t row_offset) {
+    if (e->frozen_dirty) {
+        hipError_t er = vmf_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = vmf_dims(e, B, n_total, beta);
+    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), update, use_eps, step_id, row_offset, 0, (float*)nullptr,
+                        (float*)nullptr);
+}
+
+hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
+    if (e->frozen_dirty) {
+        hipError_t er = vmf_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = vmf_dims(e, B, B, 1.f);
+    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), false, false, (uint64_t)0, (int64_t)0, 1, d_mean, d_lnvar);
+}
+
+}  // namespace mmvae

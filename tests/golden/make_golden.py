@@ -17,7 +17,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
-from oracle import nb_oracle, synth  # noqa: E402
+from oracle import nb_oracle, synth, vmf_oracle  # noqa: E402
 
 NB_CASES = [
     # name, N, D, K, C, H, R, B, steps, lib, seed
@@ -86,7 +86,77 @@ def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed):
     print(name, "loss", [float(out[f"s{t}/loss"]) for t in range(steps)], os.path.getsize(path), "bytes")
 
 
+VMF_CASES = [
+    # name, N, D, Z, C, B, steps, lib, seed, ln_kappa (None = reference init log(kappa_min), Q4)
+    ("vmf_small", 40, 50, 8, 1, 16, 3, 200.0, 11, None),
+    ("vmf_generic", 60, 70, 5, 2, 32, 3, 150.0, 12, float(np.log(np.float32(2.0)))),
+    ("vmf_k32", 128, 256, 32, 1, 128, 2, 500.0, 13, float(np.log(np.float32(5.0)))),
+    ("vmf_dups", 10, 40, 8, 1, 24, 2, 120.0, 14, float(np.log(np.float32(0.7)))),
+    ("vmf_z64", 100, 300, 64, 1, 64, 2, 400.0, 15, float(np.log(np.float32(9.0)))),
+]
+
+
+def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa):
+    rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    if C == 1:
+        covar = np.ones((N, 1), dtype=np.float32)  # vmf_vae_main.cc auto ones covariate
+    else:
+        covar = rng.standard_normal((N, C)).astype(np.float32)
+    params, frozen = vmf_oracle.init_params(D, C=C, Z=Z, seed=seed)
+    if ln_kappa is not None:
+        params["ln_kappa"] = torch.tensor([ln_kappa], dtype=torch.float32)
+    tr = vmf_oracle.VMFTrainer(params, frozen)
+    out = dict(N=N, D=D, K=Z, C=C, H=1, R=1, B=B, steps=steps, model="vmf",
+               rowptr=rowptr, col=col, val=val, covar=covar)
+    for k, v in params.items():
+        out["init/" + k] = v.numpy()
+    for k, v in frozen.items():
+        out["frozen/" + k] = v.numpy()
+    nbatch = (N + B - 1) // B
+    for t in range(steps):
+        b = t % nbatch
+        batch = (b * B + np.arange(B)) % N            # mmvae_alg.hh:264-266
+        ridx = rng.integers(0, B, size=B)             # mmvae_alg.hh:292-293
+        cells = batch[ridx]
+        x = torch.from_numpy(synth.densify(rowptr, col, val, cells, D))
+        c = torch.from_numpy(covar[cells])
+        eps = torch.from_numpy(rng.standard_normal((B, Z)).astype(np.float32))
+        beta = nb_oracle.kl_beta(t)
+        r = tr.step(x, c, eps, beta)
+        out[f"s{t}/cells"] = cells.astype(np.int64)
+        out[f"s{t}/eps_mu"] = eps.numpy()
+        out[f"s{t}/eps_nu"] = np.zeros((B, 0), np.float32)
+        out[f"s{t}/beta"] = np.float32(beta)
+        out[f"s{t}/loss"] = np.float32(r["loss"])
+        out[f"s{t}/total_norm"] = np.float64(r["total_norm"])
+        for k, v in r["grads"].items():
+            out[f"s{t}/grad/" + k] = v.numpy()
+        for k, v in tr.params().items():
+            out[f"s{t}/param/" + k] = v.numpy()
+    cells = (np.arange(B) % N).astype(np.int64)
+    x = torch.from_numpy(synth.densify(rowptr, col, val, cells, D))
+    c = torch.from_numpy(covar[cells])
+    eps = torch.from_numpy(rng.standard_normal((B, Z)).astype(np.float32))
+    out["eval/cells"] = cells
+    out["eval/eps_mu"] = eps.numpy()
+    out["eval/eps_nu"] = np.zeros((B, 0), np.float32)
+    out["eval/beta"] = np.float32(0.5)
+    out["eval/loss"] = np.float32(tr.eval_loss(x, c, eps, 0.5))
+    m, lv = tr.encode(x)
+    out["eval/enc_mean"] = m.numpy()
+    out["eval/enc_lnvar"] = lv.numpy()
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(name, "loss", [float(out[f"s{t}/loss"]) for t in range(steps)], os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(1)
-    for case in NB_CASES:
-        make_nb(*case)
+    which = sys.argv[1:] or ["nb", "vmf"]
+    if "nb" in which:
+        for case in NB_CASES:
+            make_nb(*case)
+    if "vmf" in which:
+        for case in VMF_CASES:
+            make_vmf(*case)

@@ -28,10 +28,16 @@ def eps_of(z, tag):
     return np.concatenate([z[f"{tag}/eps_mu"].ravel(), z[f"{tag}/eps_nu"].ravel()]).astype(np.float32)
 
 
+def model_of(z):
+    return str(z["model"]) if "model" in z else "nb"
+
+
 def engine_from_fixture(z, dtype="f32"):
-    from mmvae_amd import Engine
+    from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
     d = dims(z)
-    eng = Engine(D=d["D"], K=d["K"], C=d["C"], H=d["H"], R=d["R"], max_batch=max(d["B"], 64), dtype=dtype)
+    model = MODEL_VMF if model_of(z) == "vmf" else MODEL_NB
+    eng = Engine(D=d["D"], K=d["K"], C=d["C"], H=d["H"], R=d["R"], max_batch=max(d["B"], 64), dtype=dtype,
+                 model=model)
     eng.upload_csr(z["rowptr"], z["col"], z["val"], covar=z["covar"])
     eng.set_params(params_of(z, "init/"))
     eng.set_params(params_of(z, "frozen/"))
@@ -54,7 +60,7 @@ def assert_grads_close(got, want, rtol, ctx=""):
     assert not bad, f"{ctx} gradient mismatch (rtol {rtol}): {bad}"
 
 
-def assert_adam_close(got, want, grads, lr=1e-3, atol=2e-5, ctx=""):
+def assert_adam_close(got, want, grads, lr=1e-3, atol=2e-5, ctx="", noisy_keys=()):
     """Post-Adam params.  Adam's first steps move every coordinate by ~lr*sign(g): a
     coordinate whose gradient is at the fp32 noise floor may flip sign, so those are
     allowed an lr-sized difference; all others must agree to atol."""
@@ -63,6 +69,8 @@ def assert_adam_close(got, want, grads, lr=1e-3, atol=2e-5, ctx=""):
         g = np.abs(np.asarray(grads[k], np.float64).ravel())
         d = np.abs(np.asarray(got[k], np.float64).ravel() - np.asarray(w, np.float64).ravel())
         noisy = g <= 1e-4 * (g.max() + 1e-30)
+        if k in noisy_keys:
+            noisy = np.ones_like(noisy)
         lim = np.where(noisy, 2.5 * lr, atol)
         if np.any(d > lim):
             i = int(np.argmax(d - lim))
