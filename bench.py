@@ -30,24 +30,39 @@ PEAK_BF16 = 2.5e15           # dense MFMA flop/s
 PEAK_F32_MFMA = 157.3e12
 PEAK_TRANS = 256 * 4 * 8 * 2.4e9   # quarter-rate transcendental lane-ops/s = 19.66e12
 TRANS_PER_ELEM_NB = 6        # pass B: exp(p), softplus exp+log, 2 rcp, log1p
+TRANS_PER_ELEM_VMF = 1       # vMF decoder backward: exp(z_dec(z))
+# dominant kernel per model: (name, transcendentals per element, GEMM flops per element / latent)
+DOMINANT = {"nb": ("k_dec_nb", TRANS_PER_ELEM_NB, 6), "vmf": ("k_vdec_bwd", TRANS_PER_ELEM_VMF, 4)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="nb", choices=["nb", "vmf"])
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--genes", type=int, default=20000)
     ap.add_argument("--cells", type=int, default=100000)
-    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--latent", type=int, default=0, help="0 = 64 for NB (configs[1]), 32 for vMF (configs[2])")
     ap.add_argument("--lib-size", type=float, default=2000.0)
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=5)
     return ap.parse_args()
+
+
+def pmc_traffic(model, dtype, kernel):
+    """HBM bytes per launch of `kernel` from the last committed rocprofv3 PMC passes
+    (tools/pmc.sh -> profiles/pmc_traffic.json: (2 FETCH_SIZE + WRITE_SIZE) KiB, the gfx950
+    FETCH_SIZE correction of MI355X_MICROARCH.md §HBM), or None if never profiled."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(f"{model}/{dtype}/{kernel}")
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(eng, args, Ncells):
@@ -63,15 +78,26 @@ def cpu_baseline(eng, args, Ncells):
     info = eng.param_info()
     P = {n: torch.from_numpy(eng.get_param(n, k)) for n, k, r in info if r}
     FR = {n: torch.from_numpy(eng.get_param(n, k)) for n, k, r in info if not r}
-    params, frozen = nb_oracle.init_params(args.genes, K=args.latent)
-    params = {k: P[k].reshape(v.shape) for k, v in params.items()}
-    frozen = {k: FR[k].reshape(v.shape) for k, v in frozen.items()}
-    tr = nb_oracle.NBTrainer(params, frozen)
     g = torch.Generator().manual_seed(0)
-    def one():
-        em = torch.randn(B, args.latent, generator=g)
-        en = torch.randn(B, 1, generator=g)
-        tr.step(x, c, em, en, 1.0)
+    if args.model == "vmf":
+        from oracle import vmf_oracle
+        params, frozen = vmf_oracle.init_params(args.genes, Z=args.latent)
+        params = {k: P[k].reshape(v.shape) for k, v in params.items()}
+        frozen = {k: FR[k].reshape(v.shape) for k, v in frozen.items()}
+        tr = vmf_oracle.VMFTrainer(params, frozen)
+
+        def one():
+            tr.step(x, c, torch.randn(B, args.latent, generator=g), 1.0)
+    else:
+        params, frozen = nb_oracle.init_params(args.genes, K=args.latent)
+        params = {k: P[k].reshape(v.shape) for k, v in params.items()}
+        frozen = {k: FR[k].reshape(v.shape) for k, v in frozen.items()}
+        tr = nb_oracle.NBTrainer(params, frozen)
+
+        def one():
+            em = torch.randn(B, args.latent, generator=g)
+            en = torch.randn(B, 1, generator=g)
+            tr.step(x, c, em, en, 1.0)
     one()  # warm-up
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
@@ -79,7 +105,7 @@ def cpu_baseline(eng, args, Ncells):
     dt = time.perf_counter() - t0
     return {"value": round(B * args.cpu_steps / dt, 2), "unit": "cells/sec", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{args.cpu_steps} NB ELBO steps (fwd+bwd+clip+Adam) of B={B} cells of the same "
+            "sample": f"{args.cpu_steps} {args.model.upper()} ELBO steps (fwd+bwd+clip+Adam) of B={B} cells of the same "
                       f"synthetic {args.genes}-gene dataset, K={args.latent}, fp32 ATen CPU "
                       f"({dt:.1f} s)"}
 
@@ -96,8 +122,11 @@ def main():
     torch.cuda.set_device(local)
     import mmvae_amd
 
+    if args.latent == 0:
+        args.latent = 32 if args.model == "vmf" else 64
     B, D, K, Ncells = args.batch, args.genes, args.latent, args.cells
-    eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=args.dtype, device=local, seed=1234)
+    model = mmvae_amd.MODEL_VMF if args.model == "vmf" else mmvae_amd.MODEL_NB
+    eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=args.dtype, device=local, seed=1234, model=model)
     nnz = eng.synth_csr(Ncells, lib_size=args.lib_size, seed=2024)
     eng.init_params(seed=7)
     if world > 1:
@@ -151,19 +180,26 @@ def main():
         return
     per_kernel = {k: v[0] / max(v[1], 1) for k, v in tm.items()}
     step_dev_ms = sum(v[0] for v in tm.values()) / args.kernel_steps
-    dom = "k_dec_nb"
+    dom, tpe, fpe = DOMINANT[args.model]
     t_dom = per_kernel[dom] * 1e-3
-    trans = TRANS_PER_ELEM_NB * B * D
-    flops = 6.0 * D * K * B
+    trans = tpe * B * D
+    flops = float(fpe) * D * K * B
     achieved = trans / t_dom
+    # algorithmic HBM bytes of one launch: the batch's CSR entries (int32 gene + f32 count) +
+    # the frozen decoder operands it streams once ([DP][KP] and, in the backward, [KP][DP])
+    esz = 2 if args.dtype == "bf16" else 4
+    alg_bytes = 8.0 * nnz / Ncells * B + 2 * ((D + 63) // 64 * 64) * (32 if K <= 32 else 64) * esz
+    traffic = pmc_traffic(args.model, args.dtype, dom)
     roof = {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_TRANS / 1e12, 3),
-            "unit": "Tops/s (quarter-rate transcendental)", "frac": round(achieved / PEAK_TRANS, 4), "traffic": None,
+            "unit": "Tops/s (quarter-rate transcendental)", "frac": round(achieved / PEAK_TRANS, 4), "traffic": traffic,
             "kernel": dom, "kernel_ms": round(per_kernel[dom], 4),
+            "hbm": {"algorithmic_bytes": alg_bytes, "achieved_gbs": round(alg_bytes / t_dom / 1e9, 1),
+                    "peak_gbs": PEAK_HBM / 1e9, "frac": round(alg_bytes / t_dom / PEAK_HBM, 4)},
             "mfma": {"achieved_tflops": round(flops / t_dom / 1e12, 2),
                      "peak_tflops": (PEAK_BF16 if args.dtype == "bf16" else PEAK_F32_MFMA) / 1e12,
                      "frac": round(flops / t_dom / (PEAK_BF16 if args.dtype == "bf16" else PEAK_F32_MFMA), 4)}}
     out = {
-        "metric": "cells/sec (ELBO step) NB-VAE 20k genes",
+        "metric": f"cells/sec (ELBO step) {'vMF' if args.model == 'vmf' else 'NB'}-VAE {D // 1000}k genes",
         "value": round(value, 1),
         "unit": "cells/sec",
         "n_gpus": world,
@@ -175,7 +211,8 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded device-side generator, SURVEY §8(d) count distribution), random-init weights",
-        "config": {"workload": f"NB-VAE ELBO step, {Ncells} cells x {D} genes, latent {K}, batch {B}/GPU",
+        "config": {"workload": f"{'vMF' if args.model == 'vmf' else 'NB'}-VAE ELBO step, {Ncells} cells x {D} genes, "
+                               f"latent {K}, batch {B}/GPU",
                    "global_batch": B * world, "genes": D, "latent": K, "cells": Ncells,
                    "nnz_per_cell": round(nnz / Ncells, 1), "parallelism": f"dp{world}"},
         "roofline": roof,

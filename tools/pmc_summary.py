@@ -1,10 +1,22 @@
-"""Summarise tools/pmc.sh output: per kernel mean duration and counters per dispatch."""
-import collections, csv, glob, os, sys
+"""Summarise tools/pmc.sh output: per kernel mean duration and counters per dispatch.
+
+    python tools/pmc_summary.py ROOT TAG [KEY_PREFIX]
+With KEY_PREFIX (e.g. nb/bf16) the per-launch HBM traffic of every kernel is also written to
+ROOT/TAG_traffic.json as {"KEY_PREFIX/kernel": bytes} (FETCH_SIZE doubled: gfx950 counts 64 B
+per 128-B streaming request, MI355X_MICROARCH.md §HBM; both counters are KiB)."""
+import collections, csv, glob, json, os, sys
 
 root, tag = sys.argv[1], sys.argv[2]
+prefix = sys.argv[3] if len(sys.argv) > 3 else None
+traffic = {}
 
 
 def short(n):
+    import re
+    m = re.match(r"_ZN5mmvae(\d+)", n)
+    if m:  # mangled template instance: keep the kernel's own name
+        L = int(m.group(1))
+        return n[m.end():m.end() + L]
     n = n.split("(")[0].replace("void ", "")
     for a, b in (("mmvae::", ""), ("__bf16", "bf16")):
         n = n.replace(a, b)
@@ -40,4 +52,8 @@ for k in ks:
         if "FETCH_SIZE" in c:
             # gfx950: FETCH_SIZE counts 64 B per 128-B request (MI355X_MICROARCH.md) -> x2, KB -> MB
             line += f" | fetch {2 * c['FETCH_SIZE'] / 1024:7.1f} MB write {c.get('WRITE_SIZE', 0) / 1024:6.1f} MB"
+            if prefix:
+                traffic[f"{prefix}/{k.split('<')[0]}"] = (2 * c["FETCH_SIZE"] + c.get("WRITE_SIZE", 0)) * 1024.0
     print(line)
+if prefix:
+    json.dump(traffic, open(os.path.join(root, f"{tag}_traffic.json"), "w"), indent=1, sort_keys=True)
