@@ -76,6 +76,8 @@ const char* mmvae_last_error(mmvae_h h);
  * covar: [N, C] row-major (NULL -> all ones, the reference's auto covariate). */
 int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
                      int64_t N, int64_t D, const float* covar);
+/* Dataset size after upload/synth (mtx_data_block_t::ntot / nfeature, mmvae_io.hh:73-74). */
+int mmvae_dataset_size(mmvae_h h, int64_t* N, int64_t* D);
 /* Device-side synthetic dataset (bench / smoke): SURVEY §8(d) count distribution. */
 int mmvae_synth_csr(mmvae_h h, int64_t N, double lib_size, uint64_t seed, int64_t* nnz_out);
 /* Copy dataset rows back to the host (recorder / CPU baseline sampling).  rowptr_out
@@ -90,6 +92,9 @@ int mmvae_get_rows(mmvae_h h, const int64_t* rows, int64_t nrows, int64_t* rowpt
  * "z_enc.0.weight", "z_dec.decoding.weight|bias" (vMF). */
 int mmvae_num_params(mmvae_h h, int32_t* count);
 int mmvae_param_info(mmvae_h h, int32_t idx, const char** name, int64_t* numel, int32_t* registered);
+/* Tensor shape of parameter idx (1 or 2 dims, LibTorch layout) — the recorder writes 2-D
+ * tensors as matrices and 1-D ones as columns (write_tensor, mmvae_io.hh:11-28). */
+int mmvae_param_shape(mmvae_h h, int32_t idx, int32_t* ndim, int64_t* shape2);
 int mmvae_set_param(mmvae_h h, const char* name, const float* host, int64_t numel);
 int mmvae_get_param(mmvae_h h, const char* name, float* host, int64_t numel);
 /* Pre-clip gradient of a registered parameter from the last update step (parity tests). */
@@ -132,6 +137,9 @@ int mmvae_sync(mmvae_h h);
  * registered gradients before clip + Adam (new: the reference has no distribution). */
 int mmvae_comm_unique_id(void* out128);
 int mmvae_comm_init(mmvae_h h, int32_t rank, int32_t world, const void* id128);
+/* SUM-all-reduce n host floats across the ranks (RCCL on the handle's stream; a copy when
+ * world == 1).  Used by the host driver for the reported per-batch loss. */
+int mmvae_comm_allreduce(mmvae_h h, float* values, int64_t n);
 
 /* ---- instrumentation -----------------------------------------------------------------
  * HIP-event timing of every kernel launch on the handle's stream. */

@@ -311,7 +311,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk};
+                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (e->h_cells_pin) hipHostFree(e->h_cells_pin);
@@ -372,6 +372,13 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     return MMVAE_OK;
 }
 
+int mmvae_dataset_size(mmvae_h e, int64_t* N, int64_t* D) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "dataset_size: null");
+    if (N) *N = e->N;
+    if (D) *D = e->D;
+    return MMVAE_OK;
+}
+
 int mmvae_synth_csr(mmvae_h e, int64_t N, double lib_size, uint64_t seed, int64_t* nnz_out) {
     if (!e || N < 1 || lib_size <= 0) FAIL(e, MMVAE_E_ARG, "synth_csr: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
@@ -420,6 +427,17 @@ int mmvae_param_info(mmvae_h e, int32_t idx, const char** name, int64_t* numel, 
     if (name) *name = s.name.c_str();
     if (numel) *numel = s.numel;
     if (registered) *registered = s.registered ? 1 : 0;
+    return MMVAE_OK;
+}
+
+int mmvae_param_shape(mmvae_h e, int32_t idx, int32_t* ndim, int64_t* shape2) {
+    if (!e || idx < 0 || idx >= (int)e->slots.size()) FAIL(e, MMVAE_E_ARG, "param_shape: index out of range");
+    const ParamSlot& s = e->slots[idx];
+    if (ndim) *ndim = (int32_t)s.shape.size();
+    if (shape2) {
+        shape2[0] = s.shape.size() > 0 ? s.shape[0] : 1;
+        shape2[1] = s.shape.size() > 1 ? s.shape[1] : 1;
+    }
     return MMVAE_OK;
 }
 
@@ -617,6 +635,24 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (r != ncclSuccess) FAIL(e, MMVAE_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     e->rank = rank;
     e->world = world;
+    return MMVAE_OK;
+}
+
+int mmvae_comm_allreduce(mmvae_h e, float* values, int64_t n) {
+    if (!e || !values || n < 0) FAIL(e, MMVAE_E_ARG, "comm_allreduce: bad arguments");
+    if (n == 0 || !e->comm || e->world <= 1) return MMVAE_OK;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (!e->d_tmp_ar || e->n_tmp_ar < n) {
+        if (e->d_tmp_ar) hipFree(e->d_tmp_ar);
+        e->d_tmp_ar = nullptr;
+        HIPCHK(e, dalloc(&e->d_tmp_ar, n));
+        e->n_tmp_ar = n;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_tmp_ar, values, sizeof(float) * n, hipMemcpyHostToDevice, e->stream));
+    if (ncclAllReduce(e->d_tmp_ar, e->d_tmp_ar, (size_t)n, ncclFloat, ncclSum, e->comm, e->stream) != ncclSuccess)
+        FAIL(e, MMVAE_E_COMM, "ncclAllReduce failed");
+    HIPCHK(e, hipMemcpyAsync(values, e->d_tmp_ar, sizeof(float) * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return MMVAE_OK;
 }
 

@@ -107,6 +107,8 @@ struct Engine {
     int64_t klp_off = 0;             // offset of KL partials inside d_lossp
     hipEvent_t ev_staged = nullptr;  // last H2D copy out of the pinned staging buffers
     float* d_tmp = nullptr;          // encode outputs
+    float* d_tmp_ar = nullptr;       // host-value all-reduce staging
+    int64_t n_tmp_ar = 0;
 
     // ---- comm ----
     ncclComm_t comm = nullptr;

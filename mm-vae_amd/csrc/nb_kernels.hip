@@ -465,7 +465,7 @@ struct DecPtrs {
 // Passes A and C: each tile's decoder rows + gene records are staged ONCE per workgroup into
 // LDS by LDS-DMA (double-buffered, swizzled image), shared by the four waves.
 template <class T, int KP, int PASS, int CM>
-__global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
+MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     using M = MM<T>;
     using Fr = typename M::frag;
     constexpr int KS = KP / M::KSTEP;
@@ -602,6 +602,12 @@ __global__ __launch_bounds__(256, 2) void k_dec(DecPtrs Q, Dims d) {
         }
     }
 }
+
+// distinct kernel names per pass (profiles): A = log-sum-exp, C = the E_b P column term
+template <class T, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_dec_lse(DecPtrs Q, Dims d) { dec_ac_body<T, KP, 0, CM>(Q, d); }
+template <class T, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_dec_tail(DecPtrs Q, Dims d) { dec_ac_body<T, KP, 2, CM>(Q, d); }
 
 // =======================================================================================
 // k_dec_nb<T, KP, CM, RM> — decoder pass B: softmax + NB likelihood + every gradient term
@@ -1730,8 +1736,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const bool small_cr = (d.C == 1 && d.R == 1);
     {
         ScopedTimer tm(e, "k_dec_lse");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec<T, KP, 0, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 0, CMAX>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec_lse<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_rowfin");
@@ -1761,8 +1767,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec<T, KP, 2, 1>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec<T, KP, 2, CMAX>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        else hipLaunchKernelGGL((k_dec_tail<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");

@@ -150,6 +150,7 @@ __global__ __launch_bounds__(1024) void k_vmvec(Dims d, const float* __restrict_
 //   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
 //   rowx[b] = (sum l^2, sum (l^2 + 2 eps l))  with l = log1p(x) (vmf.hh:253, 422-423)
 // =======================================================================================
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_vrowscan(const int64_t* __restrict__ cells, const int64_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, const float* __restrict__ val, Dims d,
                                                   float epsD, int32_t* __restrict__ rtp, float* __restrict__ rowx) {
@@ -180,8 +181,9 @@ __global__ __launch_bounds__(256) void k_vrowscan(const int64_t* __restrict__ ce
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const float l = log1pf(x[u]);
-            const float ly = log1pf(fmaxf(x[u], 0.f));
+            // FAST (bf16 operand mode): v_log-based log1p (rel err <= 6e-6); f32 parity mode: libm
+            const float l = FAST ? log1p_pos(fmaxf(x[u], 0.f)) : log1pf(x[u]);
+            const float ly = (x[u] >= 0.f) ? l : 0.f;   // log1p(relu x)
             sl2 = fmaf(l, l, sl2);
             sy = fmaf(ly, ly + 2.f * epsD, sy);
             const int j = j0 + 64 * u + lane;
@@ -393,7 +395,7 @@ struct VDecLds {
 };
 
 template <class T, int KP, int PASS, int CM>
-__global__ __launch_bounds__(256, 2) void k_vdec(VDecPtrs Q, Dims d, float epsD) {
+MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     using M = MM<T>;
     using Fr = typename M::frag;
     constexpr int KS = KP / M::KSTEP;
@@ -584,6 +586,11 @@ __global__ __launch_bounds__(256, 2) void k_vdec(VDecPtrs Q, Dims d, float epsD)
         }
     }
 }
+
+template <class T, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<T, KP, 0, CM>(Q, d, epsD); }
+template <class T, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_vdec_bwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<T, KP, 1, CM>(Q, d, epsD); }
 
 // =======================================================================================
 // k_vrowfin — per row (one thread): combine pass-0 splits, cos_b = <y_b, r_b>
@@ -985,7 +992,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vrowscan");
-        hipLaunchKernelGGL(k_vrowscan, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
+        hipLaunchKernelGGL(k_vrowscan<sizeof(T) == 2>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
                            d, sc.epsD, e->d_rtp, e->d_rowx);
     }
     {
@@ -1028,8 +1035,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vdec_fwd");
         const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec<T, KP, 0, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else hipLaunchKernelGGL((k_vdec<T, KP, 0, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec_fwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     {
         ScopedTimer tm(e, "k_vrowfin");
@@ -1047,8 +1054,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vdec_bwd");
         const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 1).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec<T, KP, 1, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else hipLaunchKernelGGL((k_vdec<T, KP, 1, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec_bwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");

@@ -1,0 +1,364 @@
+// nb_vae_main / vmf_vae_main drop-in CLIs (src/nb_vae_main.cc, src/vmf_vae_main.cc) over the HIP
+// engine.  The reference parses argv once per option group with getopt_long, unknown options
+// ignored (opterr = 0): mmvae options (mmvae.hh:68-209), training options (mmvae_alg.hh:36-125),
+// then the model's (nb.hh:73-194 / vmf.hh:75-186) — a short option therefore means one thing
+// per group, and this parser keeps exactly that behaviour.  A fourth group holds the engine's
+// own options (--seed, --dtype, --device, --threads, --no_csr_cache, --verbose).
+//
+// Outputs as the reference: ${out}.scores.gz (per-epoch loss), ${out}.covar.mtx.gz when --covar
+// is absent (create_ones_like), recorder files every --recording epochs.  The dataset is loaded
+// once into HBM; its parsed CSR is cached next to the mtx as ${mtx}.mmvae_csr (the role of the
+// reference's ${mtx}.index: a faster second open).
+// Data parallel: launched once per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment;
+// rank 0 publishes the RCCL id in ${out}.rccl_id, the other ranks read it.
+#include <getopt.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mmvae_host.h"
+#include "cli.hh"
+#include "host_common.hh"
+
+namespace mmvae_host {
+
+static bool file_exists(const std::string& f) {
+    struct stat st;
+    return !f.empty() && stat(f.c_str(), &st) == 0;
+}
+
+static std::vector<int64_t> split_ints(const std::string& s) {
+    std::vector<int64_t> v;
+    size_t p = 0;
+    while (p <= s.size()) {
+        size_t q = s.find(',', p);
+        if (q == std::string::npos) q = s.size();
+        if (q > p) v.push_back(std::stol(s.substr(p, q - p)));
+        p = q + 1;
+    }
+    return v;
+}
+
+struct ArgvCopy {  // getopt_long permutes argv: every group parses a fresh copy
+    std::vector<std::string> store;
+    std::vector<char*> ptrs;
+    ArgvCopy(int argc, const char** argv) {
+        for (int i = 0; i < argc; ++i) store.emplace_back(argv[i]);
+        for (auto& s : store) ptrs.push_back(&s[0]);
+        ptrs.push_back(nullptr);
+    }
+};
+
+template <class F>
+static void each_opt(int argc, const char** argv, const char* shorts, const option* longs, F&& f) {
+    ArgvCopy a(argc, argv);
+    optind = 1;
+    opterr = 0;
+    while (true) {
+        const int c = getopt_long(argc, a.ptrs.data(), shorts, longs, nullptr);
+        if (c == -1) break;
+        f(c, optarg ? std::string(optarg) : std::string());
+    }
+}
+
+int parse_options(int argc, const char** argv, int model, CliOptions& o) {
+    // ---- mmvae.hh:68-209 ----
+    static const option mm_long[] = {{"mtx", required_argument, nullptr, 'M'},         {"idx", required_argument, nullptr, 'I'},
+                                     {"out", required_argument, nullptr, 'O'},         {"output", required_argument, nullptr, 'O'},
+                                     {"cov", required_argument, nullptr, 'V'},         {"covar", required_argument, nullptr, 'V'},
+                                     {"cov_idx", required_argument, nullptr, 'J'},     {"covar_idx", required_argument, nullptr, 'J'},
+                                     {"row", required_argument, nullptr, 'r'},         {"col", required_argument, nullptr, 'c'},
+                                     {"column", required_argument, nullptr, 'c'},      {"annot", required_argument, nullptr, 'a'},
+                                     {"annotation", required_argument, nullptr, 'a'},  {"batch_size", required_argument, nullptr, 'b'},
+                                     {"batch", required_argument, nullptr, 'b'},       {"kl_discount", required_argument, nullptr, 'K'},
+                                     {"kl_max", required_argument, nullptr, 'L'},      {"kl_min", required_argument, nullptr, 'l'},
+                                     {"help", no_argument, nullptr, 'h'},              {nullptr, no_argument, nullptr, 0}};
+    each_opt(argc, argv, "M:I:O:V:J:r:c:a:b:K:L:l:h?", mm_long, [&](int c, const std::string& v) {
+        switch (c) {
+            case 'M': o.mtx = v; break;
+            case 'I': o.idx = v; break;
+            case 'V': o.covar_mtx = v; break;
+            case 'J': o.covar_idx = v; break;
+            case 'O': o.out = v; break;
+            case 'r': o.row = v; break;
+            case 'c': o.col = v; break;
+            case 'a': o.annot = v; break;
+            case 'b': o.train.batch_size = std::stol(v); break;
+            case 'K': o.train.kl_discount = std::stof(v); break;
+            case 'l': o.train.kl_min = std::stof(v); break;
+            case 'L': o.train.kl_max = std::stof(v); break;
+            case 'h': o.help = true; break;
+            default: break;
+        }
+    });
+    // ---- mmvae_alg.hh:36-125 ----
+    static const option tr_long[] = {{"lr", required_argument, nullptr, 'L'},          {"learning", required_argument, nullptr, 'L'},
+                                     {"learn_rate", required_argument, nullptr, 'L'},  {"learning_rate", required_argument, nullptr, 'L'},
+                                     {"rate", required_argument, nullptr, 'L'},        {"grad_clip", required_argument, nullptr, 'G'},
+                                     {"nboot", required_argument, nullptr, 'B'},       {"boot", required_argument, nullptr, 'B'},
+                                     {"bootstrap", required_argument, nullptr, 'B'},   {"max_epoch", required_argument, nullptr, 'E'},
+                                     {"epoch", required_argument, nullptr, 'E'},       {"recording", required_argument, nullptr, 'R'},
+                                     {"help", no_argument, nullptr, 'h'},              {nullptr, no_argument, nullptr, 0}};
+    each_opt(argc, argv, "L:G:B:E:R:h", tr_long, [&](int c, const std::string& v) {
+        switch (c) {
+            case 'L': o.lr = std::stof(v); break;
+            case 'B': o.train.nboot = std::stol(v); break;
+            case 'E': o.train.max_epoch = std::stol(v); break;
+            case 'R': o.train.recording = std::stol(v); break;
+            // 'G' (--grad_clip) is parsed but never stored by the reference (Q7): clip stays 1
+            default: break;
+        }
+    });
+    // ---- nb.hh:73-194 / vmf.hh:75-186 ----
+    if (model == MMVAE_MODEL_NB) {
+        static const option nb_long[] = {{"mean_encoding", required_argument, nullptr, 'E'},
+                                         {"mean-encoding", required_argument, nullptr, 'E'},
+                                         {"mean_decoding", required_argument, nullptr, 'D'},
+                                         {"mean-decoding", required_argument, nullptr, 'D'},
+                                         {"mean_latent", required_argument, nullptr, 'L'},
+                                         {"mean-latent", required_argument, nullptr, 'L'},
+                                         {"overdisp_encoding", required_argument, nullptr, 'e'},
+                                         {"overdisp-encoding", required_argument, nullptr, 'e'},
+                                         {"overdispersion_encoding", required_argument, nullptr, 'e'},
+                                         {"overdispersion-encoding", required_argument, nullptr, 'e'},
+                                         {"overdispersion_latent", required_argument, nullptr, 'l'},
+                                         {"overdispersion-latent", required_argument, nullptr, 'l'},
+                                         {"relu", no_argument, nullptr, 'R'},
+                                         {"no_relu", no_argument, nullptr, 'r'},
+                                         {"no-relu", no_argument, nullptr, 'r'},
+                                         {"help", no_argument, nullptr, 'h'},
+                                         {nullptr, no_argument, nullptr, 0}};
+        each_opt(argc, argv, "E:D:L:e:l:rRh", nb_long, [&](int c, const std::string& v) {
+            switch (c) {
+                case 'E': o.enc_layers = split_ints(v); break;
+                case 'D': o.dec_layers = split_ints(v); break;
+                case 'L': o.latent = std::stol(v); break;
+                case 'e': o.H = std::stol(v); break;
+                case 'l': o.R = std::stol(v); break;
+                case 'r': o.relu = false; break;
+                case 'R': o.relu = true; break;
+                default: break;
+            }
+        });
+    } else {
+        static const option vmf_long[] = {{"encoding", required_argument, nullptr, 'E'},  {"decoding", required_argument, nullptr, 'D'},
+                                          {"latent", required_argument, nullptr, 'L'},    {"kappa_min", required_argument, nullptr, 'k'},
+                                          {"kappa-min", required_argument, nullptr, 'k'}, {"kappa_max", required_argument, nullptr, 'K'},
+                                          {"kappa-max", required_argument, nullptr, 'K'}, {"relu", no_argument, nullptr, 'R'},
+                                          {"no_relu", no_argument, nullptr, 'r'},         {"no-relu", no_argument, nullptr, 'r'},
+                                          {"help", no_argument, nullptr, 'h'},            {nullptr, no_argument, nullptr, 0}};
+        each_opt(argc, argv, "E:D:L:k:K:Rrh", vmf_long, [&](int c, const std::string& v) {
+            switch (c) {
+                case 'E': o.enc_layers = split_ints(v); break;
+                case 'D': o.dec_layers = split_ints(v); break;
+                case 'L': o.latent = std::stol(v); break;
+                case 'k': o.kappa_min = std::stof(v); break;
+                case 'K': o.kappa_max = std::stof(v); break;
+                case 'r': o.relu = false; break;
+                case 'R': o.relu = true; break;
+                default: break;
+            }
+        });
+    }
+    // ---- engine options (not in the reference) ----
+    static const option en_long[] = {{"seed", required_argument, nullptr, 1},      {"dtype", required_argument, nullptr, 2},
+                                     {"device", required_argument, nullptr, 3},    {"threads", required_argument, nullptr, 4},
+                                     {"no_csr_cache", no_argument, nullptr, 5},    {"verbose", no_argument, nullptr, 6},
+                                     {"quiet", no_argument, nullptr, 7},           {nullptr, no_argument, nullptr, 0}};
+    each_opt(argc, argv, "", en_long, [&](int c, const std::string& v) {
+        switch (c) {
+            case 1: o.seed = std::stoull(v); break;
+            case 2: o.dtype = v; break;
+            case 3: o.device = std::stoi(v); break;
+            case 4: o.threads = std::stoi(v); break;
+            case 5: o.csr_cache = false; break;
+            case 6: o.verbose = true; break;
+            case 7: o.verbose = false; break;
+            default: break;
+        }
+    });
+    if (o.idx.empty()) o.idx = o.mtx + ".index";
+    if (o.covar_idx.empty()) o.covar_idx = o.covar_mtx + ".index";
+    return MMVAE_OK;
+}
+
+const char* usage_text(int model) {
+    return model == MMVAE_MODEL_NB
+               ? "nb_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
+                 "             --mean_latent 2 --overdisp_encoding 1 --overdispersion_latent 1 --kl_discount .1\n"
+                 "             --kl_max 1 --kl_min .01 --recording 10 --covar C.mtx.gz]\n"
+                 "engine: [--dtype f32|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n"
+               : "vmf_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
+                 "             --latent 2 --kappa_min .1 --kappa_max 10 --kl_discount .1 --kl_max 1 --kl_min .01\n"
+                 "             --recording 10 --covar C.mtx.gz]\n"
+                 "engine: [--dtype f32|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n";
+}
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int load_dataset(const CliOptions& o, mmvae_csr& csr) {
+    const std::string cache = o.mtx + ".mmvae_csr";
+    struct stat sm, sc;
+    if (o.csr_cache && stat(cache.c_str(), &sc) == 0 && stat(o.mtx.c_str(), &sm) == 0 && sc.st_mtime >= sm.st_mtime &&
+        mmvae_csr_load(cache.c_str(), &csr) == MMVAE_OK)
+        return MMVAE_OK;
+    int rc = mmvae_mtx_read(o.mtx.c_str(), o.threads, &csr);
+    if (rc) return rc;
+    if (o.csr_cache) mmvae_csr_save(cache.c_str(), &csr);  // best effort (read-only dirs are fine)
+    return MMVAE_OK;
+}
+
+static int rendezvous(mmvae_h h, const CliOptions& o, int rank, int world) {
+    const std::string path = o.out + ".rccl_id";
+    unsigned char id[128];
+    if (rank == 0) {
+        if (mmvae_comm_unique_id(id)) return fail(MMVAE_E_COMM, mmvae_last_error(nullptr));
+        const std::string tmp = path + ".tmp";
+        FILE* fp = std::fopen(tmp.c_str(), "wb");
+        if (!fp || std::fwrite(id, 1, 128, fp) != 128 || std::fclose(fp) != 0) return fail(MMVAE_E_COMM, "cannot write " + tmp);
+        std::rename(tmp.c_str(), path.c_str());
+    } else {
+        const double t0 = now_s();
+        for (;;) {
+            FILE* fp = std::fopen(path.c_str(), "rb");
+            if (fp) {
+                const size_t n = std::fread(id, 1, 128, fp);
+                std::fclose(fp);
+                if (n == 128) break;
+            }
+            if (now_s() - t0 > 300) return fail(MMVAE_E_COMM, "timed out waiting for " + path);
+            std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        }
+    }
+    if (mmvae_comm_init(h, rank, world, id)) return fail(MMVAE_E_COMM, mmvae_last_error(h));
+    return MMVAE_OK;
+}
+
+int run_cli(int argc, const char** argv, int model) {
+    CliOptions o;
+    parse_options(argc, argv, model, o);
+    if (o.help) {
+        std::fputs(usage_text(model), stderr);
+        return EXIT_SUCCESS;
+    }
+    // mmvae.hh:199-200 and nb_vae_main.cc:51-52
+    if (!file_exists(o.mtx)) {
+        std::fprintf(stderr, "missing mtx file\n%s", usage_text(model));
+        return EXIT_FAILURE;
+    }
+    if (o.out.empty()) {
+        std::fprintf(stderr, "need output file header\n%s", usage_text(model));
+        return EXIT_FAILURE;
+    }
+    if (!o.enc_layers.empty() || !o.dec_layers.empty()) {
+        std::fprintf(stderr, "hidden encoder/decoder layers are not built in this engine (default architecture only)\n");
+        return EXIT_FAILURE;
+    }
+    const int rank = std::getenv("RANK") ? std::atoi(std::getenv("RANK")) : 0;
+    const int world = std::getenv("WORLD_SIZE") ? std::atoi(std::getenv("WORLD_SIZE")) : 1;
+    const int local = std::getenv("LOCAL_RANK") ? std::atoi(std::getenv("LOCAL_RANK")) : 0;
+    const int device = o.device >= 0 ? o.device : local;
+    if (o.train.batch_size % world) {
+        std::fprintf(stderr, "--batch_size must be divisible by WORLD_SIZE\n");
+        return EXIT_FAILURE;
+    }
+    const double t0 = now_s();
+    mmvae_csr csr;
+    if (load_dataset(o, csr)) {
+        std::fprintf(stderr, "failed to read %s: %s\n", o.mtx.c_str(), mmvae_host_last_error());
+        return EXIT_FAILURE;
+    }
+    if (o.verbose && rank == 0)
+        std::fprintf(stderr, "[mmvae] Sparse Mtx Data: %lld x %lld (%lld nonzeros) from %s in %.2f s\n", (long long)csr.D,
+                     (long long)csr.N, (long long)csr.nnz, o.mtx.c_str(), now_s() - t0);
+    // covariates (nb_vae_main.cc:63-83): a separate MatrixMarket, or the all-ones column
+    std::vector<float> covar;
+    int64_t C = 1;
+    if (file_exists(o.covar_mtx)) {
+        int64_t Nc = 0;
+        float* m = nullptr;
+        if (mmvae_mtx_read_dense_t(o.covar_mtx.c_str(), o.threads, &Nc, &C, &m)) {
+            std::fprintf(stderr, "failed to read %s: %s\n", o.covar_mtx.c_str(), mmvae_host_last_error());
+            return EXIT_FAILURE;
+        }
+        if (Nc != csr.N) {
+            std::fprintf(stderr, "data and covar on the same set of data points (%lld vs %lld)\n", (long long)csr.N,
+                         (long long)Nc);
+            return EXIT_FAILURE;
+        }
+        covar.assign(m, m + Nc * C);
+        mmvae_free(m);
+    } else if (rank == 0) {
+        const std::string f = o.out + ".covar.mtx.gz";
+        if (mmvae_mtx_write_ones(f.c_str(), csr.N)) std::fprintf(stderr, "warning: %s\n", mmvae_host_last_error());
+        else if (o.verbose) std::fprintf(stderr, "[mmvae] No covariate file is given. So we use this: %s\n", f.c_str());
+    }
+    mmvae_cfg cfg;
+    mmvae_cfg_default(&cfg, model);
+    cfg.dtype = (o.dtype == "bf16") ? MMVAE_DTYPE_BF16 : MMVAE_DTYPE_F32;
+    cfg.D = csr.D;
+    cfg.C = C;
+    cfg.K = o.latent;
+    cfg.H = o.H;
+    cfg.R = o.R;
+    cfg.max_batch = o.train.batch_size / world;
+    cfg.lr = o.lr;
+    cfg.kappa_min = o.kappa_min;
+    cfg.kappa_max = o.kappa_max;
+    cfg.seed = o.seed;
+    mmvae_h h = nullptr;
+    if (mmvae_create(&cfg, device, &h)) {
+        std::fprintf(stderr, "engine: %s\n", mmvae_last_error(nullptr));
+        return EXIT_FAILURE;
+    }
+    int rc = mmvae_upload_csr(h, csr.rowptr, csr.col, csr.val, csr.N, csr.D, covar.empty() ? nullptr : covar.data());
+    mmvae_csr_free(&csr);
+    if (!rc) rc = mmvae_init_params(h, o.seed);
+    if (!rc && world > 1) rc = rendezvous(h, o, rank, world);
+    if (rc) {
+        std::fprintf(stderr, "engine: %s %s\n", mmvae_last_error(h), mmvae_host_last_error());
+        mmvae_destroy(h);
+        return EXIT_FAILURE;
+    }
+    mmvae_train_opts t = o.train;
+    t.seed = o.seed;
+    t.out = o.out.c_str();
+    t.verbose = o.verbose ? 1 : 0;
+    t.rank = rank;
+    t.world = world;
+    std::vector<float> scores((size_t)std::max<int64_t>(t.max_epoch, 1));
+    const double t1 = now_s();
+    rc = mmvae_train(h, &t, scores.data());
+    if (rc) {
+        std::fprintf(stderr, "training failed: %s\n", mmvae_host_last_error());
+        mmvae_destroy(h);
+        return EXIT_FAILURE;
+    }
+    if (o.verbose && rank == 0)
+        std::fprintf(stderr, "[mmvae] trained %lld epochs in %.2f s\n", (long long)t.max_epoch, now_s() - t1);
+    if (rank == 0) {  // write_vector_file(out + ".scores.gz") (nb_vae_main.cc:133)
+        TextWriter w;
+        const std::string f = o.out + ".scores.gz";
+        if (!w.open(f)) {
+            std::fprintf(stderr, "cannot write %s\n", f.c_str());
+            mmvae_destroy(h);
+            return EXIT_FAILURE;
+        }
+        for (int64_t e = 0; e < t.max_epoch; ++e) w.write(fmt_g(scores[(size_t)e]) + "\n");
+        w.close();
+        if (world > 1) std::remove((o.out + ".rccl_id").c_str());
+    }
+    mmvae_destroy(h);
+    return EXIT_SUCCESS;
+}
+
+}  // namespace mmvae_host

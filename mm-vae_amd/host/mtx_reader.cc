@@ -1,0 +1,554 @@
+// MatrixMarket (plain / gzip / BGZF) -> cell-major CSR, loaded once for an HBM-resident run.
+//
+// Replaces the reference's per-batch BGZF reader (mtx_data_block_t::read, mmvae_io.hh:208-245,
+// over visit_bgzf_block, mmutil_bgzf_util.hh:53-151) with a one-time parallel load:
+//   1. the compressed file is read whole; BGZF block boundaries come from each block's BSIZE
+//      field, so blocks inflate independently on every worker (raw deflate, ISIZE-sized slots
+//      of one text buffer); non-BGZF gzip streams inflate serially, plain text is used as is;
+//   2. the text after the "rows cols nnz" header splits at line boundaries into one chunk per
+//      worker; each parses its triplets (1-based; '%' lines and lines with < 3 fields skipped,
+//      as mmutil_bgzf_util.hh:102-127 does);
+//   3. per-chunk column histograms -> rowptr; entries scatter in file order; rows whose genes
+//      are unsorted or repeated are sorted stably and deduplicated keeping the LAST entry (the
+//      reference's dense scatter overwrites, mmvae_io.hh:115-123).
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mmvae_host.h"
+#include "host_common.hh"
+
+namespace mmvae_host {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int default_threads(int threads) {
+    if (threads > 0) return threads;
+    int n = (int)std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+        const int v = std::atoi(e);
+        if (v > 0 && (n <= 0 || v < n)) n = v;
+    }
+    return std::max(1, std::min(n, 64));
+}
+
+template <class F>
+void parallel_for(int nthreads, int64_t n, F&& f) {
+    if (n <= 0) return;
+    nthreads = (int)std::min<int64_t>(nthreads, n);
+    if (nthreads <= 1) {
+        f(0, (int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        const int64_t a = n * t / nthreads, b = n * (t + 1) / nthreads;
+        th.emplace_back([&f, t, a, b] { f(t, a, b); });
+    }
+    for (auto& x : th) x.join();
+}
+
+static bool read_whole(const char* path, std::vector<unsigned char>& buf, std::string& err) {
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) {
+        err = std::string("cannot open ") + path + ": " + std::strerror(errno);
+        return false;
+    }
+    std::fseek(fp, 0, SEEK_END);
+    const long sz = std::ftell(fp);
+    std::fseek(fp, 0, SEEK_SET);
+    if (sz < 0) {
+        std::fclose(fp);
+        err = std::string("cannot size ") + path;
+        return false;
+    }
+    buf.resize((size_t)sz);
+    size_t got = 0;
+    while (got < buf.size()) {
+        const size_t r = std::fread(buf.data() + got, 1, buf.size() - got, fp);
+        if (r == 0) break;
+        got += r;
+    }
+    std::fclose(fp);
+    if (got != buf.size()) {
+        err = std::string("short read on ") + path;
+        return false;
+    }
+    return true;
+}
+
+struct BgzfBlock {
+    size_t in_off, in_len, out_off, out_len;
+};
+
+static uint32_t le32(const unsigned char* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Every gzip member carries a 'BC' extra subfield with BSIZE (SAM/BGZF spec): true -> blocks
+static bool scan_bgzf(const std::vector<unsigned char>& b, std::vector<BgzfBlock>& blocks) {
+    size_t p = 0, out = 0;
+    while (p < b.size()) {
+        if (p + 18 > b.size()) return false;
+        if (b[p] != 31 || b[p + 1] != 139 || b[p + 2] != 8 || !(b[p + 3] & 4)) return false;
+        const size_t xlen = b[p + 10] | (b[p + 11] << 8);
+        size_t q = p + 12, qe = q + xlen;
+        long bsize = -1;
+        while (q + 4 <= qe && qe <= b.size()) {
+            const int slen = b[q + 2] | (b[q + 3] << 8);
+            if (b[q] == 'B' && b[q + 1] == 'C' && slen == 2 && q + 6 <= b.size()) bsize = b[q + 4] | (b[q + 5] << 8);
+            q += 4 + (size_t)slen;
+        }
+        if (bsize < 0) return false;
+        const size_t total = (size_t)bsize + 1, hdr = 12 + xlen;
+        if (total < hdr + 8 || p + total > b.size()) return false;
+        BgzfBlock blk;
+        blk.in_off = p + hdr;
+        blk.in_len = total - hdr - 8;
+        blk.out_len = le32(&b[p + total - 4]);
+        blk.out_off = out;
+        out += blk.out_len;
+        blocks.push_back(blk);
+        p += total;
+    }
+    return true;
+}
+
+static bool inflate_raw(const unsigned char* in, size_t in_len, char* out, size_t out_len) {
+    z_stream s;
+    std::memset(&s, 0, sizeof(s));
+    if (inflateInit2(&s, -15) != Z_OK) return false;
+    s.next_in = const_cast<unsigned char*>(in);
+    s.avail_in = (uInt)in_len;
+    s.next_out = reinterpret_cast<unsigned char*>(out);
+    s.avail_out = (uInt)out_len;
+    const int r = inflate(&s, Z_FINISH);
+    const bool ok = (r == Z_STREAM_END) && s.total_out == out_len;
+    inflateEnd(&s);
+    return ok || (out_len == 0);
+}
+
+// serial inflate of (possibly multi-member) gzip
+static bool inflate_gzip(const std::vector<unsigned char>& in, std::vector<char>& out, std::string& err) {
+    z_stream s;
+    std::memset(&s, 0, sizeof(s));
+    if (inflateInit2(&s, 15 + 32) != Z_OK) {
+        err = "inflateInit2 failed";
+        return false;
+    }
+    s.next_in = const_cast<unsigned char*>(in.data());
+    s.avail_in = (uInt)std::min<size_t>(in.size(), 1u << 30);
+    size_t consumed_base = 0;
+    out.resize(std::max<size_t>(in.size() * 4, 1 << 20));
+    size_t produced = 0;
+    for (;;) {
+        if (produced == out.size()) out.resize(out.size() * 2);
+        s.next_out = reinterpret_cast<unsigned char*>(out.data() + produced);
+        s.avail_out = (uInt)std::min<size_t>(out.size() - produced, 1u << 30);
+        const uInt before = s.avail_out;
+        const int r = inflate(&s, Z_NO_FLUSH);
+        produced += before - s.avail_out;
+        const size_t consumed = consumed_base + (size_t)(s.next_in - (in.data() + consumed_base));
+        if (r == Z_STREAM_END) {
+            if (consumed >= in.size()) break;
+            inflateReset(&s);  // next gzip member
+        } else if (r != Z_OK && r != Z_BUF_ERROR) {
+            inflateEnd(&s);
+            err = "gzip stream is corrupt";
+            return false;
+        }
+        if (s.avail_in == 0) {
+            if (consumed >= in.size()) break;
+            consumed_base = consumed;
+            s.next_in = const_cast<unsigned char*>(in.data() + consumed);
+            s.avail_in = (uInt)std::min<size_t>(in.size() - consumed, 1u << 30);
+        }
+    }
+    inflateEnd(&s);
+    out.resize(produced);
+    return true;
+}
+
+bool load_text(const char* path, int threads, std::vector<char>& text, std::string& err) {
+    std::vector<unsigned char> raw;
+    if (!read_whole(path, raw, err)) return false;
+    if (raw.size() >= 2 && raw[0] == 0x1f && raw[1] == 0x8b) {
+        std::vector<BgzfBlock> blocks;
+        if (scan_bgzf(raw, blocks)) {
+            const size_t total = blocks.empty() ? 0 : blocks.back().out_off + blocks.back().out_len;
+            text.resize(total);
+            std::atomic<bool> ok{true};
+            parallel_for(threads, (int64_t)blocks.size(), [&](int, int64_t a, int64_t bnd) {
+                for (int64_t i = a; i < bnd; ++i) {
+                    const BgzfBlock& k = blocks[(size_t)i];
+                    if (!inflate_raw(raw.data() + k.in_off, k.in_len, text.data() + k.out_off, k.out_len)) ok = false;
+                }
+            });
+            if (!ok) {
+                err = std::string("corrupt BGZF block in ") + path;
+                return false;
+            }
+            return true;
+        }
+        return inflate_gzip(raw, text, err);
+    }
+    text.assign(raw.begin(), raw.end());
+    return true;
+}
+
+// ---- triplet parsing ------------------------------------------------------------------------
+static inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+static inline float parse_float(const char* a, const char* e) {
+    // fast path: optional sign + digits (integer counts); otherwise strtof on a copy
+    const char* p = a;
+    bool neg = false;
+    if (p < e && (*p == '-' || *p == '+')) neg = (*p++ == '-');
+    uint64_t v = 0;
+    const char* d0 = p;
+    while (p < e && *p >= '0' && *p <= '9' && p - d0 < 18) v = v * 10 + (uint64_t)(*p++ - '0');
+    if (p == e && p > d0) return neg ? -(float)v : (float)v;
+    char tmp[64];
+    const size_t n = std::min<size_t>((size_t)(e - a), sizeof(tmp) - 1);
+    std::memcpy(tmp, a, n);
+    tmp[n] = 0;
+    return std::strtof(tmp, nullptr);
+}
+
+static inline int64_t parse_int(const char* a, const char* e) {
+    int64_t v = 0;
+    const char* p = a;
+    bool neg = false;
+    if (p < e && (*p == '-' || *p == '+')) neg = (*p++ == '-');
+    while (p < e && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0');
+    return neg ? -v : v;
+}
+
+struct Chunk {
+    std::vector<int32_t> cell, gene;
+    std::vector<float> val;
+    int64_t cmin = INT64_MAX, cmax = -1;
+    std::string err;
+};
+
+// visit each line of [p, e): f(tokens[3]) for lines with >= 3 fields, skipping '%' lines
+static void parse_chunk(const char* p, const char* e, int64_t D, int64_t N, Chunk& ch) {
+    ch.cell.reserve((size_t)((e - p) / 10));
+    ch.gene.reserve((size_t)((e - p) / 10));
+    ch.val.reserve((size_t)((e - p) / 10));
+    while (p < e) {
+        const char* le = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+        if (!le) le = e;
+        if (*p != '%') {
+            const char* tb[3];
+            const char* te[3];
+            int nt = 0;
+            const char* q = p;
+            while (q < le && nt < 3) {
+                while (q < le && is_ws(*q)) ++q;
+                if (q >= le) break;
+                tb[nt] = q;
+                while (q < le && !is_ws(*q)) ++q;
+                te[nt++] = q;
+            }
+            if (nt == 3) {
+                const int64_t r = parse_int(tb[0], te[0]) - 1, c = parse_int(tb[1], te[1]) - 1;
+                if (r < 0 || r >= D || c < 0 || c >= N) {
+                    if (ch.err.empty())
+                        ch.err = "entry (" + std::to_string(r + 1) + ", " + std::to_string(c + 1) +
+                                 ") outside the " + std::to_string(D) + " x " + std::to_string(N) + " header";
+                } else {
+                    ch.gene.push_back((int32_t)r);
+                    ch.cell.push_back((int32_t)c);
+                    ch.val.push_back(parse_float(tb[2], te[2]));
+                    ch.cmin = std::min(ch.cmin, c);
+                    ch.cmax = std::max(ch.cmax, c);
+                }
+            }
+        }
+        p = le + 1;
+    }
+}
+
+// header: skip '%' lines; first other line = rows cols nnz (peek_bgzf_header)
+static bool parse_header(const std::vector<char>& t, size_t& pos, int64_t& rows, int64_t& cols, int64_t& nnz) {
+    pos = 0;
+    while (pos < t.size()) {
+        const char* p = t.data() + pos;
+        const char* e = t.data() + t.size();
+        const char* le = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+        if (!le) le = e;
+        const size_t next = (size_t)(le - t.data()) + 1;
+        if (*p != '%' && le > p) {
+            int64_t v[3];
+            int nt = 0;
+            const char* q = p;
+            while (q < le && nt < 3) {
+                while (q < le && is_ws(*q)) ++q;
+                if (q >= le) break;
+                const char* a = q;
+                while (q < le && !is_ws(*q)) ++q;
+                v[nt++] = parse_int(a, q);
+            }
+            pos = next;
+            if (nt < 2) return false;
+            rows = v[0];
+            cols = v[1];
+            nnz = nt > 2 ? v[2] : 0;
+            return rows > 0 && cols > 0;
+        }
+        pos = next;
+    }
+    return false;
+}
+
+int read_triplets(const char* path, int threads, int64_t& D, int64_t& N, std::vector<Chunk>& chunks) {
+    threads = default_threads(threads);
+    std::vector<char> text;
+    std::string err;
+    if (!load_text(path, threads, text, err)) return fail(MMVAE_E_ARG, err);
+    size_t pos;
+    int64_t nnz_hdr;
+    if (!parse_header(text, pos, D, N, nnz_hdr))
+        return fail(MMVAE_E_ARG, std::string("no MatrixMarket size line in ") + path);
+    if (N >= INT32_MAX || D >= INT32_MAX) return fail(MMVAE_E_ARG, "matrix dimensions exceed int32");
+    // split the body at line boundaries
+    const size_t body = text.size() - pos;
+    const int nch = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * 4, body / (1 << 16) + 1));
+    std::vector<size_t> cut(nch + 1);
+    cut[0] = pos;
+    cut[nch] = text.size();
+    for (int k = 1; k < nch; ++k) {
+        size_t c = pos + body * k / nch;
+        c = std::max(c, cut[k - 1]);
+        while (c < text.size() && text[c - 1] != '\n') ++c;
+        cut[k] = c;
+    }
+    chunks.assign(nch, Chunk());
+    std::atomic<int> next{0};
+    parallel_for(threads, threads, [&](int, int64_t, int64_t) {
+        for (int k = next++; k < nch; k = next++) parse_chunk(text.data() + cut[k], text.data() + cut[k + 1], D, N, chunks[k]);
+    });
+    for (auto& c : chunks)
+        if (!c.err.empty()) return fail(MMVAE_E_ARG, std::string(path) + ": " + c.err);
+    return MMVAE_OK;
+}
+
+}  // namespace mmvae_host
+
+using namespace mmvae_host;
+
+extern "C" {
+
+const char* mmvae_host_last_error(void) { return g_err.c_str(); }
+
+void mmvae_free(void* p) { std::free(p); }
+
+void mmvae_csr_free(mmvae_csr* c) {
+    if (!c) return;
+    std::free(c->rowptr);
+    std::free(c->col);
+    std::free(c->val);
+    c->rowptr = nullptr;
+    c->col = nullptr;
+    c->val = nullptr;
+    c->N = c->D = c->nnz = 0;
+}
+
+int mmvae_mtx_read(const char* path, int threads, mmvae_csr* out) {
+    if (!path || !out) return fail(MMVAE_E_ARG, "mtx_read: null argument");
+    std::memset(out, 0, sizeof(*out));
+    threads = default_threads(threads);
+    int64_t D, N;
+    std::vector<Chunk> chunks;
+    int rc = read_triplets(path, threads, D, N, chunks);
+    if (rc) return rc;
+    const int nch = (int)chunks.size();
+    // per-chunk column histograms over each chunk's column range
+    std::vector<std::vector<int64_t>> cnt(nch);
+    parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k) {
+            Chunk& ch = chunks[(size_t)k];
+            if (ch.cmax < 0) continue;
+            cnt[k].assign((size_t)(ch.cmax - ch.cmin + 1), 0);
+            for (int32_t c : ch.cell) cnt[k][(size_t)(c - ch.cmin)]++;
+        }
+    });
+    std::vector<int64_t> rp((size_t)N + 1, 0);
+    for (int k = 0; k < nch; ++k)
+        for (size_t i = 0; i < cnt[k].size(); ++i) rp[(size_t)chunks[k].cmin + i + 1] += cnt[k][i];
+    for (int64_t i = 0; i < N; ++i) rp[(size_t)i + 1] += rp[(size_t)i];
+    const int64_t nnz_all = rp[(size_t)N];
+    // each chunk's start offset per column = rowptr + entries of earlier chunks (file order)
+    {
+        std::vector<int64_t> run(rp.begin(), rp.end() - 1);
+        for (int k = 0; k < nch; ++k)
+            for (size_t i = 0; i < cnt[k].size(); ++i) {
+                const size_t c = (size_t)chunks[k].cmin + i;
+                const int64_t n = cnt[k][i];
+                cnt[k][i] = run[c];
+                run[c] += n;
+            }
+    }
+    std::vector<int32_t> col((size_t)nnz_all);
+    std::vector<float> val((size_t)nnz_all);
+    parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k) {
+            Chunk& ch = chunks[(size_t)k];
+            for (size_t e = 0; e < ch.cell.size(); ++e) {
+                const int64_t o = cnt[k][(size_t)(ch.cell[e] - ch.cmin)]++;
+                col[(size_t)o] = ch.gene[e];
+                val[(size_t)o] = ch.val[e];
+            }
+            std::vector<int32_t>().swap(ch.cell);
+            std::vector<int32_t>().swap(ch.gene);
+            std::vector<float>().swap(ch.val);
+        }
+    });
+    // rows must be strictly increasing in gene: stable sort + keep-last dedupe where needed
+    std::vector<int64_t> newlen((size_t)N);
+    std::atomic<bool> compact{false};
+    parallel_for(threads, N, [&](int, int64_t a, int64_t b) {
+        std::vector<std::pair<int32_t, int64_t>> tmp;
+        std::vector<int32_t> cg;
+        std::vector<float> cv;
+        for (int64_t r = a; r < b; ++r) {
+            const int64_t s = rp[(size_t)r], e = rp[(size_t)r + 1];
+            bool ok = true;
+            for (int64_t j = s + 1; j < e && ok; ++j) ok = col[(size_t)j] > col[(size_t)j - 1];
+            newlen[(size_t)r] = e - s;
+            if (ok) continue;
+            tmp.clear();
+            for (int64_t j = s; j < e; ++j) tmp.emplace_back(col[(size_t)j], j);
+            std::stable_sort(tmp.begin(), tmp.end(),
+                             [](const std::pair<int32_t, int64_t>& x, const std::pair<int32_t, int64_t>& y) {
+                                 return x.first < y.first;
+                             });
+            cg.clear();
+            cv.clear();
+            for (size_t i = 0; i < tmp.size(); ++i) {
+                if (i + 1 < tmp.size() && tmp[i + 1].first == tmp[i].first) continue;  // keep the last
+                cg.push_back(tmp[i].first);
+                cv.push_back(val[(size_t)tmp[i].second]);
+            }
+            for (size_t i = 0; i < cg.size(); ++i) {
+                col[(size_t)s + i] = cg[i];
+                val[(size_t)s + i] = cv[i];
+            }
+            if ((int64_t)cg.size() != e - s) compact = true;
+            newlen[(size_t)r] = (int64_t)cg.size();
+        }
+    });
+    out->N = N;
+    out->D = D;
+    out->rowptr = static_cast<int64_t*>(std::malloc(sizeof(int64_t) * ((size_t)N + 1)));
+    int64_t nnz = nnz_all;
+    if (compact) {
+        std::vector<int64_t> np((size_t)N + 1, 0);
+        for (int64_t r = 0; r < N; ++r) np[(size_t)r + 1] = np[(size_t)r] + newlen[(size_t)r];
+        nnz = np[(size_t)N];
+        for (int64_t r = 0; r < N; ++r) {
+            std::memmove(col.data() + np[(size_t)r], col.data() + rp[(size_t)r], sizeof(int32_t) * (size_t)newlen[(size_t)r]);
+            std::memmove(val.data() + np[(size_t)r], val.data() + rp[(size_t)r], sizeof(float) * (size_t)newlen[(size_t)r]);
+        }
+        rp.swap(np);
+    }
+    out->nnz = nnz;
+    out->col = static_cast<int32_t*>(std::malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1)));
+    out->val = static_cast<float*>(std::malloc(sizeof(float) * (size_t)std::max<int64_t>(nnz, 1)));
+    if (!out->rowptr || !out->col || !out->val) {
+        mmvae_csr_free(out);
+        return fail(MMVAE_E_ARG, "out of host memory");
+    }
+    std::memcpy(out->rowptr, rp.data(), sizeof(int64_t) * ((size_t)N + 1));
+    std::memcpy(out->col, col.data(), sizeof(int32_t) * (size_t)nnz);
+    std::memcpy(out->val, val.data(), sizeof(float) * (size_t)nnz);
+    return MMVAE_OK;
+}
+
+int mmvae_mtx_read_dense_t(const char* path, int threads, int64_t* N_out, int64_t* C_out, float** out) {
+    if (!path || !N_out || !C_out || !out) return fail(MMVAE_E_ARG, "mtx_read_dense_t: null argument");
+    int64_t D, N;
+    std::vector<Chunk> chunks;
+    int rc = read_triplets(path, threads, D, N, chunks);
+    if (rc) return rc;
+    float* m = static_cast<float*>(std::calloc((size_t)(N * D), sizeof(float)));
+    if (!m) return fail(MMVAE_E_ARG, "out of host memory");
+    for (auto& ch : chunks)  // file order: later entries overwrite (mmvae_io.hh:120-121)
+        for (size_t e = 0; e < ch.cell.size(); ++e) m[(size_t)ch.cell[e] * (size_t)D + (size_t)ch.gene[e]] = ch.val[e];
+    *N_out = N;
+    *C_out = D;
+    *out = m;
+    return MMVAE_OK;
+}
+
+int mmvae_csr_save(const char* path, const mmvae_csr* c) {
+    if (!path || !c) return fail(MMVAE_E_ARG, "csr_save: null argument");
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot write ") + path);
+    const char magic[8] = {'M', 'M', 'V', 'A', 'E', 'C', 'S', 'R'};
+    bool ok = std::fwrite(magic, 1, 8, fp) == 8 && std::fwrite(&c->N, 8, 1, fp) == 1 &&
+              std::fwrite(&c->D, 8, 1, fp) == 1 && std::fwrite(&c->nnz, 8, 1, fp) == 1 &&
+              std::fwrite(c->rowptr, 8, (size_t)c->N + 1, fp) == (size_t)c->N + 1 &&
+              std::fwrite(c->col, 4, (size_t)c->nnz, fp) == (size_t)c->nnz &&
+              std::fwrite(c->val, 4, (size_t)c->nnz, fp) == (size_t)c->nnz;
+    ok = (std::fclose(fp) == 0) && ok;
+    return ok ? MMVAE_OK : fail(MMVAE_E_ARG, std::string("short write on ") + path);
+}
+
+int mmvae_csr_load(const char* path, mmvae_csr* c) {
+    if (!path || !c) return fail(MMVAE_E_ARG, "csr_load: null argument");
+    std::memset(c, 0, sizeof(*c));
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot open ") + path);
+    char magic[8];
+    bool ok = std::fread(magic, 1, 8, fp) == 8 && std::memcmp(magic, "MMVAECSR", 8) == 0 &&
+              std::fread(&c->N, 8, 1, fp) == 1 && std::fread(&c->D, 8, 1, fp) == 1 && std::fread(&c->nnz, 8, 1, fp) == 1 &&
+              c->N > 0 && c->nnz >= 0;
+    if (ok) {
+        c->rowptr = static_cast<int64_t*>(std::malloc(8 * ((size_t)c->N + 1)));
+        c->col = static_cast<int32_t*>(std::malloc(4 * (size_t)std::max<int64_t>(c->nnz, 1)));
+        c->val = static_cast<float*>(std::malloc(4 * (size_t)std::max<int64_t>(c->nnz, 1)));
+        ok = c->rowptr && c->col && c->val &&
+             std::fread(c->rowptr, 8, (size_t)c->N + 1, fp) == (size_t)c->N + 1 &&
+             std::fread(c->col, 4, (size_t)c->nnz, fp) == (size_t)c->nnz &&
+             std::fread(c->val, 4, (size_t)c->nnz, fp) == (size_t)c->nnz;
+    }
+    std::fclose(fp);
+    if (!ok) {
+        mmvae_csr_free(c);
+        return fail(MMVAE_E_ARG, std::string("not a valid CSR cache: ") + path);
+    }
+    return MMVAE_OK;
+}
+
+int mmvae_mtx_write_ones(const char* path, int64_t N) {
+    if (!path || N < 1) return fail(MMVAE_E_ARG, "mtx_write_ones: bad arguments");
+    BgzfWriter w;
+    if (!w.open(path)) return fail(MMVAE_E_ARG, std::string("cannot write ") + path);
+    // write_matrix_market_stream (io.hh:191-227) of a 1 x N all-ones matrix
+    w.write("%%MatrixMarket matrix coordinate integer general\n");
+    w.write("1 " + std::to_string(N) + " " + std::to_string(N) + "\n");
+    std::string line;
+    for (int64_t j = 1; j <= N; ++j) {
+        line = "1 " + std::to_string(j) + " 1\n";
+        w.write(line);
+    }
+    return w.close() ? MMVAE_OK : fail(MMVAE_E_ARG, std::string("write failed: ") + path);
+}
+
+}  // extern "C"

@@ -60,6 +60,9 @@ def lib():
         "mmvae_last_error": (ctypes.c_char_p, [h]),
         "mmvae_upload_csr": (ctypes.c_int, [h, i64p, ctypes.POINTER(ctypes.c_int32), f32p, i64, i64, f32p]),
         "mmvae_synth_csr": (ctypes.c_int, [h, i64, ctypes.c_double, ctypes.c_uint64, i64p]),
+        "mmvae_dataset_size": (ctypes.c_int, [h, i64p, i64p]),
+        "mmvae_param_shape": (ctypes.c_int, [h, i32, ctypes.POINTER(i32), i64p]),
+        "mmvae_comm_allreduce": (ctypes.c_int, [h, f32p, i64]),
         "mmvae_get_rows": (ctypes.c_int, [h, i64p, i64, i64p, ctypes.POINTER(ctypes.c_int32), f32p, i64p]),
         "mmvae_num_params": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
         "mmvae_param_info": (ctypes.c_int, [h, i32, ctypes.POINTER(ctypes.c_char_p), i64p, ctypes.POINTER(i32)]),

@@ -1,0 +1,162 @@
+"""CPU tests of the host runtime (libmmvae_host.so): the MatrixMarket loader against a numpy
+parse of the same files (plain text, gzip, BGZF; shuffled entries, '%' lines in the body,
+short lines, duplicates where the last entry wins as in mmvae_io.hh:115-123), the CSR cache,
+the covariate reader, the all-ones covariate writer, the bootstrap index generator, every
+symbol of include/mmvae_host.h, and the CLIs' argument handling (no GPU needed)."""
+import ctypes
+import gzip
+import os
+import re
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import mmvae_amd
+from mmvae_amd import host
+from oracle import synth
+
+
+def bgzf_compress(data: bytes) -> bytes:
+    """Independent BGZF writer (SAM spec 4.1) for the loader tests."""
+    out = bytearray()
+    for i in range(0, max(len(data), 1), 65280):
+        blk = data[i:i + 65280]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cdata = c.compress(blk) + c.flush()
+        bsize = 18 + len(cdata) + 8 - 1
+        out += struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize)
+        out += cdata + struct.pack("<II", zlib.crc32(blk) & 0xffffffff, len(blk))
+    out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    return bytes(out)
+
+
+def mtx_text(rowptr, col, val, D, order=None, extra=()):
+    N = rowptr.size - 1
+    cells = np.repeat(np.arange(N), np.diff(rowptr))
+    trip = list(zip(col + 1, cells + 1, val))
+    if order is not None:
+        trip = [trip[i] for i in order]
+    lines = ["%%MatrixMarket matrix coordinate integer general", "% a comment",
+             f"{D} {N} {len(trip)}"]
+    for k, (g, c, v) in enumerate(trip):
+        lines.append(f"{g} {c} {v:g}")
+        if k == len(trip) // 2:
+            lines.extend(extra)
+    return ("\n".join(lines) + "\n").encode()
+
+
+@pytest.fixture(scope="module")
+def data():
+    rp, col, val = synth.synth_csr(300, 500, lib_size=300.0, seed=7)
+    return rp, col, val, 500
+
+
+def check(path, rp, col, val, D):
+    r2, c2, v2, D2 = host.mtx_read(path, threads=4)
+    assert D2 == D
+    np.testing.assert_array_equal(r2, rp)
+    np.testing.assert_array_equal(c2, col)
+    np.testing.assert_array_equal(v2, val.astype(np.float32))
+
+
+@pytest.mark.parametrize("fmt", ["plain", "gzip", "bgzf"])
+def test_mtx_read_formats(tmp_path, data, fmt):
+    rp, col, val, D = data
+    t = mtx_text(rp, col, val, D)
+    p = tmp_path / f"x.mtx{'' if fmt == 'plain' else '.gz'}"
+    p.write_bytes(t if fmt == "plain" else gzip.compress(t) if fmt == "gzip" else bgzf_compress(t))
+    check(str(p), rp, col, val, D)
+
+
+def test_mtx_read_shuffled_comments_short_lines(tmp_path, data):
+    rp, col, val, D = data
+    order = np.random.default_rng(0).permutation(rp[-1])
+    t = mtx_text(rp, col, val, D, order=order, extra=["% mid comment", "7 9", ""])
+    p = tmp_path / "s.mtx.gz"
+    p.write_bytes(bgzf_compress(t))
+    check(str(p), rp, col, val, D)
+
+
+def test_mtx_read_duplicates_last_wins(tmp_path):
+    t = b"%%MatrixMarket matrix coordinate real general\n4 3 6\n2 1 1.5\n1 1 2\n2 1 7.25\n4 3 1e2\n3 3 -1\n4 3 3\n"
+    p = tmp_path / "d.mtx"
+    p.write_bytes(t)
+    rp, col, val, D = host.mtx_read(str(p))
+    assert D == 4
+    np.testing.assert_array_equal(rp, [0, 2, 2, 4])
+    np.testing.assert_array_equal(col, [0, 1, 2, 3])
+    np.testing.assert_array_equal(val, np.float32([2, 7.25, -1, 3]))
+
+
+def test_mtx_read_errors(tmp_path):
+    p = tmp_path / "bad.mtx"
+    p.write_bytes(b"%%MatrixMarket matrix coordinate real general\n3 2 1\n4 1 1\n")
+    with pytest.raises(mmvae_amd.MMVAEError, match="outside"):
+        host.mtx_read(str(p))
+    with pytest.raises(mmvae_amd.MMVAEError):
+        host.mtx_read(str(tmp_path / "missing.mtx"))
+
+
+def test_csr_cache_roundtrip(tmp_path, data):
+    rp, col, val, D = data
+    host.csr_save(str(tmp_path / "c.bin"), rp, col, val, D)
+    r2, c2, v2, D2 = host.csr_load(str(tmp_path / "c.bin"))
+    assert D2 == D
+    np.testing.assert_array_equal(r2, rp)
+    np.testing.assert_array_equal(c2, col)
+    np.testing.assert_array_equal(v2, val)
+
+
+def test_covariate_reader_and_ones_writer(tmp_path):
+    rng = np.random.default_rng(3)
+    C, N = 3, 17
+    m = rng.integers(0, 3, (C, N)).astype(np.float32)
+    lines = ["%%MatrixMarket matrix coordinate real general", f"{C} {N} {int((m != 0).sum())}"]
+    lines += [f"{i + 1} {j + 1} {m[i, j]:g}" for j in range(N) for i in range(C) if m[i, j] != 0]
+    p = tmp_path / "cov.mtx"
+    p.write_text("\n".join(lines) + "\n")
+    np.testing.assert_array_equal(host.mtx_read_dense_t(str(p)), m.T)
+    q = tmp_path / "ones.mtx.gz"
+    host.mtx_write_ones(str(q), N)
+    raw = q.read_bytes()
+    assert raw[:4] == b"\x1f\x8b\x08\x04" and raw[12:14] == b"BC"        # BGZF, io.hh:230-242
+    txt = gzip.decompress(raw).decode().splitlines()
+    assert txt[0] == "%%MatrixMarket matrix coordinate integer general" and txt[1] == f"1 {N} {N}"
+    np.testing.assert_array_equal(host.mtx_read_dense_t(str(q)), np.ones((N, 1), np.float32))
+
+
+def test_ridx_deterministic_uniform():
+    a = host.ridx(5, 2, 3, 1, 4096)
+    b = host.ridx(5, 2, 3, 1, 4096)
+    c = host.ridx(5, 2, 3, 2, 4096)
+    np.testing.assert_array_equal(a, b)
+    assert (a != c).mean() > 0.99
+    assert a.min() >= 0 and a.max() < 4096
+    h = np.bincount(host.ridx(1, 0, 0, 0, 64 * 400) % 64, minlength=64)
+    assert h.min() > 300 and h.max() < 500
+
+
+def test_host_library_exports_every_declared_symbol():
+    src = re.sub(r"/\*.*?\*/", "", open(host.HOST_HEADER_PATH).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(mmvae_[a-z0-9_]+)\s*\(", src)))
+    L = ctypes.CDLL(host.HOST_LIB_PATH)
+    assert len(names) >= 11
+    assert not [n for n in names if not hasattr(L, n)]
+
+
+@pytest.mark.parametrize("exe", ["nb_vae_main", "vmf_vae_main"])
+def test_cli_arguments_without_gpu(tmp_path, exe):
+    b = os.path.join(host.BIN_DIR, exe)
+    r = subprocess.run([b, "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "--mtx" in r.stderr
+    r = subprocess.run([b, "--mtx", str(tmp_path / "nope.mtx"), "--out", str(tmp_path / "o")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "missing mtx" in r.stderr
+    p = tmp_path / "x.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate integer general\n3 2 2\n1 1 4\n3 2 1\n")
+    r = subprocess.run([b, "--mtx", str(p), "--out", str(tmp_path / "o"), "--mean_encoding" if exe == "nb_vae_main"
+                        else "--encoding", "10"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "hidden" in r.stderr
