@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -225,6 +226,16 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split((int)(2 + e->H));
+    // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
+    auto env_split = [&](const char* name, int& v) {
+        if (const char* ev = std::getenv(name)) {
+            const int x = std::atoi(ev);
+            if (x >= 1) v = (int)std::min<int64_t>(x, e->NT);
+        }
+    };
+    env_split("MMVAE_NSPLIT_E", e->nsplit_e);
+    env_split("MMVAE_NSPLIT_D", e->nsplit_d);
+    env_split("MMVAE_NSPLIT_A", e->nsplit_a);
     e->n_lat_wg = (int)(e->Bpad / 64);  // latent kernels: 64 cells per workgroup
     e->klp_off = e->nrb_max * e->nsplit_d;
 
@@ -675,6 +686,16 @@ int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms
     if (name) *name = e->timers[idx].name.c_str();
     if (total_ms) *total_ms = e->timers[idx].total_ms;
     if (launches) *launches = e->timers[idx].launches;
+    return MMVAE_OK;
+}
+
+int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
+    if (!e || !host || n < 0 || which != 0) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
+    const int64_t cap = (int64_t)e->nsplit_e * e->Bpad * e->KP;
+    if (n > cap) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds the workspace");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(host, e->d_hpart, sizeof(float) * n, hipMemcpyDeviceToHost));
     return MMVAE_OK;
 }
 

@@ -64,6 +64,14 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 MMVAE_DEV void glds16(const void* g, void* lds_wave_base) {
     __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
+// diagnostic in-kernel stamp (shader clock); only in MMVAE_DBG-gated diagnostic paths
+MMVAE_DEV uint64_t stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
 MMVAE_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Workgroup barrier that completes this wave's LDS traffic but leaves global loads in flight
 // (a __syncthreads() would drain vmcnt(0), exposing the latency of prefetches issued before it).

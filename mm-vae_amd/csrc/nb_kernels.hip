@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
     int32_t* rtl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
     int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
-    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16;
+    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16 * RING;
 
     for (int i = lane; i < 16 * S; i += 64) {
         const int rr = i / S, tt = i % S;
@@ -246,27 +246,43 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
     (void)NCH;
-    auto scatter = [&](const TileEntries& te, T* dst, int tl, int t) {
-        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val,
-                   [&](int r, int gl, float x) { dst[r * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
+    const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
+    auto scatter = [&](const RowEntries<6>& re, T* dst, int t) {
+        re.visit(t, sub, col, val, [&](int gl, float x) { dst[rl * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
     };
 
     f32x4 acc[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) acc[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    TileEntries pend;
+    const int32_t* rtr = rtl + rl * S;
+    const int64_t rbase = rbl[rl];
+    const int nt = t1 - t0;
+    // entry ring: q[0] = next tile to scatter; loads issued EDEPTH tiles ahead of their use
+    constexpr int EDEPTH = 2;
+    RowEntries<6> q[EDEPTH];
     if (t0 < t1) {
         wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
         wreg.store(wst);
-        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, col, val);
-        scatter(pend, xt, 0, t0);
-        if (t0 + 1 < t1) tile_fetch(pend, rtl, S, 1, t0 + 1, lane, rinc, rbl, col, val);
+        q[0].fetch(rtr, 0, rbase, sub, col, val);
+        scatter(q[0], xt, t0);
+#pragma unroll
+        for (int i = 0; i < EDEPTH; ++i) q[i].fetch(rtr, min(1 + i, nt - 1), rbase, sub, col, val);
     }
     vm_wait_all();
     __syncthreads();
+    const bool stamps = (d.dbg & 32) != 0;
+    uint64_t sa = 0, sb = 0, sc = 0, sd = 0, tp = stamps ? stamp_now() : 0;
+    auto lap = [&](uint64_t& acc_) {
+        if (stamps) {
+            const uint64_t tn = stamp_now();
+            acc_ += tn - tp;
+            tp = tn;
+        }
+    };
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0, buf = tl & 1;
-        if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
+        // unconditional (clamped) prefetch of the next weight tile: see RowEntries::fetch
+        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
         const T* xb = xt + buf * 16 * XS;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
@@ -278,15 +294,34 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
                 acc[lb] = M::mma(a, bw, acc[lb]);
             }
         }
+        lap(sa);
+        T* xn = xt + (buf ^ 1) * 16 * XS;
         if (t + 1 < t1) {
-            T* xn = xt + (buf ^ 1) * 16 * XS;
             for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xn)[i] = uint4{0, 0, 0, 0};
-            scatter(pend, xn, tl + 1, t + 1);
-            wreg.store(wst + (buf ^ 1) * STB);
+            wave_sync();
+            scatter(q[0], xn, t + 1);
         }
-        // the entry prefetch below stays in flight across the barrier
-        if (t + 2 < t1) tile_fetch(pend, rtl, S, tl + 2, t + 2, lane, rinc, rbl, col, val);
+        lap(sb);
+        // rotate the ring; the new tail's entry loads stay in flight across the barriers
+#pragma unroll
+        for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
+        q[EDEPTH - 1].fetch(rtr, min(tl + 1 + EDEPTH, nt - 1), rbase, sub, col, val);
+        if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB);
+        lap(sc);
         lds_barrier();
+        lap(sd);
+    }
+    if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
+        vm_wait_all();
+        __syncthreads();
+        if (lane == 0) {
+            float* o = hpart + ((int64_t)blockIdx.x * 4 + w) * 4;
+            o[0] = (float)sa;
+            o[1] = (float)sb;
+            o[2] = (float)sc;
+            o[3] = (float)sd;
+        }
+        return;
     }
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb)
@@ -521,7 +556,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
         const int buf = (t - t0) & 1;
-        if (t + 1 < t1) stage(t + 1, buf ^ 1);
+        stage(min(t + 1, t1 - 1), buf ^ 1);  // unconditional: the last one re-stages a tile nobody reads
         const char* sb = stg + buf * STB;
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
@@ -783,7 +818,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
-        if (t + 1 < t1) stage_load(t + 1);
+        stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
         // ---- 1. logits -> p ----
         float pv[4][4];
 #pragma unroll
@@ -809,7 +844,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         }
         wave_sync();
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
-        tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val, [&](int r, int gl, float x) {
+        if (!(d.dbg & 1)) tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
             const float p = q2[r * PS + gl];
             const float mu = fmaf(p, rs_[0], 1e-4f);
@@ -837,10 +872,10 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         });
         wave_sync();
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
-        if (t + 1 < t1) tile_fetch(pend, rtl, S, tl + 1, t + 1, lane, rinc, rbl, Q.col, Q.val);
+        tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
         // ---- 3. dense epilogue in the owner lanes ----
 #pragma unroll 1
-        for (int gb = 0; gb < 4; ++gb) {
+        for (int gb = 0; gb < ((d.dbg & 2) ? 0 : 4); ++gb) {
             const int gl = 16 * gb + (lane & 15);
             const int gene = 64 * t + gl;
             const bool gv = gene < d.D;
@@ -918,7 +953,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
 #pragma unroll
-        for (int s = 0; s < GK; ++s) {
+        for (int s = 0; s < ((d.dbg & 4) ? 0 : GK); ++s) {
             const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
             const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
@@ -1230,7 +1265,7 @@ struct EncBwdLds {
         o_part = o_raw + 64 * 68 * 4;
         o_scal = o_part + 4 * 64 * 4;
         o_wave = o_scal + nsc * 64 * 4;
-        wave_bytes = ((16 * S * 4 + 15) / 16) * 16 + 16 * 8 + 64;
+        wave_bytes = ((16 * S * 4 + 15) / 16) * 16 + 16 * 8 + 64 * RING;
         bytes = o_wave + 4 * wave_bytes;
     }
 };
@@ -1290,10 +1325,11 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
 #pragma unroll
             for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
     };
-    auto scatter = [&](const TileEntries& te, int tl, int t) {
-        tile_visit(te, rtl, S, tl, t, lane, rinc, rbl, col, val, [&](int r, int gl, float x) {
-            lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
-            if (RAW) raw[gl * 68 + 16 * w + r] = x;
+    const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
+    auto scatter = [&](const RowEntries<6>& re, int t) {
+        re.visit(t, sub, col, val, [&](int gl, float x) {
+            lt[gl * LS + 16 * w + rl] = to_t<T>(log1p_cnt<T>(x));
+            if (RAW) raw[gl * 68 + 16 * w + rl] = x;
         });
     };
     // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
@@ -1308,19 +1344,24 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
 
-    TileEntries pend;
+    wave_sync();  // rtl / rbl written above by this wave
+    const int32_t* rtr = rtl + rl * S;
+    const int64_t rbase = rbl[rl];
+    const int nt = t1 - t0;
+    RowEntries<6> nxt;
     if (t0 < t1) {
         wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
         wreg.store(wst);
         zero_cols();
-        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, col, val);
-        scatter(pend, 0, t0);
-        if (t0 + 1 < t1) tile_fetch(pend, rtl, S, 1, t0 + 1, lane, rinc, rbl, col, val);
+        nxt.fetch(rtr, 0, rbase, sub, col, val);
+        wave_sync();
+        scatter(nxt, t0);
+        nxt.fetch(rtr, min(1, nt - 1), rbase, sub, col, val);
     }
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
-        if (t + 1 < t1) wreg.load(wsrc(t + 1), (int64_t)d.DP * sizeof(T));
+        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
         // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
         if (RAW) {
             const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
@@ -1371,10 +1412,11 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         }
         if (t + 1 < t1) {
             zero_cols();
-            scatter(pend, tl + 1, t + 1);
+            wave_sync();
+            scatter(nxt, t + 1);
             wreg.store(wst);
         }
-        if (t + 2 < t1) tile_fetch(pend, rtl, S, tl + 2, t + 2, lane, rinc, rbl, col, val);
+        nxt.fetch(rtr, min(tl + 2, nt - 1), rbase, sub, col, val);
         lds_barrier();
     }
 }

@@ -86,22 +86,81 @@ struct TileEntries {
 MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane, int32_t* rinc,
                           const int64_t* rbl, const int32_t* __restrict__ col, const float* __restrict__ val) {
     te.total = tile_rows(rtl, S, tl, lane, rinc);
+    // branch-free: every lane issues both loads (slots past the tile read entry 0 and are
+    // masked by row = -1), so hipcc keeps counted vmcnt waits (RowEntries::fetch)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int e = lane + 64 * k;
-        te.row[k] = -1;
-        te.gl[k] = 0;
-        te.x[k] = 0.f;
-        if (e < te.total) {
-            int within;
-            const int r = tile_entry_row(rinc, e, within);
-            const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-            te.row[k] = r;
-            te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
-            te.x[k] = val[gi];
-        }
+        const bool ok = e < te.total;
+        int within;
+        const int r = min(tile_entry_row(rinc, ok ? e : 0, within), 15);
+        const int64_t gi = ok ? rbl[r] + rtl[r * S + tl] + within : 0;
+        te.row[k] = ok ? r : -1;
+        te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
+        te.x[k] = val[gi];
     }
 }
+
+// Prefetch ring of the CSR entries of the next R tiles of a wave (e[0] = next tile to visit):
+// the entry loads of a tile are issued R tiles before it is consumed, so a tile iteration no
+// longer waits out a full memory latency.  Tile tl keeps its row prefix counts in LDS slot
+// tl % R (rinc + 16 * slot), reused only after that tile has been visited.
+static constexpr int RING = 4;
+template <int R>
+struct EntryRing {
+    TileEntries e[R];
+    int slot[R];
+    MMVAE_DEV void fetch(int i, int tl, const int32_t* rtl, int S, int t0, int lane, int32_t* rinc, const int64_t* rbl,
+                         const int32_t* __restrict__ col, const float* __restrict__ val) {
+        slot[i] = tl % R;
+        tile_fetch(e[i], rtl, S, tl, t0 + tl, lane, rinc + 16 * slot[i], rbl, col, val);
+    }
+    MMVAE_DEV void shift() {
+#pragma unroll
+        for (int i = 0; i + 1 < R; ++i) {
+            e[i] = e[i + 1];
+            slot[i] = slot[i + 1];
+        }
+    }
+};
+
+// Row-per-lane form of a tile's CSR entries: lane l serves row r = l & 15 of the wave's 16 and
+// takes entries sub, sub + 4, sub + 8 (sub = l >> 4) of that row's segment in the tile;
+// entries past the NS slots are fetched on the spot.  No prefix scan, no LDS round trips
+// beyond the two tile pointers, no wave synchronisation: per tile the lane issues at most
+// 2 NS independent loads.  rbase = the row's CSR start (from rbl), rtr = the row's tile
+// pointers rtl + r * S.
+template <int NS>
+struct RowEntries {
+    int n;
+    int64_t base;
+    int gl[NS];
+    float x[NS];
+    // Loads are unconditional (an out-of-segment slot reads entry 0, always valid, and is
+    // masked afterwards): a load behind a branch makes hipcc wait vmcnt(0) at its first use,
+    // which would serialise the prefetch (cdna_hip_programming.md §5, trap (c)).
+    MMVAE_DEV void fetch(const int32_t* rtr, int tl, int64_t rbase, int sub, const int32_t* __restrict__ col,
+                         const float* __restrict__ val) {
+        const int s = rtr[tl];
+        n = rtr[tl + 1] - s;
+        base = rbase + s;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int idx = sub + 4 * k;
+            const int64_t gi = (idx < n) ? base + idx : 0;
+            gl[k] = col[gi];
+            x[k] = val[gi];
+        }
+    }
+    // f(gene-in-tile, x) for every entry of this lane
+    template <class F>
+    MMVAE_DEV void visit(int t, int sub, const int32_t* __restrict__ col, const float* __restrict__ val, F&& f) const {
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if (sub + 4 * k < n) f(gl[k] - 64 * t, x[k]);  // masked slots hold entry 0: skipped
+        for (int idx = sub + 4 * NS; idx < n; idx += 4) f(col[base + idx] - 64 * t, val[base + idx]);
+    }
+};
 
 // visit every entry of the fetched tile: f(row, gene-in-tile, x)
 template <class F>
@@ -131,7 +190,7 @@ struct EncLds {
         o_rtl = o_x + 4 * xbytes_per_wave;
         o_rbl = o_rtl + ((4 * 16 * S * 4 + 15) / 16) * 16;
         o_rinc = o_rbl + 4 * 16 * 8;
-        o_rsc = o_rinc + 4 * 16 * 4;
+        o_rsc = o_rinc + 4 * 16 * RING * 4;
         bytes = o_rsc + 4 * 16 * (1 + HMAX) * 4;
     }
 };

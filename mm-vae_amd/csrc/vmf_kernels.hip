@@ -482,14 +482,14 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
-        if (t + 1 < t1) stage_load(t + 1);
+        stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
         // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
         for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
         wave_sync();
         tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val,
                    [&](int r, int gl, float x) { lt[r * LS + gl] = log1pf(fmaxf(x, 0.f)); });
         wave_sync();
-        if (t + 1 < t1) tile_fetch(pend, rtl, S, tl + 1, t + 1, lane, rinc, rbl, Q.col, Q.val);
+        tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);

@@ -80,6 +80,7 @@ def lib():
         "mmvae_timing_count": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
         "mmvae_timing_get": (ctypes.c_int, [h, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double), i64p]),
         "mmvae_timing_reset": (ctypes.c_int, [h]),
+        "mmvae_debug_copy": (ctypes.c_int, [h, i32, f32p, i64]),
         "mmvae_lbessel": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_lbessel_grad": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_fasterlog": (ctypes.c_float, [ctypes.c_float]),

@@ -1,0 +1,21 @@
+"""Diagnostic: per-phase cycle shares of k_enc_fwd's tile loop (MMVAE_DBG=32 stamp build)."""
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "mm-vae_amd", "py"))
+os.environ["MMVAE_DBG"] = "32"
+import mmvae_amd
+B, D, K = 4096, 20000, 64
+eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
+eng.synth_csr(100000, lib_size=2000.0, seed=3)
+eng.init_params(seed=7)
+for i in range(3):
+    eng.eval_loss(np.arange(B), 1.0, step_id=i)
+nwg = (B // 64) * eng_ns if (eng_ns := int(os.environ.get("NSE", "8"))) else 0
+buf = np.zeros(nwg * 16, np.float32)
+rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 0, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
+assert rc == 0
+st = buf.reshape(-1, 4)
+tot = st.sum(1)
+print("waves", st.shape[0], "mean cycles per wave: MFMA+wait %.0f  zero+scatter %.0f  fetch+stage %.0f  barrier %.0f  total %.0f"
+      % tuple(list(st.mean(0)) + [tot.mean()]))
+print("per tile (40 tiles):", (st.mean(0) / 40).round(0))
