@@ -11,6 +11,7 @@
 
 #include "common.hpp"
 #include "engine.hpp"
+#include "tiles.hpp"
 
 using namespace mmvae;
 
@@ -236,7 +237,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     env_split("MMVAE_NSPLIT_E", e->nsplit_e);
     env_split("MMVAE_NSPLIT_D", e->nsplit_d);
     env_split("MMVAE_NSPLIT_A", e->nsplit_a);
-    e->n_lat_wg = (int)(e->Bpad / 64);  // latent kernels: 64 cells per workgroup
+    e->n_lat_wg = (int)(e->Bpad / LAT_CELLS);  // latent kernels: 16 cells per workgroup
     e->klp_off = e->nrb_max * e->nsplit_d;
 
     // latent state layout
@@ -281,8 +282,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
     HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
     HIPCHK(e, dalloc(&e->d_mvec, KP));
-    HIPCHK(e, dalloc(&e->d_rtp, Bp * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
+    HIPCHK(e, dalloc(&e->d_rowxp, (int64_t)e->nsplit_e * Bp * (1 + e->H)));
     HIPCHK(e, dalloc(&e->d_hpart, (int64_t)e->nsplit_e * Bp * KP));
     HIPCHK(e, dalloc(&e->d_lat, Bp * e->lat_stride));
     HIPCHK(e, dalloc(&e->d_zf, Bp * KP));
@@ -319,7 +320,7 @@ int mmvae_destroy(mmvae_h e) {
     if (e->comm) ncclCommDestroy(e->comm);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
-                    e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_rowx, e->d_hpart, e->d_lat,
+                    e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
                     e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar};
@@ -380,6 +381,7 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     }
     e->N = N;
     e->nnz = nnz;
+    HIPCHK(e, build_dataset_index(e));
     return MMVAE_OK;
 }
 

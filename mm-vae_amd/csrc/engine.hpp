@@ -74,8 +74,10 @@ struct Engine {
     float* h_eps_pin = nullptr;
     float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]
     float* d_mvec = nullptr;         // [KP]
-    int32_t* d_rtp = nullptr;        // [Bpad][NT+1] row tile pointers (relative to row start)
+    int32_t* d_rtp = nullptr;        // [N+1][NT+1] per-cell tile pointers (dataset index; row N = empty)
+    float* d_cellnorm = nullptr;     // [N+1] float2: vMF row norms of log1p(x) (dataset index)
     float* d_rowx = nullptr;         // [Bpad][2+H]  pre_depth, lnorm2, hnu[H]
+    float* d_rowxp = nullptr;        // [nsE][Bpad][1+H]  gene-split partials of depth(x), nu_enc(x)
     float* d_hpart = nullptr;        // [nsplitE][Bpad][KP]
     float* d_lat = nullptr;          // latent state, see LAT_* offsets
     float* d_zf = nullptr;           // [Bpad][KP]
@@ -169,6 +171,7 @@ hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const 
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
+hipError_t build_dataset_index(Engine* e);
 
 }  // namespace mmvae
 

@@ -12,8 +12,8 @@
 //
 // Kernel chain per step (one stream):
 //   k_prep        per-gene constants (softplus(ln_x_sd), bias sums), encoder mean term
-//   k_rowscan     one wave per cell row: tile pointers + raw-x sparse dots (depth, nu_enc)
-//   k_enc_fwd     densify log1p(x)/sd tiles in LDS -> MFMA with the frozen encoder
+//   k_enc_fwd     densify log1p(x)/sd tiles in LDS -> MFMA with the frozen encoder; the same
+//                 entry walk accumulates the raw-x dots of depth / nu_enc per gene split
 //   k_latent_fwd  K x K heads, clamp, reparameterise (Philox or injected eps), KL
 //   k_dec<A>      logit GEMM (MFMA) + online max/sum-exp per cell        (pass A)
 //   k_dec<B>      logit GEMM + softmax + NB likelihood + every gradient term that needs only
@@ -102,100 +102,6 @@ __global__ __launch_bounds__(1024) void k_mvec(NBPtrs P, Dims d, const float* __
 }
 
 // =======================================================================================
-// k_rowscan — one wave per batch row.  Streams the row's CSR once (coalesced, 4 chunks of
-// 64 entries in flight per lane):
-//   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
-//   pre_b = depth(x_b) (nb.hh:498, Linear D->1 on raw x), hnu_b = nu_enc(x_b) (nb.hh:448)
-// H1: the default overdispersion encoding width H = 1 (nb.hh:60).
-// =======================================================================================
-template <bool H1>
-__global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cells,
-                                                 const int64_t* __restrict__ rowptr,
-                                                 const int32_t* __restrict__ col,
-                                                 const float* __restrict__ val, NBPtrs P, Dims d,
-                                                 int32_t* __restrict__ rtp, float* __restrict__ rowx) {
-    const int lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= d.Bpad) return;
-    const int64_t cell = (b < d.B) ? cells[b] : -1;
-    int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
-    float* rx = rowx + (int64_t)b * d.rowx_stride;
-    constexpr int HN = H1 ? 1 : HMAX;
-    float pre = 0.f, hn[HN];
-#pragma unroll
-    for (int h = 0; h < HN; ++h) hn[h] = 0.f;
-    int n = 0;
-    int64_t s = 0;
-    if (cell >= 0) {
-        s = rowptr[cell];
-        n = (int)(rowptr[cell + 1] - s);
-    }
-    const int32_t* cr = col + s;
-    const float* vr = val + s;
-    const float* wdp = P.wdp;
-    const float* wne = P.Wne;
-    const int H = H1 ? 1 : d.H;
-    // chunk j0 = 256 entries (4 per lane); the next chunk's loads are issued after this
-    // chunk's table gathers, so waiting for the gathers leaves the prefetch in flight
-    int g[4], gp[4];
-    float x[4];
-    auto load_chunk = [&](int j0) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + 64 * u + lane;
-            const bool ok = j < n;
-            g[u] = ok ? cr[j] : 0;
-            x[u] = ok ? vr[j] : 0.f;
-            gp[u] = (ok && j > 0) ? cr[j - 1] : -64;
-        }
-    };
-    if (n > 0) load_chunk(0);
-    for (int j0 = 0; j0 < n; j0 += 256) {
-        int gc[4], gpc[4];
-        float xc[4], wa[4], wb[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            gc[u] = g[u];
-            gpc[u] = gp[u];
-            xc[u] = x[u];
-            wa[u] = wdp[gc[u]];
-            wb[u] = H1 ? wne[gc[u]] : 0.f;
-        }
-        if (j0 + 256 < n) load_chunk(j0 + 256);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            pre = fmaf(xc[u], wa[u], pre);   // x = 0 on padding lanes
-            if (H1) {
-                hn[0] = fmaf(xc[u], wb[u], hn[0]);
-            } else {
-                for (int h = 0; h < H; ++h)
-                    hn[h < HN ? h : 0] = fmaf(xc[u], wne[(int64_t)h * d.D + gc[u]], hn[h < HN ? h : 0]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + 64 * u + lane;
-            if (j < n)
-                for (int tt = (gpc[u] >> 6) + 1; tt <= (gc[u] >> 6); ++tt) rt[tt] = j;
-        }
-    }
-    const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
-    for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
-    pre = wave_sum(pre);
-    if (H1) {
-        hn[0] = wave_sum(hn[0]);
-    } else {
-        for (int h = 0; h < H; ++h) hn[h < HN ? h : 0] = wave_sum(hn[h < HN ? h : 0]);
-    }
-    if (lane == 0) {
-        rx[0] = pre + P.bdp[0];
-        rx[1] = 0.f;
-        for (int h = 0; h < H; ++h) rx[2 + h] = hn[h < HN ? h : 0] + P.bne[h];
-    }
-}
-
-
-// =======================================================================================
 // k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = log1p(x) (W/sd)^T - mvec, so only
 // the nonzeros are densified.  Workgroup = 64 cells x one gene split; per 64-gene tile the
 // frozen weight tile (pre-scaled by 1/sd in k_prep, [KP][DP]) is staged ONCE per workgroup
@@ -203,14 +109,18 @@ __global__ __launch_bounds__(256) void k_rowscan(const int64_t* __restrict__ cel
 // log1p(x) for the NEXT tile into a wave-private 16x64 LDS tile (entries prefetched two
 // tiles ahead).  Partial h per gene split -> hpart.
 // =======================================================================================
-template <class T, int KP>
+// DOTS (NB): the same scatter also accumulates the raw-count dots of the depth and nu encoders
+// (nb.hh:448, 498) per gene split -> rowxp [nsE][Bpad][1+H]; their 64-gene weight slices are
+// staged per tile in a 3-slot LDS ring (written two tiles ahead).  DOTS = 0 (vMF): none.
+template <class T, int KP, int DOTS>
 __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cells,
                                                  const int64_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col,
                                                  const float* __restrict__ val,
                                                  const int32_t* __restrict__ rtp,
                                                  const T* __restrict__ WeS, Dims d,
-                                                 float* __restrict__ hpart) {
+                                                 float* __restrict__ hpart, const float* __restrict__ wdp,
+                                                 const float* __restrict__ Wne, float* __restrict__ rowxp) {
     using M = MM<T>;
     using Fr = typename M::frag;
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;   // x tile row stride (elements): conflict-free
@@ -231,10 +141,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
     int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16 * RING;
 
-    for (int i = lane; i < 16 * S; i += 64) {
-        const int rr = i / S, tt = i % S;
-        rtl[i] = (t0 + tt <= d.NT) ? rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
-    }
+    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = (b < d.B) ? cells[b] : -1;
@@ -247,8 +154,37 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
     (void)NCH;
     const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
+    constexpr int NGV = DOTS == 0 ? 1 : (DOTS == 1 ? 2 : 1 + HMAX);
+    float* gvs = reinterpret_cast<float*>(smem + L.bytes);  // [3][NGV][64] depth / nu_enc slices
+    const int nqv = DOTS == 0 ? 0 : (DOTS == 1 ? 2 : 1 + d.H);
+    const int gq = DOTS ? min((int)threadIdx.x >> 4, nqv - 1) : 0, ge0 = 4 * (threadIdx.x & 15);
+    const float* gsrc = DOTS ? ((gq == 0) ? wdp : Wne + (int64_t)(gq - 1) * d.D) : nullptr;
+    float gvr[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gv_load = [&](int t) {
+        if (DOTS)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) gvr[u] = gsrc[min(64 * t + ge0 + u, d.D - 1)];
+    };
+    auto gv_store = [&](int t) {
+        if (DOTS && (int)threadIdx.x < 16 * nqv)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) gvs[((t % 3) * NGV + gq) * 64 + ge0 + u] = gvr[u];
+    };
+    constexpr int HD = DOTS == 2 ? HMAX : 1;
+    float dpre = 0.f, dhn[HD];
+#pragma unroll
+    for (int h = 0; h < HD; ++h) dhn[h] = 0.f;
     auto scatter = [&](const RowEntries<6>& re, T* dst, int t) {
-        re.visit(t, sub, col, val, [&](int gl, float x) { dst[rl * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
+        const float* gv = gvs + (t % 3) * NGV * 64;
+        re.visit(t, sub, col, val, [&](int gl, float x) {
+            dst[rl * XS + gl] = to_t<T>(log1p_cnt<T>(x));
+            if (DOTS) {
+                dpre = fmaf(x, gv[gl], dpre);
+#pragma unroll
+                for (int h = 0; h < HD; ++h)
+                    if (DOTS == 1 || h < d.H) dhn[h] = fmaf(x, gv[(1 + h) * 64 + gl], dhn[h]);
+            }
+        });
     };
 
     f32x4 acc[KP / 16];
@@ -261,6 +197,11 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     constexpr int EDEPTH = 2;
     RowEntries<6> q[EDEPTH];
     if (t0 < t1) {
+        gv_load(t0);
+        gv_store(t0);
+        gv_load(min(t0 + 1, t1 - 1));
+        gv_store(min(t0 + 1, t1 - 1));
+        __syncthreads();
         wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
         wreg.store(wst);
         q[0].fetch(rtr, 0, rbase, sub, col, val);
@@ -283,6 +224,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
         const int tl = t - t0, buf = tl & 1;
         // unconditional (clamped) prefetch of the next weight tile: see RowEntries::fetch
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
+        gv_load(min(t + 2, t1 - 1));
         const T* xb = xt + buf * 16 * XS;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
@@ -307,9 +249,26 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
         for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
         q[EDEPTH - 1].fetch(rtr, min(tl + 1 + EDEPTH, nt - 1), rbase, sub, col, val);
         if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB);
+        if (t + 2 < t1) gv_store(t + 2);
         lap(sc);
         lds_barrier();
         lap(sd);
+    }
+    if (DOTS) {  // the row's four lanes -> split partials of depth(x), nu_enc(x)
+        dpre += __shfl_xor(dpre, 16, 64);
+        dpre += __shfl_xor(dpre, 32, 64);
+#pragma unroll
+        for (int h = 0; h < HD; ++h) {
+            dhn[h] += __shfl_xor(dhn[h], 16, 64);
+            dhn[h] += __shfl_xor(dhn[h], 32, 64);
+        }
+        if (lane < 16) {
+            float* o = rowxp + ((int64_t)sp * d.Bpad + row0 + lane) * (1 + d.H);
+            o[0] = dpre;
+#pragma unroll
+            for (int h = 0; h < HD; ++h)
+                if (h < d.H) o[1 + h] = dhn[h];
+        }
     }
     if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
         vm_wait_all();
@@ -340,34 +299,45 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
 // LDS [cell][k] image read as wave-uniform broadcasts.
 //   mode 1 = recorder encode_mu(x) (nb.hh:419-431): no covariate, writes mean/lnvar out.
 // =======================================================================================
-__global__ __launch_bounds__(1024) void k_latent_fwd(
+__global__ __launch_bounds__(256) void k_latent_fwd(
     NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
-    const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowx,
-    const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowxp,
+    float* __restrict__ rowx, const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
-    __shared__ __attribute__((aligned(16))) float sH[64 * 68];  // [cell][k]
-    __shared__ float sred[16];
-    for (int i = threadIdx.x; i < K * K; i += 1024) {
+    __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
+    __shared__ float sred[4];
+    __shared__ float sRX[LAT_CELLS][1 + HMAX];  // depth pre-activation, nu_enc(x)
+    for (int i = threadIdx.x; i < K * K; i += 256) {
         sWm[(i / K) * 65 + i % K] = P.Wm[i];
         sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * 64 + 4 * w;  // first cell of this wave (4 cells per wave)
-    // h = sum of the encoder's gene-split partials - mvec + bias
-    const float hb = (k < K) ? P.be[k] - mvec[k] : 0.f;
-    for (int c = 0; c < 4; ++c) {
-        const int b = bw + c;
-        float h = 0.f;
-        if (k < K && b < d.Bpad) {
-            h = hb;
-            for (int s2 = 0; s2 < d.nsE; ++s2) h += hpart[((int64_t)s2 * d.Bpad + b) * d.KP + k];
+    const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // first cell of this wave (4 cells per wave)
+    {
+        // raw-count dots from the encoder's gene-split partials (+ bias); rowx for k_latent_bwd
+        const int nq = 1 + d.H;
+        float xs[4];
+        split_sum4(rowxp, d.nsE, (int64_t)d.Bpad * nq, (int64_t)bw * nq + (k < nq ? k : 0), nq, k < nq, xs);
+        if (k < nq) {
+            const float bias = (k == 0) ? P.bdp[0] : P.bne[k - 1];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float v = xs[c] + bias;
+                sRX[4 * w + c][k] = v;
+                if (mode == 0) rowx[(int64_t)(bw + c) * d.rowx_stride + (k == 0 ? 0 : 1 + k)] = v;
+            }
         }
-        sH[(4 * w + c) * 68 + k] = h;
     }
+    // h = sum of the encoder's gene-split partials - mvec + bias (split loads issued together)
+    const float hb = (k < K) ? P.be[k] - mvec[k] : 0.f;
+    float hs[4];
+    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sH[(4 * w + c) * 68 + k] = (k < K) ? hb + hs[c] : 0.f;
     __syncthreads();
     float mean[4], av[4];
     const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
@@ -426,12 +396,12 @@ __global__ __launch_bounds__(1024) void k_latent_fwd(
             zb[(int64_t)b * d.KP + k] = (__bf16)zz;
         }
         // ---- overdispersion latent (lanes r < R) ----
-        const float* rx = rowx + (int64_t)b * d.rowx_stride;
+        const float* rx = &sRX[4 * w + c][0];  // [0] = depth pre-activation, [1 + h] = nu_enc_h
         if (k < d.R) {
             float nm = P.bnm[k], an = P.bnl[k];
             for (int hh = 0; hh < d.H; ++hh) {
-                nm += P.Wnm[k * d.H + hh] * rx[2 + hh];
-                an += P.Wnl[k * d.H + hh] * rx[2 + hh];
+                nm += P.Wnm[k * d.H + hh] * rx[1 + hh];
+                an += P.Wnl[k * d.H + hh] * rx[1 + hh];
             }
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
@@ -457,11 +427,7 @@ __global__ __launch_bounds__(1024) void k_latent_fwd(
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int q = 0; q < 16; ++q) t += sred[q];
-        klpart[blockIdx.x] = -0.5f * t;
-    }
+    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * ((sred[0] + sred[1]) + (sred[2] + sred[3]));
 }
 
 // =======================================================================================
@@ -776,10 +742,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     float lossacc = 0.f;
     // ---- per-wave row data for the sparse pass ----
-    for (int i = lane; i < 16 * S; i += 64) {
-        const int rr = i / S, tt = i % S;
-        rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
-    }
+    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
@@ -1019,7 +982,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 // from LDS images with wave-uniform broadcast reads.  Every per-workgroup partial is a plain
 // store (fixed-order sums, no atomics); k_grad_small reduces the partials.
 // =======================================================================================
-__global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
+__global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
                                                     const float* __restrict__ covar,
                                                     float* __restrict__ lat, const float* __restrict__ rowx,
                                                     const float* __restrict__ rowB,
@@ -1032,17 +995,20 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
     float* sWm = lsm;                 // [K][65]
     float* sWl = sWm + 64 * 65;       // [K][65]
     float* sDM = sWl + 64 * 65;       // [cell][68] dmean
-    float* sDA = sDM + 64 * 68;       // [cell][68] dlnvar-pre-clamp (a)
-    float* sH = sDA + 64 * 68;        // [cell][68] h
-    float* wpart = sH + 64 * 68;      // [16][NSM] per-wave small partials
+    float* sDA = sDM + LAT_CELLS * 68;  // [cell][68] dlnvar-pre-clamp (a)
+    float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h
+    float* wpart = sH + LAT_CELLS * 68; // [4][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-    for (int i = threadIdx.x; i < K * K; i += 1024) {
+    for (int i = threadIdx.x; i < K * K; i += 256) {
         sWm[(i / K) * 65 + i % K] = P.Wm[i];
         sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * 64 + 4 * w;  // 4 cells per wave
+    const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // 4 cells per wave
+    float dzA4[4], dzP4[4];
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < K, dzA4);
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < K, dzP4);
     float* wp = wpart + w * NSM;
     float* p_dbm = wp;                 // [64]
     float* p_dbl = p_dbm + 64;         // [64]
@@ -1066,6 +1032,7 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
         rdnl[h] = 0.f;
     }
     // ---- per cell: dmean, da (lane = k) ----
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
         float* L = lat + (int64_t)b * d.lat_stride;
@@ -1078,12 +1045,8 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
         const float wb = L[d.LAT_W];
         float dmean = 0.f, da = 0.f, h = 0.f;
         if (k < K) {
-            float A2 = 0.f, Pb = 0.f;
-            for (int s2 = 0; s2 < d.nsD; ++s2) {
-                const float* dp = dzp + (((int64_t)s2 * d.Bpad + b) * 2) * KP;
-                A2 += dp[k];
-                Pb += dp[KP + k];
-            }
+            const float A2 = (c == 0) ? dzA4[0] : (c == 1) ? dzA4[1] : (c == 2) ? dzA4[2] : dzA4[3];
+            const float Pb = (c == 0) ? dzP4[0] : (c == 1) ? dzP4[1] : (c == 2) ? dzP4[2] : dzP4[3];
             const float dz = wb * (A2 - E * Pb);
             const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
             h = L[d.LAT_H + k];
@@ -1192,23 +1155,31 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
     }
     if (k < H) p_dbne[k] = rbne;
     if (k == 0) p_dbdp[0] = rbdp;
-    // ---- dWm, dWl = [dmean | da]^T h over the workgroup's 64 cells (lane = k, wave w: j = 4w..4w+3) ----
+    // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells (lane = k, wave w: j = 16w..16w+15) ----
     float* out = small + (int64_t)blockIdx.x * SMALL;
     {
-        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gl[4] = {0.f, 0.f, 0.f, 0.f};
+        float gm[16], gl[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            gm[q] = 0.f;
+            gl[q] = 0.f;
+        }
         const int kk = (k < K) ? k : 0;
-        for (int b = 0; b < 64; ++b) {
+        for (int b = 0; b < LAT_CELLS; ++b) {
             const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
-            const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 4 * w]);
-            gm[0] = fmaf(dm, h4.x, gm[0]); gm[1] = fmaf(dm, h4.y, gm[1]);
-            gm[2] = fmaf(dm, h4.z, gm[2]); gm[3] = fmaf(dm, h4.w, gm[3]);
-            gl[0] = fmaf(dl, h4.x, gl[0]); gl[1] = fmaf(dl, h4.y, gl[1]);
-            gl[2] = fmaf(dl, h4.z, gl[2]); gl[3] = fmaf(dl, h4.w, gl[3]);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 16 * w + 4 * q4]);
+                gm[4 * q4 + 0] = fmaf(dm, h4.x, gm[4 * q4 + 0]); gm[4 * q4 + 1] = fmaf(dm, h4.y, gm[4 * q4 + 1]);
+                gm[4 * q4 + 2] = fmaf(dm, h4.z, gm[4 * q4 + 2]); gm[4 * q4 + 3] = fmaf(dm, h4.w, gm[4 * q4 + 3]);
+                gl[4 * q4 + 0] = fmaf(dl, h4.x, gl[4 * q4 + 0]); gl[4 * q4 + 1] = fmaf(dl, h4.y, gl[4 * q4 + 1]);
+                gl[4 * q4 + 2] = fmaf(dl, h4.z, gl[4 * q4 + 2]); gl[4 * q4 + 3] = fmaf(dl, h4.w, gl[4 * q4 + 3]);
+            }
         }
         if (k < K) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j2 = 4 * w + q;
+            for (int q = 0; q < 16; ++q) {
+                const int j2 = 16 * w + q;
                 if (j2 < K) {
                     out[k * K + j2] = gm[q];
                     out[K * K + k * K + j2] = gl[q];
@@ -1221,12 +1192,9 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
     const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + K,
               o_bnm = o_nm + R * H, o_nl = o_bnm + R, o_bnl = o_nl + R * H, o_bne = o_bnl + R, o_bdp = o_bne + H;
     auto wsum = [&](int off) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) t += wpart[q * NSM + off];
-        return t;
+        return (wpart[0 * NSM + off] + wpart[1 * NSM + off]) + (wpart[2 * NSM + off] + wpart[3 * NSM + off]);
     };
-    for (int i = threadIdx.x; i < K; i += 1024) {
+    for (int i = threadIdx.x; i < K; i += 256) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
         out[o_dhs + i] = wsum(128 + i);
@@ -1234,16 +1202,16 @@ __global__ __launch_bounds__(1024) void k_latent_bwd(NBPtrs P, Dims d, const int
     }
     const int b_nm = 192 + 64 * CMAX, b_nl = b_nm + RMAX * HMAX, b_bnm = b_nl + RMAX * HMAX, b_bnl = b_bnm + RMAX,
               b_bne = b_bnl + RMAX, b_bdp = b_bne + HMAX;
-    for (int i = threadIdx.x; i < R * H; i += 1024) {
+    for (int i = threadIdx.x; i < R * H; i += 256) {
         const int r2 = i / H, h2 = i % H;
         out[o_nm + i] = wsum(b_nm + r2 * HMAX + h2);
         out[o_nl + i] = wsum(b_nl + r2 * HMAX + h2);
     }
-    for (int i = threadIdx.x; i < R; i += 1024) {
+    for (int i = threadIdx.x; i < R; i += 256) {
         out[o_bnm + i] = wsum(b_bnm + i);
         out[o_bnl + i] = wsum(b_bnl + i);
     }
-    for (int i = threadIdx.x; i < H; i += 1024) out[o_bne + i] = wsum(b_bne + i);
+    for (int i = threadIdx.x; i < H; i += 256) out[o_bne + i] = wsum(b_bne + i);
     if (threadIdx.x == 0) out[o_bdp] = wsum(b_bdp);
 }
 
@@ -1302,10 +1270,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     int64_t* rbl = reinterpret_cast<int64_t*>(wpb + ((16 * S * 4 + 15) / 16) * 16);
     int32_t* rinc = reinterpret_cast<int32_t*>(rbl + 16);
 
-    for (int i = lane; i < 16 * S; i += 64) {
-        const int rr = i / S, tt = i % S;
-        rtl[i] = (t0 + tt <= d.NT) ? rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
-    }
+    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = (b < d.B) ? cells[b] : -1;
@@ -1445,6 +1410,7 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
     const int i = (blockIdx.x - 1) * 256 + threadIdx.x;
     if (i >= SMALL) return;
     float s = 0.f;
+#pragma unroll 8
     for (int wg = 0; wg < nwg; ++wg) s += small[(int64_t)wg * SMALL + i];
     int o = i;
     if (o < K * K) { G.Wm[o] = s; return; }
@@ -1641,6 +1607,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_DHNU = (int)e->LAT_HNU;
     d.LAT_DPRE = (int)e->LAT_HNU + (int)e->H;
     d.rowx_stride = 2 + (int)e->H;
+    d.Ncells = (int)e->N;
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
     return d;
 }
@@ -1703,10 +1670,19 @@ static size_t dec_lds(const Dims& d, int pass, bool bf16) {
     return s;
 }
 
-template <class T, int KP>
+template <class T, int KP, int DOTS>
 static size_t enc_fwd_lds(const Dims& d) {
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes;
+    constexpr int NGV = DOTS == 0 ? 1 : (DOTS == 1 ? 2 : 1 + HMAX);
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes +
+           (DOTS ? (size_t)3 * NGV * 64 * sizeof(float) : 0);
+}
+template <class T, int KP, int DOTS>
+static void enc_fwd_nb(Engine* e, const Dims& d, const NBPtrs& P, hipStream_t st) {
+    hipLaunchKernelGGL((k_enc_fwd<T, KP, DOTS>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP, DOTS>(d)), st,
+                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp,
+                       sizeof(T) == 2 ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d, e->d_hpart, P.wdp, P.Wne,
+                       e->d_rowxp);
 }
 template <class T, int KP>
 static size_t enc_bwd_lds(const Dims& d) {
@@ -1731,24 +1707,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, gene, e->d_mvec);
     }
     {
-        ScopedTimer tm(e, "k_rowscan");
-        if (d.H == 1)
-            hipLaunchKernelGGL(k_rowscan<true>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr,
-                               e->d_col, e->d_val, P, d, e->d_rtp, e->d_rowx);
-        else
-            hipLaunchKernelGGL(k_rowscan<false>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr,
-                               e->d_col, e->d_val, P, d, e->d_rtp, e->d_rowx);
-    }
-    {
         ScopedTimer tm(e, "k_enc_fwd");
-        hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_cells,
-                           e->d_rowptr, e->d_col, e->d_val, e->d_rtp, bf ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d,
-                           e->d_hpart);
+        if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
+        else enc_fwd_nb<T, KP, 2>(e, d, P, st);
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
-        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar,
-                           e->d_hpart, e->d_mvec, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id,
+        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id,
                            row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
     }
     DecPtrs Q;
@@ -1815,8 +1781,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         ScopedTimer tm(e, "k_latent_bwd");
         const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-        const size_t lds = (size_t)(2 * 64 * 65 + 3 * 64 * 68 + 16 * NSM) * 4;
-        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(1024), lds, st, P, d, e->d_cells, e->d_covar,
+        const size_t lds = (size_t)(2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * NSM) * 4;
+        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
                            e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     {
@@ -1871,17 +1837,10 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
                        bf ? e->d_WeS_b : nullptr);
     hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, e->d_gene, e->d_mvec);
-    if (d.H == 1)
-        hipLaunchKernelGGL(k_rowscan<true>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
-                           e->d_val, P, d, e->d_rtp, e->d_rowx);
-    else
-        hipLaunchKernelGGL(k_rowscan<false>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col,
-                           e->d_val, P, d, e->d_rtp, e->d_rowx);
-    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_cells,
-                           e->d_rowptr, e->d_col, e->d_val, e->d_rtp, bf ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d,
-                           e->d_hpart);
-    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar,
-                       e->d_hpart, e->d_mvec, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
+    if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
+    else enc_fwd_nb<T, KP, 2>(e, d, P, st);
+    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
                        e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
     return hipGetLastError();
 }
@@ -1902,8 +1861,9 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
 // ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
 template <class T, int KP>
 static void enc_fwd_go(Engine* e, const Dims& d, const void* WeS, float* hpart) {
-    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), e->stream,
-                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, (const T*)WeS, d, hpart);
+    hipLaunchKernelGGL((k_enc_fwd<T, KP, 0>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP, 0>(d)), e->stream,
+                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, (const T*)WeS, d, hpart,
+                       (const float*)nullptr, (const float*)nullptr, (float*)nullptr);
 }
 template <class T, int KP>
 static void enc_bwd_go(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {

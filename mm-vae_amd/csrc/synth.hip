@@ -122,12 +122,70 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg,
                        e->d_rowptr, e->d_col, e->d_val);
     if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;
-    hipFree(d_pg);
-    hipFree(d_cnt);
     e->N = N;
     e->nnz = nnz;
+    if ((er = build_dataset_index(e)) != hipSuccess) return er;
+    hipFree(d_pg);
+    hipFree(d_cnt);
     if (nnz_out) *nnz_out = nnz;
     return hipGetLastError();
+}
+
+// =======================================================================================
+// Per-dataset index, built once after every upload / synth (the HBM-resident counterpart of the
+// reference's ${mtx}.index, mmutil_index.hh:138-228): for every cell row
+//   rtp_all[cell][t] = first CSR entry (relative) with gene >= 64 t, t = 0..NT  (the 16 x 64
+//                      tile walk of every tile kernel; row N is the all-empty padding row)
+//   cellnorm[cell]   = (sum log1p(x)^2, sum log1p(x)^2 + 2 eps log1p(x)), eps = 1e-2 / D:
+//                      the vMF row norms of vmf.hh:253 and vmf.hh:422-423 (x only; accurate log1pf)
+// One wave per row; the per-step kernels then never re-scan the batch's rows.
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                       const float* __restrict__ val, int64_t N, int NT, float epsD,
+                                                       int32_t* __restrict__ rtp, float2* __restrict__ cellnorm) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row > N) return;
+    int32_t* rt = rtp + row * (NT + 1);
+    int n = 0;
+    int64_t s = 0;
+    if (row < N) {
+        s = rowptr[row];
+        n = (int)(rowptr[row + 1] - s);
+    }
+    const int32_t* cr = col + s;
+    const float* vr = val + s;
+    float sl2 = 0.f, sy = 0.f;
+    for (int j = lane; j < n; j += 64) {
+        const int g = cr[j];
+        const int gp = j > 0 ? cr[j - 1] : -64;
+        const float x = vr[j];
+        const float l = log1pf(x), ly = log1pf(fmaxf(x, 0.f));
+        sl2 = fmaf(l, l, sl2);
+        sy = fmaf(ly, ly + 2.f * epsD, sy);
+        for (int tt = (gp >> 6) + 1; tt <= (g >> 6); ++tt) rt[tt] = j;
+    }
+    const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
+    for (int tt = tlast + 1 + lane; tt <= NT; tt += 64) rt[tt] = n;
+    sl2 = wave_sum(sl2);
+    sy = wave_sum(sy);
+    if (lane == 0) cellnorm[row] = float2{sl2, sy};
+}
+
+hipError_t build_dataset_index(Engine* e) {
+    hipFree(e->d_rtp);
+    hipFree(e->d_cellnorm);
+    e->d_rtp = nullptr;
+    e->d_cellnorm = nullptr;
+    hipError_t er;
+    if ((er = hipMalloc(&e->d_rtp, sizeof(int32_t) * (size_t)(e->N + 1) * (size_t)(e->NT + 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_cellnorm, sizeof(float2) * (size_t)(e->N + 1))) != hipSuccess) return er;
+    const float epsD = (float)(1e-2 / (double)(float)e->D);
+    ScopedTimer tm(e, "k_dataset_index");
+    hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((e->N + 1 + 3) / 4)), dim3(256), 0, e->stream, e->d_rowptr,
+                       e->d_col, e->d_val, e->N, (int)e->NT, epsD, e->d_rtp, (float2*)e->d_cellnorm);
+    if ((er = hipGetLastError()) != hipSuccess) return er;
+    return hipStreamSynchronize(e->stream);
 }
 
 }  // namespace mmvae

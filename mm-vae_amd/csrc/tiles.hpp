@@ -8,6 +8,7 @@
 namespace mmvae {
 
 static constexpr int CMAX = 8, HMAX = 8, RMAX = 8;
+static constexpr int LAT_CELLS = 16;  // cells per 256-thread workgroup of the latent-head kernels
 
 struct Dims {
     int D, DP, NT, K, KP, C, H, R;
@@ -19,8 +20,44 @@ struct Dims {
     int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,
         LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
     int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
+    int Ncells;       // dataset rows: row Ncells of the per-cell tile index is the empty row
     int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
 };
+
+// out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c = 0..3: the split
+// partials of four cells, loads issued four splits at a time (independent, then summed)
+MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, int64_t off, int64_t cstride, bool on,
+                          float (&out)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) out[c] = 0.f;
+    if (!on) return;
+    int s = 0;
+    for (; s + 4 <= ns; s += 4) {
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[u][c] = p[(int64_t)(s + u) * sstride + off + c * cstride];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[c] += (v[0][c] + v[1][c]) + (v[2][c] + v[3][c]);
+    }
+    for (; s < ns; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[c] += p[(int64_t)s * sstride + off + c * cstride];
+}
+
+// Per-wave tile pointers of the wave's 16 rows for the split's tiles t0 .. t0 + S - 1, read
+// from the per-dataset index (rtp [N+1][NT+1], row N = empty) by each row's cell id.
+MMVAE_DEV void fill_rtl(int32_t* rtl, int S, int t0, int NT, int B, int Ncells, const int64_t* __restrict__ cells,
+                        int row0, const int32_t* __restrict__ rtp, int lane) {
+    for (int i = lane; i < 16 * S; i += 64) {
+        const int rr = i / S, tt = i % S;
+        const int b = row0 + rr;
+        const int64_t cell = (b < B) ? cells[b] : -1;
+        const int64_t crow = cell >= 0 ? cell : (int64_t)Ncells;
+        rtl[i] = (t0 + tt <= NT) ? rtp[crow * (NT + 1) + t0 + tt] : 0;
+    }
+}
 
 MMVAE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -48,7 +85,7 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
 // entries past 128 are fetched on the spot.  tile_rows() runs with the whole wave active
 // and publishes the rows' inclusive prefix counts to per-wave LDS (rinc[16]);
 // tile_entry_row() then only reads LDS, so it is safe inside divergent code.
-// rtl = the wave's tile pointers [16][S] (from k_rowscan), rbl = the rows' CSR bases [16].
+// rtl = the wave's tile pointers [16][S] (per-dataset index, fill_rtl), rbl = the rows' CSR bases [16].
 // =======================================================================================
 MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
     const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;

@@ -11,7 +11,6 @@
 // encoder GEMM kernels of nb_kernels.hip (enc_forward_launch / enc_backward_launch):
 //   k_vprep        per-gene 1/(softplus(ln_x_sd)+eps), decoder gene records, W~/s
 //   k_vmvec        dense encoder term mvec = (x_mean/s) W~^T
-//   k_vrowscan     one wave per cell: tile pointers, sum l^2, sum (l+eps)^2 - D eps^2
 //   k_enc_fwd      sum_nnz l (W~/s)  on MFMA                    (shared with NB)
 //   k_vlatent_fwd  h = that / ||l|| - mvec, heads, clamp, reparameterise, KL
 //   k_vkappa       kappa = clamp(exp(ln_kappa)), lbessel terms (one thread)
@@ -146,62 +145,6 @@ __global__ __launch_bounds__(1024) void k_vmvec(Dims d, const float* __restrict_
 }
 
 // =======================================================================================
-// k_vrowscan — one wave per batch row, one coalesced sweep of the row's CSR:
-//   rtp[b][t] = first entry with gene >= 64 t (relative), t = 0..NT
-//   rowx[b] = (sum l^2, sum (l^2 + 2 eps l))  with l = log1p(x) (vmf.hh:253, 422-423)
-// =======================================================================================
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_vrowscan(const int64_t* __restrict__ cells, const int64_t* __restrict__ rowptr,
-                                                  const int32_t* __restrict__ col, const float* __restrict__ val, Dims d,
-                                                  float epsD, int32_t* __restrict__ rtp, float* __restrict__ rowx) {
-    const int lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= d.Bpad) return;
-    const int64_t cell = (b < d.B) ? cells[b] : -1;
-    int32_t* rt = rtp + (int64_t)b * (d.NT + 1);
-    int n = 0;
-    int64_t s = 0;
-    if (cell >= 0) {
-        s = rowptr[cell];
-        n = (int)(rowptr[cell + 1] - s);
-    }
-    const int32_t* cr = col + s;
-    const float* vr = val + s;
-    float sl2 = 0.f, sy = 0.f;
-    for (int j0 = 0; j0 < n; j0 += 256) {
-        int g[4], gp[4];
-        float x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + 64 * u + lane;
-            const bool ok = j < n;
-            g[u] = ok ? cr[j] : 0;
-            x[u] = ok ? vr[j] : 0.f;
-            gp[u] = (ok && j > 0) ? cr[j - 1] : -64;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            // FAST (bf16 operand mode): v_log-based log1p (rel err <= 6e-6); f32 parity mode: libm
-            const float l = FAST ? log1p_pos(fmaxf(x[u], 0.f)) : log1pf(x[u]);
-            const float ly = (x[u] >= 0.f) ? l : 0.f;   // log1p(relu x)
-            sl2 = fmaf(l, l, sl2);
-            sy = fmaf(ly, ly + 2.f * epsD, sy);
-            const int j = j0 + 64 * u + lane;
-            if (j < n)
-                for (int tt = (gp[u] >> 6) + 1; tt <= (g[u] >> 6); ++tt) rt[tt] = j;
-        }
-    }
-    const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
-    for (int tt = tlast + 1 + lane; tt <= d.NT; tt += 64) rt[tt] = n;
-    sl2 = wave_sum(sl2);
-    sy = wave_sum(sy);
-    if (lane == 0) {
-        rowx[(int64_t)b * d.rowx_stride] = sl2;
-        rowx[(int64_t)b * d.rowx_stride + 1] = sy;
-    }
-}
-
-// =======================================================================================
 // k_vlatent_fwd — encoder head + Gaussian reparameterisation for 64 cells per workgroup
 // (wave w owns cells 4w..4w+3, lane = latent k):
 //   h = (sum_nnz l W~/s) / ||l|| - mvec              (vmf.hh:253-258, Angular has no bias)
@@ -210,35 +153,37 @@ __global__ __launch_bounds__(256) void k_vrowscan(const int64_t* __restrict__ ce
 //   mode 1 = recorder encode(x) (vmf.hh:267-281): no covariate, writes mean/lnvar out.
 // Per-row state kept for the backward: h, mean, pre-clamp a, eps, 1/||l|| (LAT_D), valid.
 // =======================================================================================
-__global__ __launch_bounds__(1024) void k_vlatent_fwd(
+__global__ __launch_bounds__(256) void k_vlatent_fwd(
     VPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
-    const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowx,
-    const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    const float* __restrict__ hpart, const float* __restrict__ mvec, const float2* __restrict__ cellnorm,
+    float* __restrict__ rowx, const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
-    __shared__ __attribute__((aligned(16))) float sH[64 * 68];
-    __shared__ float sred[16];
-    for (int i = threadIdx.x; i < K * K; i += 1024) {
+    __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
+    __shared__ float sred[4];
+    for (int i = threadIdx.x; i < K * K; i += 256) {
         sWm[(i / K) * 65 + i % K] = P.Wm[i];
         sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * 64 + 4 * w;
+    const int bw = blockIdx.x * LAT_CELLS + 4 * w;
     const float mk = (k < K) ? mvec[k] : 0.f;
-    float inx[4];
+    float inx[4], hs[4];
+    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        inx[c] = 1.f / fmaxf(sqrtf(rowx[(int64_t)b * d.rowx_stride]), 1e-12f);  // F::normalize
-        float h = 0.f;
-        if (k < K) {
-            float s = 0.f;
-            for (int s2 = 0; s2 < d.nsE; ++s2) s += hpart[((int64_t)s2 * d.Bpad + b) * d.KP + k];
-            h = s * inx[c] - mk;
+        // row norms from the dataset index (row Ncells = the empty padding row)
+        const float2 cn = cellnorm[(b < d.B) ? cells[b] : (int64_t)d.Ncells];
+        inx[c] = 1.f / fmaxf(sqrtf(cn.x), 1e-12f);  // F::normalize
+        if (mode == 0 && k == 0) {
+            rowx[(int64_t)b * d.rowx_stride] = cn.x;
+            rowx[(int64_t)b * d.rowx_stride + 1] = cn.y;
         }
-        sH[(4 * w + c) * 68 + k] = h;
+        sH[(4 * w + c) * 68 + k] = (k < K) ? hs[c] * inx[c] - mk : 0.f;
     }
     __syncthreads();
     float mean[4], av[4];
@@ -307,11 +252,7 @@ __global__ __launch_bounds__(1024) void k_vlatent_fwd(
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int q = 0; q < 16; ++q) t += sred[q];
-        klpart[blockIdx.x] = -0.5f * t;
-    }
+    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * ((sred[0] + sred[1]) + (sred[2] + sred[3]));
 }
 
 // =======================================================================================
@@ -449,10 +390,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     f32x4 dz[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) dz[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int i = lane; i < 16 * S; i += 64) {
-        const int rr = i / S, tt = i % S;
-        rtl[i] = (t0 + tt <= d.NT) ? Q.rtp[(int64_t)(row0 + rr) * (d.NT + 1) + t0 + tt] : 0;
-    }
+    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
@@ -634,7 +572,7 @@ __global__ __launch_bounds__(256) void k_vrowfin(Dims d, float epsD, const float
 //   dh = dmean Wm + da Wl;  dWm += dmean^T h, dWl += da^T h (per-workgroup partials)
 // dhT (encoder backward operand) = dh / ||l||; the x_mean gradient needs the unscaled sum.
 // =======================================================================================
-__global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int64_t* __restrict__ cells,
+__global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int64_t* __restrict__ cells,
                                                      const float* __restrict__ covar, const float* __restrict__ lat,
                                                      const float* __restrict__ dzp, float* __restrict__ dhT_f,
                                                      __bf16* __restrict__ dhT_b, float* __restrict__ small) {
@@ -644,21 +582,24 @@ __global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     float* sWm = lsm;               // [K][65]
     float* sWl = sWm + 64 * 65;     // [K][65]
-    float* sDM = sWl + 64 * 65;     // [cell][68] dmean
-    float* sDA = sDM + 64 * 68;     // [cell][68] d(pre-clamp lnvar)
-    float* sH = sDA + 64 * 68;      // [cell][68] h
-    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + 64 * 68);  // [16][NSM]
-    for (int i = threadIdx.x; i < K * K; i += 1024) {
+    float* sDM = sWl + 64 * 65;            // [cell][68] dmean
+    float* sDA = sDM + LAT_CELLS * 68;     // [cell][68] d(pre-clamp lnvar)
+    float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h
+    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [4][NSM]
+    for (int i = threadIdx.x; i < K * K; i += 256) {
         sWm[(i / K) * 65 + i % K] = P.Wm[i];
         sWl[(i / K) * 65 + i % K] = P.Wl[i];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * 64 + 4 * w;
+    const int bw = blockIdx.x * LAT_CELLS + 4 * w;
+    float dz4[4];
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * KP, (int64_t)bw * KP + k, KP, k < K, dz4);
     const float bn = d.beta * d.inv_n;
     float rbm = 0.f, rbl = 0.f, rWce[CMAX], inx[4];
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) rWce[c] = 0.f;
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
         const float* L = lat + (int64_t)b * d.lat_stride;
@@ -666,8 +607,7 @@ __global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int
         inx[c] = L[d.LAT_D];
         float dmean = 0.f, da = 0.f, h = 0.f;
         if (k < K) {
-            float dz = 0.f;
-            for (int s2 = 0; s2 < d.nsD; ++s2) dz += dzp[((int64_t)s2 * d.Bpad + b) * KP + k];
+            const float dz = (c == 0) ? dz4[0] : (c == 1) ? dz4[1] : (c == 2) ? dz4[2] : dz4[3];
             const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
             h = L[d.LAT_H + k];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
@@ -730,20 +670,28 @@ __global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int
     for (int q = 0; q < CMAX; ++q) wp[192 + k * CMAX + q] = rWce[q];
     float* out = small + (int64_t)blockIdx.x * SMALL;
     {
-        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gl[4] = {0.f, 0.f, 0.f, 0.f};
+        float gm[16], gl[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            gm[q] = 0.f;
+            gl[q] = 0.f;
+        }
         const int kk = (k < K) ? k : 0;
-        for (int b = 0; b < 64; ++b) {
+        for (int b = 0; b < LAT_CELLS; ++b) {
             const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
-            const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 4 * w]);
-            gm[0] = fmaf(dm, h4.x, gm[0]); gm[1] = fmaf(dm, h4.y, gm[1]);
-            gm[2] = fmaf(dm, h4.z, gm[2]); gm[3] = fmaf(dm, h4.w, gm[3]);
-            gl[0] = fmaf(dl, h4.x, gl[0]); gl[1] = fmaf(dl, h4.y, gl[1]);
-            gl[2] = fmaf(dl, h4.z, gl[2]); gl[3] = fmaf(dl, h4.w, gl[3]);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 16 * w + 4 * q4]);
+                gm[4 * q4 + 0] = fmaf(dm, h4.x, gm[4 * q4 + 0]); gm[4 * q4 + 1] = fmaf(dm, h4.y, gm[4 * q4 + 1]);
+                gm[4 * q4 + 2] = fmaf(dm, h4.z, gm[4 * q4 + 2]); gm[4 * q4 + 3] = fmaf(dm, h4.w, gm[4 * q4 + 3]);
+                gl[4 * q4 + 0] = fmaf(dl, h4.x, gl[4 * q4 + 0]); gl[4 * q4 + 1] = fmaf(dl, h4.y, gl[4 * q4 + 1]);
+                gl[4 * q4 + 2] = fmaf(dl, h4.z, gl[4 * q4 + 2]); gl[4 * q4 + 3] = fmaf(dl, h4.w, gl[4 * q4 + 3]);
+            }
         }
         if (k < K) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j2 = 4 * w + q;
+            for (int q = 0; q < 16; ++q) {
+                const int j2 = 16 * w + q;
                 if (j2 < K) {
                     out[k * K + j2] = gm[q];
                     out[K * K + k * K + j2] = gl[q];
@@ -753,20 +701,15 @@ __global__ __launch_bounds__(1024) void k_vlatent_bwd(VPtrs P, Dims d, const int
     }
     __syncthreads();
     const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
-    auto wsum = [&](int off) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) t += wpart[q][off];
-        return t;
-    };
-    for (int i = threadIdx.x; i < K; i += 1024) {
+    auto wsum = [&](int off) { return (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]); };
+    for (int i = threadIdx.x; i < K; i += 256) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
         out[o_dhs + i] = wsum(128 + i);
         for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
     }
 }
-static constexpr size_t VLAT_BWD_LDS = (size_t)(2 * 64 * 65 + 3 * 64 * 68 + 16 * (3 * 64 + 64 * CMAX)) * 4;
+static constexpr size_t VLAT_BWD_LDS = (size_t)(2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * (3 * 64 + 64 * CMAX)) * 4;
 
 // =======================================================================================
 // k_vgrad_small — block 0: the loss (vmf.hh:429-439) and the ln_kappa gradient
@@ -808,6 +751,7 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
     const int i = (blockIdx.x - 1) * 256 + threadIdx.x;
     if (i >= SMALL) return;
     float s = 0.f;
+#pragma unroll 8
     for (int wg = 0; wg < nwg; ++wg) s += small[(int64_t)wg * SMALL + i];
     int o = i;
     if (o < K * K) { G.Wm[o] = s; return; }
@@ -969,6 +913,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_D = (int)e->LAT_D;  // vMF: 1 / ||log1p x||
     d.LAT_VALID = (int)e->LAT_VALID;
     d.rowx_stride = 2 + (int)e->H;
+    d.Ncells = (int)e->N;
     d.dbg = 0;
     return d;
 }
@@ -991,19 +936,14 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         hipLaunchKernelGGL(k_vmvec, dim3(d.KP), dim3(1024), 0, st, d, gene, e->d_WeP_f, e->d_mvec);
     }
     {
-        ScopedTimer tm(e, "k_vrowscan");
-        hipLaunchKernelGGL(k_vrowscan<sizeof(T) == 2>, dim3(d.Bpad / 4), dim3(256), 0, st, e->d_cells, e->d_rowptr, e->d_col, e->d_val,
-                           d, sc.epsD, e->d_rtp, e->d_rowx);
-    }
-    {
         ScopedTimer tm(e, "k_enc_fwd");
         hipError_t er = enc_forward_launch(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart);
         if (er != hipSuccess) return er;
     }
     {
         ScopedTimer tm(e, "k_vlatent_fwd");
-        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(1024), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
-                           e->d_mvec, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id, row_offset,
+        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
+                           e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id, row_offset,
                            e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
     }
     if (mode == 1) return hipGetLastError();
@@ -1059,7 +999,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");
-        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(1024), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
+        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
                            e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     {

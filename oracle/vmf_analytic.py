@@ -66,7 +66,7 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     xm = P["x_mean"][0]
     mvec = Wt @ (xm * inv)
 
-    # ---- k_vrowscan: row norms ---------------------------------------------------------------
+    # ---- row norms (dataset index cellnorm) ---------------------------------------------------------------
     l = np.log1p(x)
     ly = np.log1p(np.maximum(x, 0.0))
     nx = np.maximum(np.sqrt((l * l).sum(1)), 1e-12)
