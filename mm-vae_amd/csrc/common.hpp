@@ -120,6 +120,51 @@ MMVAE_DEV float softplus_sig(float u, float& sig) {
 // clamp(sp, 1e-4, 1e4) as one v_med3_f32 (nb.hh:459)
 MMVAE_DEV float clamp_nu(float sp) { return __builtin_amdgcn_fmed3f(sp, 1e-4f, 1e4f); }
 
+// ---------------------------------------------------------------------------------------
+// Packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): one issue covers two
+// elements, which halves the issue cost of a VALU-issue-bound loop run by one wave per SIMD.
+// ---------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+MMVAE_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+MMVAE_DEV f2 splat2(float v) { return f2{v, v}; }
+
+// Dense NB terms of two (cell, gene) elements at x = 0 (nb.hh:456-459, 518-528):
+//   nu = clamp(softplus(u)), nup = nu + 1e-4, sgm = d nu / d u (0 where the clamp bites),
+//   lgr = log(1 + mu / nup) = log(mu + nup) - log(nup),  q = -mu / (mu + nup).
+// Five transcendentals per element: exp(-|u|), 1/(1+e), log2(1+e), 1/(nup (mu+nup)), log2(1+y).
+// Both log1p's use the rounding-corrected form log1p(a) = log(z) - ((z - 1) - a) / z with
+// z = fl(1 + a) (exact z - 1), accurate for small a without a series branch.
+MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lgr, f2& q, f2& sgm) {
+    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+    f2 e, r, l;
+    e.x = fexp2(-fabsf(u.x) * L2E);
+    e.y = fexp2(-fabsf(u.y) * L2E);
+    const f2 z = e + 1.f;
+    r.x = frcp(z.x);
+    r.y = frcp(z.y);
+    l.x = flog2(z.x);
+    l.y = flog2(z.y);
+    const f2 sp = f2{fmaxf(u.x, 0.f), fmaxf(u.y, 0.f)} + fma2(l, splat2(LN2), -(((z - 1.f) - e) * r));
+    const f2 nu = f2{clamp_nu(sp.x), clamp_nu(sp.y)};
+    const f2 er = e * r;  // sigmoid(u) for u < 0
+    sgm.x = (nu.x == sp.x) ? ((u.x >= 0.f) ? r.x : er.x) : 0.f;
+    sgm.y = (nu.y == sp.y) ? ((u.y >= 0.f) ? r.y : er.y) : 0.f;
+    nup = nu + 1e-4f;
+    const f2 sv = mu + nup;
+    const f2 ns = nup * sv;
+    f2 rr;
+    rr.x = frcp(ns.x);
+    rr.y = frcp(ns.y);
+    const f2 rsv = nup * rr;        // 1 / (mu + nup)
+    const f2 y = mu * (sv * rr);    // mu / nup
+    const f2 zz = y + 1.f;
+    f2 lz;
+    lz.x = flog2(zz.x);
+    lz.y = flog2(zz.y);
+    lgr = fma2(lz, splat2(LN2), -(((zz - 1.f) - y) * (nup * rsv)));  // 1 / zz = nup / (mu + nup)
+    q = -mu * rsv;
+}
+
 // accurate torch softplus (libm log1p/exp), for per-row / per-gene scalars
 MMVAE_DEV float softplus_acc(float u) { return (u > 20.f) ? u : log1pf(expf(u)); }
 

@@ -713,27 +713,31 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
-    float rv[4], lse2[4], dv[4], wv[4], crow[4][CM], znu[4][RM];
-    float Eacc[4], Pacc[4], dzn[4][RM];
+    // rows 4(lane>>4) + 2h + j live in component j of the pair h (packed f32 epilogue)
+    float lse2[4];
+    f2 rv2[2], dv2[2], wv2[2], crow2[2][CM], znu2[2][RM];
+    f2 Eacc2[2], Pacc2[2], dzn2[2][RM];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+        const int h = r >> 1, j = r & 1;
         const int b = row0 + 4 * (lane >> 4) + r;
         const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
-        rv[r] = Lr[d.LAT_VALID];
-        dv[r] = Lr[d.LAT_D];
-        wv[r] = Lr[d.LAT_W];
+        rv2[h][j] = Lr[d.LAT_VALID];
+        dv2[h][j] = Lr[d.LAT_D];
+        wv2[h][j] = Lr[d.LAT_W];
         lse2[r] = Q.rowfin[2 * b];
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        for (int c = 0; c < CM; ++c) crow2[h][c][j] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
 #pragma unroll
         for (int q = 0; q < RM; ++q) {
-            znu[r][q] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
-            dzn[r][q] = 0.f;
+            znu2[h][q][j] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
+            dzn2[h][q][j] = 0.f;
         }
-        Eacc[r] = 0.f;
-        Pacc[r] = 0.f;
+        Eacc2[h][j] = 0.f;
+        Pacc2[h][j] = 0.f;
     }
+    f2 lossd2 = splat2(0.f);  // dense (x = 0) part of the loss
     f32x4 dzA[KP / 16], dzP[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) {
@@ -782,8 +786,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
         stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
-        // ---- 1. logits -> p ----
-        float pv[4][4];
+        // ---- 1. logits -> p (into the wave's LDS p tile) ----
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
@@ -800,9 +803,8 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             for (int r = 0; r < 4; ++r) {
                 float lg = acc[r] + g4.x;
 #pragma unroll
-                for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
-                pv[gb][r] = fexp2(fmaf(lg, L2E, -lse2[r]));           // nb.hh:440-441
-                q2[(4 * (lane >> 4) + r) * PS + gl] = pv[gb][r];
+                for (int c = 0; c < CM; ++c) lg = fmaf(crow2[r >> 1][c][r & 1], wcd[c], lg);
+                q2[(4 * (lane >> 4) + r) * PS + gl] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
             }
         }
         wave_sync();
@@ -849,66 +851,58 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 #pragma unroll
             for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
             const float gvf = gv ? 1.f : 0.f;
-            float cs1[1 + CM], csdu = 0.f, csduz[RM];
+            f2 cs1[1 + CM], csdu = splat2(0.f), csduz[RM];
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c) cs1[c] = 0.f;
+            for (int c = 0; c < 1 + CM; ++c) cs1[c] = splat2(0.f);
 #pragma unroll
-            for (int q = 0; q < RM; ++q) csduz[q] = 0.f;
-            float pg[4];
+            for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pg[r] = (gb == 0) ? pv[0][r] : (gb == 1) ? pv[1][r] : (gb == 2) ? pv[2][r] : pv[3][r];
+            for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
+                const int rl = 4 * (lane >> 4) + 2 * h;
+                const f2 p = f2{q2[rl * PS + gl], q2[(rl + 1) * PS + gl]};
+                const f2 mu = fma2(p, dv2[h], splat2(1e-4f));                // nb.hh:519
+                f2 u = splat2(cn);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rl = 4 * (lane >> 4) + r;
-                const float p = pg[r];
-                const float mu = fmaf(p, dv[r], 1e-4f);              // nb.hh:519
-                float u = cn;
-#pragma unroll
-                for (int q = 0; q < RM; ++q) u = fmaf(wnd[q], znu[r][q], u);
-                float sig;
-                const float spv = softplus_sig(u, sig);              // nb.hh:458
-                const float nu = clamp_nu(spv);                      // nb.hh:459
-                const float sgm = (nu == spv) ? sig : 0.f;           // clamp mask folded into sig
-                const float nup = nu + 1e-4f;                        // nb.hh:518
-                const float sv = mu + nup;
-                const float rsv = frcp(sv);
-                const float lgr = log1p_pos(mu * frcp(nup));         // log(s) - log(nup)
-                const float me = rv[r] * gvf;
-                lossacc = fmaf(nup * lgr, me, lossacc);              // nb.hh:528, x = 0 part
-                const float q = -mu * rsv;                           // n dL/dmu' - 1 at x = 0
-                float cpq, cdu;
-                CP::unpack(cc[rl * 64 + gl], cpq, cdu);
-                const float pq = fmaf(p, q, cpq);
-                const float du = fmaf((lgr + q) * sgm, me, cdu);
-                Eacc[r] += pq;
-                Pacc[r] += p;
-                const float wpq = wv[r] * pq;
+                for (int q = 0; q < RM; ++q) u = fma2(splat2(wnd[q]), znu2[h][q], u);  // nb.hh:456-457
+                f2 nup, lgr, qv, sgm;
+                nb_dense2(mu, u, nup, lgr, qv, sgm);                         // nb.hh:458-459, 518-528
+                const f2 me = rv2[h] * gvf;
+                lossd2 = fma2(nup * lgr, me, lossd2);                        // nb.hh:528, x = 0 part
+                float cpa, cda, cpb, cdb;
+                CP::unpack(cc[rl * 64 + gl], cpa, cda);
+                CP::unpack(cc[(rl + 1) * 64 + gl], cpb, cdb);
+                const f2 pq = fma2(p, qv, f2{cpa, cpb});                     // qv = n dL/dmu' - 1 at x = 0
+                const f2 du = fma2((lgr + qv) * sgm, me, f2{cda, cdb});
+                Eacc2[h] += pq;
+                Pacc2[h] += p;
+                const f2 wpq = wv2[h] * pq;
                 cs1[0] += wpq;
 #pragma unroll
-                for (int c = 0; c < CM; ++c) cs1[1 + c] = fmaf(wpq, crow[r][c], cs1[1 + c]);
+                for (int c = 0; c < CM; ++c) cs1[1 + c] = fma2(wpq, crow2[h][c], cs1[1 + c]);
                 csdu += du;
 #pragma unroll
                 for (int qq = 0; qq < RM; ++qq) {
-                    csduz[qq] = fmaf(du, znu[r][qq], csduz[qq]);
-                    dzn[r][qq] = fmaf(du, wnd[qq], dzn[r][qq]);
+                    csduz[qq] = fma2(du, znu2[h][qq], csduz[qq]);
+                    dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                 }
-                q1[rl * QS + gl] = to_t<T>(pq);
+                q1[rl * QS + gl] = to_t<T>(pq.x);
+                q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
             }
             float* pw = part + w * nq * 64 + gl;
 #pragma unroll
             for (int c = 0; c < 1 + CM; ++c)
                 if (c <= C) {
-                    const float v = sum_rowgroups(cs1[c]);
+                    const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
                     if (lane < 16) pw[c * 64] = v;
                 }
             {
-                const float v = sum_rowgroups(csdu);
+                const float v = sum_rowgroups(csdu.x + csdu.y);
                 if (lane < 16) pw[(1 + C) * 64] = v;
             }
 #pragma unroll
             for (int qq = 0; qq < RM; ++qq)
                 if (qq < R) {
-                    const float v = sum_rowgroups(csduz[qq]);
+                    const float v = sum_rowgroups(csduz[qq].x + csduz[qq].y);
                     if (lane < 16) pw[(2 + C + qq) * 64] = v;
                 }
         }
@@ -941,10 +935,10 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     // ---- per-row outputs ----
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        float E = Eacc[r], Pp = Pacc[r];
+        float E = Eacc2[r >> 1][r & 1], Pp = Pacc2[r >> 1][r & 1];
         float dz2[RM];
 #pragma unroll
-        for (int q = 0; q < RM; ++q) dz2[q] = dzn[r][q];
+        for (int q = 0; q < RM; ++q) dz2[q] = dzn2[r >> 1][q][r & 1];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
             E += __shfl_xor(E, o, 64);
@@ -966,7 +960,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             dp[KP] = dzP[lb][r];
         }
     }
-    const float lw = wave_sum(lossacc);
+    const float lw = wave_sum(lossacc + (lossd2.x + lossd2.y));
     __syncthreads();
     if (lane == 0) part[w] = lw;
     __syncthreads();
