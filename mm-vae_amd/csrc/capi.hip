@@ -692,12 +692,13 @@ int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms
 }
 
 int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
-    if (!e || !host || n < 0 || which != 0) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
-    const int64_t cap = (int64_t)e->nsplit_e * e->Bpad * e->KP;
+    if (!e || !host || n < 0 || which < 0 || which > 1) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
+    // 0: encoder split partials (k_enc_fwd stamps), 1: decoder dz partials (k_dec_nb stamps)
+    const int64_t cap = which == 0 ? (int64_t)e->nsplit_e * e->Bpad * e->KP : (int64_t)e->nsplit_d * e->Bpad * 2 * e->KP;
     if (n > cap) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds the workspace");
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipMemcpy(host, e->d_hpart, sizeof(float) * n, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(host, which == 0 ? e->d_hpart : e->d_dzp, sizeof(float) * n, hipMemcpyDeviceToHost));
     return MMVAE_OK;
 }
 

@@ -238,6 +238,25 @@ MMVAE_DEV float sum_rowgroups(float v) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// four quantities summed over the four row groups at once (transposed butterfly: 3 swaps,
+// 3 adds); lane group g = lane >> 4 receives the total of quantity g
+MMVAE_DEV float sum_rowgroups4(float a0, float a1, float a2, float a3) {
+    const auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a2), false, false);
+    const auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a3), false, false);
+    const float b02 = __uint_as_float(s02[0]) + __uint_as_float(s02[1]);  // halves: a0 | a2 over g, g+2
+    const float b13 = __uint_as_float(s13[0]) + __uint_as_float(s13[1]);  // halves: a1 | a3
+    const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(b02), __float_as_uint(b13), false, false);
+    return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+}
+
+// two quantities: lanes 0-31 receive the total of a0, lanes 32-63 that of a1
+MMVAE_DEV float sum_rowgroups2(float a0, float a1) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a1), false, false);
+    const float b = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+    const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(b), __float_as_uint(b), false, false);
+    return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+}
+
 MMVAE_DEV float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -566,12 +566,17 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 }
                 // per-wave partial of this tile (fixed-order combine after the tile barrier)
                 float* pw = part + ((buf * 4 + w) * nq) * 64 + gl;
+                if (CM == 1) {  // nq = 2
+                    const float v = sum_rowgroups2(cs[0], cs[1]);
+                    if (!(lane & 16)) pw[(lane >> 5) * 64] = v;
+                } else {
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c)
-                    if (c <= C) {
-                        const float v = sum_rowgroups(cs[c]);
-                        if (lane < 16) pw[c * 64] = v;
-                    }
+                    for (int c = 0; c < 1 + CM; ++c)
+                        if (c <= C) {
+                            const float v = sum_rowgroups(cs[c]);
+                            if (lane < 16) pw[c * 64] = v;
+                        }
+                }
             }
         }
         __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
@@ -783,6 +788,16 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     __syncthreads();
 
+    // diagnostic (MMVAE_DBG & 64): per-wave phase cycles into dzp (outputs invalid)
+    const bool stamps = (d.dbg & 64) != 0;
+    uint64_t st_[7] = {0, 0, 0, 0, 0, 0, 0}, tp_ = stamps ? stamp_now() : 0;
+    auto lap = [&](int i_) {
+        if (stamps) {
+            const uint64_t tn = stamp_now();
+            st_[i_] += tn - tp_;
+            tp_ = tn;
+        }
+    };
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
         stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
@@ -808,6 +823,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             }
         }
         wave_sync();
+        lap(0);
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
         if (!(d.dbg & 1)) tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
@@ -836,8 +852,10 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             cc[r * 64 + gl] = CP::pack(p * dq, ddu);
         });
         wave_sync();
+        lap(1);
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
         tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
+        lap(2);
         // ---- 3. dense epilogue in the owner lanes ----
 #pragma unroll 1
         for (int gb = 0; gb < ((d.dbg & 2) ? 0 : 4); ++gb) {
@@ -889,25 +907,31 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                 q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
             }
             float* pw = part + w * nq * 64 + gl;
+            if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
+                pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
+                                                      csduz[0].x + csduz[0].y);
+            } else {
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c)
-                if (c <= C) {
-                    const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
-                    if (lane < 16) pw[c * 64] = v;
+                for (int c = 0; c < 1 + CM; ++c)
+                    if (c <= C) {
+                        const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
+                        if (lane < 16) pw[c * 64] = v;
+                    }
+                {
+                    const float v = sum_rowgroups(csdu.x + csdu.y);
+                    if (lane < 16) pw[(1 + C) * 64] = v;
                 }
-            {
-                const float v = sum_rowgroups(csdu.x + csdu.y);
-                if (lane < 16) pw[(1 + C) * 64] = v;
+#pragma unroll
+                for (int qq = 0; qq < RM; ++qq)
+                    if (qq < R) {
+                        const float v = sum_rowgroups(csduz[qq].x + csduz[qq].y);
+                        if (lane < 16) pw[(2 + C + qq) * 64] = v;
+                    }
             }
-#pragma unroll
-            for (int qq = 0; qq < RM; ++qq)
-                if (qq < R) {
-                    const float v = sum_rowgroups(csduz[qq].x + csduz[qq].y);
-                    if (lane < 16) pw[(2 + C + qq) * 64] = v;
-                }
         }
         wave_sync();
         for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        lap(3);
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
 #pragma unroll
         for (int s = 0; s < ((d.dbg & 4) ? 0 : GK); ++s) {
@@ -921,6 +945,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                 dzP[lb] = M::mma(a2, bw, dzP[lb]);
             }
         }
+        lap(4);
         // ---- 5. combine the waves' column partials -> slab (fixed order) ----
         lds_barrier();
         for (int i = threadIdx.x; i < nq * 64; i += 256) {
@@ -929,8 +954,19 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                             part[(3 * nq + q) * 64 + g];
             Q.slabB[((int64_t)rb * nq + q) * d.DP + 64 * t + g] = v;
         }
+        lap(5);
         if (t + 1 < t1) stage_store();
         lds_barrier();
+        lap(6);
+    }
+    if (stamps) {
+        vm_wait_all();
+        __syncthreads();
+        if (lane == 0) {
+            float* o = Q.dzp + ((int64_t)blockIdx.x * 4 + w) * 8;
+            for (int i_ = 0; i_ < 7; ++i_) o[i_] = (float)st_[i_];
+        }
+        return;
     }
     // ---- per-row outputs ----
 #pragma unroll

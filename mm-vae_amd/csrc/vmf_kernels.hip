@@ -466,12 +466,17 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             }
             if (PASS) {
                 float* pw = part + w * nq * 64 + gl;
+                if (CM == 1) {  // nq = 2
+                    const float s = sum_rowgroups2(cs[0], cs[1]);
+                    if (!(lane & 16)) pw[(lane >> 5) * 64] = s;
+                } else {
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c)
-                    if (c <= C) {
-                        const float s = sum_rowgroups(cs[c]);
-                        if (lane < 16) pw[c * 64] = s;
-                    }
+                    for (int c = 0; c < 1 + CM; ++c)
+                        if (c <= C) {
+                            const float s = sum_rowgroups(cs[c]);
+                            if (lane < 16) pw[c * 64] = s;
+                        }
+                }
             }
         }
         if (PASS) {

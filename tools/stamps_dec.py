@@ -1,0 +1,25 @@
+"""Diagnostic: per-phase cycle shares of k_dec_nb's tile loop (MMVAE_DBG=64 stamp build)."""
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "mm-vae_amd", "py"))
+os.environ["MMVAE_DBG"] = "64"
+import mmvae_amd
+B, D, K = 4096, 20000, 64
+eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
+eng.synth_csr(100000, lib_size=2000.0, seed=3)
+eng.init_params(seed=7)
+for i in range(3):
+    eng.eval_loss(np.arange(B), 1.0, step_id=i)
+nsd = int(os.environ.get("NSD", "8"))
+nwg = (B // 64) * nsd
+buf = np.zeros(nwg * 4 * 8, np.float32)
+rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
+assert rc == 0
+st = buf.reshape(-1, 8)[:, :7]
+names = ["logits+exp", "sparse", "fetch", "epilogue", "dz+zero", "barrier+slab", "stage+barrier"]
+tot = st.sum(1)
+ntile = (313 + nsd - 1) // nsd
+print("waves", st.shape[0], "mean total cycles/wave %.0f (%.0f per tile)" % (tot.mean(), tot.mean() / ntile))
+for n, v in zip(names, st.mean(0)):
+    print("  %-14s %8.0f cyc/wave  %6.0f per tile  %5.1f%%" % (n, v, v / ntile, 100 * v / tot.mean()))
+print("max-wave total / mean: %.3f" % (tot.max() / tot.mean()))
