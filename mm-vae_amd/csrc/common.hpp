@@ -130,11 +130,12 @@ MMVAE_DEV f2 splat2(float v) { return f2{v, v}; }
 
 // Dense NB terms of two (cell, gene) elements at x = 0 (nb.hh:456-459, 518-528):
 //   nu = clamp(softplus(u)), nup = nu + 1e-4, sgm = d nu / d u (0 where the clamp bites),
-//   lgr = log(1 + mu / nup) = log(mu + nup) - log(nup),  q = -mu / (mu + nup).
-// Five transcendentals per element: exp(-|u|), 1/(1+e), log2(1+e), 1/(nup (mu+nup)), log2(1+y).
-// Both log1p's use the rounding-corrected form log1p(a) = log(z) - ((z - 1) - a) / z with
-// z = fl(1 + a) (exact z - 1), accurate for small a without a series branch.
-MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lgr, f2& q, f2& sgm) {
+//   lg2 = log2((mu + nup) / nup)  (log2 units),  q = -mu / (mu + nup).
+// Five transcendentals per element: exp(-|u|), 1/(1+e), log2(1+e), 1/(nup (mu+nup)), log2(s/nup).
+// softplus' log1p uses the rounding-corrected form log1p(a) = log(z) - ((z - 1) - a) / z with
+// z = fl(1 + a) (exact z - 1): accurate for small a, as torch's log1p.  lg2 is the reference's
+// own cancelling difference log(mu + nu) - log(nu) (nb.hh:527), to the same absolute error.
+MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lg2, f2& q, f2& sgm) {
     constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
     f2 e, r, l;
     e.x = fexp2(-fabsf(u.x) * L2E);
@@ -155,13 +156,10 @@ MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lgr, f2& q, f2& sgm) {
     f2 rr;
     rr.x = frcp(ns.x);
     rr.y = frcp(ns.y);
-    const f2 rsv = nup * rr;        // 1 / (mu + nup)
-    const f2 y = mu * (sv * rr);    // mu / nup
-    const f2 zz = y + 1.f;
-    f2 lz;
-    lz.x = flog2(zz.x);
-    lz.y = flog2(zz.y);
-    lgr = fma2(lz, splat2(LN2), -(((zz - 1.f) - y) * (nup * rsv)));  // 1 / zz = nup / (mu + nup)
+    const f2 rsv = nup * rr;          // 1 / (mu + nup)
+    const f2 zz = sv * (sv * rr);     // (mu + nup) / nup
+    lg2.x = flog2(zz.x);
+    lg2.y = flog2(zz.y);
     q = -mu * rsv;
 }
 

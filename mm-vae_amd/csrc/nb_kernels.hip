@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     // rows 4(lane>>4) + 2h + j live in component j of the pair h (packed f32 epilogue)
     float lse2[4];
     f2 rv2[2], dv2[2], wv2[2], crow2[2][CM], znu2[2][RM];
-    f2 Eacc2[2], Pacc2[2], dzn2[2][RM];
+    f2 Eacc2[2], dzn2[2][RM], wc2[2][CM];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int h = r >> 1, j = r & 1;
@@ -740,8 +740,11 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             dzn2[h][q][j] = 0.f;
         }
         Eacc2[h][j] = 0.f;
-        Pacc2[h][j] = 0.f;
     }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < CM; ++c) wc2[h][c] = wv2[h] * crow2[h][c];  // w_b c_b (covar_decoding column sums)
     f2 lossd2 = splat2(0.f);  // dense (x = 0) part of the loss
     f32x4 dzA[KP / 16], dzP[KP / 16];
 #pragma unroll
@@ -857,77 +860,91 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
         lap(2);
         // ---- 3. dense epilogue in the owner lanes ----
-#pragma unroll 1
-        for (int gb = 0; gb < ((d.dbg & 2) ? 0 : 4); ++gb) {
-            const int gl = 16 * gb + (lane & 15);
-            const int gene = 64 * t + gl;
-            const bool gv = gene < d.D;
-            const float4 g4 = gst[gl];
-            const float cn = g4.y;
-            float wnd[RM];
-            wnd[0] = g4.w;
+        // MASK: some of the wave's rows (last row block) or the tile's genes (last tile) are
+        // padding; the common case runs without the validity products.
+        auto epilogue = [&](auto mask_c) {
+            constexpr bool MASK = decltype(mask_c)::value;
+            constexpr float LN2 = 0.6931471805599453f;
+            constexpr int GBU = (CM == 1 && RM == 1) ? 4 : 1;  // the general variant stays rolled
+#pragma unroll GBU
+            for (int gb = 0; gb < 4; ++gb) {
+                const int gl = 16 * gb + (lane & 15);
+                const int gene = 64 * t + gl;
+                const bool gv = gene < d.D;
+                const float4 g4 = gst[gl];
+                const float cn = g4.y;
+                float wnd[RM];
+                wnd[0] = g4.w;
 #pragma unroll
-            for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
-            const float gvf = gv ? 1.f : 0.f;
-            f2 cs1[1 + CM], csdu = splat2(0.f), csduz[RM];
+                for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
+                const float gvf = gv ? 1.f : 0.f;
+                f2 cs1[1 + CM], csdu = splat2(0.f), csduz[RM];
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c) cs1[c] = splat2(0.f);
+                for (int c = 0; c < 1 + CM; ++c) cs1[c] = splat2(0.f);
 #pragma unroll
-            for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
+                for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
-                const int rl = 4 * (lane >> 4) + 2 * h;
-                const f2 p = f2{q2[rl * PS + gl], q2[(rl + 1) * PS + gl]};
-                const f2 mu = fma2(p, dv2[h], splat2(1e-4f));                // nb.hh:519
-                f2 u = splat2(cn);
+                for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
+                    const int rl = 4 * (lane >> 4) + 2 * h;
+                    const f2 p = f2{q2[rl * PS + gl], q2[(rl + 1) * PS + gl]};
+                    const f2 mu = fma2(p, dv2[h], splat2(1e-4f));                // nb.hh:519
+                    f2 u = splat2(cn);
 #pragma unroll
-                for (int q = 0; q < RM; ++q) u = fma2(splat2(wnd[q]), znu2[h][q], u);  // nb.hh:456-457
-                f2 nup, lgr, qv, sgm;
-                nb_dense2(mu, u, nup, lgr, qv, sgm);                         // nb.hh:458-459, 518-528
-                const f2 me = rv2[h] * gvf;
-                lossd2 = fma2(nup * lgr, me, lossd2);                        // nb.hh:528, x = 0 part
-                float cpa, cda, cpb, cdb;
-                CP::unpack(cc[rl * 64 + gl], cpa, cda);
-                CP::unpack(cc[(rl + 1) * 64 + gl], cpb, cdb);
-                const f2 pq = fma2(p, qv, f2{cpa, cpb});                     // qv = n dL/dmu' - 1 at x = 0
-                const f2 du = fma2((lgr + qv) * sgm, me, f2{cda, cdb});
-                Eacc2[h] += pq;
-                Pacc2[h] += p;
-                const f2 wpq = wv2[h] * pq;
-                cs1[0] += wpq;
-#pragma unroll
-                for (int c = 0; c < CM; ++c) cs1[1 + c] = fma2(wpq, crow2[h][c], cs1[1 + c]);
-                csdu += du;
-#pragma unroll
-                for (int qq = 0; qq < RM; ++qq) {
-                    csduz[qq] = fma2(du, znu2[h][qq], csduz[qq]);
-                    dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
-                }
-                q1[rl * QS + gl] = to_t<T>(pq.x);
-                q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
-            }
-            float* pw = part + w * nq * 64 + gl;
-            if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
-                pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
-                                                      csduz[0].x + csduz[0].y);
-            } else {
-#pragma unroll
-                for (int c = 0; c < 1 + CM; ++c)
-                    if (c <= C) {
-                        const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
-                        if (lane < 16) pw[c * 64] = v;
+                    for (int q = 0; q < RM; ++q) u = fma2(splat2(wnd[q]), znu2[h][q], u);  // nb.hh:456-457
+                    f2 nup, lg2, qv, sgm;
+                    nb_dense2(mu, u, nup, lg2, qv, sgm);                         // nb.hh:458-459, 518-528
+                    if (MASK) {
+                        const f2 me = rv2[h] * gvf;
+                        sgm *= me;
+                        lossd2 = fma2(nup * me, lg2, lossd2);                    // nb.hh:528, x = 0 part
+                    } else {
+                        lossd2 = fma2(nup, lg2, lossd2);
                     }
-                {
-                    const float v = sum_rowgroups(csdu.x + csdu.y);
-                    if (lane < 16) pw[(1 + C) * 64] = v;
-                }
+                    float cpa, cda, cpb, cdb;
+                    CP::unpack(cc[rl * 64 + gl], cpa, cda);
+                    CP::unpack(cc[(rl + 1) * 64 + gl], cpb, cdb);
+                    const f2 pq = fma2(p, qv, f2{cpa, cpb});                     // qv = n dL/dmu' - 1 at x = 0
+                    const f2 du = fma2(fma2(lg2, splat2(LN2), qv), sgm, f2{cda, cdb});
+                    Eacc2[h] += pq;
+                    cs1[0] = fma2(wv2[h], pq, cs1[0]);
 #pragma unroll
-                for (int qq = 0; qq < RM; ++qq)
-                    if (qq < R) {
-                        const float v = sum_rowgroups(csduz[qq].x + csduz[qq].y);
-                        if (lane < 16) pw[(2 + C + qq) * 64] = v;
+                    for (int c = 0; c < CM; ++c) cs1[1 + c] = fma2(wc2[h][c], pq, cs1[1 + c]);
+                    csdu += du;
+#pragma unroll
+                    for (int qq = 0; qq < RM; ++qq) {
+                        csduz[qq] = fma2(du, znu2[h][qq], csduz[qq]);
+                        dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                     }
+                    q1[rl * QS + gl] = to_t<T>(pq.x);
+                    q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
+                }
+                float* pw = part + w * nq * 64 + gl;
+                if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
+                    pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
+                                                          csduz[0].x + csduz[0].y);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 1 + CM; ++c)
+                        if (c <= C) {
+                            const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
+                            if (lane < 16) pw[c * 64] = v;
+                        }
+                    {
+                        const float v = sum_rowgroups(csdu.x + csdu.y);
+                        if (lane < 16) pw[(1 + C) * 64] = v;
+                    }
+#pragma unroll
+                    for (int qq = 0; qq < RM; ++qq)
+                        if (qq < R) {
+                            const float v = sum_rowgroups(csduz[qq].x + csduz[qq].y);
+                            if (lane < 16) pw[(2 + C + qq) * 64] = v;
+                        }
+                }
             }
+        };
+        if (!(d.dbg & 2)) {
+            if (row0 + 16 <= d.B && 64 * t + 64 <= d.D) epilogue(std::false_type{});
+            else epilogue(std::true_type{});
         }
         wave_sync();
         for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
@@ -971,14 +988,13 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     // ---- per-row outputs ----
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        float E = Eacc2[r >> 1][r & 1], Pp = Pacc2[r >> 1][r & 1];
+        float E = Eacc2[r >> 1][r & 1];
         float dz2[RM];
 #pragma unroll
         for (int q = 0; q < RM; ++q) dz2[q] = dzn2[r >> 1][q][r & 1];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
             E += __shfl_xor(E, o, 64);
-            Pp += __shfl_xor(Pp, o, 64);
 #pragma unroll
             for (int q = 0; q < RM; ++q) dz2[q] += __shfl_xor(dz2[q], o, 64);
         }
@@ -986,7 +1002,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         if ((lane & 15) == 0) {
             float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
             rp[0] = E;
-            rp[1] = Pp;
+            rp[1] = 0.f;  // unused slot (sum_g p_bg = 1: k_latent_bwd)
             for (int q = 0; q < R; ++q) rp[2 + q] = dz2[q < RM ? q : 0];
         }
 #pragma unroll
@@ -996,7 +1012,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             dp[KP] = dzP[lb][r];
         }
     }
-    const float lw = wave_sum(lossacc + (lossd2.x + lossd2.y));
+    const float lw = wave_sum(fmaf(0.6931471805599453f, lossd2.x + lossd2.y, lossacc));
     __syncthreads();
     if (lane == 0) part[w] = lw;
     __syncthreads();
@@ -1067,11 +1083,8 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         const int b = bw + c;
         float* L = lat + (int64_t)b * d.lat_stride;
         const bool valid = (b < d.Bpad) && L[d.LAT_VALID] > 0.f;
-        float E = 0.f, Ps = 0.f;
-        for (int s2 = 0; s2 < d.nsD; ++s2) {
-            E += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
-            Ps += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R) + 1];
-        }
+        float E = 0.f;
+        for (int s2 = 0; s2 < d.nsD; ++s2) E += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
         const float wb = L[d.LAT_W];
         float dmean = 0.f, da = 0.f, h = 0.f;
         if (k < K) {
@@ -1130,7 +1143,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
             if (valid) rbne += dhn;
         }
         if (k == 0 && b < d.Bpad) {
-            const float dd = (E + Ps) * d.inv_n;   // dL/dd_b = sum_g dmu' p
+            const float dd = (E + 1.f) * d.inv_n;   // dL/dd_b = sum_g dmu' p = (E_b + sum_g p_bg) / n, sum p = 1
             const float pre = rx[0];
             const float dpre = valid ? dd * dsoftplus(pre) : 0.f;
             L[d.LAT_DPRE] = dpre;
