@@ -212,9 +212,10 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         build_registry_nb(e);
     }
 
-    // gene splits: enough workgroups to fill 256 CUs twice, LDS column accumulators <= 40 KB
-    auto pick_split = [&](int nq) {
-        int ns = (int)((512 + e->nrb_max - 1) / e->nrb_max);
+    // gene splits: enough workgroups for `per_cu` resident workgroups on each of the 256 CUs
+    // (the occupancy the kernel's LDS / VGPR budget allows), LDS column accumulators <= 40 KB
+    auto pick_split = [&](int nq, int per_cu) {
+        int ns = (int)((256 * per_cu + e->nrb_max - 1) / e->nrb_max);
         if (ns < 1) ns = 1;
         const int tps_max = (int)(40 * 1024 / (nq * 64 * 4));
         const int ns_min = (int)((e->NT + tps_max - 1) / tps_max);
@@ -223,10 +224,12 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         if (ns > 64) ns = 64;
         return ns;
     };
-    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R));
+    // NB pass B holds ~75 KB of LDS per workgroup (2 per CU); the vMF decoder and the shared
+    // encoder kernels fit 3 (measured: 12 splits at 64 row blocks beat 8 and 16)
+    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R), cfg->model == MMVAE_MODEL_VMF ? 3 : 2);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
-    e->nsplit_e = pick_split((int)(2 + e->H));
+    e->nsplit_e = pick_split((int)(2 + e->H), 3);
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
     auto env_split = [&](const char* name, int& v) {
         if (const char* ev = std::getenv(name)) {

@@ -455,7 +455,7 @@ struct DecPtrs {
     const void* WdP;  // [DP][KP] T
     const void* WdT;  // [KP][DP] T
     float* lsep;      // [nsA][Bpad][2]
-    float* rowfin;    // [Bpad][2]: lse (log2 units) after pass A, w_b E_b after pass B
+    float* rowfin;    // [Bpad][2]: lse (log2 units), published by k_dec_nb for pass C
     float* rowB;      // [nsD][Bpad][2+R]
     float* dzp;       // [nsD][Bpad][2][KP]
     float* slabB;     // [nrb][nqB][DP]
@@ -488,6 +488,16 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
 
+    if (PASS == 2) {  // w_b E_b from pass B's per-split row sums, 4 threads per row
+        const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
+        const int b = rb * 64 + rr;
+        float E = 0.f;
+        for (int s2 = pp; s2 < d.nsD; s2 += 4) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + d.R)];
+        E += __shfl_xor(E, 1, 64);
+        E += __shfl_xor(E, 2, 64);
+        if (pp == 0) part[rr] = Q.lat[(int64_t)b * d.lat_stride + d.LAT_W] * E;
+        __syncthreads();
+    }
     Fr zfr[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -499,8 +509,8 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
 #pragma unroll
         for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
-        lse2[r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;      // k_rowfin<0>
-        wE[r] = (PASS == 2) ? Q.rowfin[2 * b + 1] : 0.f;    // k_rowfin<1>
+        lse2[r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;      // written by k_dec_nb (split 0)
+        wE[r] = (PASS == 2) ? part[16 * w + 4 * (lane >> 4) + r] : 0.f;
         mrun[r] = -1e30f;
         srun[r] = 0.f;
     }
@@ -718,6 +728,29 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    // row log-sum-exp (log2 units) from pass A's split partials, 4 threads per row; split 0
+    // also publishes it for pass C
+    {
+        const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
+        const int b = rb * 64 + rr;
+        float mm = -INFINITY;
+        for (int s2 = pp; s2 < d.nsA; s2 += 4) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
+        mm = fmaxf(mm, __shfl_xor(mm, 1, 64));
+        mm = fmaxf(mm, __shfl_xor(mm, 2, 64));
+        float ss = 0.f;
+        for (int s2 = pp; s2 < d.nsA; s2 += 4) {
+            const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
+            ss += lp[1] * expf(lp[0] - mm);
+        }
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        if (pp == 0) {
+            const float l2 = (mm + logf(ss)) * L2E;
+            part[rr] = l2;
+            if (sp == 0) Q.rowfin[2 * b] = l2;
+        }
+        __syncthreads();
+    }
     // rows 4(lane>>4) + 2h + j live in component j of the pair h (packed f32 epilogue)
     float lse2[4];
     f2 rv2[2], dv2[2], wv2[2], crow2[2][CM], znu2[2][RM];
@@ -730,7 +763,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         rv2[h][j] = Lr[d.LAT_VALID];
         dv2[h][j] = Lr[d.LAT_D];
         wv2[h][j] = Lr[d.LAT_W];
-        lse2[r] = Q.rowfin[2 * b];
+        lse2[r] = part[16 * w + 4 * (lane >> 4) + r];
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
 #pragma unroll
         for (int c = 0; c < CM; ++c) crow2[h][c][j] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
@@ -1686,26 +1719,6 @@ hipError_t nb_prepare_frozen(Engine* e) {
 // Per-row finalisation between decoder passes (one thread per row):
 //   MODE 0: combine pass A's per-split (max, sum-exp) -> log-sum-exp in log2 units
 //   MODE 1: E_b = sum over pass-B splits, stored as w_b E_b for pass C
-template <int MODE>
-__global__ __launch_bounds__(256) void k_rowfin(DecPtrs Q, Dims d) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= d.Bpad) return;
-    if (MODE == 0) {
-        float mm = -INFINITY;
-        for (int s2 = 0; s2 < d.nsA; ++s2) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
-        float ss = 0.f;
-        for (int s2 = 0; s2 < d.nsA; ++s2) {
-            const float* lp = Q.lsep + ((int64_t)s2 * d.Bpad + b) * 2;
-            ss += lp[1] * expf(lp[0] - mm);
-        }
-        Q.rowfin[2 * b] = (mm + logf(ss)) * 1.4426950408889634f;
-    } else {
-        float E = 0.f;
-        for (int s2 = 0; s2 < d.nsD; ++s2) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + d.R)];
-        Q.rowfin[2 * b + 1] = Q.lat[(int64_t)b * d.lat_stride + d.LAT_W] * E;
-    }
-}
-
 static size_t dec_lds(const Dims& d, int pass, bool bf16) {
     const int nq = 1 + d.C;
     size_t s = 2 * ((size_t)64 * d.KP * (bf16 ? 2 : 4) + 1024);  // double-buffered W + grec stage
@@ -1791,10 +1804,6 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         else hipLaunchKernelGGL((k_dec_lse<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
     }
     {
-        ScopedTimer tm(e, "k_rowfin");
-        hipLaunchKernelGGL(k_rowfin<0>, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, Q, d);
-    }
-    {
         ScopedTimer tm(e, "k_dec_nb");
         const int nqB = (1 + d.C) + 1 + d.R;
         const int csz = bf ? 4 : 8;
@@ -1811,10 +1820,6 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         hipLaunchKernelGGL(k_grad_small, dim3(1), dim3(256), 0, st, d, e->d_small, 0, G, e->d_smallg, e->d_lossp,
                            (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
         return hipGetLastError();
-    }
-    {
-        ScopedTimer tm(e, "k_rowfin");
-        hipLaunchKernelGGL(k_rowfin<1>, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_dec_tail");

@@ -15,8 +15,9 @@
 //   k_vlatent_fwd  h = that / ||l|| - mvec, heads, clamp, reparameterise, KL
 //   k_vkappa       kappa = clamp(exp(ln_kappa)), lbessel terms (one thread)
 //   k_vdec<0>      logits on MFMA, u = exp, v = u + hc: row sums |v|^2, sum v, sum l v
-//   k_vrowfin      cos_b = <y_b, r_b>, per-row backward coefficients alpha_b, beta_b
-//   k_vdec<1>      dv = alpha (l + eps) + beta v, da = dv u: column sums + dz GEMM on MFMA
+//   k_vdec<1>      per-row cos_b, alpha_b, beta_b from the pass-0 split sums (vrow_coeffs);
+//                  dv = alpha (l + eps) + beta v, da = dv u: column sums + dz GEMM on MFMA
+//   (k_vrowfin     the same row coefficients, eval path only)
 //   k_vlatent_bwd  heads backward, KL grads, dh (scaled by 1/||l|| for the encoder)
 //   k_enc_bwd      sum_k W~ (dh/||l||)^T log1p(x)                (shared with NB)
 //   k_vgrad_small / k_vgrad_genes   fixed-order reductions into the flat gradient
@@ -312,11 +313,52 @@ struct VDecPtrs {
     const int32_t* rtp;
     const void* WdP;       // [DP][KP] T
     const void* WdT;       // [KP][DP] T
-    const float* rowfin;   // [Bpad][2]: alpha, beta
+    const float* rowfin;   // [Bpad][2]: alpha, beta (eval path: k_vrowfin)
     float* rowB;           // [nsD][Bpad][3]: |v|^2, sum v, sum l v
+    const float* rowx;     // [Bpad][..]: [1] = sum (l^2 + 2 eps l)
+    const float* vk;       // kappa scalars (k_vkappa)
+    float* rowcos;         // [Bpad] cos_b (written by split 0 of the backward pass)
     float* dzp;            // [nsD][Bpad][KP]
     float* slabB;          // [nrb][1+C][DP]
 };
+
+// Per-row combine of pass 0's split sums (threads p0, p0 + np, ... of a row's np-thread group,
+// combined with xor-shuffles over the group) -> alpha_b, beta_b, cos_b (vmf.hh:422-432):
+//   alpha_b = -(kappa/n) / (nv ny),  beta_b = (kappa/n) cos_b / nv^2
+// (below the normalize eps, r = v / eps and the clamp passes no gradient: beta = 0).
+MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ lat, const float* __restrict__ rowx,
+                           const float* __restrict__ rowB, const float* __restrict__ vk, int b, int p0, int np,
+                           float& al, float& be, float& cosb) {
+    float Svv = 0.f, Sv = 0.f, Slv = 0.f;
+    for (int s = p0; s < d.nsD; s += np) {
+        const float* rp = rowB + ((int64_t)s * d.Bpad + b) * 3;
+        Svv += rp[0];
+        Sv += rp[1];
+        Slv += rp[2];
+    }
+    for (int o = 1; o < np; o <<= 1) {
+        Svv += __shfl_xor(Svv, o, 64);
+        Sv += __shfl_xor(Sv, o, 64);
+        Slv += __shfl_xor(Slv, o, 64);
+    }
+    const bool valid = lat[(int64_t)b * d.lat_stride + d.LAT_VALID] > 0.f;
+    const float nvr = sqrtf(Svv);
+    const float nv = fmaxf(nvr, 1e-12f);
+    const float ny = fmaxf(sqrtf(rowx[(int64_t)b * d.rowx_stride + 1] + (float)d.D * epsD * epsD), 1e-12f);
+    cosb = (Slv + epsD * Sv) / (ny * nv);
+    const float kn = vk[VK_KAPPA] * d.inv_n;
+    al = -kn / (nv * ny);
+    be = kn * cosb / (nv * nv);
+    if (!(nvr >= 1e-12f)) {
+        al = -kn / (1e-12f * ny);
+        be = 0.f;
+    }
+    if (!valid) {
+        al = 0.f;
+        be = 0.f;
+        cosb = 0.f;
+    }
+}
 
 struct VDecLds {
     int o_g, o_t, o_part, o_wave, o_q1, o_rtl, o_rbl, o_rinc, wave_bytes, bytes;
@@ -370,6 +412,18 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
 
+    if (PASS) {  // the per-row backward coefficients from pass 0's split sums (k_vrowfin), 4 threads per row
+        const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
+        const int b = rb * 64 + rr;
+        float al, be, cosb;
+        vrow_coeffs(d, epsD, Q.lat, Q.rowx, Q.rowB, Q.vk, b, pp, 4, al, be, cosb);
+        if (pp == 0) {
+            part[2 * rr] = al;
+            part[2 * rr + 1] = be;
+            if (sp == 0) Q.rowcos[b] = cosb;
+        }
+        __syncthreads();
+    }
     Fr zfr[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -381,8 +435,8 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
 #pragma unroll
         for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
-        ra[r] = PASS ? Q.rowfin[2 * b] : 0.f;
-        rbt[r] = PASS ? Q.rowfin[2 * b + 1] : 0.f;
+        ra[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r)] : 0.f;
+        rbt[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r) + 1] : 0.f;
         svv[r] = 0.f;
         sv[r] = 0.f;
         slv[r] = 0.f;
@@ -547,27 +601,11 @@ __global__ __launch_bounds__(256) void k_vrowfin(Dims d, float epsD, const float
                                                  float* __restrict__ rowcos) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= d.Bpad) return;
-    float Svv = 0.f, Sv = 0.f, Slv = 0.f;
-    for (int s = 0; s < d.nsD; ++s) {
-        const float* rp = rowB + ((int64_t)s * d.Bpad + b) * 3;
-        Svv += rp[0];
-        Sv += rp[1];
-        Slv += rp[2];
-    }
-    const bool valid = lat[(int64_t)b * d.lat_stride + d.LAT_VALID] > 0.f;
-    const float nvr = sqrtf(Svv);
-    const float nv = fmaxf(nvr, 1e-12f);
-    const float ny = fmaxf(sqrtf(rowx[(int64_t)b * d.rowx_stride + 1] + (float)d.D * epsD * epsD), 1e-12f);
-    const float cosb = (Slv + epsD * Sv) / (ny * nv);
-    const float kn = vk[VK_KAPPA] * d.inv_n;
-    float al = -kn / (nv * ny), be = kn * cosb / (nv * nv);
-    if (!(nvr >= 1e-12f)) {
-        al = -kn / (1e-12f * ny);
-        be = 0.f;
-    }
-    rowfin[2 * b] = valid ? al : 0.f;
-    rowfin[2 * b + 1] = valid ? be : 0.f;
-    rowcos[b] = valid ? cosb : 0.f;
+    float al, be, cosb;
+    vrow_coeffs(d, epsD, lat, rowx, rowB, vk, b, 0, 1, al, be, cosb);
+    rowfin[2 * b] = al;
+    rowfin[2 * b + 1] = be;
+    rowcos[b] = cosb;
 }
 
 // =======================================================================================
@@ -972,6 +1010,9 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
     Q.rowfin = e->d_rowfin;
     Q.rowB = e->d_rowB;
+    Q.rowx = e->d_rowx;
+    Q.vk = e->d_vk;
+    Q.rowcos = e->d_rowv;
     Q.dzp = e->d_dzp;
     Q.slabB = e->d_slabB;
     const dim3 gdec(nrb * d.nsD);
@@ -983,14 +1024,14 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
         else hipLaunchKernelGGL((k_vdec_fwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
-    {
-        ScopedTimer tm(e, "k_vrowfin");
-        hipLaunchKernelGGL(k_vrowfin, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, d, sc.epsD, e->d_lat, e->d_rowx,
-                           e->d_rowB, e->d_vk, e->d_rowfin, e->d_rowv);
-    }
     VGrads G = vmf_grads(e);
     const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K;
-    if (!update) {
+    if (!update) {  // eval: cos_b for the loss (the update path derives it inside k_vdec_bwd)
+        {
+            ScopedTimer tm(e, "k_vrowfin");
+            hipLaunchKernelGGL(k_vrowfin, dim3((d.Bpad + 255) / 256), dim3(256), 0, st, d, sc.epsD, e->d_lat,
+                               e->d_rowx, e->d_rowB, e->d_vk, e->d_rowfin, e->d_rowv);
+        }
         ScopedTimer tm(e, "k_loss");
         hipLaunchKernelGGL(k_vgrad_small, dim3(1), dim3(256), 0, st, d, sc, e->d_small, 0, G, e->d_smallg, e->d_rowv,
                            e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 0);

@@ -10,7 +10,7 @@ eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 for i in range(3):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)
-nwg = (B // 64) * eng_ns if (eng_ns := int(os.environ.get("NSE", "8"))) else 0
+nwg = (B // 64) * eng_ns if (eng_ns := int(os.environ.get("NSE", "12"))) else 0
 buf = np.zeros(nwg * 16, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 0, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
