@@ -370,7 +370,8 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     HIPCHK(e, dalloc(&e->d_rowptr, N + 1));
     HIPCHK(e, dalloc(&e->d_col, nnz));
     HIPCHK(e, dalloc(&e->d_val, nnz));
-    HIPCHK(e, dalloc(&e->d_covar, N * e->C));
+    HIPCHK(e, dalloc(&e->d_covar, (N + 1) * e->C));  // row N: zeros (padding rows)
+    HIPCHK(e, hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C));
     HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice));
     if (nnz > 0) {
         HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
@@ -556,8 +557,11 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         if (c < 0 || c >= e->N) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
         e->h_cells_pin[j] = c;
     }
-    const int64_t Bp = (B + 63) / 64 * 64;
-    for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = -1;
+    // padding rows (up to the handle's padded max batch: the latent-head grids cover it) point
+    // at row N: the empty row of the dataset index, a zero covariate row and rowptr[N] — so
+    // every per-row load in the kernels is unconditional
+    const int64_t Bp = e->Bpad;
+    for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = e->N;
     HIPCHK(e, hipMemcpyAsync(e->d_cells, e->h_cells_pin, sizeof(int64_t) * Bp, hipMemcpyHostToDevice, e->stream));
     return MMVAE_OK;
 }

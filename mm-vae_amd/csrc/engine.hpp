@@ -44,7 +44,7 @@ struct Engine {
     int64_t* d_rowptr = nullptr;
     int32_t* d_col = nullptr;
     float* d_val = nullptr;
-    float* d_covar = nullptr;  // [N][C]
+    float* d_covar = nullptr;  // [N+1][C], row N = zeros (padding rows)
 
     // ---- parameters ----
     std::vector<ParamSlot> slots;

@@ -144,8 +144,8 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
-        rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        rbl[lane] = rowptr[cell];
     }
     for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
     wave_sync();
@@ -360,14 +360,14 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
-        const bool valid = cell >= 0;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        const bool valid = b < d.B;
         float* L = lat + (int64_t)b * d.lat_stride;
         const float h = sH[(4 * w + c) * 68 + k];
         float mn = mean[c], a = av[c];
         if (k < K && mode == 0) {
             float cm = P.bce[k];
-            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * (valid ? covar[cell * d.C + q] : 0.f);
+            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
             mn += cm;
         }
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
@@ -506,9 +506,9 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int b = row0 + 4 * (lane >> 4) + r;
-        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
         lse2[r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;      // written by k_dec_nb (split 0)
         wE[r] = (PASS == 2) ? part[16 * w + 4 * (lane >> 4) + r] : 0.f;
         mrun[r] = -1e30f;
@@ -764,9 +764,9 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         dv2[h][j] = Lr[d.LAT_D];
         wv2[h][j] = Lr[d.LAT_W];
         lse2[r] = part[16 * w + 4 * (lane >> 4) + r];
-        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow2[h][c][j] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        for (int c = 0; c < CM; ++c) crow2[h][c][j] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
 #pragma unroll
         for (int q = 0; q < RM; ++q) {
             znu2[h][q][j] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
@@ -790,15 +790,15 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
-        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
-        rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
+        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
+        rbl[lane] = Q.rowptr[cell];
         const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
         float* rs = rsc + lane * NRS;
         rs[0] = Lr[d.LAT_D];
         rs[1] = Lr[d.LAT_W];
         rs[2] = Lr[d.LAT_VALID];
         for (int q = 0; q < RM; ++q) rs[3 + q] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
-        for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C) ? Q.covar[cell * C + c] : 0.f;
     }
     for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
 
@@ -1141,10 +1141,10 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         sH[(4 * w + c) * 68 + k] = h;
         rbm += dmean;
         rbl += da;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
 #pragma unroll
         for (int q = 0; q < CMAX; ++q)
-            if (q < C && cell >= 0) rWce[q] += dmean * covar[cell * C + q];
+            if (q < C) rWce[q] += dmean * covar[cell * C + q];
         // ---- overdispersion path (lanes < R) and depth (lane 0) ----
         const float* rx = rowx + (int64_t)b * d.rowx_stride;
         float dnm = 0.f, dan = 0.f;
@@ -1349,12 +1349,13 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
-        rbl[lane] = cell >= 0 ? rowptr[cell] : 0;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        rbl[lane] = rowptr[cell];
         if (RAW) {
             const float* Lr = lat + (int64_t)b * d.lat_stride;
-            scal[16 * w + lane] = cell >= 0 ? Lr[d.LAT_DPRE] : 0.f;
-            for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = cell >= 0 ? Lr[d.LAT_DHNU + h] : 0.f;
+            const float ok = (b < d.B) ? 1.f : 0.f;
+            scal[16 * w + lane] = ok * Lr[d.LAT_DPRE];
+            for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = ok * Lr[d.LAT_DHNU + h];
         }
     }
     // this wave's 16 cell columns of both tiles

@@ -115,7 +115,8 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     if ((er = hipMalloc(&e->d_rowptr, sizeof(int64_t) * (N + 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_col, sizeof(int32_t) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_val, sizeof(float) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
-    if ((er = hipMalloc(&e->d_covar, sizeof(float) * N * e->C)) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_covar, sizeof(float) * (N + 1) * e->C)) != hipSuccess) return er;  // row N: zeros
+    if ((er = hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C)) != hipSuccess) return er;
     hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice);
     std::vector<float> ones((size_t)N * e->C, 1.f);
     hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice);

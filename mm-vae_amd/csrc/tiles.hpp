@@ -53,9 +53,8 @@ MMVAE_DEV void fill_rtl(int32_t* rtl, int S, int t0, int NT, int B, int Ncells, 
     for (int i = lane; i < 16 * S; i += 64) {
         const int rr = i / S, tt = i % S;
         const int b = row0 + rr;
-        const int64_t cell = (b < B) ? cells[b] : -1;
-        const int64_t crow = cell >= 0 ? cell : (int64_t)Ncells;
-        rtl[i] = (t0 + tt <= NT) ? rtp[crow * (NT + 1) + t0 + tt] : 0;
+        const int64_t crow = cells[b];  // padding rows hold the empty row Ncells
+        rtl[i] = rtp[crow * (NT + 1) + min(t0 + tt, NT)];
     }
 }
 

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
         // row norms from the dataset index (row Ncells = the empty padding row)
-        const float2 cn = cellnorm[(b < d.B) ? cells[b] : (int64_t)d.Ncells];
+        const float2 cn = cellnorm[cells[b]];
         inx[c] = 1.f / fmaxf(sqrtf(cn.x), 1e-12f);  // F::normalize
         if (mode == 0 && k == 0) {
             rowx[(int64_t)b * d.rowx_stride] = cn.x;
@@ -208,15 +208,15 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
-        const bool valid = cell >= 0;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        const bool valid = b < d.B;
         float* L = lat + (int64_t)b * d.lat_stride;
         const float h = sH[(4 * w + c) * 68 + k];
         float mn = mean[c];
         const float a = av[c];
         if (k < K && mode == 0) {
             float cm = P.bce[k];
-            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * (valid ? covar[cell * d.C + q] : 0.f);
+            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
             mn += cm;
         }
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
@@ -432,9 +432,9 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int b = row0 + 4 * (lane >> 4) + r;
-        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
+        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C && cell >= 0) ? Q.covar[cell * C + c] : 0.f;
+        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
         ra[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r)] : 0.f;
         rbt[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r) + 1] : 0.f;
         svv[r] = 0.f;
@@ -447,8 +447,8 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
-        const int64_t cell = (b < d.B) ? Q.cells[b] : -1;
-        rbl[lane] = cell >= 0 ? Q.rowptr[cell] : 0;
+        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
+        rbl[lane] = Q.rowptr[cell];
     }
 
     RegStage<64, RBW> wreg;
@@ -668,10 +668,10 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         sH[(4 * w + c) * 68 + k] = h;
         rbm += dmean;
         rbl += da;
-        const int64_t cell = (b < d.B) ? cells[b] : -1;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
 #pragma unroll
         for (int q = 0; q < CMAX; ++q)
-            if (q < C && cell >= 0) rWce[q] += dmean * covar[cell * C + q];
+            if (q < C) rWce[q] += dmean * covar[cell * C + q];
     }
     __syncthreads();
     float* wp = wpart[w];
