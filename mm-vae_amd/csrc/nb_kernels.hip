@@ -1257,8 +1257,8 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
             for (int q = 0; q < 16; ++q) {
                 const int j2 = 16 * w + q;
                 if (j2 < K) {
-                    out[k * K + j2] = gm[q];
-                    out[K * K + k * K + j2] = gl[q];
+                    out[j2 * K + k] = gm[q];  // transposed: lanes store consecutive floats
+                    out[K * K + j2 * K + k] = gl[q];
                 }
             }
         }
@@ -1484,15 +1484,14 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
         return;
     }
     if (!with_grads) return;
-    const int i = (blockIdx.x - 1) * 256 + threadIdx.x;
-    if (i >= SMALL) return;
-    float s = 0.f;
-#pragma unroll 8
-    for (int wg = 0; wg < nwg; ++wg) s += small[(int64_t)wg * SMALL + i];
+    __shared__ float red[8][32];
+    const int i = (blockIdx.x - 1) * 32 + (threadIdx.x & 31);
+    const float s = sum_partials(small, nwg, SMALL, i, red);
+    if ((threadIdx.x >> 5) != 0 || i >= SMALL) return;
     int o = i;
-    if (o < K * K) { G.Wm[o] = s; return; }
+    if (o < K * K) { G.Wm[(o % K) * K + o / K] = s; return; }  // partials are [j][k]
     o -= K * K;
-    if (o < K * K) { G.Wl[o] = s; return; }
+    if (o < K * K) { G.Wl[(o % K) * K + o / K] = s; return; }
     o -= K * K;
     if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
     o -= K;
@@ -1848,7 +1847,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         ScopedTimer tm(e, "k_grad_small");
         const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
-        hipLaunchKernelGGL(k_grad_small, dim3(1 + (SMALL + 255) / 256), dim3(256), 0, st, d, e->d_small,
+        hipLaunchKernelGGL(k_grad_small, dim3(1 + (SMALL + 31) / 32), dim3(256), 0, st, d, e->d_small,
                            e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg,
                            e->d_out, 1);
     }

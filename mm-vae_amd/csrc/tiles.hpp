@@ -217,6 +217,25 @@ MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int 
 // log1p of a count: exact libm form in the f32 parity mode, fast form for bf16 tiles
 template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : log1p_pos(x); }
 
+// Fixed-order sum over nwg per-workgroup partials [nwg][SMALL] for output i: a 256-thread block
+// covers 32 outputs x 8 workgroup chunks (each thread's loads independent, 16 in flight), the
+// chunk sums combined in chunk order through LDS.  Valid in threads 0..31 (threadIdx.x >> 5 == 0).
+MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL, int i, float (*red)[32]) {
+    const int col = threadIdx.x & 31, ch = threadIdx.x >> 5;
+    float s = 0.f;
+    if (i < SMALL) {
+#pragma unroll 16
+        for (int wg = ch; wg < nwg; wg += 8) s += small[(int64_t)wg * SMALL + i];
+    }
+    red[ch][col] = s;
+    __syncthreads();
+    float t = 0.f;
+    if (ch == 0)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) t += red[c][col];
+    return t;
+}
+
 // LDS carve shared by the two encoder kernels (host computes the same size)
 struct EncLds {
     int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;
