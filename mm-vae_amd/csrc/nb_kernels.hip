@@ -514,25 +514,22 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         mrun[r] = -1e30f;
         srun[r] = 0.f;
     }
-    auto stage = [&](int t, int buf) {
-        char* sb = stg + buf * STB;
-        const char* Wt = WdPc + (int64_t)64 * t * RB;
-        for (int pc = w; pc <= NCH; pc += 4) {
-            if (pc < NCH) {
-                const int pos = pc * 1024 + lane * 16;
-                const int g = pos / RB, cp = (pos % RB) >> 4;
-                glds16(Wt + g * RB + ((cp ^ ((g >> 1) & (NCH - 1))) << 4), sb + pc * 1024);
-            } else {
-                glds16(grec + 64 * t + lane, sb + 64 * RB);
-            }
-        }
+    // Register-staged decoder tiles, two in flight: tile t + 2 is loaded while tile t is
+    // computed from LDS, tile t + 1 (loaded an iteration earlier) is written to the other LDS
+    // buffer at the end — one LDS barrier per tile, no vmcnt(0) drain of a fresh DMA.
+    RegStage<64, RB> wrA, wrB;
+    float4 grA = float4{0.f, 0.f, 0.f, 0.f}, grB = grA;
+    auto ld = [&](RegStage<64, RB>& R, float4& G, int t) {
+        R.load(WdPc + (int64_t)64 * t * RB, RB);
+        if (threadIdx.x < 64) G = grec[64 * t + threadIdx.x];
     };
-    if (t0 < t1) stage(t0, 0);
-    vm_wait_all();
-    __syncthreads();
-    for (int t = t0; t < t1; ++t) {
+    auto st = [&](const RegStage<64, RB>& R, const float4& G, int buf) {
+        R.store(stg + buf * STB);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(stg + buf * STB + 64 * RB)[threadIdx.x] = G;
+    };
+    auto tile = [&](int t, RegStage<64, RB>& hold, float4& ghold, RegStage<64, RB>& nxt, float4& gnxt) {
         const int buf = (t - t0) & 1;
-        stage(min(t + 1, t1 - 1), buf ^ 1);  // unconditional: the last one re-stages a tile nobody reads
+        ld(nxt, gnxt, min(t + 2, t1 - 1));  // unconditional (clamped): counted waits
         const char* sb = stg + buf * STB;
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
@@ -589,7 +586,8 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 }
             }
         }
-        __syncthreads();  // drains this wave's LDS-DMA for t+1; frees buffer `buf`
+        if (t + 1 < t1) st(hold, ghold, buf ^ 1);
+        lds_barrier();
         if (PASS == 2) {
             const float* pb = part + (buf * 4 * nq) * 64;
             for (int i = threadIdx.x; i < nq * 64; i += 256) {
@@ -598,6 +596,16 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                     pb[(0 * nq + q) * 64 + g] + pb[(1 * nq + q) * 64 + g] + pb[(2 * nq + q) * 64 + g] + pb[(3 * nq + q) * 64 + g];
             }
         }
+    };
+    if (t0 < t1) {
+        ld(wrA, grA, t0);
+        ld(wrB, grB, min(t0 + 1, t1 - 1));
+        st(wrA, grA, 0);
+    }
+    __syncthreads();
+    for (int t = t0; t < t1; t += 2) {
+        tile(t, wrB, grB, wrA, grA);
+        if (t + 1 < t1) tile(t + 1, wrA, grA, wrB, grB);
     }
     if (PASS == 0) {
 #pragma unroll
