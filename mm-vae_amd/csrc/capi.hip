@@ -699,13 +699,17 @@ int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms
 }
 
 int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
-    if (!e || !host || n < 0 || which < 0 || which > 1) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
-    // 0: encoder split partials (k_enc_fwd stamps), 1: decoder dz partials (k_dec_nb stamps)
-    const int64_t cap = which == 0 ? (int64_t)e->nsplit_e * e->Bpad * e->KP : (int64_t)e->nsplit_d * e->Bpad * 2 * e->KP;
+    if (!e || !host || n < 0 || which < 0 || which > 2) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
+    // 0: encoder split partials (k_enc_fwd stamps), 1: decoder dz partials (k_dec_nb stamps),
+    // 2: pass-C column slab (k_dec_lse stamps)
+    const int64_t cap = which == 0   ? (int64_t)e->nsplit_e * e->Bpad * e->KP
+                        : which == 1 ? (int64_t)e->nsplit_d * e->Bpad * 2 * e->KP
+                                     : (int64_t)e->nrb_max * (1 + e->C) * e->DP;
     if (n > cap) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds the workspace");
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipMemcpy(host, which == 0 ? e->d_hpart : e->d_dzp, sizeof(float) * n, hipMemcpyDeviceToHost));
+    const float* src = which == 0 ? e->d_hpart : which == 1 ? e->d_dzp : e->d_slabC;
+    HIPCHK(e, hipMemcpy(host, src, sizeof(float) * n, hipMemcpyDeviceToHost));
     return MMVAE_OK;
 }
 

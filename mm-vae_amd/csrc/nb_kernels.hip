@@ -527,6 +527,16 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         R.store(stg + buf * STB);
         if (threadIdx.x < 64) reinterpret_cast<float4*>(stg + buf * STB + 64 * RB)[threadIdx.x] = G;
     };
+    // diagnostic (MMVAE_DBG & 256): per-wave phase cycles into slabC (outputs invalid)
+    const bool stamps = (d.dbg & 256) != 0;
+    uint64_t st_[3] = {0, 0, 0}, tp_ = 0;
+    auto lap = [&](int i_) {
+        if (stamps) {
+            const uint64_t tn = stamp_now();
+            st_[i_] += tn - tp_;
+            tp_ = tn;
+        }
+    };
     auto tile = [&](int t, RegStage<64, RB>& hold, float4& ghold, RegStage<64, RB>& nxt, float4& gnxt) {
         const int buf = (t - t0) & 1;
         ld(nxt, gnxt, min(t + 2, t1 - 1));  // unconditional (clamped): counted waits
@@ -586,8 +596,10 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 }
             }
         }
+        lap(0);
         if (t + 1 < t1) st(hold, ghold, buf ^ 1);
         lds_barrier();
+        lap(1);
         if (PASS == 2) {
             const float* pb = part + (buf * 4 * nq) * 64;
             for (int i = threadIdx.x; i < nq * 64; i += 256) {
@@ -603,9 +615,21 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         st(wrA, grA, 0);
     }
     __syncthreads();
+    if (stamps) tp_ = stamp_now();
     for (int t = t0; t < t1; t += 2) {
         tile(t, wrB, grB, wrA, grA);
+        lap(2);
         if (t + 1 < t1) tile(t + 1, wrA, grA, wrB, grB);
+        lap(2);
+    }
+    if (stamps) {
+        if (lane == 0) {
+            float* o = Q.slabC + ((int64_t)blockIdx.x * 4 + w) * 4;
+            o[0] = (float)st_[0];
+            o[1] = (float)st_[1];
+            o[2] = (float)st_[2];
+        }
+        return;
     }
     if (PASS == 0) {
 #pragma unroll

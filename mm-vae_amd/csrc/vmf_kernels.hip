@@ -479,7 +479,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
         wave_sync();
         tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val,
-                   [&](int r, int gl, float x) { lt[r * LS + gl] = log1pf(fmaxf(x, 0.f)); });
+                   [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<T>(fmaxf(x, 0.f)); });
         wave_sync();
         tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
 #pragma unroll
