@@ -1216,38 +1216,24 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         }
     }
     __syncthreads();
-    // ---- dh for the wave's 4 cells (lane = j): 4 latents per step via 16-byte broadcasts ----
+    // ---- dh[16 cells][K] on f32 MFMA (wave w: latents 16w..16w+15) ----
     {
-        const int jj = (k < K) ? k : 0;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int k4 = 0; k4 < K; k4 += 4) {
-            float wm[4], wl[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                wm[u] = (k4 + u < K) ? sWm[(k4 + u) * 65 + jj] : 0.f;
-                wl[u] = (k4 + u < K) ? sWl[(k4 + u) * 65 + jj] : 0.f;
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 dm = *reinterpret_cast<const float4*>(&sDM[(4 * w + c) * 68 + k4]);
-                const float4 dl = *reinterpret_cast<const float4*>(&sDA[(4 * w + c) * 68 + k4]);
-                acc[c] = fmaf(dm.x, wm[0], fmaf(dm.y, wm[1], fmaf(dm.z, wm[2], fmaf(dm.w, wm[3], acc[c]))));
-                acc[c] = fmaf(dl.x, wl[0], fmaf(dl.y, wl[1], fmaf(dl.z, wl[2], fmaf(dl.w, wl[3], acc[c]))));
-            }
-        }
+        const f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, w, lane);
+        const int j = 16 * w + (lane & 15);
         float rdhs = 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = bw + c;
-            if (k < KP) {
-                const float v = (k < K) ? acc[c] : 0.f;
-                dh[(int64_t)b * KP + k] = v;
-                dhT_f[(int64_t)k * d.Bpad + b] = v;
-                dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)v;
+        for (int r = 0; r < 4; ++r) {
+            const int b = blockIdx.x * LAT_CELLS + 4 * (lane >> 4) + r;
+            if (j < KP) {
+                const float v = (j < K) ? acc[r] : 0.f;
+                dh[(int64_t)b * KP + j] = v;
+                dhT_f[(int64_t)j * d.Bpad + b] = v;
+                dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)v;
                 rdhs += v;
             }
         }
-        p_dhs[k] = rdhs;
+        rdhs = sum_rowgroups(rdhs);
+        if (lane < 16) p_dhs[j] = rdhs;  // the other waves' partials of latent j stay 0
     }
     p_dbm[k] = rbm;
     p_dbl[k] = rbl;
@@ -1263,38 +1249,9 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     }
     if (k < H) p_dbne[k] = rbne;
     if (k == 0) p_dbdp[0] = rbdp;
-    // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells (lane = k, wave w: j = 16w..16w+15) ----
+    // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells on f32 MFMA ----
     float* out = small + (int64_t)blockIdx.x * SMALL;
-    {
-        float gm[16], gl[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            gm[q] = 0.f;
-            gl[q] = 0.f;
-        }
-        const int kk = (k < K) ? k : 0;
-        for (int b = 0; b < LAT_CELLS; ++b) {
-            const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 16 * w + 4 * q4]);
-                gm[4 * q4 + 0] = fmaf(dm, h4.x, gm[4 * q4 + 0]); gm[4 * q4 + 1] = fmaf(dm, h4.y, gm[4 * q4 + 1]);
-                gm[4 * q4 + 2] = fmaf(dm, h4.z, gm[4 * q4 + 2]); gm[4 * q4 + 3] = fmaf(dm, h4.w, gm[4 * q4 + 3]);
-                gl[4 * q4 + 0] = fmaf(dl, h4.x, gl[4 * q4 + 0]); gl[4 * q4 + 1] = fmaf(dl, h4.y, gl[4 * q4 + 1]);
-                gl[4 * q4 + 2] = fmaf(dl, h4.z, gl[4 * q4 + 2]); gl[4 * q4 + 3] = fmaf(dl, h4.w, gl[4 * q4 + 3]);
-            }
-        }
-        if (k < K) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int j2 = 16 * w + q;
-                if (j2 < K) {
-                    out[j2 * K + k] = gm[q];  // transposed: lanes store consecutive floats
-                    out[K * K + j2 * K + k] = gl[q];
-                }
-            }
-        }
-    }
+    heads_dW(sDM, sDA, sH, K, w, lane, out);
     __syncthreads();
     // ---- the small vectors: fixed-order sum of the four waves' partials ----
     const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + K,
@@ -1521,9 +1478,9 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
     const float s = sum_partials(small, nwg, SMALL, i, red);
     if ((threadIdx.x >> 5) != 0 || i >= SMALL) return;
     int o = i;
-    if (o < K * K) { G.Wm[(o % K) * K + o / K] = s; return; }  // partials are [j][k]
+    if (o < K * K) { G.Wm[o] = s; return; }
     o -= K * K;
-    if (o < K * K) { G.Wl[(o % K) * K + o / K] = s; return; }
+    if (o < K * K) { G.Wl[o] = s; return; }
     o -= K * K;
     if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
     o -= K;

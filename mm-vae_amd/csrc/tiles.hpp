@@ -238,6 +238,57 @@ MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL
     return t;
 }
 
+// ---- latent-head backward products on f32 MFMA (exact f32 FMA chains) ------------------
+// LDS images of the workgroup's LAT_CELLS = 16 cells: sDM / sDA / sH [cell][68] (latents >= K
+// hold 0), the head weights sWm / sWl [k][65] (valid for k, j < K).
+// dh[cell][j] = sum_k dmean[cell][k] Wm[k][j] + da[cell][k] Wl[k][j]: wave w owns latents
+// j = 16 w + (lane & 15); returns the C-layout tile, acc[r] = dh[4 (lane >> 4) + r][j].
+MMVAE_DEV f32x4 heads_dh(const float* sDM, const float* sDA, const float* sWm, const float* sWl, int K, int w,
+                         int lane) {
+    const int j = 16 * w + (lane & 15), row = lane & 15, kq = lane >> 4;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; 4 * s < K; ++s) {
+        const int kk = 4 * s + kq;
+        const bool ok = kk < K && j < K;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sDM[row * 68 + kk], ok ? sWm[kk * 65 + j] : 0.f, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sDA[row * 68 + kk], ok ? sWl[kk * 65 + j] : 0.f, acc, 0, 0, 0);
+    }
+    return acc;
+}
+// Per-workgroup partials of dWm = dmean^T h and dWl = da^T h over the 16 cells: wave w owns
+// rows k = 16 w .. 16 w + 15; stored [k][j] into out[0 .. K*K) and out[K*K .. 2 K*K).
+MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int K, int w, int lane,
+                        float* __restrict__ out) {
+    const int kr = 16 * w + (lane & 15), cq = lane >> 4, jc = lane & 15;
+    f32x4 am[4], al[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+        am[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        al[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s = 0; s < LAT_CELLS / 4; ++s) {
+        const int c = 4 * s + cq;
+        const float a_m = sDM[c * 68 + kr], a_l = sDA[c * 68 + kr];
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            const float hb = sH[c * 68 + 16 * nb + jc];
+            am[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_m, hb, am[nb], 0, 0, 0);
+            al[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_l, hb, al[nb], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int kk = 16 * w + 4 * cq + r, jj = 16 * nb + jc;
+            if (kk < K && jj < K) {
+                out[kk * K + jj] = am[nb][r];
+                out[K * K + kk * K + jj] = al[nb][r];
+            }
+        }
+}
+
 // LDS carve shared by the two encoder kernels (host computes the same size)
 struct EncLds {
     int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;

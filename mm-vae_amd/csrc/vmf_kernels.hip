@@ -666,6 +666,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         sDM[(4 * w + c) * 68 + k] = dmean;
         sDA[(4 * w + c) * 68 + k] = da;
         sH[(4 * w + c) * 68 + k] = h;
+        if (k == 0) sH[(4 * w + c) * 68 + 64] = inx[c];  // 1/||l|| beside the cell's h
         rbm += dmean;
         rbl += da;
         const int64_t cell = cells[b];  // padding rows hold the empty row N
@@ -673,75 +674,33 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         for (int q = 0; q < CMAX; ++q)
             if (q < C) rWce[q] += dmean * covar[cell * C + q];
     }
+    for (int i = lane; i < NSM; i += 64) wpart[w][i] = 0.f;
     __syncthreads();
     float* wp = wpart[w];
-    {
-        const int jj = (k < K) ? k : 0;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int k4 = 0; k4 < K; k4 += 4) {
-            float wm[4], wl[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                wm[u] = (k4 + u < K) ? sWm[(k4 + u) * 65 + jj] : 0.f;
-                wl[u] = (k4 + u < K) ? sWl[(k4 + u) * 65 + jj] : 0.f;
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 dm = *reinterpret_cast<const float4*>(&sDM[(4 * w + c) * 68 + k4]);
-                const float4 dl = *reinterpret_cast<const float4*>(&sDA[(4 * w + c) * 68 + k4]);
-                acc[c] = fmaf(dm.x, wm[0], fmaf(dm.y, wm[1], fmaf(dm.z, wm[2], fmaf(dm.w, wm[3], acc[c]))));
-                acc[c] = fmaf(dl.x, wl[0], fmaf(dl.y, wl[1], fmaf(dl.z, wl[2], fmaf(dl.w, wl[3], acc[c]))));
-            }
-        }
+    {  // dh[16 cells][K] on f32 MFMA (wave w: latents 16w..16w+15), scaled by 1/||l|| for k_enc_bwd
+        const f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, w, lane);
+        const int j = 16 * w + (lane & 15);
         float rdhs = 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = bw + c;
-            if (k < KP) {
-                const float v = (k < K) ? acc[c] : 0.f;
-                const float vs = v * inx[c];
-                dhT_f[(int64_t)k * d.Bpad + b] = vs;
-                dhT_b[(int64_t)k * d.Bpad + b] = (__bf16)vs;
+        for (int r = 0; r < 4; ++r) {
+            const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
+            if (j < KP) {
+                const float v = (j < K) ? acc[r] : 0.f;
+                const float vs = v * sH[cl * 68 + 64];
+                dhT_f[(int64_t)j * d.Bpad + b] = vs;
+                dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)vs;
                 rdhs += v;
             }
         }
-        wp[128 + k] = rdhs;
+        rdhs = sum_rowgroups(rdhs);
+        if (lane < 16) wp[128 + j] = rdhs;  // the other waves' partials of latent j stay 0
     }
     wp[k] = rbm;
     wp[64 + k] = rbl;
 #pragma unroll
     for (int q = 0; q < CMAX; ++q) wp[192 + k * CMAX + q] = rWce[q];
     float* out = small + (int64_t)blockIdx.x * SMALL;
-    {
-        float gm[16], gl[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            gm[q] = 0.f;
-            gl[q] = 0.f;
-        }
-        const int kk = (k < K) ? k : 0;
-        for (int b = 0; b < LAT_CELLS; ++b) {
-            const float dm = sDM[b * 68 + kk], dl = sDA[b * 68 + kk];
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                const float4 h4 = *reinterpret_cast<const float4*>(&sH[b * 68 + 16 * w + 4 * q4]);
-                gm[4 * q4 + 0] = fmaf(dm, h4.x, gm[4 * q4 + 0]); gm[4 * q4 + 1] = fmaf(dm, h4.y, gm[4 * q4 + 1]);
-                gm[4 * q4 + 2] = fmaf(dm, h4.z, gm[4 * q4 + 2]); gm[4 * q4 + 3] = fmaf(dm, h4.w, gm[4 * q4 + 3]);
-                gl[4 * q4 + 0] = fmaf(dl, h4.x, gl[4 * q4 + 0]); gl[4 * q4 + 1] = fmaf(dl, h4.y, gl[4 * q4 + 1]);
-                gl[4 * q4 + 2] = fmaf(dl, h4.z, gl[4 * q4 + 2]); gl[4 * q4 + 3] = fmaf(dl, h4.w, gl[4 * q4 + 3]);
-            }
-        }
-        if (k < K) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int j2 = 16 * w + q;
-                if (j2 < K) {
-                    out[j2 * K + k] = gm[q];  // transposed: lanes store consecutive floats
-                    out[K * K + j2 * K + k] = gl[q];
-                }
-            }
-        }
-    }
+    heads_dW(sDM, sDA, sH, K, w, lane, out);
     __syncthreads();
     const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
     auto wsum = [&](int off) { return (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]); };
@@ -796,9 +755,9 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
     const float s = sum_partials(small, nwg, SMALL, i, red);
     if ((threadIdx.x >> 5) != 0 || i >= SMALL) return;
     int o = i;
-    if (o < K * K) { G.Wm[(o % K) * K + o / K] = s; return; }  // partials are [j][k]
+    if (o < K * K) { G.Wm[o] = s; return; }
     o -= K * K;
-    if (o < K * K) { G.Wl[(o % K) * K + o / K] = s; return; }
+    if (o < K * K) { G.Wl[o] = s; return; }
     o -= K * K;
     if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
     o -= K;
