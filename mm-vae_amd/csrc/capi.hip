@@ -284,7 +284,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
     HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
-    HIPCHK(e, dalloc(&e->d_mvec, KP));
+    HIPCHK(e, dalloc(&e->d_mvec, ((DP + 255) / 256) * KP));  // per-256-gene-block partials of mvec
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
     HIPCHK(e, dalloc(&e->d_rowxp, (int64_t)e->nsplit_e * Bp * (1 + e->H)));
     HIPCHK(e, dalloc(&e->d_hpart, (int64_t)e->nsplit_e * Bp * KP));

@@ -73,7 +73,7 @@ struct Engine {
     float* d_eps = nullptr;          // [Bpad][K] + [Bpad][R]
     float* h_eps_pin = nullptr;
     float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]
-    float* d_mvec = nullptr;         // [KP]
+    float* d_mvec = nullptr;         // [DP/256][KP] partials of mvec (k_prep / k_vprep)
     int32_t* d_rtp = nullptr;        // [N+1][NT+1] per-cell tile pointers (dataset index; row N = empty)
     float* d_cellnorm = nullptr;     // [N+1] float2: vMF row norms of log1p(x) (dataset index)
     float* d_rowx = nullptr;         // [Bpad][2+H]  pre_depth, lnorm2, hnu[H]

@@ -48,13 +48,16 @@ struct NBGrads {
 // mvec[k] = sum_g x_mean_g / (softplus(ln_x_sd_g) + 1e-4) * W_enc[k, g].
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, const float* __restrict__ WeP_f,
-                                              float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b) {
+                                              float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b,
+                                              float* __restrict__ mvecp) {
     // grid (genes / 256, KP / 8): every y-slice packs 8 latent rows of the scaled encoder weight
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= d.DP) return;
+    // and writes its block's partial of mvec (mvec_partial; summed by k_latent_fwd)
+    const int g0 = blockIdx.x * 256 + threadIdx.x;
+    const bool in = g0 < d.DP;
+    const int g = in ? g0 : d.DP - 1;
     float inv = 0.f;
     if (g < d.D) inv = 1.f / (softplus_acc(P.lsd[g]) + 1e-4f);
-    if (blockIdx.y == 0) {
+    if (blockIdx.y == 0 && in) {
         float bias = -INFINITY, cnu = 0.f, xmi = 0.f;
         if (g < d.D) {
             bias = P.bd[g] + P.bcd[g] + P.mub[g];
@@ -71,34 +74,19 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
             float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
     }
     // encoder weight pre-scaled by 1/(softplus(ln_x_sd)+1e-4): x~ W^T = log1p(x) (W inv)^T - mvec
+    const float xmv = (in && g < d.D) ? P.xm[g] : 0.f;
+    float mp[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
         const int k = blockIdx.y * 8 + kk;
         const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
-        if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
-        else WeS_f[(int64_t)k * d.DP + g] = ws;
+        if (in) {
+            if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+            else WeS_f[(int64_t)k * d.DP + g] = ws;
+        }
+        mp[kk] = xmv * ws;  // x_mean_g / sd_g * W_enc[k, g]
     }
-}
-
-// mvec[k] = sum_g x_mean_g / sd_g * W_enc[k, g]  (the dense part of the encoder input)
-__global__ __launch_bounds__(1024) void k_mvec(NBPtrs P, Dims d, const float* __restrict__ gene, float* mvec) {
-    __shared__ float sbuf[16];
-    const int k = blockIdx.x;
-    const float* xmi = gene + 3 * d.DP;
-    float acc = 0.f;
-    if (k < d.K) {
-        const float* wr = P.We + (int64_t)k * d.D;
-#pragma unroll 4
-        for (int g = threadIdx.x; g < d.D; g += 1024) acc += xmi[g] * wr[g];
-    }
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) sbuf[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int q = 0; q < 16; ++q) t += sbuf[q];
-        mvec[k] = t;
-    }
+    mvec_partial(mp, mvecp, d.KP, blockIdx.y * 8);
 }
 
 // =======================================================================================
@@ -310,10 +298,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
     __shared__ float sred[4];
     __shared__ float sRX[LAT_CELLS][1 + HMAX];  // depth pre-activation, nu_enc(x)
-    for (int i = threadIdx.x; i < K * K; i += 256) {
-        sWm[(i / K) * 65 + i % K] = P.Wm[i];
-        sWl[(i / K) * 65 + i % K] = P.Wl[i];
-    }
+    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // first cell of this wave (4 cells per wave)
@@ -333,28 +318,23 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         }
     }
     // h = sum of the encoder's gene-split partials - mvec + bias (split loads issued together)
-    const float hb = (k < K) ? P.be[k] - mvec[k] : 0.f;
+    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
+    const float hb = (k < K) ? P.be[k] - mvk : 0.f;
     float hs[4];
     split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
 #pragma unroll
     for (int c = 0; c < 4; ++c) sH[(4 * w + c) * 68 + k] = (k < K) ? hb + hs[c] : 0.f;
     __syncthreads();
+    // heads on f32 MFMA (nb.hh:412-416), transposed back to lane = latent through LDS
+    __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
+    heads_fwd(sH, sWm, sWl, K, w, lane, sM, sA);
+    __syncthreads();
     float mean[4], av[4];
     const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        mean[c] = bm;
-        av[c] = bl;
-    }
-    const int kk = (k < K) ? k : 0;
-    for (int jj = 0; jj < K; ++jj) {
-        const float wm = sWm[kk * 65 + jj], wl = sWl[kk * 65 + jj];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float hj = sH[(4 * w + c) * 68 + jj];
-            mean[c] = fmaf(wm, hj, mean[c]);
-            av[c] = fmaf(wl, hj, av[c]);
-        }
+        mean[c] = bm + sM[(4 * w + c) * 68 + k];
+        av[c] = bl + sA[(4 * w + c) * 68 + k];
     }
     float kl = 0.f;
 #pragma unroll
@@ -1110,10 +1090,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h
     float* wpart = sH + LAT_CELLS * 68; // [4][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-    for (int i = threadIdx.x; i < K * K; i += 256) {
-        sWm[(i / K) * 65 + i % K] = P.Wm[i];
-        sWl[(i / K) * 65 + i % K] = P.Wl[i];
-    }
+    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // 4 cells per wave
@@ -1673,6 +1650,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_DPRE = (int)e->LAT_HNU + (int)e->H;
     d.rowx_stride = 2 + (int)e->H;
     d.Ncells = (int)e->N;
+    d.nmv = (int)((e->DP + 255) / 256);
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
     return d;
 }
@@ -1745,11 +1723,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         ScopedTimer tm(e, "k_prep");
         hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, gene, e->d_WeP_f, e->d_WeS_f,
-                           bf ? e->d_WeS_b : nullptr);
-    }
-    {
-        ScopedTimer tm(e, "k_mvec");
-        hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, gene, e->d_mvec);
+                           bf ? e->d_WeS_b : nullptr, e->d_mvec);
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
@@ -1872,8 +1846,7 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
-                       bf ? e->d_WeS_b : nullptr);
-    hipLaunchKernelGGL(k_mvec, dim3(d.KP), dim3(1024), 0, st, P, d, e->d_gene, e->d_mvec);
+                       bf ? e->d_WeS_b : nullptr, e->d_mvec);
     if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
     else enc_fwd_nb<T, KP, 2>(e, d, P, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,

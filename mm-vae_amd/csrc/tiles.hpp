@@ -21,6 +21,7 @@ struct Dims {
         LAT_W, LAT_VALID, LAT_DHNU, LAT_DPRE;
     int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
     int Ncells;       // dataset rows: row Ncells of the per-cell tile index is the empty row
+    int nmv;          // mvec partial blocks (256 genes each) written by the prep kernel
     int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
 };
 
@@ -219,6 +220,37 @@ MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int 
 // exact to f32 rounding for counts >= 1)
 template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : flog(1.f + x); }
 
+// mvec[k] from the per-256-gene-block partials [nblk][KP] written by k_prep / k_vprep: the
+// workgroup's 256 threads each sum a quarter of the blocks of one latent (fixed order), the
+// quarters are combined in order through LDS.  All threads call it; valid for k < 64.
+MMVAE_DEV float mvec_sum(const float* __restrict__ mvecp, int nblk, int KP, int k) {
+    __shared__ float smv[4][64];
+    const int kk = threadIdx.x & 63, part = threadIdx.x >> 6;
+    float s = 0.f;
+    if (kk < KP)
+#pragma unroll 8
+        for (int i = part; i < nblk; i += 4) s += mvecp[(int64_t)i * KP + kk];
+    smv[part][kk] = s;
+    __syncthreads();
+    return (smv[0][k] + smv[1][k]) + (smv[2][k] + smv[3][k]);
+}
+
+// Per-block partial of mvec for 8 latents k0..k0+7: sum over the block's 256 genes of
+// v[kk] (one per thread), written to mvecp[blockIdx.x][k0 + kk].  All 256 threads call it.
+MMVAE_DEV void mvec_partial(const float (&v)[8], float* __restrict__ mvecp, int KP, int k0) {
+    __shared__ float sred[4][8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const float t = wave_sum(v[kk]);
+        if (lane == 0) sred[w][kk] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 8)
+        mvecp[(int64_t)blockIdx.x * KP + k0 + threadIdx.x] =
+            (sred[0][threadIdx.x] + sred[1][threadIdx.x]) + (sred[2][threadIdx.x] + sred[3][threadIdx.x]);
+}
+
 // Fixed-order sum over nwg per-workgroup partials [nwg][SMALL] for output i: a 256-thread block
 // covers 32 outputs x 8 workgroup chunks (each thread's loads independent, 16 in flight), the
 // chunk sums combined in chunk order through LDS.  Valid in threads 0..31 (threadIdx.x >> 5 == 0).
@@ -238,6 +270,29 @@ MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL
     return t;
 }
 
+// K x K head weights (K <= 64) into LDS images [k][65]: all 2 x 16 loads of a thread issued
+// before any store (clamped, unconditional addresses — counted waits, not one round trip per
+// element)
+MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, float* sWm,
+                              float* sWl) {
+    const int KK = K * K;
+    float tm[16], tl[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int i = min((int)threadIdx.x + 256 * u, KK - 1);
+        tm[u] = Wm[i];
+        tl[u] = Wl[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int i = (int)threadIdx.x + 256 * u;
+        if (i < KK) {
+            sWm[(i / K) * 65 + i % K] = tm[u];
+            sWl[(i / K) * 65 + i % K] = tl[u];
+        }
+    }
+}
+
 // ---- latent-head backward products on f32 MFMA (exact f32 FMA chains) ------------------
 // LDS images of the workgroup's LAT_CELLS = 16 cells: sDM / sDA / sH [cell][68] (latents >= K
 // hold 0), the head weights sWm / sWl [k][65] (valid for k, j < K).
@@ -255,6 +310,27 @@ MMVAE_DEV f32x4 heads_dh(const float* sDM, const float* sDA, const float* sWm, c
     }
     return acc;
 }
+// Forward heads for the 16 cells: mean_pre[cell][k] = sum_j h[cell][j] Wm[k][j] (and the
+// same with Wl): wave w owns latents k = 16 w + (lane & 15); the C-layout results are stored
+// to sM / sA [cell][68] (rows 4 (lane >> 4) + r).
+MMVAE_DEV void heads_fwd(const float* sH, const float* sWm, const float* sWl, int K, int w, int lane, float* sM,
+                         float* sA) {
+    const int kc = 16 * w + (lane & 15), row = lane & 15, jq = lane >> 4;
+    f32x4 am = f32x4{0.f, 0.f, 0.f, 0.f}, al = am;
+    for (int s = 0; 4 * s < K; ++s) {
+        const int jj = 4 * s + jq;
+        const bool ok = jj < K && kc < K;
+        const float hj = sH[row * 68 + jj];
+        am = __builtin_amdgcn_mfma_f32_16x16x4f32(hj, ok ? sWm[kc * 65 + jj] : 0.f, am, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x4f32(hj, ok ? sWl[kc * 65 + jj] : 0.f, al, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sM[(4 * jq + r) * 68 + kc] = am[r];
+        sA[(4 * jq + r) * 68 + kc] = al[r];
+    }
+}
+
 // Per-workgroup partials of dWm = dmean^T h and dWl = da^T h over the 16 cells: wave w owns
 // rows k = 16 w .. 16 w + 15; stored [k][j] into out[0 .. K*K) and out[K*K .. 2 K*K).
 MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int K, int w, int lane,

@@ -9,8 +9,8 @@
 //
 // Kernel chain per step (one stream), sharing the CSR tile machinery of tiles.hpp and the
 // encoder GEMM kernels of nb_kernels.hip (enc_forward_launch / enc_backward_launch):
-//   k_vprep        per-gene 1/(softplus(ln_x_sd)+eps), decoder gene records, W~/s
-//   k_vmvec        dense encoder term mvec = (x_mean/s) W~^T
+//   k_vprep        per-gene 1/(softplus(ln_x_sd)+eps), decoder gene records, W~/s, and the
+//                  per-block partials of the dense encoder term mvec = (x_mean/s) W~^T
 //   k_enc_fwd      sum_nnz l (W~/s)  on MFMA                    (shared with NB)
 //   k_vlatent_fwd  h = that / ||l|| - mvec, heads, clamp, reparameterise, KL
 //   k_vkappa       kappa = clamp(exp(ln_kappa)), lbessel terms (one thread)
@@ -105,44 +105,31 @@ __global__ void k_vpack_dec(const float* Wd, int D, int DP, int K, int KP, float
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, float* __restrict__ gene,
                                                const float* __restrict__ WeP_f, float* __restrict__ WeS_f,
-                                               __bf16* __restrict__ WeS_b) {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= d.DP) return;
-    const bool v = g < d.D;
+                                               __bf16* __restrict__ WeS_b, float* __restrict__ mvecp) {
+    const int g0 = blockIdx.x * 256 + threadIdx.x;
+    const bool in = g0 < d.DP;
+    const int g = in ? g0 : d.DP - 1;
+    const bool v = in && g < d.D;
     const float inv = v ? 1.f / (softplus_acc(P.lsd[g]) + epsD) : 0.f;
-    if (blockIdx.y == 0) {
+    if (blockIdx.y == 0 && in) {
         gene[g] = inv;
         gene[3 * d.DP + g] = v ? P.xm[g] * inv : 0.f;
         reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
             float4{v ? P.bd[g] : 0.f, v ? P.bcd[g] : 0.f, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? 1.f : 0.f};
     }
+    const float xmv = v ? P.xm[g] : 0.f;
+    float mp[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
         const int k = blockIdx.y * 8 + kk;
         const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
-        if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
-        else WeS_f[(int64_t)k * d.DP + g] = ws;
+        if (in) {
+            if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+            else WeS_f[(int64_t)k * d.DP + g] = ws;
+        }
+        mp[kk] = xmv * ws;  // xmi_g W~[k][g]
     }
-}
-
-// mvec[k] = sum_g xmi_g W~[k][g]
-__global__ __launch_bounds__(1024) void k_vmvec(Dims d, const float* __restrict__ gene, const float* __restrict__ WeP_f,
-                                                float* __restrict__ mvec) {
-    __shared__ float sb[16];
-    const int k = blockIdx.x;
-    const float* xmi = gene + 3 * d.DP;
-    const float* wr = WeP_f + (int64_t)k * d.DP;
-    float acc = 0.f;
-#pragma unroll 4
-    for (int g = threadIdx.x; g < d.D; g += 1024) acc = fmaf(xmi[g], wr[g], acc);
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int q = 0; q < 16; ++q) t += sb[q];
-        mvec[k] = t;
-    }
+    mvec_partial(mp, mvecp, d.KP, blockIdx.y * 8);  // summed by k_vlatent_fwd
 }
 
 // =======================================================================================
@@ -164,14 +151,12 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
     __shared__ float sred[4];
-    for (int i = threadIdx.x; i < K * K; i += 256) {
-        sWm[(i / K) * 65 + i % K] = P.Wm[i];
-        sWl[(i / K) * 65 + i % K] = P.Wl[i];
-    }
+    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;
-    const float mk = (k < K) ? mvec[k] : 0.f;
+    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
+    const float mk = (k < K) ? mvk : 0.f;
     float inx[4], hs[4];
     split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
 #pragma unroll
@@ -187,22 +172,16 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         sH[(4 * w + c) * 68 + k] = (k < K) ? hs[c] * inx[c] - mk : 0.f;
     }
     __syncthreads();
+    // heads on f32 MFMA (vmf.hh:259-264), transposed back to lane = latent through LDS
+    __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
+    heads_fwd(sH, sWm, sWl, K, w, lane, sM, sA);
+    __syncthreads();
     float mean[4], av[4];
     const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        mean[c] = bm;
-        av[c] = bl;
-    }
-    const int kk = (k < K) ? k : 0;
-    for (int jj = 0; jj < K; ++jj) {
-        const float wm = sWm[kk * 65 + jj], wl = sWl[kk * 65 + jj];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float hj = sH[(4 * w + c) * 68 + jj];
-            mean[c] = fmaf(wm, hj, mean[c]);
-            av[c] = fmaf(wl, hj, av[c]);
-        }
+        mean[c] = bm + sM[(4 * w + c) * 68 + k];
+        av[c] = bl + sA[(4 * w + c) * 68 + k];
     }
     float kl = 0.f;
 #pragma unroll
@@ -629,10 +608,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
     float* sDA = sDM + LAT_CELLS * 68;     // [cell][68] d(pre-clamp lnvar)
     float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h
     float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [4][NSM]
-    for (int i = threadIdx.x; i < K * K; i += 256) {
-        sWm[(i / K) * 65 + i % K] = P.Wm[i];
-        sWl[(i / K) * 65 + i % K] = P.Wl[i];
-    }
+    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;
@@ -915,6 +891,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.LAT_VALID = (int)e->LAT_VALID;
     d.rowx_stride = 2 + (int)e->H;
     d.Ncells = (int)e->N;
+    d.nmv = (int)((e->DP + 255) / 256);
     d.dbg = 0;
     return d;
 }
@@ -930,11 +907,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vprep");
         hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, sc.epsD, gene,
-                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr);
-    }
-    {
-        ScopedTimer tm(e, "k_vmvec");
-        hipLaunchKernelGGL(k_vmvec, dim3(d.KP), dim3(1024), 0, st, d, gene, e->d_WeP_f, e->d_mvec);
+                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec);
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
