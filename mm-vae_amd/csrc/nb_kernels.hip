@@ -117,6 +117,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     constexpr int STB = KP * RB;
     constexpr int XB = 2 * 16 * XS * (int)sizeof(T);  // per wave: two x tiles
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint64_t t_entry = (d.dbg & 32) ? stamp_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
     const int row0 = rb * 64 + 16 * w;
@@ -129,6 +130,10 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
     int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16 * RING;
 
+    RegStage<KP, RB> wreg;
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
+    // prologue loads with no dependence on the CSR index go out first (W tile t0)
+    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
         const int b = row0 + lane;
@@ -137,9 +142,6 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     }
     for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
     wave_sync();
-
-    RegStage<KP, RB> wreg;
-    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
     (void)NCH;
     const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
     constexpr int NGV = DOTS == 0 ? 1 : (DOTS == 1 ? 2 : 1 + HMAX);
@@ -185,20 +187,25 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     constexpr int EDEPTH = 2;
     RowEntries<6> q[EDEPTH];
     if (t0 < t1) {
-        gv_load(t0);
-        gv_store(t0);
-        gv_load(min(t0 + 1, t1 - 1));
-        gv_store(min(t0 + 1, t1 - 1));
-        __syncthreads();
-        wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
-        wreg.store(wst);
-        q[0].fetch(rtr, 0, rbase, sub, col, val);
-        scatter(q[0], xt, t0);
+        // every remaining prologue load is issued before the first wait
+        RowEntries<6> first;
+        first.fetch(rtr, 0, rbase, sub, col, val);
 #pragma unroll
         for (int i = 0; i < EDEPTH; ++i) q[i].fetch(rtr, min(1 + i, nt - 1), rbase, sub, col, val);
+        float g0[4];
+        gv_load(t0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g0[u] = gvr[u];
+        gv_load(min(t0 + 1, t1 - 1));
+        wreg.store(wst);
+        gv_store(min(t0 + 1, t1 - 1));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gvr[u] = g0[u];
+        gv_store(t0);
+        __syncthreads();  // gv slices visible to every wave before the first scatter
+        scatter(first, xt, t0);
     }
-    vm_wait_all();
-    __syncthreads();
+    lds_barrier();
     const bool stamps = (d.dbg & 32) != 0;
     uint64_t sa = 0, sb = 0, sc = 0, sd = 0, tp = stamps ? stamp_now() : 0;
     auto lap = [&](uint64_t& acc_) {
@@ -259,14 +266,18 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
         }
     }
     if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
+        const uint64_t t_loop_end = stamp_now();
         vm_wait_all();
         __syncthreads();
         if (lane == 0) {
-            float* o = hpart + ((int64_t)blockIdx.x * 4 + w) * 4;
+            float* o = hpart + ((int64_t)blockIdx.x * 4 + w) * 8;
             o[0] = (float)sa;
             o[1] = (float)sb;
             o[2] = (float)sc;
             o[3] = (float)sd;
+            o[4] = (float)(t_loop_end - t_entry - (sa + sb + sc + sd));  // prologue + tail
+            o[5] = (float)(t_entry & 0xffffffu);                          // entry time (low bits)
+            o[6] = (float)(t_loop_end - t_entry);
         }
         return;
     }

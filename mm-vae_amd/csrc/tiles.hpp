@@ -49,13 +49,27 @@ MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, 
 
 // Per-wave tile pointers of the wave's 16 rows for the split's tiles t0 .. t0 + S - 1, read
 // from the per-dataset index (rtp [N+1][NT+1], row N = empty) by each row's cell id.
+// The 16 cell ids are loaded once (lanes 0..15) and broadcast by shuffles; the index loads of
+// a batch of 8 entries per lane are issued together (no dependent round trip per entry).
 MMVAE_DEV void fill_rtl(int32_t* rtl, int S, int t0, int NT, int B, int Ncells, const int64_t* __restrict__ cells,
                         int row0, const int32_t* __restrict__ rtp, int lane) {
-    for (int i = lane; i < 16 * S; i += 64) {
-        const int rr = i / S, tt = i % S;
-        const int b = row0 + rr;
-        const int64_t crow = cells[b];  // padding rows hold the empty row Ncells
-        rtl[i] = rtp[crow * (NT + 1) + min(t0 + tt, NT)];
+    const int64_t mycell = cells[row0 + (lane & 15)];  // padding rows hold the empty row Ncells
+    const int lo = (int)(uint32_t)mycell, hi = (int)(mycell >> 32);
+    constexpr int U = 8;
+    for (int i0 = 0; i0 < 16 * S; i0 += 64 * U) {
+        int32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = min(i0 + lane + 64 * u, 16 * S - 1);
+            const int rr = i / S, tt = i % S;
+            const int64_t c = ((int64_t)__shfl(hi, rr, 64) << 32) | (uint32_t)__shfl(lo, rr, 64);
+            v[u] = rtp[c * (NT + 1) + min(t0 + tt, NT)];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + lane + 64 * u;
+            if (i < 16 * S) rtl[i] = v[u];
+        }
     }
 }
 

@@ -10,12 +10,13 @@ eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 for i in range(3):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)
-nwg = (B // 64) * eng_ns if (eng_ns := int(os.environ.get("NSE", "12"))) else 0
-buf = np.zeros(nwg * 16, np.float32)
+nse = int(os.environ.get("NSE", "12"))
+nwg = (B // 64) * nse
+buf = np.zeros(nwg * 4 * 8, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 0, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
-st = buf.reshape(-1, 4)
-tot = st.sum(1)
-print("waves", st.shape[0], "mean cycles per wave: MFMA+wait %.0f  zero+scatter %.0f  fetch+stage %.0f  barrier %.0f  total %.0f"
-      % tuple(list(st.mean(0)) + [tot.mean()]))
-print("per tile (40 tiles):", (st.mean(0) / 40).round(0))
+st = buf.reshape(-1, 8)
+ntile = (313 + nse - 1) // nse
+m = st.mean(0)
+print("waves", st.shape[0], "per tile: MFMA+wait %.0f  zero+scatter %.0f  fetch+stage %.0f  barrier %.0f" % tuple(m[:4] / ntile))
+print("prologue+tail %.0f cycles, wave wall %.0f mean / %.0f max cycles" % (m[4], m[6], st[:, 6].max()))
