@@ -751,6 +751,21 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    // ---- staging of the decoder tile, its gene records and the WdT tile ----
+    RegStage<64, RBW> wreg;
+    RegStage<KP, RBT> treg;
+    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    auto stage_load = [&](int t) {
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
+        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
+    };
+    auto stage_store = [&]() {
+        wreg.store(wst);
+        treg.store(tst);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[threadIdx.x] = greg;
+    };
+    stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
     // row log-sum-exp (log2 units) from pass A's split partials, 4 threads per row; split 0
     // also publishes it for pass C
     {
@@ -825,27 +840,12 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
 
-    // ---- staging of the decoder tile, its gene records and the WdT tile ----
-    RegStage<64, RBW> wreg;
-    RegStage<KP, RBT> treg;
-    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
-    auto stage_load = [&](int t) {
-        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
-        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
-        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
-    };
-    auto stage_store = [&]() {
-        wreg.store(wst);
-        treg.store(tst);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[threadIdx.x] = greg;
-    };
     TileEntries pend;
     if (t0 < t1) {
-        stage_load(t0);
-        stage_store();
         tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+        stage_store();
     }
-    __syncthreads();
+    lds_barrier();  // the first tile's entry loads stay in flight
 
     // diagnostic (MMVAE_DBG & 64): per-wave phase cycles into dzp (outputs invalid)
     const bool stamps = (d.dbg & 64) != 0;
@@ -1322,6 +1322,17 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     int32_t* rtl = reinterpret_cast<int32_t*>(wpb);
     int64_t* rbl = reinterpret_cast<int64_t*>(wpb + ((16 * S * 4 + 15) / 16) * 16);
     int32_t* rinc = reinterpret_cast<int32_t*>(rbl + 16);
+    // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
+    RegStage<KP, RB> wreg;
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
+    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
+    const int lb = w;  // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
+    constexpr int KSB = 64 / M::KSTEP;
+    Fr afr[KSB];
+#pragma unroll
+    for (int s = 0; s < KSB; ++s)  // unconditional (clamped) loads; blocks past KP zeroed below
+        afr[s] = M::load(&dhT[(int64_t)(16 * min(lb, KP / 16 - 1) + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
+                              (lane >> 4) * M::EPL]);
 
     fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
     if (lane < 16) {
@@ -1351,17 +1362,9 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
             if (RAW) raw[gl * 68 + 16 * w + rl] = x;
         });
     };
-    // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
-    const int lb = w;
-    constexpr int KSB = 64 / M::KSTEP;
-    Fr afr[KSB];
+    if (lb >= KP / 16)
 #pragma unroll
-    for (int s = 0; s < KSB; ++s)
-        afr[s] = (lb < KP / 16) ? M::load(&dhT[(int64_t)(16 * lb + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
-                                               (lane >> 4) * M::EPL])
-                                : M::zero();
-    RegStage<KP, RB> wreg;
-    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
+        for (int s = 0; s < KSB; ++s) afr[s] = M::zero();
 
     wave_sync();  // rtl / rbl written above by this wave
     const int32_t* rtr = rtl + rl * S;
@@ -1369,15 +1372,15 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     const int nt = t1 - t0;
     RowEntries<6> nxt;
     if (t0 < t1) {
-        wreg.load(wsrc(t0), (int64_t)d.DP * sizeof(T));
+        RowEntries<6> first;
+        first.fetch(rtr, 0, rbase, sub, col, val);
+        nxt.fetch(rtr, min(1, nt - 1), rbase, sub, col, val);
         wreg.store(wst);
         zero_cols();
-        nxt.fetch(rtr, 0, rbase, sub, col, val);
         wave_sync();
-        scatter(nxt, t0);
-        nxt.fetch(rtr, min(1, nt - 1), rbase, sub, col, val);
+        scatter(first, t0);
     }
-    __syncthreads();
+    lds_barrier();
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));

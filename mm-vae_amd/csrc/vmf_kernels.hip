@@ -391,6 +391,20 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
 
+    RegStage<64, RBW> wreg;
+    RegStage<KP, RBT> treg;
+    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    auto stage_load = [&](int t) {
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
+        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
+    };
+    auto stage_store = [&]() {
+        wreg.store(wst);
+        if (PASS) treg.store(tst);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
+    };
+    stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
     if (PASS) {  // the per-row backward coefficients from pass 0's split sums (k_vrowfin), 4 threads per row
         const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
         const int b = rb * 64 + rr;
@@ -430,26 +444,12 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         rbl[lane] = Q.rowptr[cell];
     }
 
-    RegStage<64, RBW> wreg;
-    RegStage<KP, RBT> treg;
-    float4 greg = float4{0.f, 0.f, 0.f, 0.f};
-    auto stage_load = [&](int t) {
-        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
-        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
-        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
-    };
-    auto stage_store = [&]() {
-        wreg.store(wst);
-        if (PASS) treg.store(tst);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
-    };
     TileEntries pend;
     if (t0 < t1) {
-        stage_load(t0);
-        stage_store();
         tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+        stage_store();
     }
-    __syncthreads();
+    lds_barrier();  // the first tile's entry loads stay in flight
 
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
