@@ -281,6 +281,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_WeS_b, KP * DP));
     HIPCHK(e, dalloc(&e->d_cells, Bp));
     HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, sizeof(int64_t) * Bp));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_perm_pin, sizeof(int32_t) * Bp));
+    HIPCHK(e, hipMalloc(&e->d_perm, sizeof(int32_t) * Bp));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
     HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
@@ -330,6 +332,8 @@ int mmvae_destroy(mmvae_h e) {
     for (void* b : bufs)
         if (b) hipFree(b);
     if (e->h_cells_pin) hipHostFree(e->h_cells_pin);
+    if (e->h_perm_pin) hipHostFree(e->h_perm_pin);
+    if (e->d_perm) hipFree(e->d_perm);
     if (e->h_eps_pin) hipHostFree(e->h_eps_pin);
     if (e->h_out_pin) hipHostFree(e->h_out_pin);
     for (auto ev : e->event_pool) hipEventDestroy(ev);
@@ -385,6 +389,8 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     }
     e->N = N;
     e->nnz = nnz;
+    e->cell_nnz.resize((size_t)N);
+    for (int64_t i = 0; i < N; ++i) e->cell_nnz[(size_t)i] = (int32_t)(rowptr[i + 1] - rowptr[i]);
     HIPCHK(e, build_dataset_index(e));
     return MMVAE_OK;
 }
@@ -544,7 +550,32 @@ int mmvae_reset_optimizer(mmvae_h e) {
     return MMVAE_OK;
 }
 
-static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B) {
+// Row balancing for the tile kernels: a workgroup's time is set by its heaviest 16-row wave,
+// and the CSR entry count per row varies with the library size.  The batch's rows are ordered
+// by nonzero count (bucketed counting sort, O(B)) and dealt to the B/16 waves in a snake, so
+// every wave holds an even spread of light and heavy cells.  Per-row results are independent
+// of the order and every batch sum is a fixed-order reduction; the reparameterisation noise
+// stays keyed by the ORIGINAL batch position (perm), as is the injected eps.
+static void balance_rows(Engine* e, int64_t B) {
+    std::vector<int64_t> cells(e->h_cells_pin, e->h_cells_pin + B);
+    int32_t mx = 1;
+    for (int64_t j = 0; j < B; ++j) mx = std::max(mx, e->cell_nnz[(size_t)cells[(size_t)j]]);
+    int sh = 0;
+    while ((mx >> sh) >= 1024) ++sh;
+    std::vector<int32_t> cnt(1025, 0), order((size_t)B);
+    for (int64_t j = 0; j < B; ++j) ++cnt[(size_t)(1023 - (e->cell_nnz[(size_t)cells[(size_t)j]] >> sh)) + 1];
+    for (int i = 0; i < 1024; ++i) cnt[(size_t)i + 1] += cnt[(size_t)i];
+    for (int64_t j = 0; j < B; ++j) order[(size_t)cnt[(size_t)(1023 - (e->cell_nnz[(size_t)cells[(size_t)j]] >> sh))]++] = (int32_t)j;
+    const int64_t nw = B / 16;
+    for (int64_t s2 = 0; s2 < B; ++s2) {
+        const int64_t pass = s2 / nw, q = s2 % nw, wv = (pass & 1) ? nw - 1 - q : q;
+        const int64_t slot = wv * 16 + pass;
+        e->h_cells_pin[slot] = cells[(size_t)order[(size_t)s2]];
+        e->h_perm_pin[slot] = order[(size_t)s2];
+    }
+}
+
+static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
     // wait until the previous step's H2D copies have consumed the pinned staging buffers
     HIPCHK(e, hipEventSynchronize(e->ev_staged));
     for (int64_t j = 0; j < B; ++j) {
@@ -556,6 +587,12 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         const int64_t c = cell_ids[r];
         if (c < 0 || c >= e->N) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
         e->h_cells_pin[j] = c;
+    }
+    e->perm_active = balance && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == e->N &&
+                     !std::getenv("MMVAE_NO_BALANCE");
+    if (e->perm_active) {
+        balance_rows(e, B);
+        HIPCHK(e, hipMemcpyAsync(e->d_perm, e->h_perm_pin, sizeof(int32_t) * B, hipMemcpyHostToDevice, e->stream));
     }
     // padding rows (up to the handle's padded max batch: the latent-head grids cover it) point
     // at row N: the empty row of the dataset index, a zero covariate row and rowptr[N] — so
@@ -572,7 +609,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "run: no dataset uploaded");
     const int64_t n_total = a->n_total > 0 ? a->n_total : a->B;
     HIPCHK(e, hipSetDevice(e->device));
-    int rc = stage_rows(e, a->cell_ids, a->ridx, a->B);
+    int rc = stage_rows(e, a->cell_ids, a->ridx, a->B, /*balance=*/true);
     if (rc) return rc;
     const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
     if (a->eps) {

@@ -70,6 +70,10 @@ struct Engine {
     // ---- per-step workspace ----
     int64_t* d_cells = nullptr;      // [Bpad] gathered dataset rows (-1 = padding)
     int64_t* h_cells_pin = nullptr;  // pinned staging
+    int32_t* h_perm_pin = nullptr;   // pinned: original batch position of every (balanced) row
+    int32_t* d_perm = nullptr;       // [Bpad]
+    bool perm_active = false;        // the last staged batch was reordered (noise keyed by d_perm)
+    std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing)
     float* d_eps = nullptr;          // [Bpad][K] + [Bpad][R]
     float* h_eps_pin = nullptr;
     float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]

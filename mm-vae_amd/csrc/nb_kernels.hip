@@ -301,7 +301,8 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
 __global__ __launch_bounds__(256) void k_latent_fwd(
     NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowxp,
-    float* __restrict__ rowx, const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
+    uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K;
@@ -353,6 +354,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         const int b = bw + c;
         const int64_t cell = cells[b];  // padding rows hold the empty row N
         const bool valid = b < d.B;
+        const int pb = (perm && valid) ? perm[b] : b;  // original batch position: the noise key
         float* L = lat + (int64_t)b * d.lat_stride;
         const float h = sH[(4 * w + c) * 68 + k];
         float mn = mean[c], a = av[c];
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         const float sig = expf(lnvar / 2.f);
         float eps = 0.f;
         if (k < K && b < d.B)
-            eps = eps_in ? eps_in[(int64_t)b * K + k] : philox_normal(seed, step, row_offset + b, k);
+            eps = eps_in ? eps_in[(int64_t)pb * K + k] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
         if (k < K) {
             L[d.LAT_H + k] = h;
@@ -397,8 +399,8 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
             if (b < d.B)
-                en = eps_in ? eps_in[(int64_t)d.B * K + (int64_t)b * d.R + k]
-                            : philox_normal(seed, step, row_offset + b, 4096 + k);
+                en = eps_in ? eps_in[(int64_t)d.B * K + (int64_t)pb * d.R + k]
+                            : philox_normal(seed, step, row_offset + pb, 4096 + k);
             const float zn = nm + en * expf(nlv / 2.f);
             L[d.LAT_NMEAN + k] = nm;
             L[d.LAT_AN + k] = an;
@@ -1747,7 +1749,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         ScopedTimer tm(e, "k_latent_fwd");
         hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id,
+                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr,
+                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, step_id,
                            row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
     }
     DecPtrs Q;
@@ -1864,7 +1867,8 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
     else enc_fwd_nb<T, KP, 2>(e, d, P, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, e->cfg.seed, (uint64_t)0, (int64_t)0, e->d_lat,
+                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, (uint64_t)0,
+                       (int64_t)0, e->d_lat,
                        e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
     return hipGetLastError();
 }

@@ -125,6 +125,8 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;
     e->N = N;
     e->nnz = nnz;
+    e->cell_nnz.resize((size_t)N);
+    for (int64_t i = 0; i < N; ++i) e->cell_nnz[(size_t)i] = (int32_t)cnt[(size_t)i];
     if ((er = build_dataset_index(e)) != hipSuccess) return er;
     hipFree(d_pg);
     hipFree(d_cnt);

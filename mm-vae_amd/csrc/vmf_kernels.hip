@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
 __global__ __launch_bounds__(256) void k_vlatent_fwd(
     VPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float2* __restrict__ cellnorm,
-    float* __restrict__ rowx, const float* __restrict__ eps_in, uint64_t seed, uint64_t step, int64_t row_offset,
+    float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
+    uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K;
@@ -208,8 +209,9 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         }
         const float sig = expf(lnvar / 2.f);
         float eps = 0.f;
+        const int pb = (perm && b < d.B) ? perm[b] : b;  // original batch position: the noise key
         if (k < K && b < d.B)
-            eps = eps_in ? eps_in[(int64_t)b * K + k] : philox_normal(seed, step, row_offset + b, k);
+            eps = eps_in ? eps_in[(int64_t)pb * K + k] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
         if (k < K) {
             L[d.LAT_H + k] = h;
@@ -917,7 +919,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vlatent_fwd");
         hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
-                           e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr, e->cfg.seed, step_id, row_offset,
+                           e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr,
+                           (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, step_id, row_offset,
                            e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
     }
     if (mode == 1) return hipGetLastError();

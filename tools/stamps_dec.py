@@ -23,3 +23,12 @@ print("waves", st.shape[0], "mean total cycles/wave %.0f (%.0f per tile)" % (tot
 for n, v in zip(names, st.mean(0)):
     print("  %-14s %8.0f cyc/wave  %6.0f per tile  %5.1f%%" % (n, v, v / ntile, 100 * v / tot.mean()))
 print("max-wave total / mean: %.3f" % (tot.max() / tot.mean()))
+# imbalance: per-wave totals by gene split and by row block (blockIdx = rb * nsD + sp)
+tw = tot.reshape(-1, 4)            # [wg][wave]
+wg = tw.max(1)                     # a workgroup ends with its slowest wave
+sp = np.arange(wg.size) % nsd
+rb = np.arange(wg.size) // nsd
+print("per split (mean of wg max, k cycles):", [round(float(wg[sp == s].mean()) / 1e3, 1) for s in range(nsd)])
+rbm = np.array([wg[rb == r].mean() for r in range(rb.max() + 1)])
+print("row blocks: min %.1f mean %.1f max %.1f (k cycles)" % (rbm.min() / 1e3, rbm.mean() / 1e3, rbm.max() / 1e3))
+print("wave spread inside a workgroup (max/min): %.3f" % float((tw.max(1) / tw.min(1)).mean()))
