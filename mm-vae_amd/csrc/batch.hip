@@ -1,0 +1,154 @@
+// Per-step batch entry lists: the batch's CSR entries regrouped by (16-row wave block, 64-gene
+// tile), so every tile kernel reads a tile's entries of its 16 rows as one contiguous, lane-
+// balanced list — no per-tile prefix scans over the rows, no per-row pointers in LDS.
+//
+//   ents  uint2 [E + 64]: (pos = row-in-block << 6 | gene-in-tile, bits of x), row-major inside a
+//         tile (rows ascending, genes ascending — the order of the reference's dense row read,
+//         mmvae_io.hh:208-245)
+//   seg   int64 [WB + 1]: first entry of wave block wb (host prefix of the rows' nonzero counts)
+//   toff  int32 [WB][NT + 1]: first entry of tile t inside the block's segment
+// Built from the per-dataset tile index (rtp) by one launch, k_batch_lists (one workgroup per
+// wave block).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.hpp"
+#include "engine.hpp"
+#include "tiles.hpp"
+
+namespace mmvae {
+
+// One workgroup per 16-row wave block, one wave per row, everything in LDS:
+//   1. the 16 rows' tile pointers (from the dataset index rtp) -> per-tile counts, the rows'
+//      prefix inside every tile list and the block's tile offsets (exclusive scan) -> toff
+//   2. the block's list segment is built in chunks of whole tiles (<= cap entries): every wave
+//      drops its row's entries of the chunk's tiles at their final positions, then the workgroup
+//      streams the chunk out with contiguous, full-line stores (no partial lines written from
+//      different waves or CUs).
+static constexpr int COPY_CAP_MAX = 12288;  // entries per LDS chunk (96 KB), less for very wide D
+__global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict__ cells,
+                                                      const int64_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col, const float* __restrict__ val,
+                                                      const int32_t* __restrict__ rtp, const int64_t* __restrict__ seg,
+                                                      int NT, int cap, int32_t* __restrict__ toff,
+                                                      uint2* __restrict__ ents, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) char csm[];
+    uint2* stage = reinterpret_cast<uint2*>(csm);                      // [cap]
+    int32_t* tw = reinterpret_cast<int32_t*>(csm + 8 * (size_t)cap);    // [NT + 1] tile offsets
+    int32_t* srt = tw + (NT + 1);                                       // [16][NT + 1] rows' tile pointers
+    int32_t* sbase = srt + 16 * (NT + 1);                               // [16][NT] rows' list bases
+    __shared__ int32_t wsum[16];
+    __shared__ int32_t scarry;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+    const int wb = blockIdx.x, b = wb * 16 + w;
+    const int64_t c = cells[b];
+    const int64_t s = rowptr[c];
+    for (int t = lane; t <= NT; t += 64) srt[w * (NT + 1) + t] = rtp[c * (int64_t)(NT + 1) + t];
+    if (tid == 0) scarry = 0;
+    __syncthreads();
+    // per tile: the rows' prefix (sbase, before the tile offset) and the tile count (into tw)
+    for (int t = tid; t < NT; t += 1024) {
+        int32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int32_t a0 = srt[r * (NT + 1) + t], a1 = srt[r * (NT + 1) + t + 1];
+            sbase[r * NT + t] = acc - a0;
+            acc += a1 - a0;
+        }
+        tw[t] = acc;
+    }
+    __syncthreads();
+    // exclusive scan of the tile counts in chunks of 1024 tiles; tw[NT] = the block's total
+    for (int t0 = 0; t0 <= NT; t0 += 1024) {
+        const int t = t0 + tid;
+        const int32_t v = (t < NT) ? tw[t] : 0;
+        int32_t incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int32_t carry = scarry;
+        for (int i = 0; i < w; ++i) carry += wsum[i];
+        if (t <= NT) tw[t] = carry + incl - v;
+        __syncthreads();
+        if (tid == 0) {
+            int32_t tot = 0;
+            for (int i = 0; i < 16; ++i) tot += wsum[i];
+            scarry += tot;
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t <= NT; t += 1024) toff[(int64_t)wb * (NT + 1) + t] = tw[t];
+    for (int i = tid; i < 16 * NT; i += 1024) sbase[i] += tw[i % NT];
+    __syncthreads();
+    if (dbg & 512) return;  // diagnostic: index phase only (lists invalid)
+    const int64_t base = seg[wb];
+    const int32_t* sb = sbase + w * NT;
+    const int32_t* rt = srt + w * (NT + 1);
+    // chunk bounds: the largest tB with tw[tB] - tw[tA] <= cap (a tile holds <= 1024 entries)
+    auto chunk_end = [&](int tA) {
+        int lo = tA + 1, hi = NT;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tw[mid] - tw[tA] <= cap) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    // software pipeline over chunks: the next chunk's first 1024 entries of the row are loaded
+    // while the current chunk streams out
+    constexpr int U = 16;
+    int g[U];
+    float x[U];
+    auto load = [&](int jA, int jB) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads
+            const int j = min(jA + 64 * u + lane, max(jB - 1, 0));
+            g[u] = col[s + j];
+            x[u] = val[s + j];
+        }
+    };
+    auto drop = [&](int j0, int jB, int cb) {  // masked LDS stores at the final positions
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + 64 * u + lane;
+            if (j < jB) stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+        }
+    };
+    int tA = 0, tB = NT > 0 ? chunk_end(0) : 0;
+    if (NT > 0) load(rt[0], rt[tB]);
+    while (tA < NT) {
+        const int cb = tw[tA], cnt = tw[tB] - cb;
+        const int jA = rt[tA], jB = rt[tB];
+        drop(jA, jB, cb);
+        for (int j0 = jA + 64 * U; j0 < jB; j0 += 64 * U) {  // rows with more than 1024 entries in the chunk
+            load(j0, jB);
+            drop(j0, jB, cb);
+        }
+        lds_barrier();
+        const int tC = tB < NT ? chunk_end(tB) : NT;
+        if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
+        uint2* dst = ents + base + cb;
+        for (int i = tid; i < cnt; i += 1024) dst[i] = stage[i];
+        lds_barrier();  // stage reusable (the stores carry register copies)
+        tA = tB;
+        tB = tC;
+    }
+}
+
+hipError_t build_batch_lists(Engine* e, int64_t B) {
+    const int64_t Bp = (B + 63) / 64 * 64, WB = Bp / 16;
+    ScopedTimer tm(e, "k_batch_lists");
+    const size_t tab = sizeof(int32_t) * ((size_t)e->NT + 1 + 16 * ((size_t)e->NT + 1) + 16 * (size_t)e->NT);
+    if (tab + 8 * 1024 > 160 * 1024) return hipErrorInvalidValue;  // D beyond ~75k genes
+    const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - tab) / 8) & ~1;
+    hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
+                       e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
+                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }());
+    return hipGetLastError();
+}
+
+}  // namespace mmvae

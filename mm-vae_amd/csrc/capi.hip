@@ -283,6 +283,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, sizeof(int64_t) * Bp));
     HIPCHK(e, hipHostMalloc((void**)&e->h_perm_pin, sizeof(int32_t) * Bp));
     HIPCHK(e, hipMalloc(&e->d_perm, sizeof(int32_t) * Bp));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_seg_pin, sizeof(int64_t) * (Bp / 16 + 1)));
+    HIPCHK(e, hipMalloc(&e->d_seg, sizeof(int64_t) * (Bp / 16 + 1)));
+    HIPCHK(e, hipMalloc(&e->d_toff, sizeof(int32_t) * (Bp / 16) * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
     HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
@@ -334,6 +337,9 @@ int mmvae_destroy(mmvae_h e) {
     if (e->h_cells_pin) hipHostFree(e->h_cells_pin);
     if (e->h_perm_pin) hipHostFree(e->h_perm_pin);
     if (e->d_perm) hipFree(e->d_perm);
+    if (e->h_seg_pin) hipHostFree(e->h_seg_pin);
+    for (void* b : {(void*)e->d_seg, (void*)e->d_toff, (void*)e->d_ents})
+        if (b) hipFree(b);
     if (e->h_eps_pin) hipHostFree(e->h_eps_pin);
     if (e->h_out_pin) hipHostFree(e->h_out_pin);
     for (auto ev : e->event_pool) hipEventDestroy(ev);
@@ -600,6 +606,27 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
     const int64_t Bp = e->Bpad;
     for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = e->N;
     HIPCHK(e, hipMemcpyAsync(e->d_cells, e->h_cells_pin, sizeof(int64_t) * Bp, hipMemcpyHostToDevice, e->stream));
+    // entry-list segments of the batch's 16-row wave blocks (batch.hip): host prefix of the
+    // rows' nonzero counts; the list buffer grows (outside any step) when a batch needs more
+    const int64_t Bq = (B + 63) / 64 * 64, WB = Bq / 16;
+    int64_t tot = 0;
+    for (int64_t wb = 0; wb < WB; ++wb) {
+        e->h_seg_pin[wb] = tot;
+        for (int r = 0; r < 16; ++r) {
+            const int64_t c = e->h_cells_pin[wb * 16 + r];
+            tot += (c < e->N) ? e->cell_nnz[(size_t)c] : 0;
+        }
+    }
+    e->h_seg_pin[WB] = tot;
+    if (tot + 64 > e->ent_cap) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (e->d_ents) hipFree(e->d_ents);
+        e->d_ents = nullptr;
+        e->ent_cap = tot + tot / 4 + 1024;
+        HIPCHK(e, hipMalloc(&e->d_ents, sizeof(uint2) * e->ent_cap));
+        HIPCHK(e, hipMemset(e->d_ents, 0, sizeof(uint2) * e->ent_cap));
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_seg, e->h_seg_pin, sizeof(int64_t) * (WB + 1), hipMemcpyHostToDevice, e->stream));
     return MMVAE_OK;
 }
 
@@ -618,6 +645,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    HIPCHK(e, build_batch_lists(e, a->B));
     if (vmf)
         HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
                                        a->row_offset));
@@ -652,6 +680,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    HIPCHK(e, build_batch_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
     else HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));

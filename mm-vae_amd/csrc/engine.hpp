@@ -73,7 +73,13 @@ struct Engine {
     int32_t* h_perm_pin = nullptr;   // pinned: original batch position of every (balanced) row
     int32_t* d_perm = nullptr;       // [Bpad]
     bool perm_active = false;        // the last staged batch was reordered (noise keyed by d_perm)
-    std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing)
+    std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing, lists)
+    // per-step batch entry lists (batch.hip)
+    uint2* d_ents = nullptr;         // [ent_cap]
+    int64_t ent_cap = 0;
+    int64_t* d_seg = nullptr;        // [Bpad/16 + 1]
+    int64_t* h_seg_pin = nullptr;    // pinned staging of seg
+    int32_t* d_toff = nullptr;       // [Bpad/16][NT+1]
     float* d_eps = nullptr;          // [Bpad][K] + [Bpad][R]
     float* h_eps_pin = nullptr;
     float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]
@@ -171,6 +177,7 @@ hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
 hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart);
+hipError_t build_batch_lists(Engine* e, int64_t B);
 hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab);
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);

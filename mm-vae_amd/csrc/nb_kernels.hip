@@ -454,6 +454,9 @@ struct DecPtrs {
     float* slabB;     // [nrb][nqB][DP]
     float* slabC;     // [nrb][1+C][DP]
     float* lossp;     // [grid]
+    const uint2* ents;     // per-step batch entry lists (batch.hip)
+    const int64_t* seg;    // [Bpad/16 + 1]
+    const int32_t* toff;   // [Bpad/16][NT+1]
 };
 
 // Passes A and C: each tile's decoder rows + gene records are staged ONCE per workgroup into
@@ -827,11 +830,12 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     float lossacc = 0.f;
     // ---- per-wave row data for the sparse pass ----
-    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
+    const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
+    fill_toffl(rtl, S, t0, d.NT, Q.toff, wbk, lane);
+    const int64_t segw = Q.seg[wbk];
     if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
-        rbl[lane] = Q.rowptr[cell];
         const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
         float* rs = rsc + lane * NRS;
         rs[0] = Lr[d.LAT_D];
@@ -842,9 +846,10 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
 
-    TileEntries pend;
+    wave_sync();  // toffl
+    ListEntries pend;
     if (t0 < t1) {
-        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+        pend.fetch(Q.ents, segw, rtl, 0, lane);
         stage_store();
     }
     lds_barrier();  // the first tile's entry loads stay in flight
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         wave_sync();
         lap(0);
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
-        if (!(d.dbg & 1)) tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val, [&](int r, int gl, float x) {
+        if (!(d.dbg & 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
             const float p = q2[r * PS + gl];
             const float mu = fmaf(p, rs_[0], 1e-4f);
@@ -915,7 +920,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         wave_sync();
         lap(1);
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
-        tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
+        pend.fetch(Q.ents, segw, rtl, min(tl + 1, t1 - t0 - 1), lane);
         lap(2);
         // ---- 3. dense epilogue in the owner lanes ----
         // MASK: some of the wave's rows (last row block) or the tile's genes (last tile) are
@@ -1766,6 +1771,9 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     Q.col = e->d_col;
     Q.val = e->d_val;
     Q.rtp = e->d_rtp;
+    Q.ents = e->d_ents;
+    Q.seg = e->d_seg;
+    Q.toff = e->d_toff;
     Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
     Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
     Q.lsep = e->d_lsep;

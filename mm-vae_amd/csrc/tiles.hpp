@@ -152,6 +152,43 @@ MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, in
     }
 }
 
+// One tile's entries of a wave's 16 rows from the per-step batch lists (batch.hip): lane l
+// takes entries l and l + 64 (prefetched a tile ahead), entries past 128 are read on the spot.
+// toffl = the wave block's tile offsets t0 .. t0 + S - 1 (LDS), seg = the block's first entry.
+struct ListEntries {
+    int n;
+    int64_t base;
+    int pos[2];
+    float x[2];
+    MMVAE_DEV void fetch(const uint2* __restrict__ ents, int64_t seg, const int32_t* toffl, int tl, int lane) {
+        const int a = toffl[tl];
+        n = toffl[tl + 1] - a;
+        base = seg + a;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {  // unconditional loads (the list buffer has 64 spare entries)
+            const int e = lane + 64 * k;
+            const uint2 r = ents[base + (e < n ? e : 0)];
+            pos[k] = (e < n) ? (int)r.x : -1;
+            x[k] = __uint_as_float(r.y);
+        }
+    }
+    // f(row-in-block, gene-in-tile, x) for every entry of the tile
+    template <class F>
+    MMVAE_DEV void visit(const uint2* __restrict__ ents, int lane, F&& f) const {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (pos[k] >= 0) f(pos[k] >> 6, pos[k] & 63, x[k]);
+        for (int e = 128 + lane; e < n; e += 64) {
+            const uint2 r = ents[base + e];
+            f((int)(r.x >> 6), (int)(r.x & 63), __uint_as_float(r.y));
+        }
+    }
+};
+// the wave block's tile offsets for the split's tiles t0 .. t0 + S - 1 into LDS
+MMVAE_DEV void fill_toffl(int32_t* toffl, int S, int t0, int NT, const int32_t* __restrict__ toff, int wb, int lane) {
+    for (int i = lane; i < S; i += 64) toffl[i] = toff[(int64_t)wb * (NT + 1) + min(t0 + i, NT)];
+}
+
 // Prefetch ring of the CSR entries of the next R tiles of a wave (e[0] = next tile to visit):
 // the entry loads of a tile are issued R tiles before it is consumed, so a tile iteration no
 // longer waits out a full memory latency.  Tile tl keeps its row prefix counts in LDS slot
