@@ -31,7 +31,9 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
                                                       const int32_t* __restrict__ col, const float* __restrict__ val,
                                                       const int32_t* __restrict__ rtp, const int64_t* __restrict__ seg,
                                                       int NT, int cap, int32_t* __restrict__ toff,
-                                                      uint2* __restrict__ ents, int dbg) {
+                                                      uint2* __restrict__ ents, int dbg,
+                                                      const float* __restrict__ wdp, const float* __restrict__ Wne,
+                                                      int H, int D, float* __restrict__ rowdots) {
     extern __shared__ __attribute__((aligned(16))) char csm[];
     uint2* stage = reinterpret_cast<uint2*>(csm);                      // [cap]
     int32_t* tw = reinterpret_cast<int32_t*>(csm + 8 * (size_t)cap);    // [NT + 1] tile offsets
@@ -111,11 +113,23 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
             x[u] = val[s + j];
         }
     };
+    // NB (wdp != null): the raw-count dots of depth and nu_enc (nb.hh:448, 498) ride along,
+    // every entry of the row passes through this wave exactly once
+    const bool dots = wdp != nullptr;
+    float dpre = 0.f, dhn[HMAX];
+#pragma unroll
+    for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
     auto drop = [&](int j0, int jB, int cb) {  // masked LDS stores at the final positions
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u + lane;
-            if (j < jB) stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+            if (j < jB) {
+                stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+                if (dots) {
+                    dpre = fmaf(x[u], wdp[g[u]], dpre);
+                    for (int h = 0; h < H; ++h) dhn[h < HMAX ? h : 0] = fmaf(x[u], Wne[(int64_t)h * D + g[u]], dhn[h < HMAX ? h : 0]);
+                }
+            }
         }
     };
     int tA = 0, tB = NT > 0 ? chunk_end(0) : 0;
@@ -137,9 +151,18 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
         tA = tB;
         tB = tC;
     }
+    if (dots) {
+        dpre = wave_sum(dpre);
+        for (int h = 0; h < H; ++h) dhn[h < HMAX ? h : 0] = wave_sum(dhn[h < HMAX ? h : 0]);
+        if (lane == 0) {
+            float* o = rowdots + (int64_t)b * (1 + H);
+            o[0] = dpre;
+            for (int h = 0; h < H; ++h) o[1 + h] = dhn[h < HMAX ? h : 0];
+        }
+    }
 }
 
-hipError_t build_batch_lists(Engine* e, int64_t B) {
+hipError_t build_batch_lists(Engine* e, int64_t B, const float* wdp, const float* Wne, float* rowdots) {
     const int64_t Bp = (B + 63) / 64 * 64, WB = Bp / 16;
     ScopedTimer tm(e, "k_batch_lists");
     const size_t tab = sizeof(int32_t) * ((size_t)e->NT + 1 + 16 * ((size_t)e->NT + 1) + 16 * (size_t)e->NT);
@@ -147,7 +170,8 @@ hipError_t build_batch_lists(Engine* e, int64_t B) {
     const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - tab) / 8) & ~1;
     hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
                        e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
-                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }());
+                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(), wdp, Wne,
+                       (int)e->H, (int)e->D, rowdots);
     return hipGetLastError();
 }
 

@@ -581,6 +581,12 @@ static void balance_rows(Engine* e, int64_t B) {
     }
 }
 
+// the batch entry lists (+ the NB raw-count dots of depth / nu_enc, split 0 of rowxp)
+static hipError_t build_lists(Engine* e, int64_t B) {
+    if (e->cfg.model == MMVAE_MODEL_VMF) return build_batch_lists(e, B, nullptr, nullptr, nullptr);
+    return build_batch_lists(e, B, e->preg("depth.weight"), e->preg("nu_encoding.weight"), e->d_rowxp);
+}
+
 static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
     // wait until the previous step's H2D copies have consumed the pinned staging buffers
     HIPCHK(e, hipEventSynchronize(e->ev_staged));
@@ -645,7 +651,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
-    HIPCHK(e, build_batch_lists(e, a->B));
+    HIPCHK(e, build_lists(e, a->B));
     if (vmf)
         HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
                                        a->row_offset));
@@ -680,7 +686,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
-    HIPCHK(e, build_batch_lists(e, B));
+    HIPCHK(e, build_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
     else HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));

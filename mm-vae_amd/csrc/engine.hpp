@@ -177,7 +177,7 @@ hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
 hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart);
-hipError_t build_batch_lists(Engine* e, int64_t B);
+hipError_t build_batch_lists(Engine* e, int64_t B, const float* wdp, const float* Wne, float* rowdots);
 hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab);
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);

@@ -92,28 +92,21 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // =======================================================================================
 // k_enc_fwd — mu encoder (nb.hh:410-411) on MFMA.  x~ W^T = log1p(x) (W/sd)^T - mvec, so only
 // the nonzeros are densified.  Workgroup = 64 cells x one gene split; per 64-gene tile the
-// frozen weight tile (pre-scaled by 1/sd in k_prep, [KP][DP]) is staged ONCE per workgroup
-// into LDS by LDS-DMA (double-buffered, swizzled), while each wave scatters its 16 cells'
-// log1p(x) for the NEXT tile into a wave-private 16x64 LDS tile (entries prefetched two
-// tiles ahead).  Partial h per gene split -> hpart.
+// pre-scaled frozen weight tile ([KP][DP], k_prep) is register-staged once per workgroup into
+// LDS (double-buffered, swizzled), while each wave scatters its 16 cells' log1p(x) for the
+// NEXT tile from the batch entry lists (tiles t+1, t+2 prefetched, entries balanced over the
+// lanes) into a wave-private 16x64 LDS tile.  Partial h per gene split -> hpart.  (The raw-count
+// dots of depth / nu_enc, nb.hh:448, 498, are taken by k_batch_lists, which visits every entry
+// with its row known.)
 // =======================================================================================
-// DOTS (NB): the same scatter also accumulates the raw-count dots of the depth and nu encoders
-// (nb.hh:448, 498) per gene split -> rowxp [nsE][Bpad][1+H]; their 64-gene weight slices are
-// staged per tile in a 3-slot LDS ring (written two tiles ahead).  DOTS = 0 (vMF): none.
-template <class T, int KP, int DOTS>
-__global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cells,
-                                                 const int64_t* __restrict__ rowptr,
-                                                 const int32_t* __restrict__ col,
-                                                 const float* __restrict__ val,
-                                                 const int32_t* __restrict__ rtp,
-                                                 const T* __restrict__ WeS, Dims d,
-                                                 float* __restrict__ hpart, const float* __restrict__ wdp,
-                                                 const float* __restrict__ Wne, float* __restrict__ rowxp) {
+template <class T, int KP>
+__global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                                                 const int32_t* __restrict__ toff, const T* __restrict__ WeS, Dims d,
+                                                 float* __restrict__ hpart) {
     using M = MM<T>;
     using Fr = typename M::frag;
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;   // x tile row stride (elements): conflict-free
     constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
-    constexpr int NCH = RB / 16;
     constexpr int STB = KP * RB;
     constexpr int XB = 2 * 16 * XS * (int)sizeof(T);  // per wave: two x tiles
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -126,84 +119,35 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     const EncLds L(KP, (int)sizeof(T), S, XB, 0);
     char* wst = smem;
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
-    int32_t* rtl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
-    int64_t* rbl = reinterpret_cast<int64_t*>(smem + L.o_rbl) + w * 16;
-    int32_t* rinc = reinterpret_cast<int32_t*>(smem + L.o_rinc) + w * 16 * RING;
+    int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
 
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
-    // prologue loads with no dependence on the CSR index go out first (W tile t0)
+    // prologue loads with no dependence on the lists go out first (W tile t0)
     wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
-    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
-    if (lane < 16) {
-        const int b = row0 + lane;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
-        rbl[lane] = rowptr[cell];
-    }
+    const int wbk = row0 >> 4;
+    fill_toffl(toffl, S, t0, d.NT, toff, wbk, lane);
+    const int64_t segw = seg[wbk];
     for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
     wave_sync();
-    (void)NCH;
-    const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
-    constexpr int NGV = DOTS == 0 ? 1 : (DOTS == 1 ? 2 : 1 + HMAX);
-    float* gvs = reinterpret_cast<float*>(smem + L.bytes);  // [3][NGV][64] depth / nu_enc slices
-    const int nqv = DOTS == 0 ? 0 : (DOTS == 1 ? 2 : 1 + d.H);
-    const int gq = DOTS ? min((int)threadIdx.x >> 4, nqv - 1) : 0, ge0 = 4 * (threadIdx.x & 15);
-    const float* gsrc = DOTS ? ((gq == 0) ? wdp : Wne + (int64_t)(gq - 1) * d.D) : nullptr;
-    float gvr[4] = {0.f, 0.f, 0.f, 0.f};
-    auto gv_load = [&](int t) {
-        if (DOTS)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) gvr[u] = gsrc[min(64 * t + ge0 + u, d.D - 1)];
-    };
-    auto gv_store = [&](int t) {
-        if (DOTS && (int)threadIdx.x < 16 * nqv)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) gvs[((t % 3) * NGV + gq) * 64 + ge0 + u] = gvr[u];
-    };
-    constexpr int HD = DOTS == 2 ? HMAX : 1;
-    float dpre = 0.f, dhn[HD];
-#pragma unroll
-    for (int h = 0; h < HD; ++h) dhn[h] = 0.f;
-    auto scatter = [&](const RowEntries<6>& re, T* dst, int t) {
-        const float* gv = gvs + (t % 3) * NGV * 64;
-        re.visit(t, sub, col, val, [&](int gl, float x) {
-            dst[rl * XS + gl] = to_t<T>(log1p_cnt<T>(x));
-            if (DOTS) {
-                dpre = fmaf(x, gv[gl], dpre);
-#pragma unroll
-                for (int h = 0; h < HD; ++h)
-                    if (DOTS == 1 || h < d.H) dhn[h] = fmaf(x, gv[(1 + h) * 64 + gl], dhn[h]);
-            }
-        });
+    auto scatter = [&](const ListEntries& le, T* dst) {
+        le.visit(ents, lane, [&](int r, int gl, float x) { dst[r * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
     };
 
     f32x4 acc[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) acc[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int32_t* rtr = rtl + rl * S;
-    const int64_t rbase = rbl[rl];
     const int nt = t1 - t0;
     // entry ring: q[0] = next tile to scatter; loads issued EDEPTH tiles ahead of their use
     constexpr int EDEPTH = 2;
-    RowEntries<6> q[EDEPTH];
+    ListEntries q[EDEPTH];
     if (t0 < t1) {
-        // every remaining prologue load is issued before the first wait
-        RowEntries<6> first;
-        first.fetch(rtr, 0, rbase, sub, col, val);
+        ListEntries first;  // every prologue load is issued before the first wait
+        first.fetch(ents, segw, toffl, 0, lane);
 #pragma unroll
-        for (int i = 0; i < EDEPTH; ++i) q[i].fetch(rtr, min(1 + i, nt - 1), rbase, sub, col, val);
-        float g0[4];
-        gv_load(t0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) g0[u] = gvr[u];
-        gv_load(min(t0 + 1, t1 - 1));
+        for (int i = 0; i < EDEPTH; ++i) q[i].fetch(ents, segw, toffl, min(1 + i, nt - 1), lane);
         wreg.store(wst);
-        gv_store(min(t0 + 1, t1 - 1));
-#pragma unroll
-        for (int u = 0; u < 4; ++u) gvr[u] = g0[u];
-        gv_store(t0);
-        __syncthreads();  // gv slices visible to every wave before the first scatter
-        scatter(first, xt, t0);
+        scatter(first, xt);
     }
     lds_barrier();
     const bool stamps = (d.dbg & 32) != 0;
@@ -217,9 +161,8 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
     };
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0, buf = tl & 1;
-        // unconditional (clamped) prefetch of the next weight tile: see RowEntries::fetch
+        // unconditional (clamped) prefetch of the next weight tile: counted vmcnt waits
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
-        gv_load(min(t + 2, t1 - 1));
         const T* xb = xt + buf * 16 * XS;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
@@ -236,34 +179,17 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const int64_t* __restrict__ cel
         if (t + 1 < t1) {
             for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xn)[i] = uint4{0, 0, 0, 0};
             wave_sync();
-            scatter(q[0], xn, t + 1);
+            scatter(q[0], xn);
         }
         lap(sb);
         // rotate the ring; the new tail's entry loads stay in flight across the barriers
 #pragma unroll
         for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
-        q[EDEPTH - 1].fetch(rtr, min(tl + 1 + EDEPTH, nt - 1), rbase, sub, col, val);
+        q[EDEPTH - 1].fetch(ents, segw, toffl, min(tl + 1 + EDEPTH, nt - 1), lane);
         if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB);
-        if (t + 2 < t1) gv_store(t + 2);
         lap(sc);
         lds_barrier();
         lap(sd);
-    }
-    if (DOTS) {  // the row's four lanes -> split partials of depth(x), nu_enc(x)
-        dpre += __shfl_xor(dpre, 16, 64);
-        dpre += __shfl_xor(dpre, 32, 64);
-#pragma unroll
-        for (int h = 0; h < HD; ++h) {
-            dhn[h] += __shfl_xor(dhn[h], 16, 64);
-            dhn[h] += __shfl_xor(dhn[h], 32, 64);
-        }
-        if (lane < 16) {
-            float* o = rowxp + ((int64_t)sp * d.Bpad + row0 + lane) * (1 + d.H);
-            o[0] = dpre;
-#pragma unroll
-            for (int h = 0; h < HD; ++h)
-                if (h < d.H) o[1 + h] = dhn[h];
-        }
     }
     if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
         const uint64_t t_loop_end = stamp_now();
@@ -318,7 +244,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         // raw-count dots from the encoder's gene-split partials (+ bias); rowx for k_latent_bwd
         const int nq = 1 + d.H;
         float xs[4];
-        split_sum4(rowxp, d.nsE, (int64_t)d.Bpad * nq, (int64_t)bw * nq + (k < nq ? k : 0), nq, k < nq, xs);
+        split_sum4(rowxp, 1, (int64_t)d.Bpad * nq, (int64_t)bw * nq + (k < nq ? k : 0), nq, k < nq, xs);  // k_batch_lists
         if (k < nq) {
             const float bias = (k == 0) ? P.bdp[0] : P.bne[k - 1];
 #pragma unroll
@@ -1714,19 +1640,15 @@ static size_t dec_lds(const Dims& d, int pass, bool bf16) {
     return s;
 }
 
-template <class T, int KP, int DOTS>
+template <class T, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;
-    constexpr int NGV = DOTS == 0 ? 1 : (DOTS == 1 ? 2 : 1 + HMAX);
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes +
-           (DOTS ? (size_t)3 * NGV * 64 * sizeof(float) : 0);
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes;
 }
-template <class T, int KP, int DOTS>
-static void enc_fwd_nb(Engine* e, const Dims& d, const NBPtrs& P, hipStream_t st) {
-    hipLaunchKernelGGL((k_enc_fwd<T, KP, DOTS>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP, DOTS>(d)), st,
-                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp,
-                       sizeof(T) == 2 ? (const T*)e->d_WeS_b : (const T*)e->d_WeS_f, d, e->d_hpart, P.wdp, P.Wne,
-                       e->d_rowxp);
+template <class T, int KP>
+static void enc_fwd_run(Engine* e, const Dims& d, const void* WeS, float* hpart, hipStream_t st) {
+    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_ents,
+                       e->d_seg, e->d_toff, (const T*)WeS, d, hpart);
 }
 template <class T, int KP>
 static size_t enc_bwd_lds(const Dims& d) {
@@ -1748,8 +1670,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
-        if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
-        else enc_fwd_nb<T, KP, 2>(e, d, P, st);
+        enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
@@ -1872,8 +1793,7 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     hipStream_t st = e->stream;
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
                        bf ? e->d_WeS_b : nullptr, e->d_mvec);
-    if (d.H == 1) enc_fwd_nb<T, KP, 1>(e, d, P, st);
-    else enc_fwd_nb<T, KP, 2>(e, d, P, st);
+    enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, (uint64_t)0,
                        (int64_t)0, e->d_lat,
@@ -1897,9 +1817,7 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
 // ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
 template <class T, int KP>
 static void enc_fwd_go(Engine* e, const Dims& d, const void* WeS, float* hpart) {
-    hipLaunchKernelGGL((k_enc_fwd<T, KP, 0>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP, 0>(d)), e->stream,
-                       e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, (const T*)WeS, d, hpart,
-                       (const float*)nullptr, (const float*)nullptr, (float*)nullptr);
+    enc_fwd_run<T, KP>(e, d, WeS, hpart, e->stream);
 }
 template <class T, int KP>
 static void enc_bwd_go(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
