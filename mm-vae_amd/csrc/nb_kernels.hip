@@ -1219,17 +1219,14 @@ struct EncBwdLds {
         o_part = o_raw + 64 * 68 * 4;
         o_scal = o_part + 4 * 64 * 4;
         o_wave = o_scal + nsc * 64 * 4;
-        wave_bytes = ((16 * S * 4 + 15) / 16) * 16 + 16 * 8 + 64 * RING;
+        wave_bytes = ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
         bytes = o_wave + 4 * wave_bytes;
     }
 };
 
 template <class T, int KP, bool H1, bool RAW>
-__global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cells,
-                                                 const int64_t* __restrict__ rowptr,
-                                                 const int32_t* __restrict__ col,
-                                                 const float* __restrict__ val,
-                                                 const int32_t* __restrict__ rtp, const float* __restrict__ lat,
+__global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                                                 const int32_t* __restrict__ toff, const float* __restrict__ lat,
                                                  const T* __restrict__ dhT, const T* __restrict__ WeP,
                                                  Dims d, float* __restrict__ slabE) {
     using M = MM<T>;
@@ -1251,10 +1248,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
     float* raw = reinterpret_cast<float*>(smem + L.o_raw);  // [64 genes][68] x
     float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][64]
     float* scal = reinterpret_cast<float*>(smem + L.o_scal);  // [1+H][64 cells]: dpre, dhnu_h
-    char* wpb = smem + L.o_wave + w * L.wave_bytes;
-    int32_t* rtl = reinterpret_cast<int32_t*>(wpb);
-    int64_t* rbl = reinterpret_cast<int64_t*>(wpb + ((16 * S * 4 + 15) / 16) * 16);
-    int32_t* rinc = reinterpret_cast<int32_t*>(rbl + 16);
+    int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_wave + w * L.wave_bytes);  // [S] tile offsets
     // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
@@ -1267,17 +1261,15 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         afr[s] = M::load(&dhT[(int64_t)(16 * min(lb, KP / 16 - 1) + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
                               (lane >> 4) * M::EPL]);
 
-    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, cells, row0, rtp, lane);
-    if (lane < 16) {
+    const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
+    fill_toffl(toffl, S, t0, d.NT, toff, wbk, lane);
+    const int64_t segw = seg[wbk];
+    if (RAW && lane < 16) {
         const int b = row0 + lane;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
-        rbl[lane] = rowptr[cell];
-        if (RAW) {
-            const float* Lr = lat + (int64_t)b * d.lat_stride;
-            const float ok = (b < d.B) ? 1.f : 0.f;
-            scal[16 * w + lane] = ok * Lr[d.LAT_DPRE];
-            for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = ok * Lr[d.LAT_DHNU + h];
-        }
+        const float* Lr = lat + (int64_t)b * d.lat_stride;
+        const float ok = (b < d.B) ? 1.f : 0.f;
+        scal[16 * w + lane] = ok * Lr[d.LAT_DPRE];
+        for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = ok * Lr[d.LAT_DHNU + h];
     }
     // this wave's 16 cell columns of both tiles
     auto zero_cols = [&]() {
@@ -1288,30 +1280,27 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
 #pragma unroll
             for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
     };
-    const int rl = lane & 15, sub = lane >> 4;  // row-per-lane entry walk (RowEntries)
-    auto scatter = [&](const RowEntries<6>& re, int t) {
-        re.visit(t, sub, col, val, [&](int gl, float x) {
-            lt[gl * LS + 16 * w + rl] = to_t<T>(log1p_cnt<T>(x));
-            if (RAW) raw[gl * 68 + 16 * w + rl] = x;
+    auto scatter = [&](const ListEntries& le) {
+        le.visit(ents, lane, [&](int r, int gl, float x) {
+            lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
+            if (RAW) raw[gl * 68 + 16 * w + r] = x;
         });
     };
     if (lb >= KP / 16)
 #pragma unroll
         for (int s = 0; s < KSB; ++s) afr[s] = M::zero();
 
-    wave_sync();  // rtl / rbl written above by this wave
-    const int32_t* rtr = rtl + rl * S;
-    const int64_t rbase = rbl[rl];
+    wave_sync();  // toffl written above by this wave
     const int nt = t1 - t0;
-    RowEntries<6> nxt;
+    ListEntries nxt;
     if (t0 < t1) {
-        RowEntries<6> first;
-        first.fetch(rtr, 0, rbase, sub, col, val);
-        nxt.fetch(rtr, min(1, nt - 1), rbase, sub, col, val);
+        ListEntries first;
+        first.fetch(ents, segw, toffl, 0, lane);
+        nxt.fetch(ents, segw, toffl, min(1, nt - 1), lane);
         wreg.store(wst);
         zero_cols();
         wave_sync();
-        scatter(first, t0);
+        scatter(first);
     }
     lds_barrier();
     for (int t = t0; t < t1; ++t) {
@@ -1368,10 +1357,10 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const int64_t* __restrict__ cel
         if (t + 1 < t1) {
             zero_cols();
             wave_sync();
-            scatter(nxt, t + 1);
+            scatter(nxt);
             wreg.store(wst);
         }
-        nxt.fetch(rtr, min(tl + 2, nt - 1), rbase, sub, col, val);
+        nxt.fetch(ents, segw, toffl, min(tl + 2, nt - 1), lane);
         lds_barrier();
     }
 }
@@ -1748,10 +1737,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
         if (d.H == 1)
             hipLaunchKernelGGL((k_enc_bwd<T, KP, true, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE);
         else
             hipLaunchKernelGGL((k_enc_bwd<T, KP, false, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, dhT, WeT, d, e->d_slabE);
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE);
     }
     {
         ScopedTimer tm(e, "k_grad_small");
@@ -1822,7 +1811,7 @@ static void enc_fwd_go(Engine* e, const Dims& d, const void* WeS, float* hpart) 
 template <class T, int KP>
 static void enc_bwd_go(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
     hipLaunchKernelGGL((k_enc_bwd<T, KP, true, false>), dim3(d.nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)),
-                       e->stream, e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_lat, (const T*)dhT,
+                       e->stream, e->d_ents, e->d_seg, e->d_toff, e->d_lat, (const T*)dhT,
                        (const T*)WeP, d, slab);
 }
 

@@ -288,10 +288,9 @@ struct VDecPtrs {
     const float* Wcd;
     const float* covar;
     const int64_t* cells;
-    const int64_t* rowptr;
-    const int32_t* col;
-    const float* val;
-    const int32_t* rtp;
+    const uint2* ents;     // batch entry lists (k_batch_lists)
+    const int64_t* seg;
+    const int32_t* toff;
     const void* WdP;       // [DP][KP] T
     const void* WdT;       // [KP][DP] T
     const float* rowfin;   // [Bpad][2]: alpha, beta (eval path: k_vrowfin)
@@ -342,7 +341,7 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 }
 
 struct VDecLds {
-    int o_g, o_t, o_part, o_wave, o_q1, o_rtl, o_rbl, o_rinc, wave_bytes, bytes;
+    int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, bytes;
     MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass) {
         o_g = 64 * KP * esz;
         o_t = o_g + 1024;
@@ -350,10 +349,8 @@ struct VDecLds {
         o_wave = o_part + (pass ? 4 * nq * 64 * 4 : 0);
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q1 = 16 * 68 * 4;                                   // after the l tile
-        o_rtl = o_q1 + (pass ? ((16 * QS * esz + 15) / 16) * 16 : 0);
-        o_rbl = o_rtl + ((16 * S * 4 + 15) / 16) * 16;
-        o_rinc = o_rbl + 16 * 8;
-        wave_bytes = o_rinc + 64;
+        o_toff = o_q1 + (pass ? ((16 * QS * esz + 15) / 16) * 16 : 0);
+        wave_bytes = o_toff + ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
         bytes = o_wave + 4 * wave_bytes;
     }
 };
@@ -385,9 +382,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     char* wp = smem + L.o_wave + w * L.wave_bytes;
     float* lt = reinterpret_cast<float*>(wp);
     T* q1 = reinterpret_cast<T*>(wp + L.o_q1);
-    int32_t* rtl = reinterpret_cast<int32_t*>(wp + L.o_rtl);
-    int64_t* rbl = reinterpret_cast<int64_t*>(wp + L.o_rbl);
-    int32_t* rinc = reinterpret_cast<int32_t*>(wp + L.o_rinc);
+    int32_t* toffl = reinterpret_cast<int32_t*>(wp + L.o_toff);
     const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
@@ -439,16 +434,14 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     f32x4 dz[KP / 16];
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) dz[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    fill_rtl(rtl, S, t0, d.NT, d.B, d.Ncells, Q.cells, row0, Q.rtp, lane);
-    if (lane < 16) {
-        const int b = row0 + lane;
-        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
-        rbl[lane] = Q.rowptr[cell];
-    }
+    const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
+    fill_toffl(toffl, S, t0, d.NT, Q.toff, wbk, lane);
+    const int64_t segw = Q.seg[wbk];
+    wave_sync();
 
-    TileEntries pend;
+    ListEntries pend;
     if (t0 < t1) {
-        tile_fetch(pend, rtl, S, 0, t0, lane, rinc, rbl, Q.col, Q.val);
+        pend.fetch(Q.ents, segw, toffl, 0, lane);
         stage_store();
     }
     lds_barrier();  // the first tile's entry loads stay in flight
@@ -459,10 +452,9 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
         for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
         wave_sync();
-        tile_visit(pend, rtl, S, tl, t, lane, rinc, rbl, Q.col, Q.val,
-                   [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<T>(fmaxf(x, 0.f)); });
+        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<T>(fmaxf(x, 0.f)); });
         wave_sync();
-        tile_fetch(pend, rtl, S, min(tl + 1, t1 - t0 - 1), min(t + 1, t1 - 1), lane, rinc, rbl, Q.col, Q.val);
+        pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
@@ -936,10 +928,9 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.Wcd = P.Wcd;
     Q.covar = e->d_covar;
     Q.cells = e->d_cells;
-    Q.rowptr = e->d_rowptr;
-    Q.col = e->d_col;
-    Q.val = e->d_val;
-    Q.rtp = e->d_rtp;
+    Q.ents = e->d_ents;
+    Q.seg = e->d_seg;
+    Q.toff = e->d_toff;
     Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
     Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
     Q.rowfin = e->d_rowfin;
