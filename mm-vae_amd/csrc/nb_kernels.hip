@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     const EncLds L(KP, (int)sizeof(T), S, XB, 0);
     char* wst = smem;
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
-    int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_rtl) + w * 16 * S;
+    int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_toff) + w * S;
 
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
@@ -617,7 +617,7 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
 };
 
 struct DecNBLds {
-    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_rtl, o_rbl, o_rsc, o_rinc, bytes;
+    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_toff, o_rsc, bytes;
     MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz) {
         const int wtile = 64 * KP * esz;
         o_gst = wtile;
@@ -627,11 +627,9 @@ struct DecNBLds {
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q2 = 16 * QS * esz;
         o_cc = o_q2 + 16 * 68 * 4;
-        o_rtl = o_cc + 16 * 64 * csz;
-        o_rbl = o_rtl + ((16 * S * 4 + 15) / 16) * 16;
-        o_rsc = o_rbl + 16 * 8;
-        o_rinc = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
-        wave_bytes = o_rinc + 64;
+        o_toff = o_cc + 16 * 64 * csz;
+        o_rsc = o_toff + ((S * 4 + 15) / 16) * 16;
+        wave_bytes = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
         bytes = o_wave + 4 * wave_bytes;
     }
 };
@@ -668,10 +666,8 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     T* q1 = reinterpret_cast<T*>(wp);
     float* q2 = reinterpret_cast<float*>(wp + L.o_q2);
     CT* cc = reinterpret_cast<CT*>(wp + L.o_cc);
-    int32_t* rtl = reinterpret_cast<int32_t*>(wp + L.o_rtl);
-    int64_t* rbl = reinterpret_cast<int64_t*>(wp + L.o_rbl);
+    int32_t* toffl = reinterpret_cast<int32_t*>(wp + L.o_toff);
     float* rsc = reinterpret_cast<float*>(wp + L.o_rsc);
-    int32_t* rinc = reinterpret_cast<int32_t*>(wp + L.o_rinc);
     const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
@@ -757,7 +753,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     float lossacc = 0.f;
     // ---- per-wave row data for the sparse pass ----
     const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
-    fill_toffl(rtl, S, t0, d.NT, Q.toff, wbk, lane);
+    fill_toffl(toffl, S, t0, d.NT, Q.toff, wbk, lane);
     const int64_t segw = Q.seg[wbk];
     if (lane < 16) {
         const int b = row0 + lane;
@@ -775,7 +771,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     wave_sync();  // toffl
     ListEntries pend;
     if (t0 < t1) {
-        pend.fetch(Q.ents, segw, rtl, 0, lane);
+        pend.fetch(Q.ents, segw, toffl, 0, lane);
         stage_store();
     }
     lds_barrier();  // the first tile's entry loads stay in flight
@@ -846,7 +842,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         wave_sync();
         lap(1);
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
-        pend.fetch(Q.ents, segw, rtl, min(tl + 1, t1 - t0 - 1), lane);
+        pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
         lap(2);
         // ---- 3. dense epilogue in the owner lanes ----
         // MASK: some of the wave's rows (last row block) or the tile's genes (last tile) are
@@ -939,18 +935,19 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
         for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         lap(3);
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
+        if (!(d.dbg & 4))
 #pragma unroll
-        for (int s = 0; s < ((d.dbg & 4) ? 0 : GK); ++s) {
-            const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
-            const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+            for (int s = 0; s < GK; ++s) {
+                const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
-            for (int lb = 0; lb < KP / 16; ++lb) {
-                const Fr bw = *reinterpret_cast<const Fr*>(
-                    tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
-                dzA[lb] = M::mma(a1, bw, dzA[lb]);
-                dzP[lb] = M::mma(a2, bw, dzP[lb]);
+                for (int lb = 0; lb < KP / 16; ++lb) {
+                    const Fr bw = *reinterpret_cast<const Fr*>(
+                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                    dzA[lb] = M::mma(a1, bw, dzA[lb]);
+                    dzP[lb] = M::mma(a2, bw, dzP[lb]);
+                }
             }
-        }
         lap(4);
         // ---- 5. combine the waves' column partials -> slab (fixed order) ----
         lds_barrier();

@@ -1,5 +1,5 @@
 // Shared device-side pieces of the NB and vMF engines: launch dimensions, wave helpers,
-// CSR tile streaming (cell-major rows densified 16 cells x 64 genes at a time) and the
+// the batch entry-list reader (16 cells x 64 genes densified per tile) and the
 // register-staged LDS tile copy.  Device-inline only: every __global__ kernel lives in
 // exactly one translation unit (nb_kernels.hip / vmf_kernels.hip).
 #pragma once
@@ -47,32 +47,6 @@ MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, 
         for (int c = 0; c < 4; ++c) out[c] += p[(int64_t)s * sstride + off + c * cstride];
 }
 
-// Per-wave tile pointers of the wave's 16 rows for the split's tiles t0 .. t0 + S - 1, read
-// from the per-dataset index (rtp [N+1][NT+1], row N = empty) by each row's cell id.
-// The 16 cell ids are loaded once (lanes 0..15) and broadcast by shuffles; the index loads of
-// a batch of 8 entries per lane are issued together (no dependent round trip per entry).
-MMVAE_DEV void fill_rtl(int32_t* rtl, int S, int t0, int NT, int B, int Ncells, const int64_t* __restrict__ cells,
-                        int row0, const int32_t* __restrict__ rtp, int lane) {
-    const int64_t mycell = cells[row0 + (lane & 15)];  // padding rows hold the empty row Ncells
-    const int lo = (int)(uint32_t)mycell, hi = (int)(mycell >> 32);
-    constexpr int U = 8;
-    for (int i0 = 0; i0 < 16 * S; i0 += 64 * U) {
-        int32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = min(i0 + lane + 64 * u, 16 * S - 1);
-            const int rr = i / S, tt = i % S;
-            const int64_t c = ((int64_t)__shfl(hi, rr, 64) << 32) | (uint32_t)__shfl(lo, rr, 64);
-            v[u] = rtp[c * (NT + 1) + min(t0 + tt, NT)];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + lane + 64 * u;
-            if (i < 16 * S) rtl[i] = v[u];
-        }
-    }
-}
-
 MMVAE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -90,66 +64,6 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
     if (threadIdx.x == 0)
         for (int i = 0; i < NW; ++i) t += sbuf[i];
     return t;  // valid in thread 0
-}
-
-// =======================================================================================
-// Per-wave CSR entry streams over 64-gene tiles (a wave owns 16 rows).  A tile's entries are
-// flattened over the rows (row-major, genes ascending) and spread over the lanes: lane l
-// takes entries l and l + 64 (the common case, prefetched a tile ahead into registers);
-// entries past 128 are fetched on the spot.  tile_rows() runs with the whole wave active
-// and publishes the rows' inclusive prefix counts to per-wave LDS (rinc[16]);
-// tile_entry_row() then only reads LDS, so it is safe inside divergent code.
-// rtl = the wave's tile pointers [16][S] (per-dataset index, fill_rtl), rbl = the rows' CSR bases [16].
-// =======================================================================================
-MMVAE_DEV int tile_rows(const int32_t* rtl, int S, int tl, int lane, int32_t* rinc) {
-    const int cnt = (lane < 16) ? rtl[lane * S + tl + 1] - rtl[lane * S + tl] : 0;
-    int inc = cnt;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const int v = __shfl_up(inc, o, 16);
-        if ((lane & 15) >= o) inc += v;
-    }
-    if (lane < 16) rinc[lane] = inc;
-    const int total = __shfl(inc, 15, 64);
-    wave_sync();
-    return total;
-}
-
-// row (0..15) holding flattened entry e (< total), and e's offset inside that row's range
-MMVAE_DEV int tile_entry_row(const int32_t* rinc, int e, int& within) {
-    const int4* r4 = reinterpret_cast<const int4*>(rinc);
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int4 v = r4[i];
-        r += (v.x <= e) + (v.y <= e) + (v.z <= e) + (i < 3 ? (v.w <= e) : 0);
-    }
-    within = e - (r > 0 ? rinc[r - 1] : 0);
-    return r;
-}
-
-struct TileEntries {
-    int total;
-    int row[2], gl[2];
-    float x[2];
-};
-
-MMVAE_DEV void tile_fetch(TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane, int32_t* rinc,
-                          const int64_t* rbl, const int32_t* __restrict__ col, const float* __restrict__ val) {
-    te.total = tile_rows(rtl, S, tl, lane, rinc);
-    // branch-free: every lane issues both loads (slots past the tile read entry 0 and are
-    // masked by row = -1), so hipcc keeps counted vmcnt waits (RowEntries::fetch)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int e = lane + 64 * k;
-        const bool ok = e < te.total;
-        int within;
-        const int r = min(tile_entry_row(rinc, ok ? e : 0, within), 15);
-        const int64_t gi = ok ? rbl[r] + rtl[r * S + tl] + within : 0;
-        te.row[k] = ok ? r : -1;
-        te.gl[k] = col[gi];  // raw gene id: consumed a tile later (no wait here)
-        te.x[k] = val[gi];
-    }
 }
 
 // One tile's entries of a wave's 16 rows from the per-step batch lists (batch.hip): lane l
@@ -187,83 +101,6 @@ struct ListEntries {
 // the wave block's tile offsets for the split's tiles t0 .. t0 + S - 1 into LDS
 MMVAE_DEV void fill_toffl(int32_t* toffl, int S, int t0, int NT, const int32_t* __restrict__ toff, int wb, int lane) {
     for (int i = lane; i < S; i += 64) toffl[i] = toff[(int64_t)wb * (NT + 1) + min(t0 + i, NT)];
-}
-
-// Prefetch ring of the CSR entries of the next R tiles of a wave (e[0] = next tile to visit):
-// the entry loads of a tile are issued R tiles before it is consumed, so a tile iteration no
-// longer waits out a full memory latency.  Tile tl keeps its row prefix counts in LDS slot
-// tl % R (rinc + 16 * slot), reused only after that tile has been visited.
-static constexpr int RING = 4;
-template <int R>
-struct EntryRing {
-    TileEntries e[R];
-    int slot[R];
-    MMVAE_DEV void fetch(int i, int tl, const int32_t* rtl, int S, int t0, int lane, int32_t* rinc, const int64_t* rbl,
-                         const int32_t* __restrict__ col, const float* __restrict__ val) {
-        slot[i] = tl % R;
-        tile_fetch(e[i], rtl, S, tl, t0 + tl, lane, rinc + 16 * slot[i], rbl, col, val);
-    }
-    MMVAE_DEV void shift() {
-#pragma unroll
-        for (int i = 0; i + 1 < R; ++i) {
-            e[i] = e[i + 1];
-            slot[i] = slot[i + 1];
-        }
-    }
-};
-
-// Row-per-lane form of a tile's CSR entries: lane l serves row r = l & 15 of the wave's 16 and
-// takes entries sub, sub + 4, sub + 8 (sub = l >> 4) of that row's segment in the tile;
-// entries past the NS slots are fetched on the spot.  No prefix scan, no LDS round trips
-// beyond the two tile pointers, no wave synchronisation: per tile the lane issues at most
-// 2 NS independent loads.  rbase = the row's CSR start (from rbl), rtr = the row's tile
-// pointers rtl + r * S.
-template <int NS>
-struct RowEntries {
-    int n;
-    int64_t base;
-    int gl[NS];
-    float x[NS];
-    // Loads are unconditional (an out-of-segment slot reads entry 0, always valid, and is
-    // masked afterwards): a load behind a branch makes hipcc wait vmcnt(0) at its first use,
-    // which would serialise the prefetch (cdna_hip_programming.md §5, trap (c)).
-    MMVAE_DEV void fetch(const int32_t* rtr, int tl, int64_t rbase, int sub, const int32_t* __restrict__ col,
-                         const float* __restrict__ val) {
-        const int s = rtr[tl];
-        n = rtr[tl + 1] - s;
-        base = rbase + s;
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const int idx = sub + 4 * k;
-            const int64_t gi = (idx < n) ? base + idx : 0;
-            gl[k] = col[gi];
-            x[k] = val[gi];
-        }
-    }
-    // f(gene-in-tile, x) for every entry of this lane
-    template <class F>
-    MMVAE_DEV void visit(int t, int sub, const int32_t* __restrict__ col, const float* __restrict__ val, F&& f) const {
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            if (sub + 4 * k < n) f(gl[k] - 64 * t, x[k]);  // masked slots hold entry 0: skipped
-        for (int idx = sub + 4 * NS; idx < n; idx += 4) f(col[base + idx] - 64 * t, val[base + idx]);
-    }
-};
-
-// visit every entry of the fetched tile: f(row, gene-in-tile, x)
-template <class F>
-MMVAE_DEV void tile_visit(const TileEntries& te, const int32_t* rtl, int S, int tl, int t, int lane,
-                          const int32_t* rinc, const int64_t* rbl, const int32_t* __restrict__ col,
-                          const float* __restrict__ val, F&& f) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (te.row[k] >= 0) f(te.row[k], te.gl[k] - 64 * t, te.x[k]);
-    for (int e = 128 + lane; e < te.total; e += 64) {
-        int within;
-        const int r = tile_entry_row(rinc, e, within);
-        const int64_t gi = rbl[r] + rtl[r * S + tl] + within;
-        f(r, col[gi] - 64 * t, val[gi]);
-    }
 }
 
 // log1p of a count: exact libm form in the f32 parity mode; for bf16 operand tiles one v_log of
@@ -416,17 +253,14 @@ MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int
         }
 }
 
-// LDS carve shared by the two encoder kernels (host computes the same size)
+// LDS carve of k_enc_fwd (host computes the same size)
 struct EncLds {
-    int o_x, o_rtl, o_rbl, o_rinc, o_rsc, bytes;
+    int o_x, o_toff, bytes;
     MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre) {
         const int stb = KP * 64 * esz;
         o_x = pre + 2 * stb;
-        o_rtl = o_x + 4 * xbytes_per_wave;
-        o_rbl = o_rtl + ((4 * 16 * S * 4 + 15) / 16) * 16;
-        o_rinc = o_rbl + 4 * 16 * 8;
-        o_rsc = o_rinc + 4 * 16 * RING * 4;
-        bytes = o_rsc + 4 * 16 * (1 + HMAX) * 4;
+        o_toff = o_x + 4 * xbytes_per_wave;  // [4 waves][S] tile offsets
+        bytes = o_toff + ((4 * S * 4 + 15) / 16) * 16;
     }
 };
 
