@@ -163,7 +163,7 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
 }
 
 hipError_t build_batch_lists(Engine* e, int64_t B, const float* wdp, const float* Wne, float* rowdots) {
-    const int64_t Bp = (B + 63) / 64 * 64, WB = Bp / 16;
+    const int64_t Bp = pad_rows(B), WB = Bp / 16;
     ScopedTimer tm(e, "k_batch_lists");
     const size_t tab = sizeof(int32_t) * ((size_t)e->NT + 1 + 16 * ((size_t)e->NT + 1) + 16 * (size_t)e->NT);
     if (tab + 8 * 1024 > 160 * 1024) return hipErrorInvalidValue;  // D beyond ~75k genes

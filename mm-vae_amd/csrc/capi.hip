@@ -203,7 +203,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->H = cfg->H;
     e->R = cfg->R;
     e->Bmax = cfg->max_batch;
-    e->Bpad = (cfg->max_batch + 63) / 64 * 64;
+    e->Bpad = pad_rows(cfg->max_batch);
     e->nrb_max = e->Bpad / 64;
     if (cfg->model == MMVAE_MODEL_VMF) {
         e->H = e->R = 1;  // unused by the vMF model
@@ -614,7 +614,7 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
     HIPCHK(e, hipMemcpyAsync(e->d_cells, e->h_cells_pin, sizeof(int64_t) * Bp, hipMemcpyHostToDevice, e->stream));
     // entry-list segments of the batch's 16-row wave blocks (batch.hip): host prefix of the
     // rows' nonzero counts; the list buffer grows (outside any step) when a batch needs more
-    const int64_t Bq = (B + 63) / 64 * 64, WB = Bq / 16;
+    const int64_t Bq = pad_rows(B), WB = Bq / 16;
     int64_t tot = 0;
     for (int64_t wb = 0; wb < WB; ++wb) {
         e->h_seg_pin[wb] = tot;

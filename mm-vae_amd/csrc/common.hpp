@@ -65,6 +65,20 @@ MMVAE_DEV void glds16(const void* g, void* lds_wave_base) {
     __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 // diagnostic in-kernel stamp (shader clock); only in MMVAE_DBG-gated diagnostic paths
+// constant-rate (100 MHz) clock shared by all CUs, and this wave's placement (diagnostics)
+MMVAE_DEV uint64_t realtime_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+// xcc << 16 | se << 8 | cu  (HW_REG_HW_ID = 4, HW_REG_XCC_ID = 20)
+MMVAE_DEV uint32_t wave_place() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xf;
+    return (xcc << 16) | (((hw >> 13) & 7) << 8) | ((hw >> 8) & 15);
+}
 MMVAE_DEV uint64_t stamp_now() {
     uint64_t t;
     __builtin_amdgcn_sched_barrier(0);

@@ -11,6 +11,11 @@
 
 namespace mmvae {
 
+// Batch rows are padded to whole 128-row blocks: decoder pass B runs 128 rows per workgroup,
+// the other row-blocked kernels 64 (padding rows point at the dataset's empty row N).
+static constexpr int64_t ROW_ALIGN = 128;
+inline int64_t pad_rows(int64_t B) { return (B + ROW_ALIGN - 1) / ROW_ALIGN * ROW_ALIGN; }
+
 struct ParamSlot {
     std::string name;
     std::vector<int64_t> shape;
@@ -36,7 +41,7 @@ struct Engine {
     int64_t D = 0, DP = 0, NT = 0;  // genes, padded to 64, #64-gene tiles
     int64_t K = 0, KP = 0;          // latent, padded (32 or 64)
     int64_t C = 1, H = 1, R = 1;
-    int64_t Bmax = 0, Bpad = 0;     // max rows, padded to 64
+    int64_t Bmax = 0, Bpad = 0;     // max rows, padded (pad_rows)
     int64_t nrb_max = 0;            // row blocks of 64 at Bmax
 
     // ---- dataset ----

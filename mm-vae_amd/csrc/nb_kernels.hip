@@ -23,6 +23,7 @@
 //   k_enc_bwd     dh^T x log1p(x) tiles on MFMA -> ln_x_sd grad; raw-x column sums
 //   k_grad_small / k_grad_genes   deterministic slab reductions -> flat gradient buffer
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 #include "engine.hpp"
@@ -616,26 +617,35 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
     }
 };
 
+// Pass B runs NW = 8 waves (128 rows, two 64-row slab blocks) per workgroup and one
+// workgroup per CU where the LDS allows (bf16): all waves of a CU advance tile by tile behind
+// the same barriers (two co-resident 4-wave workgroups drift apart under the oldest-first
+// issue arbitration and the younger one finishes alone at half occupancy), and the staged
+// decoder tiles serve 128 rows instead of 64.  NW = 4 (64 rows, two workgroups per CU) otherwise.
 struct DecNBLds {
     int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_toff, o_rsc, bytes;
-    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz) {
-        const int wtile = 64 * KP * esz;
-        o_gst = wtile;
-        o_tst = o_gst + 1024;
-        o_part = o_tst + KP * 64 * esz;
-        o_wave = o_part + ((4 * nq * 64 * 4 + 15) / 16) * 16;
+    int sw, st, sp;  // per-buffer strides: W tile, WdT tile (bytes), column partials (floats)
+    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW) {
+        const int nbuf = NW == 8 ? 2 : 1;  // double-buffered stage + partials: one barrier per tile
+        sw = 64 * KP * esz;
+        st = KP * 64 * esz;
+        sp = ((NW * nq * 64 * 4 + 15) / 16) * 4;
+        o_gst = nbuf * sw;
+        o_tst = o_gst + nbuf * 1024;
+        o_part = o_tst + nbuf * st;
+        o_wave = o_part + nbuf * sp * 4;
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q2 = 16 * QS * esz;
         o_cc = o_q2 + 16 * 68 * 4;
         o_toff = o_cc + 16 * 64 * csz;
         o_rsc = o_toff + ((S * 4 + 15) / 16) * 16;
         wave_bytes = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
-        bytes = o_wave + 4 * wave_bytes;
+        bytes = o_wave + NW * wave_bytes;
     }
 };
 
-template <class T, int KP, int CM, int RM>
-__global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
+template <class T, int KP, int CM, int RM, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     using M = MM<T>;
     using Fr = typename M::frag;
     using CP = CorrPair<T>;
@@ -651,13 +661,14 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
-    const int row0 = rb * 64 + 16 * w;
+    constexpr int NTH = 64 * NW;
+    const int sp = blockIdx.x % d.nsD, rbw = blockIdx.x / d.nsD;
+    const int row0 = rbw * 16 * NW + 16 * w;
     const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT));
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
@@ -679,25 +690,25 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
     // ---- staging of the decoder tile, its gene records and the WdT tile ----
-    RegStage<64, RBW> wreg;
-    RegStage<KP, RBT> treg;
+    RegStage<64, RBW, NTH> wreg;
+    RegStage<KP, RBT, NTH> treg;
     float4 greg = float4{0.f, 0.f, 0.f, 0.f};
     auto stage_load = [&](int t) {
         wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
         treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
-    auto stage_store = [&]() {
-        wreg.store(wst);
-        treg.store(tst);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[threadIdx.x] = greg;
+    auto stage_store = [&](int b_) {
+        wreg.store(wst + b_ * L.sw);
+        treg.store(tst + b_ * L.st);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
     // row log-sum-exp (log2 units) from pass A's split partials, 4 threads per row; split 0
     // also publishes it for pass C
     {
         const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
-        const int b = rb * 64 + rr;
+        const int b = rbw * 16 * NW + rr;
         float mm = -INFINITY;
         for (int s2 = pp; s2 < d.nsA; s2 += 4) mm = fmaxf(mm, Q.lsep[((int64_t)s2 * d.Bpad + b) * 2]);
         mm = fmaxf(mm, __shfl_xor(mm, 1, 64));
@@ -772,12 +783,13 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     ListEntries pend;
     if (t0 < t1) {
         pend.fetch(Q.ents, segw, toffl, 0, lane);
-        stage_store();
+        stage_store(0);
     }
     lds_barrier();  // the first tile's entry loads stay in flight
 
     // diagnostic (MMVAE_DBG & 64): per-wave phase cycles into dzp (outputs invalid)
     const bool stamps = (d.dbg & 64) != 0;
+    const uint64_t rt0 = stamps ? realtime_now() : 0;
     uint64_t st_[7] = {0, 0, 0, 0, 0, 0, 0}, tp_ = stamps ? stamp_now() : 0;
     auto lap = [&](int i_) {
         if (stamps) {
@@ -789,6 +801,12 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
         stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
+        constexpr bool DB = NW == 8;
+        const int buf = DB ? (tl & 1) : 0;
+        const char* wsb = wst + buf * L.sw;
+        const char* tsb = tst + buf * L.st;
+        const float4* gsb = gst + 64 * buf;
+        float* pb = part + buf * L.sp;
         // ---- 1. logits -> p (into the wave's LDS p tile) ----
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
@@ -796,8 +814,8 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
-            const float4 g4 = gst[gl];
+                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wsb + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+            const float4 g4 = gsb[gl];
             float wcd[CM];
             wcd[0] = g4.z;
 #pragma unroll
@@ -817,7 +835,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
             const float* rs_ = rsc + r * NRS;
             const float p = q2[r * PS + gl];
             const float mu = fmaf(p, rs_[0], 1e-4f);
-            const float4 g4 = gst[gl];
+            const float4 g4 = gsb[gl];
             float wnd[RM];
             wnd[0] = g4.w;
 #pragma unroll
@@ -856,7 +874,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                 const int gl = 16 * gb + (lane & 15);
                 const int gene = 64 * t + gl;
                 const bool gv = gene < d.D;
-                const float4 g4 = gst[gl];
+                const float4 g4 = gsb[gl];
                 const float cn = g4.y;
                 float wnd[RM];
                 wnd[0] = g4.w;
@@ -903,7 +921,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
                     q1[rl * QS + gl] = to_t<T>(pq.x);
                     q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
                 }
-                float* pw = part + w * nq * 64 + gl;
+                float* pw = pb + w * nq * 64 + gl;
                 if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
                     pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
                                                           csduz[0].x + csduz[0].y);
@@ -943,31 +961,41 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
                     const Fr bw = *reinterpret_cast<const Fr*>(
-                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                        tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
                     dzA[lb] = M::mma(a1, bw, dzA[lb]);
                     dzP[lb] = M::mma(a2, bw, dzP[lb]);
                 }
             }
         lap(4);
         // ---- 5. combine the waves' column partials -> slab (fixed order) ----
+        // double-buffered (NW = 8): the next tile's stage goes into the other buffer before the
+        // tile's single barrier; buffer b is rewritten only after the next barrier, which every
+        // wave reaches after its combine reads of b
+        if (DB && t + 1 < t1) stage_store(buf ^ 1);
         lds_barrier();
-        for (int i = threadIdx.x; i < nq * 64; i += 256) {
-            const int q = i >> 6, g = i & 63;
-            const float v = part[(0 * nq + q) * 64 + g] + part[(1 * nq + q) * 64 + g] + part[(2 * nq + q) * 64 + g] +
-                            part[(3 * nq + q) * 64 + g];
-            Q.slabB[((int64_t)rb * nq + q) * d.DP + 64 * t + g] = v;
+        for (int i = threadIdx.x; i < (NW / 4) * nq * 64; i += NTH) {  // per 64-row slab block h
+            const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
+            const float* ph = pb + 4 * h * nq * 64;
+            const float v = ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
+                            ph[(3 * nq + q) * 64 + g];
+            Q.slabB[((int64_t)(rbw * (NW / 4) + h) * nq + q) * d.DP + 64 * t + g] = v;
         }
         lap(5);
-        if (t + 1 < t1) stage_store();
-        lds_barrier();
+        if (!DB) {
+            if (t + 1 < t1) stage_store(0);
+            lds_barrier();
+        }
         lap(6);
     }
     if (stamps) {
         vm_wait_all();
         __syncthreads();
         if (lane == 0) {
-            float* o = Q.dzp + ((int64_t)blockIdx.x * 4 + w) * 8;
+            float* o = Q.dzp + ((int64_t)blockIdx.x * NW + w) * 16;
             for (int i_ = 0; i_ < 7; ++i_) o[i_] = (float)st_[i_];
+            o[8] = (float)wave_place();
+            o[9] = (float)(rt0 & 0xffffffu);           // start / end, 100 MHz ticks (low bits)
+            o[10] = (float)(realtime_now() & 0xffffffu);
         }
         return;
     }
@@ -1002,7 +1030,12 @@ __global__ __launch_bounds__(256, 2) void k_dec_nb(DecPtrs Q, Dims d) {
     __syncthreads();
     if (lane == 0) part[w] = lw;
     __syncthreads();
-    if (threadIdx.x == 0) Q.lossp[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+    if (threadIdx.x == 0) {
+        float l = 0.f;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) l += part[i];
+        Q.lossp[blockIdx.x] = l;
+    }
 }
 
 // =======================================================================================
@@ -1557,7 +1590,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.H = (int)e->H;
     d.R = (int)e->R;
     d.B = (int)B;
-    d.Bpad = (int)((B + 63) / 64 * 64);
+    d.Bpad = (int)pad_rows(B);
     d.nrb = d.Bpad / 64;
     d.nsE = e->nsplit_e;
     d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
@@ -1642,6 +1675,11 @@ static size_t enc_bwd_lds(const Dims& d) {
     return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX)).bytes;
 }
 
+static bool getenv_is(const char* name, const char* value) {
+    const char* v = std::getenv(name);
+    return v && std::strcmp(v, value) == 0;
+}
+
 template <class T, int KP>
 static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
                                 uint64_t step_id, int64_t row_offset) {
@@ -1690,9 +1728,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     Q.slabB = e->d_slabB;
     Q.slabC = e->d_slabC;
     Q.lossp = e->d_lossp;
-    const dim3 gdec(nrb * d.nsD);
-    const dim3 gdecA(nrb * d.nsA);
     const bool small_cr = (d.C == 1 && d.R == 1);
+    // pass B: 16 NW rows per workgroup (NW = 8 where the LDS carve fits, MMVAE_DEC_NW=4 forces 4)
+    const int nqB = (1 + d.C) + 1 + d.R;
+    const int csz = bf ? 4 : 8;
+    const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8).bytes;
+    const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !getenv_is("MMVAE_DEC_NW", "4")) ? 8 : 4;
+    const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
+    const dim3 gdecA(nrb * d.nsA);
     {
         ScopedTimer tm(e, "k_dec_lse");
         if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
@@ -1700,20 +1743,20 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_nb");
-        const int nqB = (1 + d.C) + 1 + d.R;
-        const int csz = bf ? 4 : 8;
-        if (small_cr)
-            hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1>), gdec, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz).bytes, st, Q, d);
+        if (nwB == 8) {
+            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1, 8>), gdecB, dim3(512), ldsB8, st, Q, d);
+        } else if (small_cr)
+            hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1, 4>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4).bytes, st, Q, d);
         else
-            hipLaunchKernelGGL((k_dec_nb<T, KP, CMAX, RMAX>), gdec, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<T, KP, CMAX, RMAX, 4>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4).bytes, st, Q, d);
     }
     NBGrads G = nb_grads(e);
     if (!update) {
         ScopedTimer tm(e, "k_loss");
         hipLaunchKernelGGL(k_grad_small, dim3(1), dim3(256), 0, st, d, e->d_small, 0, G, e->d_smallg, e->d_lossp,
-                           (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
+                           (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
         return hipGetLastError();
     }
     {
@@ -1743,7 +1786,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         ScopedTimer tm(e, "k_grad_small");
         const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
         hipLaunchKernelGGL(k_grad_small, dim3(1 + (SMALL + 31) / 32), dim3(256), 0, st, d, e->d_small,
-                           e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdec.x, e->d_lossp + e->klp_off, e->n_lat_wg,
+                           e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg,
                            e->d_out, 1);
     }
     {

@@ -268,18 +268,21 @@ struct EncLds {
 // swizzled LDS image read by swz_off<RB>: loads issued early, ds_write_b128 late, so the
 // copy overlaps a compute phase without an LDS-DMA in flight (hipcc drains vmcnt(0) before
 // LDS reads while a DMA is outstanding).
-template <int NR, int RB>
+template <int NR, int RB, int NTH = 256>
 struct RegStage {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    static constexpr int NC = NR * RB / 16 / 256;  // 16-byte chunks per thread (1, 2 or 4)
-    static_assert(NC >= 1 && NC <= 4, "RegStage: 1..4 chunks per thread");
+    static constexpr int CH = NR * RB / 16;             // 16-byte chunks of the tile
+    static constexpr int NC = (CH + NTH - 1) / NTH;     // chunks per thread (1, 2 or 4)
+    static constexpr bool PART = CH < NTH;              // fewer chunks than threads: the rest idle
+    static_assert(NC >= 1 && NC <= 4 && (PART || CH % NTH == 0), "RegStage: 1..4 whole chunks per thread");
     u32x4 v0, v1, v2, v3;
     MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
-        const int c = (int)threadIdx.x + 256 * i;
+        const int c = PART ? min((int)threadIdx.x, CH - 1) : (int)threadIdx.x + NTH * i;
         return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
     }
     MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
-        const int c = (int)threadIdx.x + 256 * i;
+        const int c = (int)threadIdx.x + NTH * i;
+        if (PART && c >= CH) return;
         *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
     }
     MMVAE_DEV void load(const char* src, int64_t ld) {

@@ -866,7 +866,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.H = 1;
     d.R = 1;
     d.B = (int)B;
-    d.Bpad = (int)((B + 63) / 64 * 64);
+    d.Bpad = (int)pad_rows(B);
     d.nrb = d.Bpad / 64;
     d.nsE = e->nsplit_e;
     d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);

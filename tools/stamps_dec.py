@@ -11,11 +11,14 @@ eng.init_params(seed=7)
 for i in range(3):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)
 nsd = int(os.environ.get("NSD", "8"))
-nwg = (B // 64) * nsd
-buf = np.zeros(nwg * 4 * 8, np.float32)
+NW = 8  # waves per pass-B workgroup (DEC_NW)
+nwg = (B // (16 * NW)) * nsd
+buf = np.zeros(nwg * NW * 16, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
-st = buf.reshape(-1, 8)[:, :7]
+full = buf.reshape(-1, 16)
+np.save(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "stamps_dec.npy"), full)
+st = full[:, :7]
 names = ["logits+exp", "sparse", "fetch", "epilogue", "dz+zero", "barrier+slab", "stage+barrier"]
 tot = st.sum(1)
 ntile = (313 + nsd - 1) // nsd
@@ -24,7 +27,7 @@ for n, v in zip(names, st.mean(0)):
     print("  %-14s %8.0f cyc/wave  %6.0f per tile  %5.1f%%" % (n, v, v / ntile, 100 * v / tot.mean()))
 print("max-wave total / mean: %.3f" % (tot.max() / tot.mean()))
 # imbalance: per-wave totals by gene split and by row block (blockIdx = rb * nsD + sp)
-tw = tot.reshape(-1, 4)            # [wg][wave]
+tw = tot.reshape(-1, NW)           # [wg][wave]
 wg = tw.max(1)                     # a workgroup ends with its slowest wave
 sp = np.arange(wg.size) % nsd
 rb = np.arange(wg.size) // nsd
