@@ -148,7 +148,8 @@ int mmvae_timing_count(mmvae_h h, int32_t* n);
 int mmvae_timing_get(mmvae_h h, int32_t idx, const char** name, double* total_ms, int64_t* launches);
 int mmvae_timing_reset(mmvae_h h);
 /* Diagnostics: copy n floats of an internal workspace (0 = encoder partials, 1 = decoder dz, 2 = pass-C slab
- * partials; the MMVAE_DBG stamp builds write per-wave phase cycles there) to the host. */
+ * partials; the MMVAE_DBG stamp builds write per-wave phase cycles there; 3 = the last step's latent
+ * noise eps [Bpad][K], rows in the staged order) to the host. */
 int mmvae_debug_copy(mmvae_h h, int32_t which, float* host, int64_t n);
 
 /* ---- operators.hh (vMF observation model scalars) ----------------------------------

@@ -771,9 +771,19 @@ int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms
 }
 
 int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
-    if (!e || !host || n < 0 || which < 0 || which > 2) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
+    if (!e || !host || n < 0 || which < 0 || which > 3) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
     // 0: encoder split partials (k_enc_fwd stamps), 1: decoder dz partials (k_dec_nb stamps),
-    // 2: pass-C column slab (k_dec_lse stamps)
+    // 2: pass-C column slab (k_dec_lse / latent stamps), 3: the last step's latent noise eps
+    //    [Bpad][K] (rows in the step's staged order)
+    if (which == 3) {
+        if (n > e->Bpad * e->K) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds Bpad * K");
+        HIPCHK(e, hipSetDevice(e->device));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        std::vector<float> lat((size_t)(e->Bpad * e->lat_stride));
+        HIPCHK(e, hipMemcpy(lat.data(), e->d_lat, sizeof(float) * lat.size(), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i) host[i] = lat[(size_t)((i / e->K) * e->lat_stride + e->LAT_EPS + i % e->K)];
+        return MMVAE_OK;
+    }
     const int64_t cap = which == 0   ? (int64_t)e->nsplit_e * e->Bpad * e->KP
                         : which == 1 ? (int64_t)e->nsplit_d * e->Bpad * 2 * e->KP
                                      : (int64_t)e->nrb_max * (1 + e->C) * e->DP;

@@ -73,11 +73,11 @@ MMVAE_DEV uint64_t realtime_now() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
-// xcc << 16 | se << 8 | cu  (HW_REG_HW_ID = 4, HW_REG_XCC_ID = 20)
+// xcc << 16 | se << 12 | cu << 4 | simd  (HW_REG_HW_ID = 4, HW_REG_XCC_ID = 20)
 MMVAE_DEV uint32_t wave_place() {
     const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xf;
-    return (xcc << 16) | (((hw >> 13) & 7) << 8) | ((hw >> 8) & 15);
+    return (xcc << 16) | (((hw >> 13) & 7) << 12) | (((hw >> 8) & 15) << 4) | ((hw >> 4) & 3);
 }
 MMVAE_DEV uint64_t stamp_now() {
     uint64_t t;
@@ -305,9 +305,10 @@ MMVAE_DEV float philox_normal(uint64_t seed, uint64_t step, uint64_t row, uint32
     uint32_t c[4] = {(uint32_t)(k >> 1), (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)step,
                      (uint32_t)(step >> 32)};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    float u1 = ((c[0] >> 8) + 1) * (1.f / 16777217.f);  // (0,1]
-    float u2 = (c[1] >> 8) * (1.f / 16777216.f);        // [0,1)
-    float r = sqrtf(-2.f * logf(u1));
-    float a = 6.2831853071795864f * u2;
-    return (k & 1) ? r * sinf(a) : r * cosf(a);
+    const float u1 = ((c[0] >> 8) + 1) * (1.f / 16777217.f);  // (0,1]
+    const float u2 = (c[1] >> 8) * (1.f / 16777216.f);        // [0,1)
+    // Box-Muller on the hardware transcendentals: v_sin / v_cos take the angle in revolutions
+    // (sin(2 pi u2) with no range reduction), v_log is log2
+    const float r = __builtin_amdgcn_sqrtf(-2.f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
+    return r * ((k & 1) ? __builtin_amdgcn_sinf(u2) : __builtin_amdgcn_cosf(u2));
 }

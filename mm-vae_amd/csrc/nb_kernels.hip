@@ -35,6 +35,7 @@ struct NBPtrs {
     const float *xm, *lsd, *mub, *nub, *Wce, *bce, *Wm, *bm, *Wl, *bl, *Wcd, *bcd, *Wne, *bne, *Wnm,
         *bnm, *Wnl, *bnl, *Wnd, *bnd, *wdp, *bdp;
     const float *We, *be, *Wd, *bd;  // frozen (reference layouts: We [K][D], Wd [D][K])
+    float* dbg_out;                  // diagnostics only (MMVAE_DBG stamps)
 };
 
 struct NBGrads {
@@ -237,15 +238,47 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
     __shared__ float sred[4];
     __shared__ float sRX[LAT_CELLS][1 + HMAX];  // depth pre-activation, nu_enc(x)
-    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // first cell of this wave (4 cells per wave)
+    // diagnostic (MMVAE_DBG & 2048): realtime stamps of the phases into P.dbg_out (outputs invalid)
+    const bool rts = (d.dbg & 2048) != 0 && mode == 0;
+    uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i_) {  // constant index at every call: rt_ stays in registers
+        if (rts) rt_[i_] = realtime_now();
+    };
+    mark(0);
+    // every global input first, waits in issue order (one memory round, plus one for the loads
+    // that depend on a cell id); the per-cell loop below then only stores
+    HeadsStage hst;
+    hst.issue(P.Wm, P.Wl, K);
+    const int nqx = 1 + d.H;
+    float xs[4];  // raw-count dots (k_batch_lists), lanes < 1 + H
+    split_sum4(rowxp, 1, (int64_t)d.Bpad * nqx, (int64_t)bw * nqx + (k < nqx ? k : 0), nqx, k < nqx, xs);
+    float hs[4];  // the encoder's gene-split partials of h
+    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+    int pbv[4];
+    float cmv[4], epv[4], enp[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        const bool valid = b < d.B;
+        pbv[c] = (perm && valid) ? perm[b] : b;  // original batch position: the noise key
+        float cm = 0.f;
+        if (k < K && mode == 0) {
+            cm = P.bce[k];
+            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
+        }
+        cmv[c] = cm;
+        epv[c] = (eps_in && k < K && valid) ? eps_in[(int64_t)pbv[c] * K + k] : 0.f;
+        enp[c] = (eps_in && k < d.R && valid) ? eps_in[(int64_t)d.B * K + (int64_t)pbv[c] * d.R + k] : 0.f;
+    }
+    hst.store(K, sWm, sWl);
+    mark(1);
     {
-        // raw-count dots from the encoder's gene-split partials (+ bias); rowx for k_latent_bwd
-        const int nq = 1 + d.H;
-        float xs[4];
-        split_sum4(rowxp, 1, (int64_t)d.Bpad * nq, (int64_t)bw * nq + (k < nq ? k : 0), nq, k < nq, xs);  // k_batch_lists
+        // raw-count dots (+ bias) -> sRX, and rowx for k_latent_bwd
+        const int nq = nqx;
         if (k < nq) {
             const float bias = (k == 0) ? P.bdp[0] : P.bne[k - 1];
 #pragma unroll
@@ -256,11 +289,10 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
             }
         }
     }
-    // h = sum of the encoder's gene-split partials - mvec + bias (split loads issued together)
+    // h = sum of the encoder's gene-split partials - mvec + bias
     const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
     const float hb = (k < K) ? P.be[k] - mvk : 0.f;
-    float hs[4];
-    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+    mark(2);
 #pragma unroll
     for (int c = 0; c < 4; ++c) sH[(4 * w + c) * 68 + k] = (k < K) ? hb + hs[c] : 0.f;
     __syncthreads();
@@ -268,6 +300,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
     heads_fwd(sH, sWm, sWl, K, w, lane, sM, sA);
     __syncthreads();
+    mark(3);
     float mean[4], av[4];
     const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
 #pragma unroll
@@ -279,17 +312,11 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
         const bool valid = b < d.B;
-        const int pb = (perm && valid) ? perm[b] : b;  // original batch position: the noise key
+        const int pb = pbv[c];
         float* L = lat + (int64_t)b * d.lat_stride;
         const float h = sH[(4 * w + c) * 68 + k];
-        float mn = mean[c], a = av[c];
-        if (k < K && mode == 0) {
-            float cm = P.bce[k];
-            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
-            mn += cm;
-        }
+        float mn = mean[c] + cmv[c], a = av[c];
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
         if (mode == 1) {
             if (k < K && b < d.B) {
@@ -301,7 +328,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         const float sig = expf(lnvar / 2.f);
         float eps = 0.f;
         if (k < K && b < d.B)
-            eps = eps_in ? eps_in[(int64_t)pb * K + k] : philox_normal(seed, step, row_offset + pb, k);
+            eps = eps_in ? epv[c] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
         if (k < K) {
             L[d.LAT_H + k] = h;
@@ -326,8 +353,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
             if (b < d.B)
-                en = eps_in ? eps_in[(int64_t)d.B * K + (int64_t)pb * d.R + k]
-                            : philox_normal(seed, step, row_offset + pb, 4096 + k);
+                en = eps_in ? enp[c] : philox_normal(seed, step, row_offset + pb, 4096 + k);
             const float zn = nm + en * expf(nlv / 2.f);
             L[d.LAT_NMEAN + k] = nm;
             L[d.LAT_AN + k] = an;
@@ -344,10 +370,21 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         }
     }
     if (mode == 1) return;
+    mark(4);
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
     if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * ((sred[0] + sred[1]) + (sred[2] + sred[3]));
+    if (rts) {
+        vm_wait_all();
+        mark(5);
+        if (lane == 0) {
+            float* o = P.dbg_out + ((int64_t)blockIdx.x * 4 + w) * 8;
+            for (int i = 0; i < 6; ++i) o[i] = (float)(rt_[i] & 0xffffffu);
+            o[6] = o[5];
+            o[7] = (float)wave_place();
+        }
+    }
 }
 
 // =======================================================================================
@@ -399,6 +436,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     constexpr int STB = 64 * RB + 1024;      // one stage buffer: W tile + grec tile
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint64_t rt_entry = (d.dbg & 256) ? realtime_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsA, rb = blockIdx.x / d.nsA;
     const int row0 = rb * 64 + 16 * w;
@@ -539,6 +577,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     }
     __syncthreads();
     if (stamps) tp_ = stamp_now();
+    const uint64_t rt_loop = stamps ? realtime_now() : 0;
     for (int t = t0; t < t1; t += 2) {
         tile(t, wrB, grB, wrA, grA);
         lap(2);
@@ -547,10 +586,14 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     }
     if (stamps) {
         if (lane == 0) {
-            float* o = Q.slabC + ((int64_t)blockIdx.x * 4 + w) * 4;
+            float* o = Q.slabC + ((int64_t)blockIdx.x * 4 + w) * 8;
             o[0] = (float)st_[0];
             o[1] = (float)st_[1];
             o[2] = (float)st_[2];
+            o[3] = (float)(rt_entry & 0xffffffu);  // 100 MHz ticks: entry, loop start, loop end
+            o[4] = (float)(rt_loop & 0xffffffu);
+            o[5] = (float)(realtime_now() & 0xffffffu);
+            o[6] = (float)wave_place();
         }
         return;
     }
@@ -1064,13 +1107,50 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h
     float* wpart = sH + LAT_CELLS * 68; // [4][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
+    // diagnostic (MMVAE_DBG & 1024): realtime stamps of the phases into slabC (outputs invalid)
+    const bool rts = (d.dbg & 1024) != 0;
+    uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i_) {  // constant index at every call: rt_ stays in registers
+        if (rts) rt_[i_] = realtime_now();
+    };
+    mark(0);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // 4 cells per wave
+    // ---- every global input first (the waits are in issue order: one memory round) ----
+    const int kk = min(k, K - 1), kr = min(k, R - 1);
+    float vval[4], vw[4], vmean[4], va[4], veps[4], vh[4], vnm[4], van[4], ven[4], vpre[4], vrx[4][HMAX];
+    int64_t vcell[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        vcell[c] = cells[b];  // padding rows hold the empty row N
+        const float* L = lat + (int64_t)b * d.lat_stride;
+        vval[c] = L[d.LAT_VALID];
+        vw[c] = L[d.LAT_W];
+        vmean[c] = L[d.LAT_MEAN + kk];
+        va[c] = L[d.LAT_A + kk];
+        veps[c] = L[d.LAT_EPS + kk];
+        vh[c] = L[d.LAT_H + kk];
+        vnm[c] = L[d.LAT_NMEAN + kr];
+        van[c] = L[d.LAT_AN + kr];
+        ven[c] = L[d.LAT_EPSN + kr];
+        const float* rx = rowx + (int64_t)b * d.rowx_stride;
+        vpre[c] = rx[0];
+#pragma unroll
+        for (int hh = 0; hh < HMAX; ++hh) vrx[c][hh] = (hh < H) ? rx[2 + hh] : 0.f;
+    }
+    HeadsStage hst;
+    hst.issue(P.Wm, P.Wl, K);
     float dzA4[4], dzP4[4];
     split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < K, dzA4);
     split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < K, dzP4);
+    float E4[4], dzn4[4];  // pass B's per-split row sums: E_b and dL/dznu_b (lanes < R)
+    split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R), 2 + R, true, E4);
+    split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R) + 2 + kr, 2 + R, k < R, dzn4);
+    hst.store(K, sWm, sWl);
+    mark(1);
+    mark(2);
     float* wp = wpart + w * NSM;
     float* p_dbm = wp;                 // [64]
     float* p_dbl = p_dbm + 64;         // [64]
@@ -1093,22 +1173,20 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         rdnm[h] = 0.f;
         rdnl[h] = 0.f;
     }
-    // ---- per cell: dmean, da (lane = k) ----
+    // ---- per cell: dmean, da (lane = k); the per-cell outputs to lat are stored after the loop ----
+    float o_dhn[4], o_dpre[4];
+    bool o_valid[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        float* L = lat + (int64_t)b * d.lat_stride;
-        const bool valid = (b < d.Bpad) && L[d.LAT_VALID] > 0.f;
-        float E = 0.f;
-        for (int s2 = 0; s2 < d.nsD; ++s2) E += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R)];
-        const float wb = L[d.LAT_W];
+        const bool valid = (b < d.Bpad) && vval[c] > 0.f;
+        const float E = E4[c];
+        const float wb = vw[c];
         float dmean = 0.f, da = 0.f, h = 0.f;
         if (k < K) {
-            const float A2 = (c == 0) ? dzA4[0] : (c == 1) ? dzA4[1] : (c == 2) ? dzA4[2] : dzA4[3];
-            const float Pb = (c == 0) ? dzP4[0] : (c == 1) ? dzP4[1] : (c == 2) ? dzP4[2] : dzP4[3];
-            const float dz = wb * (A2 - E * Pb);
-            const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
-            h = L[d.LAT_H + k];
+            const float dz = wb * (dzA4[c] - E * dzP4[c]);
+            const float mean = vmean[c], a = va[c], eps = veps[c];
+            h = vh[c];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
             const float sig = expf(lnvar / 2.f);
             dmean = dz + bn * mean;
@@ -1124,18 +1202,14 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         sH[(4 * w + c) * 68 + k] = h;
         rbm += dmean;
         rbl += da;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
 #pragma unroll
         for (int q = 0; q < CMAX; ++q)
-            if (q < C) rWce[q] += dmean * covar[cell * C + q];
+            if (q < C) rWce[q] += dmean * covar[vcell[c] * C + q];
         // ---- overdispersion path (lanes < R) and depth (lane 0) ----
-        const float* rx = rowx + (int64_t)b * d.rowx_stride;
         float dnm = 0.f, dan = 0.f;
         if (k < R && valid) {
-            float dzn = 0.f;
-            for (int s2 = 0; s2 < d.nsD; ++s2) dzn += rowB[((int64_t)s2 * d.Bpad + b) * (2 + R) + 2 + k];
-            dzn *= d.inv_n;
-            const float nm = L[d.LAT_NMEAN + k], an = L[d.LAT_AN + k], en = L[d.LAT_EPSN + k];
+            const float dzn = dzn4[c] * d.inv_n;
+            const float nm = vnm[c], an = van[c], en = ven[c];
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             dnm = dzn + bn * nm;
             const float dnl = dzn * en * expf(nlv / 2.f) * 0.5f + bn * 0.5f * (expf(nlv) - 1.f);
@@ -1143,8 +1217,8 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
 #pragma unroll
             for (int hh = 0; hh < HMAX; ++hh)
                 if (hh < H) {
-                    rdnm[hh] += dnm * rx[2 + hh];
-                    rdnl[hh] += dan * rx[2 + hh];
+                    rdnm[hh] += dnm * vrx[c][hh];
+                    rdnl[hh] += dan * vrx[c][hh];
                 }
             rbnm += dnm;
             rbnl += dan;
@@ -1154,18 +1228,23 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
             const float a1 = __shfl(dnm, q, 64), a2 = __shfl(dan, q, 64);
             if (k < H) dhn += P.Wnm[q * H + k] * a1 + P.Wnl[q * H + k] * a2;
         }
-        if (k < H && b < d.Bpad) {
-            L[d.LAT_DHNU + k] = valid ? dhn : 0.f;
-            if (valid) rbne += dhn;
-        }
-        if (k == 0 && b < d.Bpad) {
+        o_valid[c] = valid;
+        o_dhn[c] = dhn;
+        if (k < H && b < d.Bpad && valid) rbne += dhn;
+        {
             const float dd = (E + 1.f) * d.inv_n;   // dL/dd_b = sum_g dmu' p = (E_b + sum_g p_bg) / n, sum p = 1
-            const float pre = rx[0];
-            const float dpre = valid ? dd * dsoftplus(pre) : 0.f;
-            L[d.LAT_DPRE] = dpre;
-            rbdp += dpre;
+            o_dpre[c] = valid ? dd * dsoftplus(vpre[c]) : 0.f;
+            if (k == 0 && b < d.Bpad) rbdp += o_dpre[c];
         }
     }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b = bw + c;
+        float* L = lat + (int64_t)b * d.lat_stride;
+        if (k < H && b < d.Bpad) L[d.LAT_DHNU + k] = o_valid[c] ? o_dhn[c] : 0.f;
+        if (k == 0 && b < d.Bpad) L[d.LAT_DPRE] = o_dpre[c];
+    }
+    mark(3);
     __syncthreads();
     // ---- dh[16 cells][K] on f32 MFMA (wave w: latents 16w..16w+15) ----
     {
@@ -1202,7 +1281,9 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     if (k == 0) p_dbdp[0] = rbdp;
     // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells on f32 MFMA ----
     float* out = small + (int64_t)blockIdx.x * SMALL;
+    mark(4);
     heads_dW(sDM, sDA, sH, K, w, lane, out);
+    mark(5);
     __syncthreads();
     // ---- the small vectors: fixed-order sum of the four waves' partials ----
     const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + K,
@@ -1229,6 +1310,15 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     }
     for (int i = threadIdx.x; i < H; i += 256) out[o_bne + i] = wsum(b_bne + i);
     if (threadIdx.x == 0) out[o_bdp] = wsum(b_bdp);
+    if (rts) {
+        vm_wait_all();
+        mark(6);
+        if (lane == 0) {
+            float* o = P.dbg_out + ((int64_t)blockIdx.x * 4 + w) * 8;
+            for (int i = 0; i < 7; ++i) o[i] = (float)(rt_[i] & 0xffffffu);
+            o[7] = (float)wave_place();
+        }
+    }
 }
 
 // =======================================================================================
@@ -1523,6 +1613,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
 // =======================================================================================
 static NBPtrs nb_ptrs(Engine* e) {
     NBPtrs P;
+    P.dbg_out = e->d_slabC;
     P.xm = e->preg("x_mean");
     P.lsd = e->preg("ln_x_sd");
     P.mub = e->preg("mu_bias");

@@ -161,24 +161,36 @@ MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL
 // K x K head weights (K <= 64) into LDS images [k][65]: all 2 x 16 loads of a thread issued
 // before any store (clamped, unconditional addresses — counted waits, not one round trip per
 // element)
-MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, float* sWm,
-                              float* sWl) {
-    const int KK = K * K;
+// The K x K head weights (Wm, Wl) into LDS [k][65]: issue() loads into registers (no wait),
+// store() writes LDS — other loads issued between the two share the same memory round.
+struct HeadsStage {
     float tm[16], tl[16];
+    MMVAE_DEV void issue(const float* __restrict__ Wm, const float* __restrict__ Wl, int K) {
+        const int KK = K * K;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int i = min((int)threadIdx.x + 256 * u, KK - 1);
-        tm[u] = Wm[i];
-        tl[u] = Wl[i];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int i = (int)threadIdx.x + 256 * u;
-        if (i < KK) {
-            sWm[(i / K) * 65 + i % K] = tm[u];
-            sWl[(i / K) * 65 + i % K] = tl[u];
+        for (int u = 0; u < 16; ++u) {
+            const int i = min((int)threadIdx.x + 256 * u, KK - 1);
+            tm[u] = Wm[i];
+            tl[u] = Wl[i];
         }
     }
+    MMVAE_DEV void store(int K, float* sWm, float* sWl) const {
+        const int KK = K * K;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = (int)threadIdx.x + 256 * u;
+            if (i < KK) {
+                sWm[(i / K) * 65 + i % K] = tm[u];
+                sWl[(i / K) * 65 + i % K] = tl[u];
+            }
+        }
+    }
+};
+MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, float* sWm,
+                              float* sWl) {
+    HeadsStage hs;
+    hs.issue(Wm, Wl, K);
+    hs.store(K, sWm, sWl);
 }
 
 // ---- latent-head backward products on f32 MFMA (exact f32 FMA chains) ------------------

@@ -12,9 +12,11 @@ for i in range(2):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)   # pass A stamps land in dzp (pass B overwrites? no: B stamps off)
 nsa = int(os.environ.get("NSA", "32"))
 nwg = (B // 64) * nsa
-buf = np.zeros(nwg * 4 * 4, np.float32)
+buf = np.zeros(nwg * 4 * 8, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 2, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
-st = buf.reshape(-1, 4)[:, :3]
+full = buf.reshape(-1, 8)
+np.save(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "stamps_ac.npy"), full)
+st = full[:, :3]
 ntile = (313 + nsa - 1) // nsa
 print("waves", st.shape[0], "per tile cycles: compute %.0f  store+barrier %.0f  slab/loop %.0f" % tuple(st.mean(0) / ntile))
