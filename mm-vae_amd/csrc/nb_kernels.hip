@@ -424,7 +424,10 @@ struct DecPtrs {
 };
 
 // Passes A and C: each tile's decoder rows + gene records are staged ONCE per workgroup into
-// LDS by LDS-DMA (double-buffered, swizzled image), shared by the four waves.
+// LDS (register-staged, double-buffered, swizzled image) and shared by the four waves; a wave
+// owns 32 rows (two 16-row MFMA blocks), so every W fragment read from LDS feeds two MFMAs.
+// Workgroup = 128 rows x one gene split.
+static constexpr int AC_RPW = 2;  // 16-row MFMA blocks per wave
 template <class T, int KP, int PASS, int CM>
 MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     using M = MM<T>;
@@ -432,49 +435,57 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     constexpr int KS = KP / M::KSTEP;
     constexpr bool BF = sizeof(T) == 2;
     constexpr int RB = KP * (int)sizeof(T);  // bytes per staged gene row
-    constexpr int NCH = RB / 16;
     constexpr int STB = 64 * RB + 1024;      // one stage buffer: W tile + grec tile
+    constexpr int J = AC_RPW;
+    constexpr int WR = 16 * J;               // rows per wave
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t rt_entry = (d.dbg & 256) ? realtime_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = blockIdx.x % d.nsA, rb = blockIdx.x / d.nsA;
-    const int row0 = rb * 64 + 16 * w;
+    const int sp = blockIdx.x % d.nsA, rbw = blockIdx.x / d.nsA;
+    const int row0 = rbw * 4 * WR + WR * w;
     const int t0 = sp * d.tpsA, t1 = min(d.NT, t0 + d.tpsA);
     const int C = (CM == 1) ? 1 : d.C;
     const int nq = 1 + C;
     char* stg = smem;
-    float* part = reinterpret_cast<float*>(smem + 2 * STB);  // C: [2][4][nq][64]
+    float* part = reinterpret_cast<float*>(smem + 2 * STB);  // C: [2][4][nq][64]; prologue: [4 WR]
     const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
 
     if (PASS == 2) {  // w_b E_b from pass B's per-split row sums, 4 threads per row
-        const int rr = threadIdx.x >> 2, pp = threadIdx.x & 3;
-        const int b = rb * 64 + rr;
-        float E = 0.f;
-        for (int s2 = pp; s2 < d.nsD; s2 += 4) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + d.R)];
-        E += __shfl_xor(E, 1, 64);
-        E += __shfl_xor(E, 2, 64);
-        if (pp == 0) part[rr] = Q.lat[(int64_t)b * d.lat_stride + d.LAT_W] * E;
+        for (int rr0 = 0; rr0 < 4 * WR; rr0 += 64) {
+            const int rr = rr0 + (threadIdx.x >> 2), pp = threadIdx.x & 3;
+            const int b = rbw * 4 * WR + rr;
+            float E = 0.f;
+            for (int s2 = pp; s2 < d.nsD; s2 += 4) E += Q.rowB[((int64_t)s2 * d.Bpad + b) * (2 + d.R)];
+            E += __shfl_xor(E, 1, 64);
+            E += __shfl_xor(E, 2, 64);
+            if (pp == 0) part[rr] = Q.lat[(int64_t)b * d.lat_stride + d.LAT_W] * E;
+        }
         __syncthreads();
     }
-    Fr zfr[KS];
+    Fr zfr[J][KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
-    float lse2[4], wE[4], crow[4][CM], mrun[4], srun[4];
+    for (int j = 0; j < J; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int b = row0 + 4 * (lane >> 4) + r;
-        const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
+        for (int s = 0; s < KS; ++s)
+            zfr[j][s] = M::load(&Z[(int64_t)(row0 + 16 * j + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+    float lse2[J][4], wE[J][4], crow[J][4][CM], mrun[J][4], srun[J][4];
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
-        lse2[r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;      // written by k_dec_nb (split 0)
-        wE[r] = (PASS == 2) ? part[16 * w + 4 * (lane >> 4) + r] : 0.f;
-        mrun[r] = -1e30f;
-        srun[r] = 0.f;
-    }
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = row0 + 16 * j + 4 * (lane >> 4) + r;
+            const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
+#pragma unroll
+            for (int c = 0; c < CM; ++c) crow[j][r][c] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
+            lse2[j][r] = (PASS == 2) ? Q.rowfin[2 * b] : 0.f;  // written by k_dec_nb (split 0)
+            wE[j][r] = (PASS == 2) ? part[WR * w + 16 * j + 4 * (lane >> 4) + r] : 0.f;
+            mrun[j][r] = -1e30f;
+            srun[j][r] = 0.f;
+        }
+    if (PASS == 2) __syncthreads();  // part is reused for the column partials below
     // Register-staged decoder tiles, two in flight: tile t + 2 is loaded while tile t is
     // computed from LDS, tile t + 1 (loaded an iteration earlier) is written to the other LDS
     // buffer at the end — one LDS barrier per tile, no vmcnt(0) drain of a fresh DMA.
@@ -502,46 +513,86 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         const int buf = (t - t0) & 1;
         ld(nxt, gnxt, min(t + 2, t1 - 1));  // unconditional (clamped): counted waits
         const char* sb = stg + buf * STB;
+        if (PASS == 0) {
+            // online log-sum-exp in log2 units with one rescale per tile: the lane's 4 genes of
+            // the tile (one per 16-gene block) are reduced to their max first
+            f32x4 acc[4][J];
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) {
+                const int gl = 16 * gb + (lane & 15);
+#pragma unroll
+                for (int j = 0; j < J; ++j) acc[gb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const Fr bw = *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+#pragma unroll
+                    for (int j = 0; j < J; ++j) acc[gb][j] = M::mma(zfr[j][s], bw, acc[gb][j]);
+                }
+            }
+            float b2[4], w2[4][CM];
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) {
+                const int gl = 16 * gb + (lane & 15);
+                const float4 g4 = reinterpret_cast<const float4*>(sb + 64 * RB)[gl];
+                b2[gb] = g4.x * L2E;  // padded genes: -inf
+                w2[gb][0] = g4.z * L2E;
+#pragma unroll
+                for (int c = 1; c < CM; ++c)
+                    w2[gb][c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] * L2E : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float l2[4];
+#pragma unroll
+                    for (int gb = 0; gb < 4; ++gb) {
+                        float v = b2[gb];
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) v = fmaf(crow[j][r][c], w2[gb][c], v);
+                        l2[gb] = fmaf(acc[gb][j][r], L2E, v);
+                    }
+                    const float mn = fmaxf(mrun[j][r], fmaxf(fmaxf(l2[0], l2[1]), fmaxf(l2[2], l2[3])));
+                    float sacc = srun[j][r] * fexp2(mrun[j][r] - mn);
+#pragma unroll
+                    for (int gb = 0; gb < 4; ++gb) sacc += fexp2(l2[gb] - mn);
+                    srun[j][r] = sacc;
+                    mrun[j][r] = mn;
+                }
+        } else
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 acc[J];
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+            for (int j = 0; j < J; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const Fr bw = *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+#pragma unroll
+                for (int j = 0; j < J; ++j) acc[j] = M::mma(zfr[j][s], bw, acc[j]);
+            }
             const float4 g4 = reinterpret_cast<const float4*>(sb + 64 * RB)[gl];
             float wcd[CM];
             wcd[0] = g4.z;
 #pragma unroll
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
-            if (PASS == 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float lg = acc[r] + g4.x;
-#pragma unroll
-                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
-                    // online max / sum-exp, branch free.  Padded genes carry bias = -inf, so
-                    // df = -inf, e = 0: they add nothing (mrun starts finite, never NaN).
-                    const float df = lg - mrun[r];
-                    const float e = fexp(-fabsf(df));
-                    const bool up = df > 0.f;
-                    srun[r] = fmaf(srun[r], up ? e : 1.f, up ? 1.f : e);
-                    mrun[r] = fmaxf(mrun[r], lg);
-                }
-            } else {
+            {  // pass C
                 float cs[1 + CM];
 #pragma unroll
                 for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float lg = acc[r] + g4.x;
+                for (int j = 0; j < J; ++j)
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) lg = fmaf(crow[r][c], wcd[c], lg);
-                    const float wp = wE[r] * fexp2(fmaf(lg, L2E, -lse2[r]));
-                    cs[0] += wp;
+                    for (int r = 0; r < 4; ++r) {
+                        float lg = acc[j][r] + g4.x;
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[r][c], cs[1 + c]);
-                }
+                        for (int c = 0; c < CM; ++c) lg = fmaf(crow[j][r][c], wcd[c], lg);
+                        const float wp = wE[j][r] * fexp2(fmaf(lg, L2E, -lse2[j][r]));
+                        cs[0] += wp;
+#pragma unroll
+                        for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[j][r][c], cs[1 + c]);
+                    }
                 // per-wave partial of this tile (fixed-order combine after the tile barrier)
                 float* pw = part + ((buf * 4 + w) * nq) * 64 + gl;
                 if (CM == 1) {  // nq = 2
@@ -561,12 +612,12 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         if (t + 1 < t1) st(hold, ghold, buf ^ 1);
         lds_barrier();
         lap(1);
-        if (PASS == 2) {
+        if (PASS == 2) {  // 64-row slab block h = waves 2h, 2h + 1
             const float* pb = part + (buf * 4 * nq) * 64;
-            for (int i = threadIdx.x; i < nq * 64; i += 256) {
-                const int q = i >> 6, g = i & 63;
-                Q.slabC[((int64_t)rb * nq + q) * d.DP + 64 * t + g] =
-                    pb[(0 * nq + q) * 64 + g] + pb[(1 * nq + q) * 64 + g] + pb[(2 * nq + q) * 64 + g] + pb[(3 * nq + q) * 64 + g];
+            for (int i = threadIdx.x; i < 2 * nq * 64; i += 256) {
+                const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
+                Q.slabC[((int64_t)(2 * rbw + h) * nq + q) * d.DP + 64 * t + g] =
+                    pb[((2 * h) * nq + q) * 64 + g] + pb[((2 * h + 1) * nq + q) * 64 + g];
             }
         }
     };
@@ -599,21 +650,23 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     }
     if (PASS == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float m = mrun[r], s = srun[r];
+        for (int j = 0; j < J; ++j)
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
-                const float mn = fmaxf(m, m2);
-                s = s * expf(m - mn) + s2 * expf(m2 - mn);
-                m = mn;
+            for (int r = 0; r < 4; ++r) {
+                float m = mrun[j][r] * 0.6931471805599453f, s = srun[j][r];  // max back to natural units
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+                    const float mn = fmaxf(m, m2);
+                    s = s * expf(m - mn) + s2 * expf(m2 - mn);
+                    m = mn;
+                }
+                if ((lane & 15) == 0) {
+                    float* lp = Q.lsep + ((int64_t)sp * d.Bpad + row0 + 16 * j + 4 * (lane >> 4) + r) * 2;
+                    lp[0] = m;
+                    lp[1] = s;
+                }
             }
-            if ((lane & 15) == 0) {
-                float* lp = Q.lsep + ((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * 2;
-                lp[0] = m;
-                lp[1] = s;
-            }
-        }
     }
 }
 
@@ -1826,7 +1879,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8).bytes;
     const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !getenv_is("MMVAE_DEC_NW", "4")) ? 8 : 4;
     const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
-    const dim3 gdecA(nrb * d.nsA);
+    const dim3 gdecA(nrb / 2 * d.nsA);  // passes A / C: 128 rows per workgroup
     {
         ScopedTimer tm(e, "k_dec_lse");
         if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);

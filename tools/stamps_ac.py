@@ -11,7 +11,7 @@ eng.init_params(seed=7)
 for i in range(2):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)   # pass A stamps land in dzp (pass B overwrites? no: B stamps off)
 nsa = int(os.environ.get("NSA", "32"))
-nwg = (B // 64) * nsa
+nwg = (B // 128) * nsa  # 128 rows per workgroup
 buf = np.zeros(nwg * 4 * 8, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 2, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
