@@ -25,14 +25,14 @@ namespace mmvae {
 //      drops its row's entries of the chunk's tiles at their final positions, then the workgroup
 //      streams the chunk out with contiguous, full-line stores (no partial lines written from
 //      different waves or CUs).
-static constexpr int COPY_CAP_MAX = 12288;  // entries per LDS chunk (96 KB), less for very wide D
+static constexpr int COPY_CAP_MAX = 16384;  // entries per LDS chunk (<= 128 KB), less for wide D
 __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict__ cells,
                                                       const int64_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const float* __restrict__ val,
                                                       const int32_t* __restrict__ rtp, const int64_t* __restrict__ seg,
                                                       int NT, int cap, int32_t* __restrict__ toff,
                                                       uint2* __restrict__ ents, int dbg,
-                                                      const float* __restrict__ wdp, const float* __restrict__ Wne,
+                                                      const float2* __restrict__ dotw, const float* __restrict__ Wne,
                                                       int H, int D, float* __restrict__ rowdots) {
     extern __shared__ __attribute__((aligned(16))) char csm[];
     uint2* stage = reinterpret_cast<uint2*>(csm);                      // [cap]
@@ -45,7 +45,33 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     const int wb = blockIdx.x, b = wb * 16 + w;
     const int64_t c = cells[b];
     const int64_t s = rowptr[c];
-    for (int t = lane; t <= NT; t += 64) srt[w * (NT + 1) + t] = rtp[c * (int64_t)(NT + 1) + t];
+    const int rn = (int)(rowptr[c + 1] - s);  // the row's nonzeros (rt[NT])
+    // the row's first 1024 entries are requested before the index phase (chunk 0 starts at
+    // entry 0 of every row) so their latency hides behind it
+    constexpr int U = 16;
+    int g[U];
+    float x[U];
+    auto load = [&](int jA, int jB) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads
+            const int j = min(jA + 64 * u + lane, max(jB - 1, 0));
+            g[u] = col[s + j];
+            x[u] = val[s + j];
+        }
+    };
+    if (!(dbg & 512)) load(0, rn);
+    // the row's tile pointers: all loads of a group of 8 issued before the first LDS store
+    {
+        const int32_t* src = rtp + c * (int64_t)(NT + 1);
+        for (int t0 = 0; t0 <= NT; t0 += 512) {
+            int32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[min(t0 + 64 * u + lane, NT)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (t0 + 64 * u + lane <= NT) srt[w * (NT + 1) + t0 + 64 * u + lane] = v[u];
+        }
+    }
     if (tid == 0) scarry = 0;
     __syncthreads();
     // per tile: the rows' prefix (sbase, before the tile offset) and the tile count (into tw)
@@ -102,38 +128,36 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     };
     // software pipeline over chunks: the next chunk's first 1024 entries of the row are loaded
     // while the current chunk streams out
-    constexpr int U = 16;
-    int g[U];
-    float x[U];
-    auto load = [&](int jA, int jB) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads
-            const int j = min(jA + 64 * u + lane, max(jB - 1, 0));
-            g[u] = col[s + j];
-            x[u] = val[s + j];
-        }
-    };
-    // NB (wdp != null): the raw-count dots of depth and nu_enc (nb.hh:448, 498) ride along,
+    // NB (dotw != null): the raw-count dots of depth and nu_enc (nb.hh:448, 498) ride along,
     // every entry of the row passes through this wave exactly once
-    const bool dots = wdp != nullptr;
+    const bool dots = dotw != nullptr && !(dbg & 4096);  // 4096: diagnostic, dots skipped
     float dpre = 0.f, dhn[HMAX];
 #pragma unroll
     for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
     auto drop = [&](int j0, int jB, int cb) {  // masked LDS stores at the final positions
+        float2 wv[U];
+        if (dots) {  // every weight gather of the group in flight at once (clamped gene ids)
+#pragma unroll
+            for (int u = 0; u < U; ++u) wv[u] = dotw[(unsigned)g[u] < (unsigned)D ? g[u] : 0];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u + lane;
-            if (j < jB) {
-                stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
-                if (dots) {
-                    dpre = fmaf(x[u], wdp[g[u]], dpre);
-                    for (int h = 0; h < H; ++h) dhn[h < HMAX ? h : 0] = fmaf(x[u], Wne[(int64_t)h * D + g[u]], dhn[h < HMAX ? h : 0]);
-                }
+            if (j < jB) stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+        }
+        if (dots) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool in = j0 + 64 * u + lane < jB;
+                const float xv = in ? x[u] : 0.f;
+                dpre = fmaf(xv, wv[u].x, dpre);
+                dhn[0] = fmaf(xv, wv[u].y, dhn[0]);
+                for (int h = 1; h < H; ++h)
+                    if (in) dhn[h < HMAX ? h : 0] = fmaf(xv, Wne[(int64_t)h * D + g[u]], dhn[h < HMAX ? h : 0]);
             }
         }
     };
     int tA = 0, tB = NT > 0 ? chunk_end(0) : 0;
-    if (NT > 0) load(rt[0], rt[tB]);
     while (tA < NT) {
         const int cb = tw[tA], cnt = tw[tB] - cb;
         const int jA = rt[tA], jB = rt[tB];
@@ -146,7 +170,8 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
         const int tC = tB < NT ? chunk_end(tB) : NT;
         if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
         uint2* dst = ents + base + cb;
-        for (int i = tid; i < cnt; i += 1024) dst[i] = stage[i];
+        if (!(dbg & 8192))  // 8192: diagnostic, stream-out skipped (lists invalid)
+            for (int i = tid; i < cnt; i += 1024) dst[i] = stage[i];
         lds_barrier();  // stage reusable (the stores carry register copies)
         tA = tB;
         tB = tC;
@@ -162,15 +187,15 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     }
 }
 
-hipError_t build_batch_lists(Engine* e, int64_t B, const float* wdp, const float* Wne, float* rowdots) {
+hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const float* Wne, float* rowdots) {
     const int64_t Bp = pad_rows(B), WB = Bp / 16;
     ScopedTimer tm(e, "k_batch_lists");
     const size_t tab = sizeof(int32_t) * ((size_t)e->NT + 1 + 16 * ((size_t)e->NT + 1) + 16 * (size_t)e->NT);
     if (tab + 8 * 1024 > 160 * 1024) return hipErrorInvalidValue;  // D beyond ~75k genes
-    const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - tab) / 8) & ~1;
+    const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - 256 - tab) / 8) & ~1;  // 256: static LDS
     hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
                        e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
-                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(), wdp, Wne,
+                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(), dotw, Wne,
                        (int)e->H, (int)e->D, rowdots);
     return hipGetLastError();
 }

@@ -288,7 +288,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipMalloc(&e->d_toff, sizeof(int32_t) * (Bp / 16) * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
     HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
-    HIPCHK(e, dalloc(&e->d_gene, 8 * DP));
+    HIPCHK(e, dalloc(&e->d_gene, 10 * DP));
     HIPCHK(e, dalloc(&e->d_mvec, ((DP + 255) / 256) * KP));  // per-256-gene-block partials of mvec
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
     HIPCHK(e, dalloc(&e->d_rowxp, (int64_t)e->nsplit_e * Bp * (1 + e->H)));
@@ -584,7 +584,9 @@ static void balance_rows(Engine* e, int64_t B) {
 // the batch entry lists (+ the NB raw-count dots of depth / nu_enc, split 0 of rowxp)
 static hipError_t build_lists(Engine* e, int64_t B) {
     if (e->cfg.model == MMVAE_MODEL_VMF) return build_batch_lists(e, B, nullptr, nullptr, nullptr);
-    return build_batch_lists(e, B, e->preg("depth.weight"), e->preg("nu_encoding.weight"), e->d_rowxp);
+    // the packed dot weights come from k_prep (nb_prep ran first on the same stream)
+    return build_batch_lists(e, B, reinterpret_cast<const float2*>(e->d_gene + 8 * e->DP),
+                             e->preg("nu_encoding.weight"), e->d_rowxp);
 }
 
 static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
@@ -651,6 +653,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
     HIPCHK(e, build_lists(e, a->B));
     if (vmf)
         HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
@@ -686,6 +689,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));
     HIPCHK(e, build_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));

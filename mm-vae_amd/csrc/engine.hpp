@@ -87,7 +87,7 @@ struct Engine {
     int32_t* d_toff = nullptr;       // [Bpad/16][NT+1]
     float* d_eps = nullptr;          // [Bpad][K] + [Bpad][R]
     float* h_eps_pin = nullptr;
-    float* d_gene = nullptr;         // per-gene prep: inv, bias, cnu  [3][DP]
+    float* d_gene = nullptr;         // per-gene prep (k_prep / k_vprep): [10][DP] floats
     float* d_mvec = nullptr;         // [DP/256][KP] partials of mvec (k_prep / k_vprep)
     int32_t* d_rtp = nullptr;        // [N+1][NT+1] per-cell tile pointers (dataset index; row N = empty)
     float* d_cellnorm = nullptr;     // [N+1] float2: vMF row norms of log1p(x) (dataset index)
@@ -171,6 +171,7 @@ struct ScopedTimer {
 
 // NB launchers (nb_kernels.hip)
 hipError_t nb_prepare_frozen(Engine* e);
+hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta);
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
                                bool use_eps, uint64_t step_id, int64_t row_offset);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
@@ -182,7 +183,7 @@ hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
 hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart);
-hipError_t build_batch_lists(Engine* e, int64_t B, const float* wdp, const float* Wne, float* rowdots);
+hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const float* Wne, float* rowdots);
 hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab);
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);

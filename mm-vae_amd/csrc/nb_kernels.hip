@@ -74,6 +74,9 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
         const bool v = g < d.D;
         reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
             float4{bias, cnu, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? P.Wnd[(int64_t)g * d.R] : 0.f};
+        // packed raw-count dot weights (depth.weight, nu_encoding.weight row 0) for the batch
+        // lists' dots (batch.hip): one 8-byte gather per entry
+        reinterpret_cast<float2*>(gene + 8 * d.DP)[g] = float2{v ? P.wdp[g] : 0.f, v ? P.Wne[g] : 0.f};
     }
     // encoder weight pre-scaled by 1/(softplus(ln_x_sd)+1e-4): x~ W^T = log1p(x) (W inv)^T - mvec
     const float xmv = (in && g < d.D) ? P.xm[g] : 0.f;
@@ -1830,12 +1833,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
     const int nrb = d.nrb;
-    float* gene = e->d_gene;
-    {
-        ScopedTimer tm(e, "k_prep");
-        hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, gene, e->d_WeP_f, e->d_WeS_f,
-                           bf ? e->d_WeS_b : nullptr, e->d_mvec);
-    }
+    float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
     {
         ScopedTimer tm(e, "k_enc_fwd");
         enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
@@ -1945,6 +1943,21 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     return hipGetLastError();
 }
 
+// k_prep: launched ahead of the batch lists (whose raw-count dots read its packed weights)
+hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
+    if (e->frozen_dirty) {
+        hipError_t er = nb_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = nb_dims(e, B, n_total, beta);
+    const NBPtrs P = nb_ptrs(e);
+    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    ScopedTimer tm(e, "k_prep");
+    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, e->stream, P, d, e->d_gene, e->d_WeP_f,
+                       e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec);
+    return hipGetLastError();
+}
+
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,
                                uint64_t step_id, int64_t row_offset) {
     if (e->frozen_dirty) {
@@ -1964,8 +1977,6 @@ template <class T, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
-    hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, e->d_gene, e->d_WeP_f, e->d_WeS_f,
-                       bf ? e->d_WeS_b : nullptr, e->d_mvec);
     enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, (uint64_t)0,
