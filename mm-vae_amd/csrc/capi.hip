@@ -348,6 +348,10 @@ int mmvae_destroy(mmvae_h e) {
         hipEventDestroy(p.b);
     }
     if (e->ev_staged) hipEventDestroy(e->ev_staged);
+    for (auto ev : e->ev_bucket)
+        if (ev) hipEventDestroy(ev);
+    if (e->ev_comm_done) hipEventDestroy(e->ev_comm_done);
+    if (e->comm_stream) hipStreamDestroy(e->comm_stream);
     hipStreamDestroy(e->stream);
     delete e;
     return MMVAE_OK;
@@ -653,6 +657,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    e->grads_reduced = false;
     if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
     HIPCHK(e, build_lists(e, a->B));
     if (vmf)
@@ -662,7 +667,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
                                       a->row_offset));
     if (a->update) {
-        if (e->comm && e->world > 1) {
+        if (e->comm && e->world > 1 && !e->grads_reduced) {
             ScopedTimer tm(e, "allreduce_grads");
             if (ncclAllReduce(e->d_grads, e->d_grads, (size_t)e->P_reg, ncclFloat, ncclSum, e->comm, e->stream) !=
                 ncclSuccess)
@@ -718,6 +723,12 @@ int mmvae_comm_unique_id(void* out128) {
     return MMVAE_OK;
 }
 
+extern "C++" {
+namespace mmvae {
+static void build_buckets(Engine* e);
+}
+}
+
 int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (!e || !id128 || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
@@ -731,8 +742,70 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (r != ncclSuccess) FAIL(e, MMVAE_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     e->rank = rank;
     e->world = world;
+    if (!e->comm_stream) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+        for (auto& ev : e->ev_bucket) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(e, hipEventCreateWithFlags(&e->ev_comm_done, hipEventDisableTiming));
+    }
+    build_buckets(e);
     return MMVAE_OK;
 }
+
+extern "C++" {
+namespace mmvae {
+bool split_grads(const Engine* e) {
+    if (e->cfg.model == MMVAE_MODEL_VMF) return false;
+    if (e->comm && e->world > 1) return true;
+    const char* v = std::getenv("MMVAE_SPLIT_GRADS");
+    return v && v[0] == '1';
+}
+
+// bucket 0: the NB decoder-side gene vectors (mu_bias, nu_bias, covar_decoding.*, nu_decoding.*),
+// final after decoder pass C; bucket 1: the complement (encoder gene vectors + latent heads)
+static void build_buckets(Engine* e) {
+    const char* dec[] = {"mu_bias", "nu_bias", "covar_decoding.weight", "covar_decoding.bias",
+                         "nu_decoding.weight", "nu_decoding.bias"};
+    std::vector<std::pair<int64_t, int64_t>> r0;
+    for (const char* n : dec)
+        if (const ParamSlot* sl = e->slot(n)) r0.push_back({sl->off, sl->numel});
+    std::sort(r0.begin(), r0.end());
+    e->bucket_ranges[0].clear();
+    e->bucket_ranges[1].clear();
+    for (auto& r : r0) {  // merge adjacent ranges
+        auto& b = e->bucket_ranges[0];
+        if (!b.empty() && b.back().first + b.back().second == r.first) b.back().second += r.second;
+        else b.push_back(r);
+    }
+    int64_t at = 0;
+    for (auto& r : e->bucket_ranges[0]) {
+        if (r.first > at) e->bucket_ranges[1].push_back({at, r.first - at});
+        at = r.first + r.second;
+    }
+    if (at < e->P_reg) e->bucket_ranges[1].push_back({at, e->P_reg - at});
+}
+
+hipError_t comm_bucket(Engine* e, int b) {
+    if (!e->comm || e->world <= 1) return hipSuccess;
+    hipError_t er = hipEventRecord(e->ev_bucket[b], e->stream);
+    if (er != hipSuccess) return er;
+    er = hipStreamWaitEvent(e->comm_stream, e->ev_bucket[b], 0);
+    if (er != hipSuccess) return er;
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (auto& r : e->bucket_ranges[b])
+        ok = ok && ncclAllReduce(e->d_grads + r.first, e->d_grads + r.first, (size_t)r.second, ncclFloat, ncclSum,
+                                 e->comm, e->comm_stream) == ncclSuccess;
+    ok = (ncclGroupEnd() == ncclSuccess) && ok;
+    if (!ok) return hipErrorUnknown;
+    if (b == 1) {
+        er = hipEventRecord(e->ev_comm_done, e->comm_stream);
+        if (er != hipSuccess) return er;
+        er = hipStreamWaitEvent(e->stream, e->ev_comm_done, 0);
+        if (er != hipSuccess) return er;
+    }
+    return hipSuccess;
+}
+}  // namespace mmvae
+}  // extern "C++"
 
 int mmvae_comm_allreduce(mmvae_h e, float* values, int64_t n) {
     if (!e || !values || n < 0) FAIL(e, MMVAE_E_ARG, "comm_allreduce: bad arguments");

@@ -130,6 +130,14 @@ struct Engine {
     // ---- comm ----
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    // bucketed gradient all-reduce overlapped with the encoder backward:
+    // bucket 0 = the decoder-side gene vectors (ready after decoder pass C), bucket 1 = the rest.
+    // Each bucket is a list of contiguous [offset, count) ranges of the flat gradient.
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_bucket[2] = {nullptr, nullptr};
+    hipEvent_t ev_comm_done = nullptr;
+    std::vector<std::pair<int64_t, int64_t>> bucket_ranges[2];
+    bool grads_reduced = false;  // set by a model step that already all-reduced its buckets
 
     // ---- timing ----
     bool timing = false;
@@ -172,6 +180,12 @@ struct ScopedTimer {
 // NB launchers (nb_kernels.hip)
 hipError_t nb_prepare_frozen(Engine* e);
 hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta);
+// split gradient finalisation + bucketed all-reduce (capi.hip): true when the step runs the
+// decoder-side / encoder-side gradient kernels separately (world > 1, or MMVAE_SPLIT_GRADS=1)
+bool split_grads(const Engine* e);
+// all-reduce gradient bucket b on the comm stream after the work queued so far on e->stream;
+// bucket 1 also makes e->stream wait for both buckets.  No-op without a communicator.
+hipError_t comm_bucket(Engine* e, int b);
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
                                bool use_eps, uint64_t step_id, int64_t row_offset);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);

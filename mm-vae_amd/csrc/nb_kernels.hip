@@ -1595,7 +1595,10 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
 // Per-gene gradients from the per-row-block column slabs of passes B, C and k_enc_bwd,
 // summed in a fixed order (deterministic).  32 genes x 8 row-block partitions per workgroup.
 // SMALL: the default widths C = R = H = 1 (9 slab rows per gene, all compile-time).
-template <bool SMALL>
+// PART: 0 = every per-gene gradient; 1 = decoder side only (slabs B, C: mu_bias, nu_bias,
+// covar_decoding, nu_decoding — final after pass C, all-reduced while the encoder backward
+// runs); 2 = encoder side only (slab E: x_mean, ln_x_sd, depth, nu_encoding).
+template <bool SMALL, int PART>
 __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ gene,
                                                     const float* __restrict__ slabB,
@@ -1623,9 +1626,9 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
             const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
 #pragma unroll
             for (int q = 0; q < NQMAX; ++q) {
-                if (q < nqB) acc[q] += sB[(int64_t)q * d.DP];
-                else if (q < nqB + nqC) acc[q] += sC[(int64_t)(q - nqB) * d.DP];
-                else if (q < nq) acc[q] += sE[(int64_t)(q - nqB - nqC) * d.DP];
+                if (q < nqB) { if (PART != 2) acc[q] += sB[(int64_t)q * d.DP]; }
+                else if (q < nqB + nqC) { if (PART != 2) acc[q] += sC[(int64_t)(q - nqB) * d.DP]; }
+                else if (q < nq) { if (PART != 1) acc[q] += sE[(int64_t)(q - nqB - nqC) * d.DP]; }
             }
         }
     }
@@ -1645,13 +1648,16 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     const float gl = acc[nqB + nqC];
     const float* raw = acc + nqB + nqC + 1;  // depth, nu_enc[H]
     const float inv_n = d.inv_n;
-    const float dl = cs1[0] - tc[0];
-    G.mub[g] = dl;
-    G.bcd[g] = dl;
-    for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = cs1[1 + c] - tc[1 + c];
-    G.bnd[g] = du * inv_n;
-    G.nub[g] = -du * inv_n;
-    for (int q = 0; q < R; ++q) G.Wnd[(int64_t)g * R + q] = duz[q] * inv_n;
+    if (PART != 2) {
+        const float dl = cs1[0] - tc[0];
+        G.mub[g] = dl;
+        G.bcd[g] = dl;
+        for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = cs1[1 + c] - tc[1 + c];
+        G.bnd[g] = du * inv_n;
+        G.nub[g] = -du * inv_n;
+        for (int q = 0; q < R; ++q) G.Wnd[(int64_t)g * R + q] = duz[q] * inv_n;
+    }
+    if (PART == 1) return;
     // encoder normalisation params (nb.hh:408-410)
     float gs = 0.f;
 #pragma unroll 8
@@ -1906,6 +1912,19 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
         else hipLaunchKernelGGL((k_dec_tail<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
     }
+    const bool split = split_grads(e);
+    const bool small_genes = d.C == 1 && d.R == 1 && d.H == 1;
+    if (split) {  // decoder-side gene gradients final: all-reduce them under the encoder backward
+        ScopedTimer tm(e, "k_grad_genes_dec");
+        if (small_genes)
+            hipLaunchKernelGGL((k_grad_genes<true, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        else
+            hipLaunchKernelGGL((k_grad_genes<false, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        hipError_t er = comm_bucket(e, 0);
+        if (er != hipSuccess) return er;
+    }
     {
         ScopedTimer tm(e, "k_latent_bwd");
         const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
@@ -1933,12 +1952,26 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_grad_genes");
-        if (d.C == 1 && d.R == 1 && d.H == 1)
-            hipLaunchKernelGGL(k_grad_genes<true>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
-        else
-            hipLaunchKernelGGL(k_grad_genes<false>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        if (small_genes) {
+            if (split)
+                hipLaunchKernelGGL((k_grad_genes<true, 2>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+            else
+                hipLaunchKernelGGL((k_grad_genes<true, 0>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        } else {
+            if (split)
+                hipLaunchKernelGGL((k_grad_genes<false, 2>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+            else
+                hipLaunchKernelGGL((k_grad_genes<false, 0>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+        }
+    }
+    if (split) {
+        hipError_t er = comm_bucket(e, 1);
+        if (er != hipSuccess) return er;
+        e->grads_reduced = e->comm && e->world > 1;
     }
     return hipGetLastError();
 }
