@@ -214,19 +214,24 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
 
     // gene splits: enough workgroups for `per_cu` resident workgroups on each of the 256 CUs
     // (the occupancy the kernel's LDS / VGPR budget allows), LDS column accumulators <= 40 KB
-    auto pick_split = [&](int nq, int per_cu) {
+    auto pick_split = [&](int nq, int per_cu, bool lds_cols = true) {
         int ns = (int)((256 * per_cu + e->nrb_max - 1) / e->nrb_max);
         if (ns < 1) ns = 1;
         const int tps_max = (int)(40 * 1024 / (nq * 64 * 4));
         const int ns_min = (int)((e->NT + tps_max - 1) / tps_max);
-        if (ns < ns_min) ns = ns_min;
+        if (lds_cols && ns < ns_min) ns = ns_min;
         if (ns > e->NT) ns = (int)e->NT;
         if (ns > 64) ns = 64;
         return ns;
     };
     // NB pass B holds ~75 KB of LDS per workgroup (2 per CU); the vMF decoder and the shared
     // encoder kernels fit 3 (measured: 12 splits at 64 row blocks beat 8 and 16)
-    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R), cfg->model == MMVAE_MODEL_VMF ? 3 : 2);
+    // NB pass B streams its column partials out per tile (no split-long LDS accumulators), so
+    // its split is set by occupancy alone: a grid of exactly one round of resident workgroups
+    // (measured at D = 30k: 8 splits 304 us vs 12 splits 403 us — 384 workgroups on 256 CUs
+    // ran as two rounds)
+    const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
+    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R), vmf_model ? 3 : 2, vmf_model);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split((int)(2 + e->H), 3);
