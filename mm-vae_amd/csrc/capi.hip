@@ -759,17 +759,18 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
 extern "C++" {
 namespace mmvae {
 bool split_grads(const Engine* e) {
-    if (e->cfg.model == MMVAE_MODEL_VMF) return false;
     if (e->comm && e->world > 1) return true;
     const char* v = std::getenv("MMVAE_SPLIT_GRADS");
     return v && v[0] == '1';
 }
 
-// bucket 0: the NB decoder-side gene vectors (mu_bias, nu_bias, covar_decoding.*, nu_decoding.*),
-// final after decoder pass C; bucket 1: the complement (encoder gene vectors + latent heads)
+// bucket 0: the decoder-side gene vectors — NB mu_bias, nu_bias, covar_decoding.*, nu_decoding.*
+// (final after decoder pass C), vMF covar_decoding_.* (final after k_vdec_bwd); bucket 1: the
+// complement (encoder gene vectors, latent heads, ln_kappa)
 static void build_buckets(Engine* e) {
     const char* dec[] = {"mu_bias", "nu_bias", "covar_decoding.weight", "covar_decoding.bias",
-                         "nu_decoding.weight", "nu_decoding.bias"};
+                         "nu_decoding.weight", "nu_decoding.bias",
+                         "covar_decoding_.weight", "covar_decoding_.bias"};  // (vMF names)
     std::vector<std::pair<int64_t, int64_t>> r0;
     for (const char* n : dec)
         if (const ParamSlot* sl = e->slot(n)) r0.push_back({sl->off, sl->numel});

@@ -740,6 +740,9 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
 
 // Per-gene gradients from the row-block slabs (fixed order): covar_decoding_ (decoder pass 1)
 // and x_mean / ln_x_sd through the Angular encoder (k_enc_bwd's sum_k W~ M term).
+// PART: 0 = all; 1 = covar_decoding_ only (slab B, final after k_vdec_bwd: its all-reduce overlaps
+// the encoder backward); 2 = x_mean / ln_x_sd only (slab E)
+template <int PART>
 __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, const float* __restrict__ gene,
                                                      const float* __restrict__ WeP_f, const float* __restrict__ slabB,
                                                      const float* __restrict__ slabE, const float* __restrict__ smallg,
@@ -760,8 +763,8 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
             const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
 #pragma unroll
             for (int q = 0; q < NQMAX; ++q) {
-                if (q < nqB) acc[q] += sB[(int64_t)q * d.DP];
-                else if (q < nq) acc[q] += slabE[(int64_t)rb * d.DP + g];
+                if (q < nqB) { if (PART != 2) acc[q] += sB[(int64_t)q * d.DP]; }
+                else if (q < nq) { if (PART != 1) acc[q] += slabE[(int64_t)rb * d.DP + g]; }
             }
         }
     }
@@ -774,8 +777,11 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
     for (int pp = 0; pp < NPART - 1; ++pp)
 #pragma unroll
         for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
-    G.bcd[g] = acc[0];
-    for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = acc[1 + c];
+    if (PART != 2) {
+        G.bcd[g] = acc[0];
+        for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = acc[1 + c];
+    }
+    if (PART == 1) return;
     const float Gl = acc[nqB];
     float gs = 0.f;
     for (int k = 0; k < d.K; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
@@ -968,6 +974,14 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
         else hipLaunchKernelGGL((k_vdec_bwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
+    const bool split = split_grads(e);
+    if (split) {  // covar_decoding_ gradients final: all-reduce them under the encoder backward
+        ScopedTimer tm(e, "k_vgrad_genes_dec");
+        hipLaunchKernelGGL(k_vgrad_genes<1>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                           e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+        hipError_t er = comm_bucket(e, 0);
+        if (er != hipSuccess) return er;
+    }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");
         hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
@@ -986,8 +1000,17 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vgrad_genes");
-        hipLaunchKernelGGL(k_vgrad_genes, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
-                           e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+        if (split)
+            hipLaunchKernelGGL(k_vgrad_genes<2>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                               e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+        else
+            hipLaunchKernelGGL(k_vgrad_genes<0>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                               e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+    }
+    if (split) {
+        hipError_t er = comm_bucket(e, 1);
+        if (er != hipSuccess) return er;
+        e->grads_reduced = e->comm && e->world > 1;
     }
     return hipGetLastError();
 }

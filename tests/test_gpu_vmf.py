@@ -145,3 +145,24 @@ def test_vmf_full_size_properties():
         losses[dt] = l0
         assert all(np.isfinite(v).all() for v in eng.grads().values())
     assert abs(losses["bf16"] - losses["f32"]) <= 2e-3 * abs(losses["f32"])
+
+
+def test_vmf_split_gradient_buckets_agree(monkeypatch):
+    """Data-parallel vMF step: covar_decoding_ gradients finalised right after k_vdec_bwd (their
+    all-reduce overlaps the encoder backward), x_mean / ln_x_sd at the end (MMVAE_SPLIT_GRADS=1
+    forces that path at world size 1) — bit-identical to the single finalisation."""
+    import mmvae_amd
+    D, K, B, N = 3000, 32, 512, 2000
+    out = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("MMVAE_SPLIT_GRADS", split)
+        eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1, model=mmvae_amd.MODEL_VMF)
+        eng.synth_csr(N, lib_size=2000.0, seed=5)
+        eng.init_params(seed=11)
+        res = [eng.step(np.arange(B) * 3 % N, 0.5, step_id=t) for t in range(2)]
+        out[split] = (res, eng.grads(), eng.params(registered_only=True))
+    (r0, g0, p0), (r1, g1, p1) = out["0"], out["1"]
+    assert r0 == r1
+    for k in g0:
+        np.testing.assert_array_equal(g0[k], g1[k], err_msg=k)
+        np.testing.assert_array_equal(p0[k], p1[k], err_msg=k)
