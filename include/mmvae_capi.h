@@ -126,6 +126,17 @@ typedef struct mmvae_step_args {
  * receives the clip_grad_norm_ total norm.  Non-NULL outputs synchronise the stream. */
 int mmvae_run(mmvae_h h, const mmvae_step_args* args, float* loss_out, double* total_norm_out);
 
+/* The SURVEY §8(b) single-GPU entry points, thin forms of mmvae_run with n_total = B,
+ * row_offset = 0 and an internal step counter for the Philox noise (when eps == NULL):
+ *   mmvae_step — one update step (mmvae_alg.hh:290-310: resample through ridx, forward,
+ *                loss, zero_grad, backward, clip_grad_norm_, Adam::step);
+ *   mmvae_eval — the forward-only train-mode loss of mmvae_alg.hh:277-285 (Q12).
+ * loss_out (nullable) synchronises the stream. */
+int mmvae_step(mmvae_h h, const int64_t* cell_ids, int64_t B, const int64_t* ridx_or_null, float beta,
+               const float* eps_or_null, float* loss_out);
+int mmvae_eval(mmvae_h h, const int64_t* cell_ids, int64_t B, float beta, const float* eps_or_null,
+               float* loss_out);
+
 /* Recorder encoder (nb.hh:419-431 encode_mu(x); vmf.hh:267-281 encode(x)): mean/lnvar
  * [B*K] row-major, no covariate, no noise. */
 int mmvae_encode(mmvae_h h, const int64_t* cell_ids, int64_t B, float* mean, float* lnvar);

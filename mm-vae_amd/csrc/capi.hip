@@ -691,6 +691,31 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     return MMVAE_OK;
 }
 
+static int step_or_eval(mmvae_h e, const int64_t* cell_ids, int64_t B, const int64_t* ridx, float beta,
+                        const float* eps, float* loss_out, int update) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "step: null handle");
+    mmvae_step_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.cell_ids = cell_ids;
+    a.ridx = ridx;
+    a.B = B;
+    a.n_total = B;
+    a.beta = beta;
+    a.eps = eps;
+    a.step_id = e->auto_step++;
+    a.update = update;
+    return mmvae_run(e, &a, loss_out, nullptr);
+}
+
+int mmvae_step(mmvae_h e, const int64_t* cell_ids, int64_t B, const int64_t* ridx_or_null, float beta,
+               const float* eps_or_null, float* loss_out) {
+    return step_or_eval(e, cell_ids, B, ridx_or_null, beta, eps_or_null, loss_out, 1);
+}
+
+int mmvae_eval(mmvae_h e, const int64_t* cell_ids, int64_t B, float beta, const float* eps_or_null, float* loss_out) {
+    return step_or_eval(e, cell_ids, B, nullptr, beta, eps_or_null, loss_out, 0);
+}
+
 int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, float* lnvar) {
     if (!e || !cell_ids || !mean || !lnvar) FAIL(e, MMVAE_E_ARG, "encode: null arguments");
     if (B < 1 || B > e->Bmax) FAIL(e, MMVAE_E_ARG, "encode: B must be in [1, max_batch]");

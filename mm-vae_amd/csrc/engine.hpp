@@ -137,7 +137,8 @@ struct Engine {
     hipEvent_t ev_bucket[2] = {nullptr, nullptr};
     hipEvent_t ev_comm_done = nullptr;
     std::vector<std::pair<int64_t, int64_t>> bucket_ranges[2];
-    bool grads_reduced = false;  // set by a model step that already all-reduced its buckets
+    bool grads_reduced = false;
+    uint64_t auto_step = 0;  // Philox step counter of mmvae_step / mmvae_eval  // set by a model step that already all-reduced its buckets
 
     // ---- timing ----
     bool timing = false;

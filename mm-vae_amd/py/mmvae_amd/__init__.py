@@ -72,6 +72,8 @@ def lib():
         "mmvae_init_params": (ctypes.c_int, [h, ctypes.c_uint64]),
         "mmvae_reset_optimizer": (ctypes.c_int, [h]),
         "mmvae_run": (ctypes.c_int, [h, ctypes.POINTER(StepArgs), f32p, ctypes.POINTER(ctypes.c_double)]),
+        "mmvae_step": (ctypes.c_int, [h, i64p, i64, i64p, ctypes.c_float, f32p, f32p]),
+        "mmvae_eval": (ctypes.c_int, [h, i64p, i64, ctypes.c_float, f32p, f32p]),
         "mmvae_encode": (ctypes.c_int, [h, i64p, i64, f32p, f32p]),
         "mmvae_sync": (ctypes.c_int, [h]),
         "mmvae_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
