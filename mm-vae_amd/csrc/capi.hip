@@ -212,29 +212,26 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         build_registry_nb(e);
     }
 
-    // gene splits: enough workgroups for `per_cu` resident workgroups on each of the 256 CUs
-    // (the occupancy the kernel's LDS / VGPR budget allows), LDS column accumulators <= 40 KB
-    auto pick_split = [&](int nq, int per_cu, bool lds_cols = true) {
+    // gene splits: one round of `per_cu` resident workgroups on each of the 256 CUs (the
+    // occupancy the kernel's LDS / VGPR budget allows).  No tile kernel keeps split-long column
+    // accumulators in LDS (every tile's partials stream out), so the split length is free: a
+    // grid of one full round beats a longer grid with a partial second round (measured at
+    // D = 30k: pass B 403 -> 302 us with 8 instead of 12 splits; at B = 8192 the encoders
+    // ran 9 splits = 1.5 rounds).
+    auto pick_split = [&](int per_cu) {
         int ns = (int)((256 * per_cu + e->nrb_max - 1) / e->nrb_max);
         if (ns < 1) ns = 1;
-        const int tps_max = (int)(40 * 1024 / (nq * 64 * 4));
-        const int ns_min = (int)((e->NT + tps_max - 1) / tps_max);
-        if (lds_cols && ns < ns_min) ns = ns_min;
         if (ns > e->NT) ns = (int)e->NT;
         if (ns > 64) ns = 64;
         return ns;
     };
-    // NB pass B holds ~75 KB of LDS per workgroup (2 per CU); the vMF decoder and the shared
-    // encoder kernels fit 3 (measured: 12 splits at 64 row blocks beat 8 and 16)
-    // NB pass B streams its column partials out per tile (no split-long LDS accumulators), so
-    // its split is set by occupancy alone: a grid of exactly one round of resident workgroups
-    // (measured at D = 30k: 8 splits 304 us vs 12 splits 403 us — 384 workgroups on 256 CUs
-    // ran as two rounds)
+    // NB pass B holds ~150 KB of LDS per 8-wave workgroup (2 x 4-wave per CU); the vMF decoder
+    // and the shared encoder kernels fit 3 (measured: 12 splits at 64 row blocks beat 8 and 16)
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
-    e->nsplit_d = pick_split((int)((1 + e->C) + 1 + e->R), vmf_model ? 3 : 2, vmf_model);
+    e->nsplit_d = pick_split(vmf_model ? 3 : 2);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
-    e->nsplit_e = pick_split((int)(2 + e->H), 3);
+    e->nsplit_e = pick_split(3);
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
     auto env_split = [&](const char* name, int& v) {
         if (const char* ev = std::getenv(name)) {
