@@ -138,7 +138,8 @@ struct Engine {
     hipEvent_t ev_comm_done = nullptr;
     std::vector<std::pair<int64_t, int64_t>> bucket_ranges[2];
     bool grads_reduced = false;
-    uint64_t auto_step = 0;  // Philox step counter of mmvae_step / mmvae_eval  // set by a model step that already all-reduced its buckets
+    uint64_t auto_step = 0;  // Philox step counter of mmvae_step / mmvae_eval
+    size_t stage_bytes = 0;  // the per-step H2D staging block (cells | seg | perm)  // set by a model step that already all-reduced its buckets
 
     // ---- timing ----
     bool timing = false;
