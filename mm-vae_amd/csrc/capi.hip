@@ -226,10 +226,10 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         return ns;
     };
     // NB pass B holds ~150 KB of LDS per 8-wave workgroup (2 x 4-wave per CU); the vMF decoder
-    // fits 3; the shared encoder kernels (~37 KB, <= 104 VGPRs in bf16) fit 4 (measured at 64 row
+    // fits 4 (16 splits 46 + 71 us vs 12 splits 51 + 74 us); the shared encoder kernels (~37 KB, <= 104 VGPRs in bf16) fit 4 (measured at 64 row
     // blocks: 16 splits 58 + 31 us, 12 splits 62 + 34 us, 24 splits 61 + 36 us)
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
-    e->nsplit_d = pick_split(vmf_model ? 3 : 2);
+    e->nsplit_d = pick_split(vmf_model ? 4 : 2);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split(4);
