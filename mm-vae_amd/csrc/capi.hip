@@ -782,7 +782,10 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
 extern "C++" {
 namespace mmvae {
 bool split_grads(const Engine* e) {
-    if (e->comm && e->world > 1) return true;
+    // MMVAE_NO_OVERLAP=1: one all-reduce of the whole flat gradient on the main stream after the
+    // backward (no comm-stream events) instead of the two overlapped buckets
+    const char* no = std::getenv("MMVAE_NO_OVERLAP");
+    if (e->comm && e->world > 1) return !(no && no[0] == '1');
     const char* v = std::getenv("MMVAE_SPLIT_GRADS");
     return v && v[0] == '1';
 }
