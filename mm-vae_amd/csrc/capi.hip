@@ -316,7 +316,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_lossp, e->klp_off + e->n_lat_wg));
     HIPCHK(e, dalloc(&e->d_small, (int64_t)e->n_lat_wg * SMALL));
     HIPCHK(e, dalloc(&e->d_smallg, 128));
-    HIPCHK(e, dalloc(&e->d_sumsq, 256));
+    // clip-norm partials: k_sumsq's 256 blocks, or one per gradient-kernel block (NB world 1)
+    HIPCHK(e, dalloc(&e->d_sumsq, 256 + (e->D + 31) / 32 + (2 * e->K * e->K + 4 * e->K + e->K * e->C + 2 * e->R * e->H +
+                                                          2 * e->R + e->H + 1 + 31) / 32 + 1));
     HIPCHK(e, dalloc(&e->d_out, 4));
     HIPCHK(e, dalloc(&e->d_rowv, Bp));
     HIPCHK(e, dalloc(&e->d_vk, 8));
@@ -661,6 +663,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     }
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
     e->grads_reduced = false;
+    e->sq_parts = 0;
     if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
     HIPCHK(e, build_lists(e, a->B));
     if (vmf)

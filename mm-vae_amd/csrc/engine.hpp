@@ -113,6 +113,7 @@ struct Engine {
     float* d_small = nullptr;        // latent-bwd WG partials
     float* d_smallg = nullptr;       // reduced small grads scratch (colsum_dh etc.)
     double* d_sumsq = nullptr;       // sum-of-squares partials
+    int sq_parts = 0;                // > 0: the gradient kernels wrote that many partials (k_sumsq skipped)
     float* d_out = nullptr;          // [0] loss, [1] total norm (float)
     float* d_rowv = nullptr;         // vMF: [Bpad] cos_b = <y_b, r_b>
     float* d_vk = nullptr;           // vMF: kappa scalars (k_vkappa)

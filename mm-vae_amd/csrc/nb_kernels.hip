@@ -1548,7 +1548,8 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
                                                     NBGrads G, float* __restrict__ smallg,
                                                     const float* __restrict__ lossp, int nlossp,
                                                     const float* __restrict__ klpart, int nkl,
-                                                    float* __restrict__ out, int with_grads) {
+                                                    float* __restrict__ out, int with_grads,
+                                                    double* __restrict__ sqpart) {
     const int K = d.K, C = d.C, H = d.H, R = d.R;
     const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
     if (blockIdx.x == 0) {
@@ -1558,38 +1559,50 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
         for (int i = threadIdx.x; i < nkl; i += 256) ksum += klpart[i];
         float tl = block_sum<4>(lsum, sb);
         float tk = block_sum<4>(ksum, sb);
-        if (threadIdx.x == 0) out[0] = (tl + tk * d.beta) * d.inv_n;
+        if (threadIdx.x == 0) {
+            out[0] = (tl + tk * d.beta) * d.inv_n;
+            if (sqpart) sqpart[0] = 0.0;
+        }
         return;
     }
     if (!with_grads) return;
     __shared__ float red[8][32];
     const int i = (blockIdx.x - 1) * 32 + (threadIdx.x & 31);
     const float s = sum_partials(small, nwg, SMALL, i, red);
-    if ((threadIdx.x >> 5) != 0 || i >= SMALL) return;
+    // store the small gradient; returns how many gradient elements received s (0: smallg)
+    auto store = [&]() -> int {
     int o = i;
-    if (o < K * K) { G.Wm[o] = s; return; }
+    if (o < K * K) { G.Wm[o] = s; return 1; }
     o -= K * K;
-    if (o < K * K) { G.Wl[o] = s; return; }
+    if (o < K * K) { G.Wl[o] = s; return 1; }
     o -= K * K;
-    if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
+    if (o < K) { G.bm[o] = s; G.bce[o] = s; return 2; }
     o -= K;
-    if (o < K) { G.bl[o] = s; return; }
+    if (o < K) { G.bl[o] = s; return 1; }
     o -= K;
-    if (o < K * C) { G.Wce[o] = s; return; }
+    if (o < K * C) { G.Wce[o] = s; return 1; }
     o -= K * C;
-    if (o < K) { smallg[o] = s; return; }
+    if (o < K) { smallg[o] = s; return 0; }
     o -= K;
-    if (o < R * H) { G.Wnm[o] = s; return; }
+    if (o < R * H) { G.Wnm[o] = s; return 1; }
     o -= R * H;
-    if (o < R) { G.bnm[o] = s; return; }
+    if (o < R) { G.bnm[o] = s; return 1; }
     o -= R;
-    if (o < R * H) { G.Wnl[o] = s; return; }
+    if (o < R * H) { G.Wnl[o] = s; return 1; }
     o -= R * H;
-    if (o < R) { G.bnl[o] = s; return; }
+    if (o < R) { G.bnl[o] = s; return 1; }
     o -= R;
-    if (o < H) { G.bne[o] = s; return; }
+    if (o < H) { G.bne[o] = s; return 1; }
     o -= H;
     G.bdp[0] = s;
+    return 1;
+    };
+    double sq = 0.0;
+    if ((threadIdx.x >> 5) == 0 && i < SMALL) sq = (double)s * s * store();
+    if (sqpart && threadIdx.x < 64) {
+        sq = wave_sum_d(sq);
+        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+    }
 }
 
 // Per-gene gradients from the per-row-block column slabs of passes B, C and k_enc_bwd,
@@ -1604,7 +1617,8 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ slabB,
                                                     const float* __restrict__ slabC,
                                                     const float* __restrict__ slabE,
-                                                    const float* __restrict__ smallg, int nrb) {
+                                                    const float* __restrict__ smallg, int nrb,
+                                                    double* __restrict__ sqpart) {
     constexpr int NQMAX = SMALL ? 9 : (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
     constexpr int NPART = 8;
     __shared__ float cdh[64];
@@ -1636,7 +1650,10 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
 #pragma unroll
         for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
     __syncthreads();
-    if (part != 0 || g >= d.D) return;
+    // sum of squares of every gradient element this block writes (clip norm partial, world 1)
+    double sq = 0.0;
+    auto put = [&](float* dst, float v) { *dst = v; sq += (double)v * v; };
+    if (part == 0 && g < d.D) {
 #pragma unroll
     for (int pp = 0; pp < NPART - 1; ++pp)
 #pragma unroll
@@ -1650,24 +1667,30 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     const float inv_n = d.inv_n;
     if (PART != 2) {
         const float dl = cs1[0] - tc[0];
-        G.mub[g] = dl;
-        G.bcd[g] = dl;
-        for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = cs1[1 + c] - tc[1 + c];
-        G.bnd[g] = du * inv_n;
-        G.nub[g] = -du * inv_n;
-        for (int q = 0; q < R; ++q) G.Wnd[(int64_t)g * R + q] = duz[q] * inv_n;
+        put(&G.mub[g], dl);
+        put(&G.bcd[g], dl);
+        for (int c = 0; c < C; ++c) put(&G.Wcd[(int64_t)g * C + c], cs1[1 + c] - tc[1 + c]);
+        put(&G.bnd[g], du * inv_n);
+        put(&G.nub[g], -du * inv_n);
+        for (int q = 0; q < R; ++q) put(&G.Wnd[(int64_t)g * R + q], duz[q] * inv_n);
     }
-    if (PART == 1) return;
+    if (PART != 1) {
     // encoder normalisation params (nb.hh:408-410)
     float gs = 0.f;
 #pragma unroll 8
     for (int k = 0; k < d.K; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
     const float inv = gene[g];
-    G.xm[g] = -inv * gs;
+    put(&G.xm[g], -inv * gs);
     const float th = P.lsd[g];
-    G.lsd[g] = -(inv * inv) * (gl - P.xm[g] * gs) * dsoftplus(th);
-    G.wdp[g] = raw[0];
-    for (int h = 0; h < H; ++h) G.Wne[(int64_t)h * d.D + g] = raw[1 + h];
+    put(&G.lsd[g], -(inv * inv) * (gl - P.xm[g] * gs) * dsoftplus(th));
+    put(&G.wdp[g], raw[0]);
+    for (int h = 0; h < H; ++h) put(&G.Wne[(int64_t)h * d.D + g], raw[1 + h]);
+    }  // PART != 1
+    }  // part == 0 && g < D
+    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..31)
+        sq = wave_sum_d(sq);
+        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+    }
 }
 
 // =======================================================================================
@@ -1904,7 +1927,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     if (!update) {
         ScopedTimer tm(e, "k_loss");
         hipLaunchKernelGGL(k_grad_small, dim3(1), dim3(256), 0, st, d, e->d_small, 0, G, e->d_smallg, e->d_lossp,
-                           (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0);
+                           (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg, e->d_out, 0, nullptr);
         return hipGetLastError();
     }
     {
@@ -1918,10 +1941,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         ScopedTimer tm(e, "k_grad_genes_dec");
         if (small_genes)
             hipLaunchKernelGGL((k_grad_genes<true, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
         else
             hipLaunchKernelGGL((k_grad_genes<false, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
         hipError_t er = comm_bucket(e, 0);
         if (er != hipSuccess) return er;
     }
@@ -1943,35 +1966,43 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
             hipLaunchKernelGGL((k_enc_bwd<T, KP, false, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
                                e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE);
     }
+    // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
+    // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
+    const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
+    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
+    const bool fuse_sq = !split && !(e->comm && e->world > 1);  // no all-reduce after these kernels
+    double* sqS = fuse_sq ? e->d_sumsq : nullptr;
+    double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
         ScopedTimer tm(e, "k_grad_small");
-        const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
-        hipLaunchKernelGGL(k_grad_small, dim3(1 + (SMALL + 31) / 32), dim3(256), 0, st, d, e->d_small,
+        hipLaunchKernelGGL(k_grad_small, dim3(gS), dim3(256), 0, st, d, e->d_small,
                            e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg,
-                           e->d_out, 1);
+                           e->d_out, 1, sqS);
     }
     {
         ScopedTimer tm(e, "k_grad_genes");
         if (small_genes) {
             if (split)
-                hipLaunchKernelGGL((k_grad_genes<true, 2>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                hipLaunchKernelGGL((k_grad_genes<true, 2>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
             else
-                hipLaunchKernelGGL((k_grad_genes<true, 0>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                hipLaunchKernelGGL((k_grad_genes<true, 0>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
         } else {
             if (split)
-                hipLaunchKernelGGL((k_grad_genes<false, 2>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                hipLaunchKernelGGL((k_grad_genes<false, 2>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
             else
-                hipLaunchKernelGGL((k_grad_genes<false, 0>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb);
+                hipLaunchKernelGGL((k_grad_genes<false, 0>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
         }
     }
     if (split) {
         hipError_t er = comm_bucket(e, 1);
         if (er != hipSuccess) return er;
         e->grads_reduced = e->comm && e->world > 1;
+    } else if (fuse_sq) {
+        e->sq_parts = gS + gG;
     }
     return hipGetLastError();
 }

@@ -63,14 +63,18 @@ hipError_t opt_clip_adam(Engine* e) {
     const double bc1 = 1.0 - std::pow(b1, (double)e->adam_step);
     const double bc2 = 1.0 - std::pow(b2, (double)e->adam_step);
     const int64_t n = e->P_reg;
-    {
+    // the NB world-1 step leaves its own partials (gradient kernels, one per block); otherwise
+    // (vMF, or gradients all-reduced after the gradient kernels) k_sumsq computes them
+    const int nparts = e->sq_parts > 0 ? e->sq_parts : SUMSQ_BLOCKS;
+    if (e->sq_parts <= 0) {
         ScopedTimer tm(e, "k_sumsq");
         hipLaunchKernelGGL(k_sumsq, dim3(SUMSQ_BLOCKS), dim3(256), 0, e->stream, e->d_grads, n, e->d_sumsq);
     }
+    e->sq_parts = 0;
     {
         ScopedTimer tm(e, "k_adam");
         hipLaunchKernelGGL(k_adam, dim3(SUMSQ_BLOCKS), dim3(256), 0, e->stream, e->d_params, e->d_grads, e->d_m,
-                           e->d_v, n, e->d_sumsq, SUMSQ_BLOCKS, e->cfg.grad_clip, (float)(e->cfg.lr / bc1),
+                           e->d_v, n, e->d_sumsq, nparts, e->cfg.grad_clip, (float)(e->cfg.lr / bc1),
                            (float)(1.0 / std::sqrt(bc2)), (float)b1, (float)b2, e->cfg.weight_decay, 1e-8f,
                            e->d_out);
     }
