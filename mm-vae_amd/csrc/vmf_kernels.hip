@@ -695,7 +695,7 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
                                                      VGrads G, float* __restrict__ smallg,
                                                      const float* __restrict__ rowcos, const float* __restrict__ klpart,
                                                      int nkl, const float* __restrict__ vk, float* __restrict__ out,
-                                                     int with_grads) {
+                                                     int with_grads, double* __restrict__ sqpart) {
     const int K = d.K, C = d.C;
     const int SMALL = 2 * K * K + 2 * K + K * C + K;
     if (blockIdx.x == 0) {
@@ -714,7 +714,9 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
                 float dk = -tc * d.inv_n;
                 dk += (sc.df * -Bn) / kap;
                 if (sc.rank0) dk += vk[VK_BARICZ];
-                G.lk[0] = (vk[VK_MASK] > 0.f) ? dk * vk[VK_EXP] : 0.f;
+                const float glk = (vk[VK_MASK] > 0.f) ? dk * vk[VK_EXP] : 0.f;
+                G.lk[0] = glk;
+                if (sqpart) sqpart[0] = (double)glk * glk;
             }
         }
         return;
@@ -723,19 +725,28 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
     __shared__ float red[8][32];
     const int i = (blockIdx.x - 1) * 32 + (threadIdx.x & 31);
     const float s = sum_partials(small, nwg, SMALL, i, red);
-    if ((threadIdx.x >> 5) != 0 || i >= SMALL) return;
-    int o = i;
-    if (o < K * K) { G.Wm[o] = s; return; }
-    o -= K * K;
-    if (o < K * K) { G.Wl[o] = s; return; }
-    o -= K * K;
-    if (o < K) { G.bm[o] = s; G.bce[o] = s; return; }
-    o -= K;
-    if (o < K) { G.bl[o] = s; return; }
-    o -= K;
-    if (o < K * C) { G.Wce[o] = s; return; }
-    o -= K * C;
-    smallg[o] = s;  // cdh = sum_b dh_b
+    // store the small gradient; returns how many gradient elements received s (0: smallg)
+    auto store = [&]() -> int {
+        int o = i;
+        if (o < K * K) { G.Wm[o] = s; return 1; }
+        o -= K * K;
+        if (o < K * K) { G.Wl[o] = s; return 1; }
+        o -= K * K;
+        if (o < K) { G.bm[o] = s; G.bce[o] = s; return 2; }
+        o -= K;
+        if (o < K) { G.bl[o] = s; return 1; }
+        o -= K;
+        if (o < K * C) { G.Wce[o] = s; return 1; }
+        o -= K * C;
+        smallg[o] = s;  // cdh = sum_b dh_b
+        return 0;
+    };
+    double sq = 0.0;
+    if ((threadIdx.x >> 5) == 0 && i < SMALL) sq = (double)s * s * store();
+    if (sqpart && threadIdx.x < 64) {  // clip-norm partial of this block (fixed order)
+        sq = wave_sum_d(sq);
+        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+    }
 }
 
 // Per-gene gradients from the row-block slabs (fixed order): covar_decoding_ (decoder pass 1)
@@ -746,7 +757,7 @@ template <int PART>
 __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, const float* __restrict__ gene,
                                                      const float* __restrict__ WeP_f, const float* __restrict__ slabB,
                                                      const float* __restrict__ slabE, const float* __restrict__ smallg,
-                                                     int nrb) {
+                                                     int nrb, double* __restrict__ sqpart) {
     constexpr int NQMAX = 1 + CMAX + 1;
     constexpr int NPART = 8;
     __shared__ float cdh[64];
@@ -772,22 +783,30 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
 #pragma unroll
         for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
     __syncthreads();
-    if (part != 0 || g >= d.D) return;
+    double sq = 0.0;  // sum of squares of the gradient elements this block writes (clip norm)
+    auto put = [&](float* dst, float v) { *dst = v; sq += (double)v * v; };
+    if (part == 0 && g < d.D) {
 #pragma unroll
-    for (int pp = 0; pp < NPART - 1; ++pp)
+        for (int pp = 0; pp < NPART - 1; ++pp)
 #pragma unroll
-        for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
-    if (PART != 2) {
-        G.bcd[g] = acc[0];
-        for (int c = 0; c < C; ++c) G.Wcd[(int64_t)g * C + c] = acc[1 + c];
+            for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
+        if (PART != 2) {
+            put(&G.bcd[g], acc[0]);
+            for (int c = 0; c < C; ++c) put(&G.Wcd[(int64_t)g * C + c], acc[1 + c]);
+        }
+        if (PART != 1) {
+            const float Gl = acc[nqB];
+            float gs = 0.f;
+            for (int k = 0; k < d.K; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
+            const float inv = gene[g];
+            put(&G.xm[g], -inv * gs);
+            put(&G.lsd[g], -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]));
+        }
     }
-    if (PART == 1) return;
-    const float Gl = acc[nqB];
-    float gs = 0.f;
-    for (int k = 0; k < d.K; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
-    const float inv = gene[g];
-    G.xm[g] = -inv * gs;
-    G.lsd[g] = -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]);
+    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..31)
+        sq = wave_sum_d(sq);
+        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+    }
 }
 
 // =======================================================================================
@@ -965,7 +984,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         }
         ScopedTimer tm(e, "k_loss");
         hipLaunchKernelGGL(k_vgrad_small, dim3(1), dim3(256), 0, st, d, sc, e->d_small, 0, G, e->d_smallg, e->d_rowv,
-                           e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 0);
+                           e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 0, nullptr);
         return hipGetLastError();
     }
     {
@@ -978,7 +997,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     if (split) {  // covar_decoding_ gradients final: all-reduce them under the encoder backward
         ScopedTimer tm(e, "k_vgrad_genes_dec");
         hipLaunchKernelGGL(k_vgrad_genes<1>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
-                           e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+                           e->d_slabB, e->d_slabE, e->d_smallg, nrb, nullptr);
         hipError_t er = comm_bucket(e, 0);
         if (er != hipSuccess) return er;
     }
@@ -993,24 +1012,31 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
                                             bf ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f, e->d_slabE);
         if (er != hipSuccess) return er;
     }
+    // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
+    const bool fuse_sq = !split && !(e->comm && e->world > 1);
+    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
+    double* sqS = fuse_sq ? e->d_sumsq : nullptr;
+    double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
         ScopedTimer tm(e, "k_vgrad_small");
-        hipLaunchKernelGGL(k_vgrad_small, dim3(1 + (SMALL + 31) / 32), dim3(256), 0, st, d, sc, e->d_small,
-                           e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 1);
+        hipLaunchKernelGGL(k_vgrad_small, dim3(gS), dim3(256), 0, st, d, sc, e->d_small,
+                           e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 1, sqS);
     }
     {
         ScopedTimer tm(e, "k_vgrad_genes");
         if (split)
-            hipLaunchKernelGGL(k_vgrad_genes<2>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
-                               e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+            hipLaunchKernelGGL(k_vgrad_genes<2>, dim3(gG), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                               e->d_slabB, e->d_slabE, e->d_smallg, nrb, sqG);
         else
-            hipLaunchKernelGGL(k_vgrad_genes<0>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
-                               e->d_slabB, e->d_slabE, e->d_smallg, nrb);
+            hipLaunchKernelGGL(k_vgrad_genes<0>, dim3(gG), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+                               e->d_slabB, e->d_slabE, e->d_smallg, nrb, sqG);
     }
     if (split) {
         hipError_t er = comm_bucket(e, 1);
         if (er != hipSuccess) return er;
         e->grads_reduced = e->comm && e->world > 1;
+    } else if (fuse_sq) {
+        e->sq_parts = gS + gG;
     }
     return hipGetLastError();
 }
