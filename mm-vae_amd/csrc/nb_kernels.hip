@@ -1401,10 +1401,10 @@ struct EncBwdLds {
 };
 
 template <class T, int KP, bool H1, bool RAW>
-__global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
-                                                 const int32_t* __restrict__ toff, const float* __restrict__ lat,
-                                                 const T* __restrict__ dhT, const T* __restrict__ WeP,
-                                                 Dims d, float* __restrict__ slabE) {
+MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                            const int32_t* __restrict__ toff, const float* __restrict__ lat,
+                            const T* __restrict__ dhT, const T* __restrict__ WeP,
+                            const Dims& d, float* __restrict__ slabE, const int bid) {
     using M = MM<T>;
     using Fr = typename M::frag;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // log1p tile row (gene) stride, elements
@@ -1412,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents,
     constexpr int HN = H1 ? 1 : HMAX;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
+    const int sp = bid % d.nsE, rb = bid / d.nsE;
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
@@ -1541,18 +1541,24 @@ __global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents,
     }
 }
 
+template <class T, int KP, bool H1, bool RAW>
+__global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                                                 const int32_t* __restrict__ toff, const float* __restrict__ lat,
+                                                 const T* __restrict__ dhT, const T* __restrict__ WeP,
+                                                 Dims d, float* __restrict__ slabE) {
+    enc_bwd_body<T, KP, H1, RAW>(ents, seg, toff, lat, dhT, WeP, d, slabE, (int)blockIdx.x);
+}
+
 // =======================================================================================
 // Gradient assembly (deterministic, fixed-order reductions)
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restrict__ small, int nwg,
-                                                    NBGrads G, float* __restrict__ smallg,
-                                                    const float* __restrict__ lossp, int nlossp,
-                                                    const float* __restrict__ klpart, int nkl,
-                                                    float* __restrict__ out, int with_grads,
-                                                    double* __restrict__ sqpart) {
+MMVAE_DEV void grad_small_body(const Dims& d, const float* __restrict__ small, int nwg, const NBGrads& G,
+                               float* __restrict__ smallg, const float* __restrict__ lossp, int nlossp,
+                               const float* __restrict__ klpart, int nkl, float* __restrict__ out, int with_grads,
+                               double* __restrict__ sqpart, const int bid) {
     const int K = d.K, C = d.C, H = d.H, R = d.R;
     const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
         __shared__ float sb[8];
         float lsum = 0.f, ksum = 0.f;
         for (int i = threadIdx.x; i < nlossp; i += 256) lsum += lossp[i];
@@ -1567,7 +1573,7 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
     }
     if (!with_grads) return;
     __shared__ float red[8][32];
-    const int i = (blockIdx.x - 1) * 32 + (threadIdx.x & 31);
+    const int i = (bid - 1) * 32 + (threadIdx.x & 31);
     const float s = sum_partials(small, nwg, SMALL, i, red);
     // store the small gradient; returns how many gradient elements received s (0: smallg)
     auto store = [&]() -> int {
@@ -1601,8 +1607,34 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
     if ((threadIdx.x >> 5) == 0 && i < SMALL) sq = (double)s * s * store();
     if (sqpart && threadIdx.x < 64) {
         sq = wave_sum_d(sq);
-        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+        if (threadIdx.x == 0) sqpart[bid] = sq;
     }
+}
+
+__global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restrict__ small, int nwg,
+                                                    NBGrads G, float* __restrict__ smallg,
+                                                    const float* __restrict__ lossp, int nlossp,
+                                                    const float* __restrict__ klpart, int nkl,
+                                                    float* __restrict__ out, int with_grads,
+                                                    double* __restrict__ sqpart) {
+    grad_small_body(d, small, nwg, G, smallg, lossp, nlossp, klpart, nkl, out, with_grads, sqpart, (int)blockIdx.x);
+}
+
+// k_enc_bwd and k_grad_small in ONE launch: both need only k_latent_bwd's outputs, so the small-
+// gradient blocks (appended after the encoder blocks) run beside the encoder tail instead of as
+// a separate kernel on the chain
+template <class T, int KP, bool H1>
+__global__ __launch_bounds__(256) void k_enc_bwd_small(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                                                       const int32_t* __restrict__ toff, const float* __restrict__ lat,
+                                                       const T* __restrict__ dhT, const T* __restrict__ WeP, Dims d,
+                                                       float* __restrict__ slabE, int nenc, const float* __restrict__ small,
+                                                       int nwg, NBGrads G, float* __restrict__ smallg,
+                                                       const float* __restrict__ lossp, int nlossp,
+                                                       const float* __restrict__ klpart, int nkl, float* __restrict__ out,
+                                                       double* __restrict__ sqpart) {
+    const int bid = (int)blockIdx.x;
+    if (bid < nenc) enc_bwd_body<T, KP, H1, true>(ents, seg, toff, lat, dhT, WeP, d, slabE, bid);
+    else grad_small_body(d, small, nwg, G, smallg, lossp, nlossp, klpart, nkl, out, 1, sqpart, bid - nenc);
 }
 
 // Per-gene gradients from the per-row-block column slabs of passes B, C and k_enc_bwd,
@@ -1955,17 +1987,6 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
                            e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
-    {
-        ScopedTimer tm(e, "k_enc_bwd");
-        const T* WeT = bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f;
-        const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
-        if (d.H == 1)
-            hipLaunchKernelGGL((k_enc_bwd<T, KP, true, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE);
-        else
-            hipLaunchKernelGGL((k_enc_bwd<T, KP, false, true>), dim3(nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE);
-    }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
     const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
@@ -1974,10 +1995,21 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
-        ScopedTimer tm(e, "k_grad_small");
-        hipLaunchKernelGGL(k_grad_small, dim3(gS), dim3(256), 0, st, d, e->d_small,
-                           e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off, e->n_lat_wg,
-                           e->d_out, 1, sqS);
+        // encoder backward + the small-parameter gradients / loss in one launch
+        ScopedTimer tm(e, "k_enc_bwd");
+        const T* WeT = bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f;
+        const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
+        const int nenc = nrb * d.nsE;
+        if (d.H == 1)
+            hipLaunchKernelGGL((k_enc_bwd_small<T, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE, nenc, e->d_small,
+                               e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
+                               e->n_lat_wg, e->d_out, sqS);
+        else
+            hipLaunchKernelGGL((k_enc_bwd_small<T, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE, nenc, e->d_small,
+                               e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
+                               e->n_lat_wg, e->d_out, sqS);
     }
     {
         ScopedTimer tm(e, "k_grad_genes");
