@@ -13,7 +13,7 @@
 //                  per-block partials of the dense encoder term mvec = (x_mean/s) W~^T
 //   k_enc_fwd      sum_nnz l (W~/s)  on MFMA                    (shared with NB)
 //   k_vlatent_fwd  h = that / ||l|| - mvec, heads, clamp, reparameterise, KL
-//   k_vkappa       kappa = clamp(exp(ln_kappa)), lbessel terms (one thread)
+//   (k_vprep's last block: kappa = clamp(exp(ln_kappa)), lbessel terms, one thread)
 //   k_vdec<0>      logits on MFMA, u = exp, v = u + hc: row sums |v|^2, sum v, sum l v
 //   k_vdec<1>      per-row cos_b, alpha_b, beta_b from the pass-0 split sums (vrow_coeffs);
 //                  dv = alpha (l + eps) + beta v, da = dv u: column sums + dz GEMM on MFMA
@@ -51,7 +51,7 @@ struct VScal {
     int rank0;     // this rank adds the lbessel backward term (once per global batch)
 };
 
-// d_vk: kappa scalars written by k_vkappa
+// d_vk: kappa scalars written by the last block of k_vprep (vkappa_body)
 enum { VK_KAPPA = 0, VK_EXP = 1, VK_MASK = 2, VK_T = 3, VK_BARICZ = 4 };
 
 // =======================================================================================
@@ -103,9 +103,17 @@ __global__ void k_vpack_dec(const float* Wd, int D, int DP, int K, int KP, float
 //   grec_g = (b_dec_g, b_cd_g, W_cd[g][0], valid)  (vmf.hh:285-287)
 //   WeS[k][g] = inv_g W~[k][g]                     (encoder B operand, bf16 or f32)
 // =======================================================================================
+MMVAE_DEV void vkappa_body(const VPtrs& P, const VScal& s, float* __restrict__ vk);
+// the last x-block (y = 0) computes the kappa scalars (vkappa_body, vmf.hh:301 + lbessel) — they
+// depend only on ln_kappa, so they ride in this launch instead of a kernel of their own
 __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, float* __restrict__ gene,
                                                const float* __restrict__ WeP_f, float* __restrict__ WeS_f,
-                                               __bf16* __restrict__ WeS_b, float* __restrict__ mvecp) {
+                                               __bf16* __restrict__ WeS_b, float* __restrict__ mvecp, VScal sc,
+                                               float* __restrict__ vk) {
+    if (blockIdx.x == gridDim.x - 1) {
+        if (blockIdx.y == 0) vkappa_body(P, sc, vk);
+        return;
+    }
     const int g0 = blockIdx.x * 256 + threadIdx.x;
     const bool in = g0 < d.DP;
     const int g = in ? g0 : d.DP - 1;
@@ -238,13 +246,13 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
 }
 
 // =======================================================================================
-// k_vkappa — kappa = clamp(exp(ln_kappa), kappa_min, kappa_max) (vmf.hh:301) and the scalar
+// vkappa_body — kappa = clamp(exp(ln_kappa), kappa_min, kappa_max) (vmf.hh:301) and the scalar
 // loss terms T = df log kappa - lbessel(kappa, df) (vmf.hh:433, operators.hh:65-81) in the
 // reference's fp32 operation order; the lbessel backward (Baricz bound, operators.hh:34-37).
 // exp/log are evaluated in double and rounded once (correctly rounded fp32), so the clamp
 // mask agrees with ATen's at the initial ln_kappa = log(kappa_min) (Q4).
 // =======================================================================================
-__global__ void k_vkappa(VPtrs P, VScal s, float* __restrict__ vk) {
+MMVAE_DEV void vkappa_body(const VPtrs& P, const VScal& s, float* __restrict__ vk) {
     if (threadIdx.x != 0) return;
     const float lk = P.lk[0];
     const float e = (float)exp((double)lk);
@@ -296,7 +304,7 @@ struct VDecPtrs {
     const float* rowfin;   // [Bpad][2]: alpha, beta (eval path: k_vrowfin)
     float* rowB;           // [nsD][Bpad][3]: |v|^2, sum v, sum l v
     const float* rowx;     // [Bpad][..]: [1] = sum (l^2 + 2 eps l)
-    const float* vk;       // kappa scalars (k_vkappa)
+    const float* vk;       // kappa scalars (vkappa_body in k_vprep)
     float* rowcos;         // [Bpad] cos_b (written by split 0 of the backward pass)
     float* dzp;            // [nsD][Bpad][KP]
     float* slabB;          // [nrb][1+C][DP]
@@ -925,8 +933,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     float* gene = e->d_gene;
     {
         ScopedTimer tm(e, "k_vprep");
-        hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, st, P, d, sc.epsD, gene,
-                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec);
+        hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256 + 1, d.KP / 8), dim3(256), 0, st, P, d, sc.epsD, gene,
+                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, sc, e->d_vk);
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
@@ -941,10 +949,6 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
                            e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
     }
     if (mode == 1) return hipGetLastError();
-    {
-        ScopedTimer tm(e, "k_vkappa");
-        hipLaunchKernelGGL(k_vkappa, dim3(1), dim3(64), 0, st, P, sc, e->d_vk);
-    }
     VDecPtrs Q;
     Q.lat = e->d_lat;
     Q.zf = e->d_zf;
