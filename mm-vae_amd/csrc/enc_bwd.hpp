@@ -1,0 +1,180 @@
+// Encoder backward body shared by the NB (nb_kernels.hip) and vMF (vmf_kernels.hip) launches,
+// so each model can put its small-gradient blocks into the same launch (k_enc_bwd_small /
+// k_enc_bwd_vsmall).
+#pragma once
+#include "common.hpp"
+#include "tiles.hpp"
+
+namespace mmvae {
+
+// =======================================================================================
+// k_enc_bwd — gradient of x_mean / ln_x_sd through the frozen encoder (autograd of
+// nb.hh:408-411) and of depth / nu_enc weights (raw x, nb.hh:448,498):
+//   Gl_g  = sum_k W_enc[k,g] M[k,g],  M = dh^T log1p(x)   (MFMA on densified 64x64 tiles)
+//   raw_g = sum_b a_b x_bg for a in {dpre, dhnu_h}        (gene-owner lanes over an f32 tile)
+// Workgroup = 64 cells x one gene split.  The log1p(x) tile [64 genes][64 cells] and the raw
+// count tile are shared by the four waves (each wave scatters its own 16 cells); wave w owns
+// M's latent block w and the raw sums of gene block w.  Everything is written straight to the
+// row block's slab in a fixed order — no atomics.  Single-buffered tiles, two barriers per tile.
+// =======================================================================================
+struct EncBwdLds {
+    int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, bytes;
+    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc) {
+        o_lt = KP * 64 * esz;
+        o_raw = o_lt + 64 * LS * esz;
+        o_part = o_raw + 64 * 68 * 4;
+        o_scal = o_part + 4 * 64 * 4;
+        o_wave = o_scal + nsc * 64 * 4;
+        wave_bytes = ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
+        bytes = o_wave + 4 * wave_bytes;
+    }
+};
+
+template <class T, int KP, bool H1, bool RAW>
+MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                            const int32_t* __restrict__ toff, const float* __restrict__ lat,
+                            const T* __restrict__ dhT, const T* __restrict__ WeP,
+                            const Dims& d, float* __restrict__ slabE, const int bid) {
+    using M = MM<T>;
+    using Fr = typename M::frag;
+    constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // log1p tile row (gene) stride, elements
+    constexpr int RB = 64 * (int)sizeof(T);        // staged W_enc row (one latent, 64 genes)
+    constexpr int HN = H1 ? 1 : HMAX;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int sp = bid % d.nsE, rb = bid / d.nsE;
+    const int row0 = rb * 64 + 16 * w;
+    const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
+    const int S = d.tpsE + 1;
+    const int H = H1 ? 1 : d.H;
+    const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
+    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN);
+    char* wst = smem;
+    T* lt = reinterpret_cast<T*>(smem + L.o_lt);          // [64 genes][LS]  log1p(x)
+    float* raw = reinterpret_cast<float*>(smem + L.o_raw);  // [64 genes][68] x
+    float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][64]
+    float* scal = reinterpret_cast<float*>(smem + L.o_scal);  // [1+H][64 cells]: dpre, dhnu_h
+    int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_wave + w * L.wave_bytes);  // [S] tile offsets
+    // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
+    RegStage<KP, RB> wreg;
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
+    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
+    const int lb = w;  // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
+    constexpr int KSB = 64 / M::KSTEP;
+    Fr afr[KSB];
+#pragma unroll
+    for (int s = 0; s < KSB; ++s)  // unconditional (clamped) loads; blocks past KP zeroed below
+        afr[s] = M::load(&dhT[(int64_t)(16 * min(lb, KP / 16 - 1) + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
+                              (lane >> 4) * M::EPL]);
+
+    const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
+    fill_toffl(toffl, S, t0, d.NT, toff, wbk, lane);
+    const int64_t segw = seg[wbk];
+    if (RAW && lane < 16) {
+        const int b = row0 + lane;
+        const float* Lr = lat + (int64_t)b * d.lat_stride;
+        const float ok = (b < d.B) ? 1.f : 0.f;
+        scal[16 * w + lane] = ok * Lr[d.LAT_DPRE];
+        for (int h = 0; h < H; ++h) scal[(1 + h) * 64 + 16 * w + lane] = ok * Lr[d.LAT_DHNU + h];
+    }
+    // this wave's 16 cell columns of both tiles
+    auto zero_cols = [&]() {
+        constexpr int CB = 16 * (int)sizeof(T) / 16;
+#pragma unroll
+        for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(lt + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+        if (RAW)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
+    };
+    auto scatter = [&](const ListEntries& le) {
+        le.visit(ents, lane, [&](int r, int gl, float x) {
+            lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
+            if (RAW) raw[gl * 68 + 16 * w + r] = x;
+        });
+    };
+    if (lb >= KP / 16)
+#pragma unroll
+        for (int s = 0; s < KSB; ++s) afr[s] = M::zero();
+
+    wave_sync();  // toffl written above by this wave
+    const int nt = t1 - t0;
+    ListEntries nxt;
+    if (t0 < t1) {
+        ListEntries first;
+        first.fetch(ents, segw, toffl, 0, lane);
+        nxt.fetch(ents, segw, toffl, min(1, nt - 1), lane);
+        wreg.store(wst);
+        zero_cols();
+        wave_sync();
+        scatter(first);
+    }
+    lds_barrier();
+    for (int t = t0; t < t1; ++t) {
+        const int tl = t - t0;
+        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
+        // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
+        if (RAW) {
+            const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
+            const float4* xr = reinterpret_cast<const float4*>(raw + gl * 68 + 16 * q4);
+            float4 xv[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xv[c] = xr[c];
+            for (int h = 0; h < 1 + H; ++h) {
+                const float4* sc = reinterpret_cast<const float4*>(scal + h * 64 + 16 * q4);
+                float v = 0.f;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 a = sc[c];
+                    v = fmaf(xv[c].x, a.x, fmaf(xv[c].y, a.y, fmaf(xv[c].z, a.z, fmaf(xv[c].w, a.w, v))));
+                }
+                v = sum_rowgroups(v);
+                if (lane < 16) slabE[((int64_t)rb * nq + 1 + h) * d.DP + 64 * t + gl] = v;
+            }
+        }
+        // ---- M block w on MFMA, then Gl partial = sum over the block's latents of W M ----
+        if (lb < KP / 16) {
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) {
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KSB; ++s) {
+                    const Fr bx = *reinterpret_cast<const Fr*>(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    acc = M::mma(afr[s], bx, acc);
+                }
+                const int gl = 16 * gb + (lane & 15);
+                float v = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int k = 16 * lb + 4 * (lane >> 4) + r;
+                    v = fmaf(static_cast<float>(*reinterpret_cast<const T*>(wst + swz_off<RB>(k, gl * (int)sizeof(T)))), acc[r], v);
+                }
+                v = sum_rowgroups(v);
+                if (lane < 16) part[w * 64 + gl] = v;
+            }
+        } else if (lane < 16) {
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) part[w * 64 + 16 * gb + lane] = 0.f;
+        }
+        lds_barrier();
+        if (threadIdx.x < 64) {
+            const int g = threadIdx.x;
+            slabE[((int64_t)rb * nq) * d.DP + 64 * t + g] = part[g] + part[64 + g] + part[128 + g] + part[192 + g];
+        }
+        if (t + 1 < t1) {
+            zero_cols();
+            wave_sync();
+            scatter(nxt);
+            wreg.store(wst);
+        }
+        nxt.fetch(ents, segw, toffl, min(tl + 2, nt - 1), lane);
+        lds_barrier();
+    }
+}
+
+template <class T, int KP>
+inline size_t enc_bwd_lds(const Dims& d) {
+    constexpr int LS = sizeof(T) == 2 ? 80 : 68;
+    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX)).bytes;
+}
+
+}  // namespace mmvae

@@ -29,6 +29,7 @@
 #include "common.hpp"
 #include "engine.hpp"
 #include "tiles.hpp"
+#include "enc_bwd.hpp"
 
 namespace mmvae {
 
@@ -699,14 +700,13 @@ static constexpr size_t VLAT_BWD_LDS = (size_t)(2 * 64 * 65 + 3 * LAT_CELLS * 68
 //   dln_kappa = dkappa exp(ln_kappa) [kappa_min <= exp(ln_kappa) <= kappa_max]
 // other blocks: fixed-order reduction of k_vlatent_bwd's per-workgroup partials.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const float* __restrict__ small, int nwg,
-                                                     VGrads G, float* __restrict__ smallg,
-                                                     const float* __restrict__ rowcos, const float* __restrict__ klpart,
-                                                     int nkl, const float* __restrict__ vk, float* __restrict__ out,
-                                                     int with_grads, double* __restrict__ sqpart) {
+MMVAE_DEV void vgrad_small_body(const Dims& d, const VScal& sc, const float* __restrict__ small, int nwg,
+                                const VGrads& G, float* __restrict__ smallg, const float* __restrict__ rowcos,
+                                const float* __restrict__ klpart, int nkl, const float* __restrict__ vk,
+                                float* __restrict__ out, int with_grads, double* __restrict__ sqpart, const int bid) {
     const int K = d.K, C = d.C;
     const int SMALL = 2 * K * K + 2 * K + K * C + K;
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
         __shared__ float sb[8];
         float cs = 0.f, ks = 0.f;
         for (int i = threadIdx.x; i < d.Bpad; i += 256) cs += rowcos[i];
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
     }
     if (!with_grads) return;
     __shared__ float red[8][32];
-    const int i = (blockIdx.x - 1) * 32 + (threadIdx.x & 31);
+    const int i = (bid - 1) * 32 + (threadIdx.x & 31);
     const float s = sum_partials(small, nwg, SMALL, i, red);
     // store the small gradient; returns how many gradient elements received s (0: smallg)
     auto store = [&]() -> int {
@@ -753,8 +753,32 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
     if ((threadIdx.x >> 5) == 0 && i < SMALL) sq = (double)s * s * store();
     if (sqpart && threadIdx.x < 64) {  // clip-norm partial of this block (fixed order)
         sq = wave_sum_d(sq);
-        if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+        if (threadIdx.x == 0) sqpart[bid] = sq;
     }
+}
+
+__global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const float* __restrict__ small, int nwg,
+                                                     VGrads G, float* __restrict__ smallg,
+                                                     const float* __restrict__ rowcos, const float* __restrict__ klpart,
+                                                     int nkl, const float* __restrict__ vk, float* __restrict__ out,
+                                                     int with_grads, double* __restrict__ sqpart) {
+    vgrad_small_body(d, sc, small, nwg, G, smallg, rowcos, klpart, nkl, vk, out, with_grads, sqpart, (int)blockIdx.x);
+}
+
+// the encoder backward (log1p term only) and the small-gradient / loss blocks in one launch
+template <class T, int KP>
+__global__ __launch_bounds__(256) void k_enc_bwd_vsmall(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+                                                        const int32_t* __restrict__ toff, const float* __restrict__ lat,
+                                                        const T* __restrict__ dhT, const T* __restrict__ WeP, Dims d,
+                                                        float* __restrict__ slabE, int nenc, VScal sc,
+                                                        const float* __restrict__ small, int nwg, VGrads G,
+                                                        float* __restrict__ smallg, const float* __restrict__ rowcos,
+                                                        const float* __restrict__ klpart, int nkl,
+                                                        const float* __restrict__ vk, float* __restrict__ out,
+                                                        double* __restrict__ sqpart) {
+    const int bid = (int)blockIdx.x;
+    if (bid < nenc) enc_bwd_body<T, KP, true, false>(ents, seg, toff, lat, dhT, WeP, d, slabE, bid);
+    else vgrad_small_body(d, sc, small, nwg, G, smallg, rowcos, klpart, nkl, vk, out, 1, sqpart, bid - nenc);
 }
 
 // Per-gene gradients from the row-block slabs (fixed order): covar_decoding_ (decoder pass 1)
@@ -1010,21 +1034,20 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
                            e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
-    {
-        ScopedTimer tm(e, "k_enc_bwd");
-        hipError_t er = enc_backward_launch(e, d, bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f,
-                                            bf ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f, e->d_slabE);
-        if (er != hipSuccess) return er;
-    }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     const bool fuse_sq = !split && !(e->comm && e->world > 1);
     const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
-        ScopedTimer tm(e, "k_vgrad_small");
-        hipLaunchKernelGGL(k_vgrad_small, dim3(gS), dim3(256), 0, st, d, sc, e->d_small,
-                           e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk, e->d_out, 1, sqS);
+        // encoder backward + the small-parameter gradients / loss in one launch
+        ScopedTimer tm(e, "k_enc_bwd");
+        const int nenc = nrb * d.nsE;
+        hipLaunchKernelGGL((k_enc_bwd_vsmall<T, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st, e->d_ents,
+                           e->d_seg, e->d_toff, e->d_lat, (const T*)(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f),
+                           (const T*)(bf ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f), d, e->d_slabE, nenc, sc,
+                           e->d_small, e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk,
+                           e->d_out, sqS);
     }
     {
         ScopedTimer tm(e, "k_vgrad_genes");
