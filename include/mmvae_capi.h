@@ -56,6 +56,15 @@ typedef struct mmvae_cfg {
     float kappa_min;     /* vMF --kappa_min (vmf.hh:61) */
     float kappa_max;     /* vMF --kappa_max (vmf.hh:62) */
     uint64_t seed;       /* Philox seed for the reparameterisation noise when none is injected */
+    int32_t relu;        /* --relu: NB ReLU after each frozen encoder / hidden decoder Linear
+                            (nb.hh:336-346, 372-373); vMF after each Angular encoder / hidden
+                            decoder Linear (vmf.hh:342-352, 378-379).  NB with relu and >= 1
+                            hidden encoder layer is the reference's construction error (Q2,
+                            nb.hh:334-337): mmvae_create returns MMVAE_E_ARG. */
+    int32_t n_enc_hidden;    /* NB --mean_encoding / vMF --encoding: hidden widths, <= 4 layers */
+    int32_t n_dec_hidden;    /* NB --mean_decoding / vMF --decoding */
+    int32_t enc_hidden[4];
+    int32_t dec_hidden[4];
 } mmvae_cfg;
 
 /* Fill a cfg with the reference defaults (mmvae_alg.hh:19-23, nb.hh:58-61, vmf.hh:59-63). */
@@ -148,6 +157,11 @@ int mmvae_sync(mmvae_h h);
  * registered gradients before clip + Adam (new: the reference has no distribution). */
 int mmvae_comm_unique_id(void* out128);
 int mmvae_comm_init(mmvae_h h, int32_t rank, int32_t world, const void* id128);
+/* id128 == NULL: local decomposition mode (no communicator) — the handle computes rank
+ * `rank`'s shard of a world-`world` step, including terms only rank 0 contributes (the vMF
+ * lbessel backward, Q3), and reduces nothing; mmvae_get_grad then returns the shard's
+ * gradient and the clip + Adam that follow act on it alone.  Used to test the data-parallel
+ * decomposition on one GPU. */
 /* SUM-all-reduce n host floats across the ranks (RCCL on the handle's stream; a copy when
  * world == 1).  Used by the host driver for the reported per-batch loss. */
 int mmvae_comm_allreduce(mmvae_h h, float* values, int64_t n);
@@ -162,6 +176,10 @@ int mmvae_timing_reset(mmvae_h h);
  * partials; the MMVAE_DBG stamp builds write per-wave phase cycles there; 3 = the last step's latent
  * noise eps [Bpad][K], rows in the staged order) to the host. */
 int mmvae_debug_copy(mmvae_h h, int32_t which, float* host, int64_t n);
+/* Gene tiling of the handle's tile kernels (tests assert that a split walks many tiles):
+ * out[0] = 64-gene tiles NT, out[1..3] = gene splits of the encoders / decoder pass B /
+ * decoder passes A and C (each split walks ceil(NT / splits) tiles). */
+int mmvae_tiling_info(mmvae_h h, int32_t* out4);
 
 /* ---- operators.hh (vMF observation model scalars) ----------------------------------
  * lbessel(kappa, nu): piecewise log I_nu(kappa) approximation (operators.hh:49-101) with

@@ -186,6 +186,15 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
     if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32 or BF16");
+    if (cfg->n_enc_hidden < 0 || cfg->n_enc_hidden > 4 || cfg->n_dec_hidden < 0 || cfg->n_dec_hidden > 4)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "at most 4 hidden encoder / decoder layers");
+    // nb.hh:334-337 pushes a hidden encoder Linear and its ReLU under the same name: LibTorch
+    // throws at construction, so the reference has no such model
+    if (cfg->model == MMVAE_MODEL_NB && cfg->relu && cfg->n_enc_hidden > 0)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "Submodule 'mu_encoding_1' already defined (reference nb.hh:334-337: "
+                                            "--relu with hidden --mean_encoding layers)");
+    if (cfg->n_enc_hidden > 0 || cfg->n_dec_hidden > 0)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden encoder/decoder layers are not built in this engine yet");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
         FAIL((Engine*)nullptr, MMVAE_E_HIP, "no HIP device " + std::to_string(device));
@@ -387,12 +396,15 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->d_col = nullptr;
     e->d_val = nullptr;
     e->d_covar = nullptr;
-    HIPCHK(e, dalloc(&e->d_rowptr, N + 1));
+    // N + 2 row pointers: rowptr[N + 1] = nnz makes the empty padding row N (every row past the
+    // batch points there) a valid zero-length row for readers that take rowptr[c + 1]
+    HIPCHK(e, dalloc(&e->d_rowptr, N + 2));
     HIPCHK(e, dalloc(&e->d_col, nnz));
     HIPCHK(e, dalloc(&e->d_val, nnz));
     HIPCHK(e, dalloc(&e->d_covar, (N + 1) * e->C));  // row N: zeros (padding rows)
     HIPCHK(e, hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C));
     HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_rowptr + N + 1, rowptr + N, sizeof(int64_t), hipMemcpyHostToDevice));
     if (nnz > 0) {
         HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
         HIPCHK(e, hipMemcpy(e->d_val, val, sizeof(float) * nnz, hipMemcpyHostToDevice));
@@ -761,8 +773,20 @@ static void build_buckets(Engine* e);
 }
 
 int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
-    if (!e || !id128 || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
+    if (!e || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
+    if (!id128) {
+        // local decomposition mode (tests): this handle computes rank `rank`'s shard of a
+        // world-`world` step (rank-0-only terms included) but reduces nothing — the caller sums
+        // the shards' gradients and losses itself
+        if (e->comm) {
+            ncclCommDestroy(e->comm);
+            e->comm = nullptr;
+        }
+        e->rank = rank;
+        e->world = world;
+        return MMVAE_OK;
+    }
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     if (e->comm) {
@@ -904,6 +928,15 @@ int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     const float* src = which == 0 ? e->d_hpart : which == 1 ? e->d_dzp : e->d_slabC;
     HIPCHK(e, hipMemcpy(host, src, sizeof(float) * n, hipMemcpyDeviceToHost));
+    return MMVAE_OK;
+}
+
+int mmvae_tiling_info(mmvae_h e, int32_t* out) {
+    if (!e || !out) FAIL(e, MMVAE_E_ARG, "tiling_info: null");
+    out[0] = (int32_t)e->NT;
+    out[1] = e->nsplit_e;
+    out[2] = e->nsplit_d;
+    out[3] = e->nsplit_a;
     return MMVAE_OK;
 }
 

@@ -298,7 +298,10 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     const float hb = (k < K) ? P.be[k] - mvk : 0.f;
     mark(2);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) sH[(4 * w + c) * 68 + k] = (k < K) ? hb + hs[c] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+        const float hv = hb + hs[c];  // mu_enc Linear output; --relu appends ReLU(inplace) (nb.hh:345-346)
+        sH[(4 * w + c) * 68 + k] = (k < K) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
+    }
     __syncthreads();
     // heads on f32 MFMA (nb.hh:412-416), transposed back to lane = latent through LDS
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
@@ -1310,9 +1313,11 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         float rdhs = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int b = blockIdx.x * LAT_CELLS + 4 * (lane >> 4) + r;
+            const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
             if (j < KP) {
-                const float v = (j < K) ? acc[r] : 0.f;
+                // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
+                const bool pass = j < K && (!d.relu || sH[cl * 68 + j] > 0.f);
+                const float v = pass ? acc[r] : 0.f;
                 dh[(int64_t)b * KP + j] = v;
                 dhT_f[(int64_t)j * d.Bpad + b] = v;
                 dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)v;
@@ -1663,6 +1668,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.Ncells = (int)e->N;
     d.nmv = (int)((e->DP + 255) / 256);
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
+    d.relu = e->cfg.relu != 0;
     return d;
 }
 

@@ -98,12 +98,13 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     hipMemcpy(d_pg, pg.data(), sizeof(float) * D, hipMemcpyHostToDevice);
     const float loglib = (float)std::log(lib);
     hipLaunchKernelGGL(k_synth_count, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg, d_cnt);
-    std::vector<int64_t> cnt(N), rp(N + 1, 0);
+    std::vector<int64_t> cnt(N), rp(N + 2, 0);  // rp[N + 1] = nnz: the empty padding row N
     if ((er = hipMemcpyAsync(cnt.data(), d_cnt, sizeof(int64_t) * N, hipMemcpyDeviceToHost, e->stream)) != hipSuccess)
         return er;
     if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;
     for (int64_t i = 0; i < N; ++i) rp[i + 1] = rp[i] + cnt[i];
     const int64_t nnz = rp[N];
+    rp[N + 1] = nnz;
     hipFree(e->d_rowptr);
     hipFree(e->d_col);
     hipFree(e->d_val);
@@ -112,12 +113,12 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     e->d_col = nullptr;
     e->d_val = nullptr;
     e->d_covar = nullptr;
-    if ((er = hipMalloc(&e->d_rowptr, sizeof(int64_t) * (N + 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_rowptr, sizeof(int64_t) * (N + 2))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_col, sizeof(int32_t) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_val, sizeof(float) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_covar, sizeof(float) * (N + 1) * e->C)) != hipSuccess) return er;  // row N: zeros
     if ((er = hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C)) != hipSuccess) return er;
-    hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice);
+    hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 2), hipMemcpyHostToDevice);
     std::vector<float> ones((size_t)N * e->C, 1.f);
     hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice);
     hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg,

@@ -23,6 +23,7 @@ struct Dims {
     int Ncells;       // dataset rows: row Ncells of the per-cell tile index is the empty row
     int nmv;          // mvec partial blocks (256 genes each) written by the prep kernel
     int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
+    int relu;         // ReLU on the frozen encoder's output h (nb.hh:345-346, vmf.hh:351-352)
 };
 
 // out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c = 0..3: the split

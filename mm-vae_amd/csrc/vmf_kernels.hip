@@ -179,7 +179,8 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
             rowx[(int64_t)b * d.rowx_stride] = cn.x;
             rowx[(int64_t)b * d.rowx_stride + 1] = cn.y;
         }
-        sH[(4 * w + c) * 68 + k] = (k < K) ? hs[c] * inx[c] - mk : 0.f;
+        const float hv = hs[c] * inx[c] - mk;  // Angular output; --relu appends ReLU (vmf.hh:351-352)
+        sH[(4 * w + c) * 68 + k] = (k < K) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
     }
     __syncthreads();
     // heads on f32 MFMA (vmf.hh:259-264), transposed back to lane = latent through LDS
@@ -664,7 +665,9 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         for (int r = 0; r < 4; ++r) {
             const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
             if (j < KP) {
-                const float v = (j < K) ? acc[r] : 0.f;
+                // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
+                const bool pass = j < K && (!d.relu || sH[cl * 68 + j] > 0.f);
+                const float v = pass ? acc[r] : 0.f;
                 const float vs = v * sH[cl * 68 + 64];
                 dhT_f[(int64_t)j * d.Bpad + b] = vs;
                 dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)vs;
@@ -944,6 +947,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.Ncells = (int)e->N;
     d.nmv = (int)((e->DP + 255) / 256);
     d.dbg = 0;
+    d.relu = e->cfg.relu != 0;
     return d;
 }
 

@@ -213,27 +213,47 @@ static int load_dataset(const CliOptions& o, mmvae_csr& csr) {
         return MMVAE_OK;
     int rc = mmvae_mtx_read(o.mtx.c_str(), o.threads, &csr);
     if (rc) return rc;
-    if (o.csr_cache) mmvae_csr_save(cache.c_str(), &csr);  // best effort (read-only dirs are fine)
+    // best effort (read-only dirs are fine); one writer per node (tmp + rename inside csr_save)
+    const char* lr = std::getenv("LOCAL_RANK");
+    if (o.csr_cache && (!lr || std::atoi(lr) == 0)) mmvae_csr_save(cache.c_str(), &csr);
     return MMVAE_OK;
 }
 
+// The launch key ties the id file to THIS launch, so a file left by a crashed earlier run with
+// the same --out is never read: torchrun's run id, else the rendezvous address, else the parent
+// process (the launcher that started every rank).
+static std::string launch_key() {
+    if (const char* r = std::getenv("TORCHELASTIC_RUN_ID")) return std::string("run:") + r;
+    const char* a = std::getenv("MASTER_ADDR");
+    const char* p = std::getenv("MASTER_PORT");
+    if (a && p) return std::string("addr:") + a + ":" + p;
+    return "ppid:" + std::to_string((long long)getppid());
+}
+
+static std::string rccl_id_path(const CliOptions& o) { return o.out + ".rccl_id"; }
+
 static int rendezvous(mmvae_h h, const CliOptions& o, int rank, int world) {
-    const std::string path = o.out + ".rccl_id";
+    const std::string path = rccl_id_path(o);
+    std::string key = launch_key();
+    key.resize(64, '\0');
     unsigned char id[128];
     if (rank == 0) {
         if (mmvae_comm_unique_id(id)) return fail(MMVAE_E_COMM, mmvae_last_error(nullptr));
         const std::string tmp = path + ".tmp";
         FILE* fp = std::fopen(tmp.c_str(), "wb");
-        if (!fp || std::fwrite(id, 1, 128, fp) != 128 || std::fclose(fp) != 0) return fail(MMVAE_E_COMM, "cannot write " + tmp);
+        if (!fp || std::fwrite(key.data(), 1, 64, fp) != 64 || std::fwrite(id, 1, 128, fp) != 128 ||
+            std::fclose(fp) != 0)
+            return fail(MMVAE_E_COMM, "cannot write " + tmp);
         std::rename(tmp.c_str(), path.c_str());
     } else {
         const double t0 = now_s();
         for (;;) {
             FILE* fp = std::fopen(path.c_str(), "rb");
             if (fp) {
-                const size_t n = std::fread(id, 1, 128, fp);
+                char k2[64];
+                const bool got = std::fread(k2, 1, 64, fp) == 64 && std::fread(id, 1, 128, fp) == 128;
                 std::fclose(fp);
-                if (n == 128) break;
+                if (got && std::memcmp(k2, key.data(), 64) == 0) break;  // else: a stale file, keep waiting
             }
             if (now_s() - t0 > 300) return fail(MMVAE_E_COMM, "timed out waiting for " + path);
             std::this_thread::sleep_for(std::chrono::milliseconds(50));
@@ -242,6 +262,15 @@ static int rendezvous(mmvae_h h, const CliOptions& o, int rank, int world) {
     if (mmvae_comm_init(h, rank, world, id)) return fail(MMVAE_E_COMM, mmvae_last_error(h));
     return MMVAE_OK;
 }
+
+// rank 0 removes the id file on every exit path once the ranks may have read it
+struct RcclIdCleanup {
+    std::string path;
+    bool armed = false;
+    ~RcclIdCleanup() {
+        if (armed) std::remove(path.c_str());
+    }
+};
 
 int run_cli(int argc, const char** argv, int model) {
     CliOptions o;
@@ -259,8 +288,8 @@ int run_cli(int argc, const char** argv, int model) {
         std::fprintf(stderr, "need output file header\n%s", usage_text(model));
         return EXIT_FAILURE;
     }
-    if (!o.enc_layers.empty() || !o.dec_layers.empty()) {
-        std::fprintf(stderr, "hidden encoder/decoder layers are not built in this engine (default architecture only)\n");
+    if (o.enc_layers.size() > 4 || o.dec_layers.size() > 4) {
+        std::fprintf(stderr, "at most 4 hidden encoder / decoder layers\n");
         return EXIT_FAILURE;
     }
     const int rank = std::getenv("RANK") ? std::atoi(std::getenv("RANK")) : 0;
@@ -315,6 +344,11 @@ int run_cli(int argc, const char** argv, int model) {
     cfg.kappa_min = o.kappa_min;
     cfg.kappa_max = o.kappa_max;
     cfg.seed = o.seed;
+    cfg.relu = o.relu ? 1 : 0;
+    cfg.n_enc_hidden = (int32_t)o.enc_layers.size();
+    cfg.n_dec_hidden = (int32_t)o.dec_layers.size();
+    for (size_t i = 0; i < o.enc_layers.size(); ++i) cfg.enc_hidden[i] = (int32_t)o.enc_layers[i];
+    for (size_t i = 0; i < o.dec_layers.size(); ++i) cfg.dec_hidden[i] = (int32_t)o.dec_layers[i];
     mmvae_h h = nullptr;
     if (mmvae_create(&cfg, device, &h)) {
         std::fprintf(stderr, "engine: %s\n", mmvae_last_error(nullptr));
@@ -323,6 +357,9 @@ int run_cli(int argc, const char** argv, int model) {
     int rc = mmvae_upload_csr(h, csr.rowptr, csr.col, csr.val, csr.N, csr.D, covar.empty() ? nullptr : covar.data());
     mmvae_csr_free(&csr);
     if (!rc) rc = mmvae_init_params(h, o.seed);
+    RcclIdCleanup id_cleanup;
+    id_cleanup.path = rccl_id_path(o);
+    id_cleanup.armed = world > 1 && rank == 0;
     if (!rc && world > 1) rc = rendezvous(h, o, rank, world);
     if (rc) {
         std::fprintf(stderr, "engine: %s %s\n", mmvae_last_error(h), mmvae_host_last_error());
@@ -355,7 +392,6 @@ int run_cli(int argc, const char** argv, int model) {
         }
         for (int64_t e = 0; e < t.max_epoch; ++e) w.write(fmt_g(scores[(size_t)e]) + "\n");
         w.close();
-        if (world > 1) std::remove((o.out + ".rccl_id").c_str());
     }
     mmvae_destroy(h);
     return EXIT_SUCCESS;

@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -498,8 +499,11 @@ int mmvae_mtx_read_dense_t(const char* path, int threads, int64_t* N_out, int64_
 
 int mmvae_csr_save(const char* path, const mmvae_csr* c) {
     if (!path || !c) return fail(MMVAE_E_ARG, "csr_save: null argument");
-    FILE* fp = std::fopen(path, "wb");
-    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot write ") + path);
+    // written under a process-unique temporary name and renamed into place: a reader never sees
+    // a torn file, and concurrent writers (one per rank) each publish a complete copy
+    const std::string tmp = std::string(path) + ".tmp." + std::to_string((long long)getpid());
+    FILE* fp = std::fopen(tmp.c_str(), "wb");
+    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot write ") + tmp);
     const char magic[8] = {'M', 'M', 'V', 'A', 'E', 'C', 'S', 'R'};
     bool ok = std::fwrite(magic, 1, 8, fp) == 8 && std::fwrite(&c->N, 8, 1, fp) == 1 &&
               std::fwrite(&c->D, 8, 1, fp) == 1 && std::fwrite(&c->nnz, 8, 1, fp) == 1 &&
@@ -507,7 +511,11 @@ int mmvae_csr_save(const char* path, const mmvae_csr* c) {
               std::fwrite(c->col, 4, (size_t)c->nnz, fp) == (size_t)c->nnz &&
               std::fwrite(c->val, 4, (size_t)c->nnz, fp) == (size_t)c->nnz;
     ok = (std::fclose(fp) == 0) && ok;
-    return ok ? MMVAE_OK : fail(MMVAE_E_ARG, std::string("short write on ") + path);
+    if (!ok || std::rename(tmp.c_str(), path) != 0) {
+        std::remove(tmp.c_str());
+        return fail(MMVAE_E_ARG, std::string("short write on ") + path);
+    }
+    return MMVAE_OK;
 }
 
 int mmvae_csr_load(const char* path, mmvae_csr* c) {
@@ -528,7 +536,13 @@ int mmvae_csr_load(const char* path, mmvae_csr* c) {
              std::fread(c->col, 4, (size_t)c->nnz, fp) == (size_t)c->nnz &&
              std::fread(c->val, 4, (size_t)c->nnz, fp) == (size_t)c->nnz;
     }
+    // the trailing byte must be the end of the file, and the row pointers a valid CSR of nnz
+    // entries with gene ids inside [0, D): a stale or foreign file is rejected, never walked
+    ok = ok && std::fgetc(fp) == EOF;
     std::fclose(fp);
+    if (ok) ok = c->D > 0 && c->rowptr[0] == 0 && c->rowptr[c->N] == c->nnz;
+    for (int64_t i = 0; ok && i < c->N; ++i) ok = c->rowptr[i + 1] >= c->rowptr[i];
+    for (int64_t j = 0; ok && j < c->nnz; ++j) ok = c->col[j] >= 0 && c->col[j] < c->D;
     if (!ok) {
         mmvae_csr_free(c);
         return fail(MMVAE_E_ARG, std::string("not a valid CSR cache: ") + path);

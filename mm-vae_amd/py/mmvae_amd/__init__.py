@@ -30,7 +30,8 @@ class Cfg(ctypes.Structure):
                 ("C", ctypes.c_int64), ("K", ctypes.c_int64), ("H", ctypes.c_int64), ("R", ctypes.c_int64),
                 ("max_batch", ctypes.c_int64), ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("grad_clip", ctypes.c_float), ("kappa_min", ctypes.c_float), ("kappa_max", ctypes.c_float),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("relu", ctypes.c_int32), ("n_enc_hidden", ctypes.c_int32),
+                ("n_dec_hidden", ctypes.c_int32), ("enc_hidden", ctypes.c_int32 * 4), ("dec_hidden", ctypes.c_int32 * 4)]
 
 
 class StepArgs(ctypes.Structure):
@@ -83,6 +84,7 @@ def lib():
         "mmvae_timing_get": (ctypes.c_int, [h, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double), i64p]),
         "mmvae_timing_reset": (ctypes.c_int, [h]),
         "mmvae_debug_copy": (ctypes.c_int, [h, i32, f32p, i64]),
+        "mmvae_tiling_info": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
         "mmvae_lbessel": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_lbessel_grad": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_fasterlog": (ctypes.c_float, [ctypes.c_float]),
@@ -114,10 +116,18 @@ class Engine:
     """One model + optimiser + HBM dataset on one GPU (the C handle)."""
 
     def __init__(self, D, K, C=1, H=1, R=1, max_batch=100, dtype="f32", model=MODEL_NB, device=0, seed=42,
-                 lr=1e-3, kappa_min=0.1, kappa_max=10.0):
+                 lr=1e-3, kappa_min=0.1, kappa_max=10.0, relu=False, enc_hidden=(), dec_hidden=()):
         L = lib()
         c = default_cfg(model)
         c.D, c.K, c.C, c.H, c.R, c.max_batch = D, K, C, H, R, max_batch
+        c.relu = 1 if relu else 0
+        if len(enc_hidden) > 4 or len(dec_hidden) > 4:
+            raise MMVAEError("at most 4 hidden encoder / decoder layers")
+        c.n_enc_hidden, c.n_dec_hidden = len(enc_hidden), len(dec_hidden)
+        for i, v in enumerate(enc_hidden):
+            c.enc_hidden[i] = int(v)
+        for i, v in enumerate(dec_hidden):
+            c.dec_hidden[i] = int(v)
         c.dtype = _DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
         c.seed, c.lr, c.kappa_min, c.kappa_max = seed, lr, kappa_min, kappa_max
         self.cfg = c
@@ -273,8 +283,19 @@ class Engine:
         return bytes(buf.raw)
 
     def comm_init(self, rank, world, uid):
-        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        """uid = the 128-byte RCCL id, or None for the local decomposition mode (no reduction)."""
+        buf = ctypes.create_string_buffer(bytes(uid), 128) if uid is not None else None
         self._chk(lib().mmvae_comm_init(self._h, rank, world, buf), "comm_init")
+
+    def tiling(self):
+        """{'NT', 'split_enc', 'split_dec', 'split_ac'} and tiles per split (tps_*)."""
+        a = (ctypes.c_int32 * 4)()
+        self._chk(lib().mmvae_tiling_info(self._h, a), "tiling_info")
+        NT = a[0]
+        out = {"NT": NT, "split_enc": a[1], "split_dec": a[2], "split_ac": a[3]}
+        for k in ("enc", "dec", "ac"):
+            out["tps_" + k] = -(-NT // out["split_" + k])
+        return out
 
     # ---- timing ----
     def timing(self, on=True):

@@ -28,7 +28,7 @@ def _lgamma(v):
     return gammaln(v)
 
 
-def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None):
+def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     """Loss and gradients of every registered parameter (pre-clip), kernel algebra.
 
     P, FR: dicts of float64 arrays with LibTorch names (default architecture: no hidden
@@ -49,6 +49,8 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None):
     # ---- k_enc_fwd: sparse-split encoder + raw-x dots -----------------------------------
     l = np.log1p(x)
     h = (l * inv) @ We.T - mvec + be             # == W_e x~ + b_e
+    if relu:                                     # nb.hh:345-346: ReLU after mu_encoding
+        h = np.maximum(h, 0.0)
     hnu = x @ P["nu_encoding.weight"].T + P["nu_encoding.bias"]
     pre = x @ P["depth.weight"][0] + P["depth.bias"][0]
 
@@ -119,6 +121,8 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None):
     G["mu_representation_logvariance.weight"] = da.T @ h
     G["mu_representation_logvariance.bias"] = da.sum(0)
     dh = dmean @ P["mu_representation_mean.weight"] + da @ P["mu_representation_logvariance.weight"]
+    if relu:                                     # ReLU backward (mask of the stored output)
+        dh = dh * (h > 0)
     dnmean = dznu + (beta / n) * nmean
     dnlnvar = dznu * eps_nu * nsig / 2 + (beta / (2 * n)) * (np.exp(nlnvar) - 1)
     dan = dnlnvar * ((an >= -4) & (an <= 4))

@@ -46,7 +46,7 @@ def lbessel_bwd(kappa, nu):
     return 0.5 * (lb + ub) / kappa
 
 
-def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_total=None):
+def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_total=None, relu=False):
     """Loss and pre-clip gradients of every registered vMF parameter (kernel algebra)."""
     B, D = x.shape
     n = float(B if n_total is None else n_total)
@@ -74,6 +74,8 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
 
     # ---- k_enc_fwd + k_vlatent_fwd -------------------------------------------------------------
     h = ((l * inv) @ Wt.T) / nx[:, None] - mvec
+    if relu:                                          # vmf.hh:351-352: ReLU after Angular
+        h = np.maximum(h, 0.0)
     mean = h @ P["representation_mean.weight"].T + P["representation_mean.bias"] \
         + c @ P["covar_encoding.weight"].T + P["covar_encoding.bias"]
     a = h @ P["representation_logvariance.weight"].T + P["representation_logvariance.bias"]
@@ -123,6 +125,8 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     G["covar_encoding.weight"] = dmean.T @ c
     G["covar_encoding.bias"] = dmean.sum(0)
     dh = dmean @ P["representation_mean.weight"] + dA @ P["representation_logvariance.weight"]
+    if relu:
+        dh = dh * (h > 0)
 
     # ---- k_enc_bwd (dh / nx against log1p x) + k_vgrad_genes -----------------------------------
     Gl = ((dh / nx[:, None]).T @ l * Wt).sum(0)      # sum_k W~[k,g] sum_b dh_bk l_bg / nx_b

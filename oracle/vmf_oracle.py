@@ -44,8 +44,18 @@ class _LBessel(torch.autograd.Function):
         return 0.5 * (lb + ub) / x, None   # Q3: grad (the upstream) is not used
 
 
-def lbessel_op(kappa, nu):
-    return _LBessel.apply(kappa, nu)
+class _LBesselNoGrad(_LBessel):
+    """The same forward with no backward contribution: the data-parallel restatement adds the
+    upstream-independent Baricz gradient (Q3) on rank 0 only, so the ranks' summed gradient
+    equals the single-process one."""
+
+    @staticmethod
+    def backward(ctx, grad):
+        return torch.zeros_like(ctx.saved_tensors[0]), None
+
+
+def lbessel_op(kappa, nu, with_grad=True):
+    return (_LBessel if with_grad else _LBesselNoGrad).apply(kappa, nu)
 
 
 def param_names():
@@ -76,10 +86,11 @@ def init_params(D, C=1, Z=2, kappa_min=0.1, seed=0):
 
 
 class VMFModel:
-    def __init__(self, params, frozen, kappa_min=0.1, kappa_max=10.0):
+    def __init__(self, params, frozen, kappa_min=0.1, kappa_max=10.0, relu=False):
         self.p = OrderedDict((k, v.clone().requires_grad_(True)) for k, v in params.items())
         self.fr = OrderedDict((k, v.clone()) for k, v in frozen.items())
         self.kmin, self.kmax = float(np.float32(kappa_min)), float(np.float32(kappa_max))
+        self.relu = relu
 
     def lin(self, name, x):
         return F.linear(x, self.p[name + ".weight"], self.p[name + ".bias"])
@@ -95,6 +106,8 @@ class VMFModel:
         xn = F.normalize(x.log1p(), p=2.0, dim=1)
         xn_std = torch.div(torch.sub(xn, self.p["x_mean"]), F.softplus(self.p["ln_x_sd"]) + eps)
         h = self.angular(xn_std)
+        if self.relu:  # vmf.hh:351-352: z_enc = Angular, ReLU(z_dim)
+            h = F.relu(h)
         lnvar = torch.clamp(self.lin("representation_logvariance", h), -4.0, 4.0)
         mean = self.lin("representation_mean", h)
         if c is not None:
@@ -116,23 +129,26 @@ class VMFModel:
         return dict(recon=recon, mean=mean, lnvar=lnvar, kappa=kappa)
 
 
-def vmf_vae_loss(x, y, kl_weight):
-    """vmf.hh:419-440."""
+def vmf_vae_loss(x, y, kl_weight, n_total=None, lbessel_grad=True):
+    """vmf.hh:419-440.
+
+    n_total / lbessel_grad (data-parallel restatement only): the divisor is the GLOBAL batch
+    and only one rank carries the lbessel backward."""
     eps = 1e-2 / float(np.float32(x.size(1)))
     yobs = F.normalize(F.relu(x).log1p() + eps, p=2.0, dim=1)
-    n = float(yobs.size(0))
+    n = float(yobs.size(0)) if n_total is None else float(n_total)
     dd = float(yobs.size(1))
     df = float(np.float32(max(0.5 * dd - 1.0, 0.0)))
     kl = -0.5 * torch.sum(1 + y["lnvar"] - y["mean"].pow(2) - y["lnvar"].exp())
     llik = torch.sum(yobs * y["recon"], 1) * y["kappa"]
-    llik = llik + (df * torch.log(y["kappa"]) - lbessel_op(y["kappa"], df))
+    llik = llik + (df * torch.log(y["kappa"]) - lbessel_op(y["kappa"], df, lbessel_grad))
     llik = llik - 0.5 * dd * float(fasterlog(np.float32(2.0 * math.pi)))
     return kl / n * kl_weight - llik.sum() / n
 
 
 class VMFTrainer:
-    def __init__(self, params, frozen, lr=1e-3, kappa_min=0.1, kappa_max=10.0, grad_clip=1.0):
-        self.m = VMFModel(params, frozen, kappa_min, kappa_max)
+    def __init__(self, params, frozen, lr=1e-3, kappa_min=0.1, kappa_max=10.0, grad_clip=1.0, relu=False):
+        self.m = VMFModel(params, frozen, kappa_min, kappa_max, relu=relu)
         self.adam = LibTorchAdam(list(self.m.p.values()), lr=lr, weight_decay=1e-4)
         self.grad_clip = grad_clip
 
@@ -143,6 +159,21 @@ class VMFTrainer:
         L.backward()
         grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.m.p.items())
         total = clip_grad_norm_([v.grad for v in self.m.p.values()], self.grad_clip)
+        self.adam.step()
+        return dict(loss=float(L.detach()), grads=grads, total_norm=total)
+
+    def step_dp(self, x, c, eps, beta, n_total, allreduce, rank):
+        """The engine's data-parallel step (capi.hip mmvae_run, vmf_kernels.hip k_vgrad_small):
+        this rank's rows, loss over the global batch, the lbessel backward on rank 0 only, SUM
+        all-reduce of the registered gradients, then clip + Adam on every rank."""
+        y = self.m.forward(x, c, eps, True)
+        L = vmf_vae_loss(x, y, beta, n_total=n_total, lbessel_grad=(rank == 0))
+        self.adam.zero_grad()
+        L.backward()
+        gl = [v.grad for v in self.m.p.values()]
+        allreduce(gl)
+        grads = OrderedDict((k, v.grad.detach().clone()) for k, v in self.m.p.items())
+        total = clip_grad_norm_(gl, self.grad_clip)
         self.adam.step()
         return dict(loss=float(L.detach()), grads=grads, total_norm=total)
 

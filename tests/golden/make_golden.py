@@ -20,17 +20,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import nb_oracle, synth, vmf_oracle  # noqa: E402
 
 NB_CASES = [
-    # name, N, D, K, C, H, R, B, steps, lib, seed
+    # name, N, D, K, C, H, R, B, steps, lib, seed[, relu]
     ("nb_small", 40, 50, 8, 1, 1, 1, 16, 3, 200.0, 1),
     ("nb_mid", 300, 500, 16, 1, 1, 1, 64, 3, 300.0, 2),
     ("nb_generic", 60, 70, 5, 2, 2, 2, 32, 3, 150.0, 3),
     ("nb_k1", 20, 30, 1, 1, 1, 1, 8, 2, 100.0, 4),
     ("nb_dups", 10, 40, 8, 1, 1, 1, 24, 2, 120.0, 5),
     ("nb_k64", 128, 256, 64, 1, 1, 1, 128, 2, 500.0, 6),
+    ("nb_relu", 100, 300, 16, 1, 1, 1, 64, 3, 300.0, 7, True),
 ]
 
 
-def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed):
+def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed, relu=False):
     rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
     rng = np.random.default_rng(seed + 1000)
     if C == 1:
@@ -38,8 +39,8 @@ def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed):
     else:
         covar = rng.standard_normal((N, C)).astype(np.float32)
     params, frozen = nb_oracle.init_params(D, C=C, K=K, H=H, R=R, seed=seed)
-    tr = nb_oracle.NBTrainer(params, frozen)
-    out = dict(N=N, D=D, K=K, C=C, H=H, R=R, B=B, steps=steps,
+    tr = nb_oracle.NBTrainer(params, frozen, relu=relu)
+    out = dict(N=N, D=D, K=K, C=C, H=H, R=R, B=B, steps=steps, relu=np.int32(relu),
                rowptr=rowptr, col=col, val=val, covar=covar)
     for k, v in params.items():
         out["init/" + k] = v.numpy()
@@ -93,10 +94,11 @@ VMF_CASES = [
     ("vmf_k32", 128, 256, 32, 1, 128, 2, 500.0, 13, float(np.log(np.float32(5.0)))),
     ("vmf_dups", 10, 40, 8, 1, 24, 2, 120.0, 14, float(np.log(np.float32(0.7)))),
     ("vmf_z64", 100, 300, 64, 1, 64, 2, 400.0, 15, float(np.log(np.float32(9.0)))),
+    ("vmf_relu", 100, 300, 16, 1, 64, 3, 300.0, 16, float(np.log(np.float32(3.0))), True),
 ]
 
 
-def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa):
+def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa, relu=False):
     rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
     rng = np.random.default_rng(seed + 1000)
     if C == 1:
@@ -106,8 +108,8 @@ def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa):
     params, frozen = vmf_oracle.init_params(D, C=C, Z=Z, seed=seed)
     if ln_kappa is not None:
         params["ln_kappa"] = torch.tensor([ln_kappa], dtype=torch.float32)
-    tr = vmf_oracle.VMFTrainer(params, frozen)
-    out = dict(N=N, D=D, K=Z, C=C, H=1, R=1, B=B, steps=steps, model="vmf",
+    tr = vmf_oracle.VMFTrainer(params, frozen, relu=relu)
+    out = dict(N=N, D=D, K=Z, C=C, H=1, R=1, B=B, steps=steps, model="vmf", relu=np.int32(relu),
                rowptr=rowptr, col=col, val=val, covar=covar)
     for k, v in params.items():
         out["init/" + k] = v.numpy()
@@ -154,9 +156,9 @@ def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa):
 if __name__ == "__main__":
     torch.set_num_threads(1)
     which = sys.argv[1:] or ["nb", "vmf"]
-    if "nb" in which:
-        for case in NB_CASES:
+    for case in NB_CASES:
+        if "nb" in which or case[0] in which:
             make_nb(*case)
-    if "vmf" in which:
-        for case in VMF_CASES:
+    for case in VMF_CASES:
+        if "vmf" in which or case[0] in which:
             make_vmf(*case)

@@ -32,12 +32,16 @@ def model_of(z):
     return str(z["model"]) if "model" in z else "nb"
 
 
+def relu_of(z):
+    return bool(int(z["relu"])) if "relu" in z else False
+
+
 def engine_from_fixture(z, dtype="f32"):
     from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
     d = dims(z)
     model = MODEL_VMF if model_of(z) == "vmf" else MODEL_NB
     eng = Engine(D=d["D"], K=d["K"], C=d["C"], H=d["H"], R=d["R"], max_batch=max(d["B"], 64), dtype=dtype,
-                 model=model)
+                 model=model, relu=relu_of(z))
     eng.upload_csr(z["rowptr"], z["col"], z["val"], covar=z["covar"])
     eng.set_params(params_of(z, "init/"))
     eng.set_params(params_of(z, "frozen/"))

@@ -1,0 +1,148 @@
+"""Production-tiling parity (-m gpu): the tile kernels as the bench runs them, against the oracle.
+
+At the golden fixtures' sizes (D <= 500) every gene split of the default tiling holds exactly
+one 64-gene tile, so the multi-tile machinery of the decoder / encoder kernels — double-buffered
+stages, next-tile entry prefetch, cross-tile Eacc / dz / column accumulation, the 8-wave pass B
+of the bf16 mode — would go unchecked.  Two families of tests close that gap:
+
+* every golden fixture re-run with the gene splits forced to 1 and 2 (MMVAE_NSPLIT_E / _D / _A):
+  each split then walks up to NT tiles;
+* the bench's own shapes (configs[1]: D = 20k, K = 64, B = 4096; configs[2] vMF Z = 32;
+  configs[3] / [4] per-GPU: D = 30k, B = 4096 / 8192) with the production tiling (tiles per
+  split asserted > 1), compared with the oracle (oracle/nb_oracle.py, vmf_oracle.py: the
+  reference's op sequence on ATen fp32) run live on the host on the same rows, weights and
+  noise.
+
+Tolerances as the golden tests: f32 mode loss rel 2e-5, gradients norm-relative 2e-4, clip
+norm 1e-4; bf16 operand mode loss 2e-3, gradients 3e-2.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import (assert_grads_close, dims, engine_from_fixture, eps_of, golden_files, load, params_of,
+                     rel_err)
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"f32": (2e-5, 2e-4), "bf16": (2e-3, 3e-2)}
+
+
+def _eps(z, tag, vmf):
+    return z[f"{tag}/eps_mu"].ravel().astype(np.float32) if vmf else eps_of(z, tag)
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
+@pytest.mark.parametrize("path", golden_files("nb_") + golden_files("vmf_"), ids=os.path.basename)
+def test_fixture_forced_gene_splits(monkeypatch, path, split):
+    """Every fixture with 1 or 2 gene splits per kernel (each split walks many tiles): the
+    first step's loss, gradients and clip norm against the golden vectors, in f32."""
+    for v in ("MMVAE_NSPLIT_E", "MMVAE_NSPLIT_D", "MMVAE_NSPLIT_A"):
+        monkeypatch.setenv(v, split)
+    z = load(path)
+    vmf = "vmf" in os.path.basename(path)
+    eng = engine_from_fixture(z, "f32")
+    til = eng.tiling()
+    assert til["split_dec"] == min(int(split), til["NT"]) and til["split_enc"] == min(int(split), til["NT"])
+    if til["NT"] >= 4:
+        assert til["tps_dec"] >= 2 and til["tps_enc"] >= 2 and til["tps_ac"] >= 2, til
+    loss, norm = eng.step(z["s0/cells"], float(z["s0/beta"]), eps=_eps(z, "s0", vmf))
+    want = float(z["s0/loss"])
+    assert abs(loss - want) <= 2e-5 * abs(want), (loss, want)
+    gold = params_of(z, "s0/grad/")
+    got = eng.grads()
+    if vmf:  # ln_kappa: fp32 cancellation of df/kappa-sized terms (see test_gpu_vmf.py)
+        gk, wk = float(got.pop("ln_kappa")[0]), float(gold.pop("ln_kappa")[0])
+        df = max(0.5 * int(z["D"]) - 1.0, 0.0)
+        assert abs(gk - wk) <= 1e-6 * df / 0.1 + 2e-4 * abs(wk)
+    assert_grads_close(got, gold, 2e-4, ctx=f"split {split}")
+    assert abs(norm - float(z["s0/total_norm"])) <= 1e-4 * float(z["s0/total_norm"])
+
+
+# ---------------------------------------------------------------------------------------------
+# live oracle at the bench's shapes
+# ---------------------------------------------------------------------------------------------
+def _oracle_inputs(eng, cells, D):
+    from oracle import synth
+    rp, col, val = eng.get_rows(cells)
+    return torch.from_numpy(synth.densify(rp, col, val, np.arange(len(cells)), D))
+
+
+def _engine_params(eng, shapes):
+    info = {n: k for n, k, _ in eng.param_info()}
+    return {n: torch.from_numpy(eng.get_param(n, info[n]).reshape(v.shape)) for n, v in shapes.items()}
+
+
+def _run_live(model, D, K, B, dtype, N, relu=False, beta=0.8):
+    from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
+    from oracle import nb_oracle, vmf_oracle
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    vmf = model == "vmf"
+    eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=1, relu=relu, model=MODEL_VMF if vmf else MODEL_NB)
+    eng.synth_csr(N, lib_size=2000.0, seed=3)
+    eng.init_params(seed=7)
+    if vmf:  # kappa off its floor so its gradient is live (Q4)
+        eng.set_param("ln_kappa", np.array([np.log(np.float32(4.0))], np.float32))
+    til = eng.tiling()
+    assert til["tps_dec"] > 1 and til["tps_enc"] > 1 and til["tps_ac"] > 1, til
+    cells = (np.arange(B, dtype=np.int64) * 7 + 11) % N  # scattered dataset rows
+    rng = np.random.default_rng(5)
+    em = rng.standard_normal((B, K)).astype(np.float32)
+    en = rng.standard_normal((B, 1)).astype(np.float32)
+    if vmf:
+        p0, f0 = vmf_oracle.init_params(D, Z=K)
+        tr = vmf_oracle.VMFTrainer(_engine_params(eng, p0), _engine_params(eng, f0), relu=relu)
+    else:
+        p0, f0 = nb_oracle.init_params(D, K=K)
+        tr = nb_oracle.NBTrainer(_engine_params(eng, p0), _engine_params(eng, f0), relu=relu)
+    eps = em.ravel() if vmf else np.concatenate([em.ravel(), en.ravel()])
+    loss, norm = eng.step(cells, beta, eps=eps)
+    x = _oracle_inputs(eng, cells, D)
+    c = torch.ones(B, 1)
+    if vmf:
+        r = tr.step(x, c, torch.from_numpy(em), beta)
+    else:
+        r = tr.step(x, c, torch.from_numpy(em), torch.from_numpy(en), beta)
+    del x
+    tl, tg = TOL[dtype]
+    assert np.isfinite(loss) and abs(loss - r["loss"]) <= tl * abs(r["loss"]), (loss, r["loss"])
+    gold = {k: v.numpy() for k, v in r["grads"].items()}
+    got = eng.grads()
+    if vmf:
+        gk, wk = float(got.pop("ln_kappa")[0]), float(gold.pop("ln_kappa")[0])
+        df = 0.5 * D - 1.0
+        assert abs(gk - wk) <= 1e-6 * df + tg * abs(wk), (gk, wk)
+    assert_grads_close(got, gold, tg, ctx=f"{model} {dtype} D={D} B={B}")
+    assert abs(norm - r["total_norm"]) <= 10 * tg * r["total_norm"], (norm, r["total_norm"])
+    return til
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_nb_bench_shape_configs1(dtype):
+    """BASELINE configs[1] per step: NB, 20k genes, latent 64, 4096 cells (the bench line)."""
+    til = _run_live("nb", 20000, 64, 4096, dtype, N=12000)
+    assert til["tps_dec"] >= 20, til
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_vmf_bench_shape_configs2(dtype):
+    """BASELINE configs[2] per step: vMF, 20k genes, latent 32, 4096 cells."""
+    _run_live("vmf", 20000, 32, 4096, dtype, N=12000)
+
+
+def test_nb_configs3_per_gpu_shape_f32():
+    """configs[3] per GPU: 30k genes, 4096 cells per rank (the DP=8 shard of a 32k batch)."""
+    _run_live("nb", 30000, 64, 4096, "f32", N=9000)
+
+
+def test_nb_configs4_per_gpu_shape_bf16():
+    """configs[4] per GPU: 30k genes, 8192 cells per rank."""
+    _run_live("nb", 30000, 64, 8192, "bf16", N=9000)
+
+
+@pytest.mark.parametrize("model", ["nb", "vmf"])
+def test_relu_bench_shape(model):
+    """--relu at a multi-tile shape (ReLU after mu_encoding / Angular, nb.hh:345-346, vmf.hh:351-352)."""
+    _run_live(model, 20000, 64 if model == "nb" else 32, 1024, "f32", N=5000, relu=True)

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import GOLDEN, dims, golden_files, load, params_of
+from helpers import GOLDEN, dims, golden_files, load, params_of, relu_of
 from oracle import fastmath, nb_analytic, nb_oracle, synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,7 +45,7 @@ def test_oracle_reproduces_golden(path):
     d = dims(z)
     torch.set_num_threads(1)
     tr = nb_oracle.NBTrainer({k: torch.from_numpy(v) for k, v in params_of(z, "init/").items()},
-                             {k: torch.from_numpy(v) for k, v in params_of(z, "frozen/").items()})
+                             {k: torch.from_numpy(v) for k, v in params_of(z, "frozen/").items()}, relu=relu_of(z))
     for t in range(int(z["steps"])):
         cells = z[f"s{t}/cells"]
         x = torch.from_numpy(synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]))
@@ -70,7 +70,7 @@ def test_kernel_algebra_matches_golden(path):
     x = synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]).astype(np.float64)
     L, G = nb_analytic.nb_step_grads(P, FR, x, z["covar"][cells].astype(np.float64),
                                      z["s0/eps_mu"].astype(np.float64), z["s0/eps_nu"].astype(np.float64),
-                                     float(z["s0/beta"]))
+                                     float(z["s0/beta"]), relu=relu_of(z))
     assert abs(L - float(z["s0/loss"])) / abs(L) < 1e-5
     for k in nb_oracle.param_names():
         want = z[f"s0/grad/{k}"].astype(np.float64).ravel()

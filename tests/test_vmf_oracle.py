@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import dims, golden_files, load, params_of
+from helpers import dims, golden_files, load, params_of, relu_of
 from oracle import synth, vmf_analytic, vmf_oracle
 
 VMF_FILES = golden_files("vmf_")
@@ -27,7 +27,7 @@ def test_vmf_oracle_reproduces_golden(path):
     d = dims(z)
     torch.set_num_threads(1)
     tr = vmf_oracle.VMFTrainer({k: torch.from_numpy(v) for k, v in params_of(z, "init/").items()},
-                               {k: torch.from_numpy(v) for k, v in params_of(z, "frozen/").items()})
+                               {k: torch.from_numpy(v) for k, v in params_of(z, "frozen/").items()}, relu=relu_of(z))
     for t in range(int(z["steps"])):
         cells = z[f"s{t}/cells"]
         x = torch.from_numpy(synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]))
@@ -51,11 +51,11 @@ def test_vmf_kernel_algebra_equals_autograd_f64(path):
     c = torch.from_numpy(z["covar"][cells].astype(np.float64))
     eps = torch.from_numpy(z["s1/eps_mu"].astype(np.float64))
     beta = float(z["s1/beta"])
-    m = vmf_oracle.VMFModel(P, FR)
+    m = vmf_oracle.VMFModel(P, FR, relu=relu_of(z))
     L = vmf_oracle.vmf_vae_loss(x, m.forward(x, c, eps, True), beta)
     L.backward()
     La, G = vmf_analytic.vmf_step_grads({k: v.numpy() for k, v in P.items()}, {k: v.numpy() for k, v in FR.items()},
-                                        x.numpy(), c.numpy(), eps.numpy(), beta)
+                                        x.numpy(), c.numpy(), eps.numpy(), beta, relu=relu_of(z))
     assert abs(La - float(L.detach())) <= 1e-7 * abs(La)
     for k, t in m.p.items():
         g = t.grad.numpy().ravel()
@@ -72,7 +72,7 @@ def test_vmf_kernel_algebra_matches_golden_fp32(path):
     cells = z["s0/cells"]
     x = synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]).astype(np.float64)
     L, G = vmf_analytic.vmf_step_grads(P, FR, x, z["covar"][cells].astype(np.float64),
-                                       z["s0/eps_mu"].astype(np.float64), float(z["s0/beta"]))
+                                       z["s0/eps_mu"].astype(np.float64), float(z["s0/beta"]), relu=relu_of(z))
     assert abs(L - float(z["s0/loss"])) <= 1e-5 * abs(L)
     for k in vmf_oracle.param_names():
         want = z[f"s0/grad/{k}"].astype(np.float64).ravel()
