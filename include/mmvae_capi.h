@@ -38,8 +38,13 @@ enum {
 
 enum { MMVAE_MODEL_NB = 0, MMVAE_MODEL_VMF = 1 };
 /* Operand precision of the encoder/decoder GEMMs; every epilogue, reduction, gradient and
- * optimiser update is fp32.  F32 is the parity mode (exact f32 MFMA). */
-enum { MMVAE_DTYPE_F32 = 0, MMVAE_DTYPE_BF16 = 1 };
+ * optimiser update is fp32.
+ *   F32     exact f32 MFMA (v_mfma_f32_16x16x4_f32): bitwise an fp32 FMA chain.
+ *   BF16    bf16 operands, f32 accumulate (loss within ~2e-3 of fp32).
+ *   BF16X3  fp32-accurate split operands: v = hi + lo (two bf16), each product accumulated in f32
+ *           as lo*hi + hi*lo + hi*hi on the bf16 MFMA (relative product error <= ~2^-16), at a
+ *           fraction of the f32 MFMA's cost — the parity-grade production mode. */
+enum { MMVAE_DTYPE_F32 = 0, MMVAE_DTYPE_BF16 = 1, MMVAE_DTYPE_BF16X3 = 2 };
 
 typedef struct mmvae_cfg {
     int32_t model;       /* MMVAE_MODEL_NB (src/nb_vae_main.cc) / MMVAE_MODEL_VMF (src/vmf_vae_main.cc) */

@@ -49,6 +49,16 @@ void mmvae_free(void* p);
 /* The all-ones covariate file the CLIs write when --covar is absent
  * (create_ones_like, mmvae_io.hh:292-310): a 1 x N gzip MatrixMarket. */
 int mmvae_mtx_write_ones(const char* path, int64_t N);
+/* ${mtx}.index (build_mmutil_index, mmutil_index.hh:138-190): for a column-sorted BGZF
+ * MatrixMarket file, the BGZF virtual offset of every column's first line as gzip text
+ * "col voff" lines (0-based columns).  index_file NULL or "" -> mtx + ".index".  An existing
+ * index is kept.  Errors as the reference: not BGZF, columns not sorted, last column missing. */
+int mmvae_mtx_build_index(const char* mtx, const char* index_file);
+/* read_mmutil_index (mmutil_index.hh:192-228): *voff [max col + 1] (free with mmvae_free),
+ * missing columns back-filled with the next column's offset. */
+int mmvae_mtx_read_index(const char* index_file, int64_t** voff, int64_t* ncol);
+/* A cell-major CSR as a genes x cells BGZF MatrixMarket file, sorted by cell (bench / tests). */
+int mmvae_mtx_write_csr(const char* path, const mmvae_csr* csr);
 const char* mmvae_host_last_error(void);
 
 /* ---- training driver (mmvae_alg.hh:200-333) ---------------------------------------------- */

@@ -184,8 +184,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
         cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
-    if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16)
-        FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32 or BF16");
+    if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16 && cfg->dtype != MMVAE_DTYPE_BF16X3)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32, BF16 or BF16X3");
     if (cfg->n_enc_hidden < 0 || cfg->n_enc_hidden > 4 || cfg->n_dec_hidden < 0 || cfg->n_dec_hidden > 4)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "at most 4 hidden encoder / decoder layers");
     // nb.hh:334-337 pushes a hidden encoder Linear and its ReLU under the same name: LibTorch
@@ -237,11 +237,17 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // NB pass B holds ~150 KB of LDS per 8-wave workgroup (2 x 4-wave per CU); the vMF decoder
     // fits 4 (16 splits 46 + 71 us vs 12 splits 51 + 74 us); the shared encoder kernels (~37 KB, <= 104 VGPRs in bf16) fit 4 (measured at 64 row
     // blocks: 16 splits 58 + 31 us, 12 splits 62 + 34 us, 24 splits 61 + 36 us)
+    // Resident 4-wave workgroups per CU by mode (LDS / VGPR budgets of the kernels, see
+    // tools/resource_usage.py): bf16 operand tiles are the smallest; the x3 mode stages hi + lo
+    // images and f32 four-byte elements, so both fit half as many (NB pass B: bf16 and x3 run one
+    // 8-wave workgroup per CU = 2 units; f32 one 4-wave workgroup)
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
-    e->nsplit_d = pick_split(vmf_model ? 4 : 2);
+    const bool bf_ops = cfg->dtype == MMVAE_DTYPE_BF16;
+    const int dec_cu = vmf_model ? (bf_ops ? 4 : 2) : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
+    e->nsplit_d = pick_split(dec_cu);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
-    e->nsplit_e = pick_split(4);
+    e->nsplit_e = pick_split(bf_ops ? 4 : 2);
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
     auto env_split = [&](const char* name, int& v) {
         if (const char* ev = std::getenv(name)) {
@@ -284,13 +290,13 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipMemset(e->d_v, 0, sizeof(float) * e->P_reg));
     HIPCHK(e, hipMemset(e->d_frozen, 0, sizeof(float) * e->P_frz));
     HIPCHK(e, dalloc(&e->d_WeP_f, KP * DP));
-    HIPCHK(e, dalloc(&e->d_WeP_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WeP_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WdP_f, KP * DP));
-    HIPCHK(e, dalloc(&e->d_WdP_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdP_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WdT_f, KP * DP));
-    HIPCHK(e, dalloc(&e->d_WdT_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WdT_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WeS_f, KP * DP));
-    HIPCHK(e, dalloc(&e->d_WeS_b, KP * DP));
+    HIPCHK(e, dalloc(&e->d_WeS_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     // per-step host->device staging in ONE pinned block and ONE device block, so a step issues a
     // single H2D copy (each copy is a ~4.5 us blit on the stream):  cells int64 [Bp] |
     // list segments int64 [Bp/16 + 1] | balancing permutation int32 [Bp]
@@ -311,14 +317,14 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_hpart, (int64_t)e->nsplit_e * Bp * KP));
     HIPCHK(e, dalloc(&e->d_lat, Bp * e->lat_stride));
     HIPCHK(e, dalloc(&e->d_zf, Bp * KP));
-    HIPCHK(e, dalloc(&e->d_zb, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_zb, 2 * Bp * KP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_a * Bp * 2));
     HIPCHK(e, dalloc(&e->d_rowB, (int64_t)e->nsplit_d * Bp * (2 + e->R)));
     HIPCHK(e, dalloc(&e->d_rowfin, Bp * 2));
     HIPCHK(e, dalloc(&e->d_dzp, (int64_t)e->nsplit_d * Bp * 2 * KP));
     HIPCHK(e, dalloc(&e->d_dh, Bp * KP));
     HIPCHK(e, dalloc(&e->d_dhT_f, Bp * KP));
-    HIPCHK(e, dalloc(&e->d_dhT_b, Bp * KP));
+    HIPCHK(e, dalloc(&e->d_dhT_b, 2 * Bp * KP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_slabB, nrb * ((1 + e->C) + 1 + e->R) * DP));
     HIPCHK(e, dalloc(&e->d_slabC, nrb * (1 + e->C) * DP));
     HIPCHK(e, dalloc(&e->d_slabE, nrb * (2 + e->H) * DP));

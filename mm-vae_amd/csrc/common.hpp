@@ -17,10 +17,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------------------------------
 template <class T> struct MM;
 
+// Split-bf16 operands ("x3", the fp32-accurate mode): every GEMM operand v is held as two bf16
+// planes hi = bf16(v), lo = bf16(v - hi) (|v - hi - lo| <= 2^-16 |v|), and a product is
+// accumulated in f32 as lo*hi + hi*lo + hi*hi — three bf16 MFMAs (16x16x32: 16 cycles each)
+// for the 8 cycles-per-4-k of the exact f32 MFMA (16x16x4: 32 cycles per 4 k).  The lo planes
+// sit at a constant element offset `plane` from the hi planes in HBM and LDS.
+struct X3 {};
+template <class P> struct Elem { typedef P type; };   // storage element of an operand plane
+template <> struct Elem<X3> { typedef __bf16 type; };
+template <class P> struct IsX3 { static constexpr bool value = false; };
+template <> struct IsX3<X3> { static constexpr bool value = true; };
+
 template <> struct MM<float> {
     static constexpr int KSTEP = 4, EPL = 1;
     typedef float frag;
     static MMVAE_DEV frag load(const float* p) { return *p; }
+    static MMVAE_DEV frag load(const float* p, int64_t) { return *p; }
     static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
     }
@@ -32,6 +44,7 @@ template <> struct MM<__bf16> {
     static constexpr int KSTEP = 32, EPL = 8;
     typedef bf16x8 frag;
     static MMVAE_DEV frag load(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+    static MMVAE_DEV frag load(const __bf16* p, int64_t) { return *reinterpret_cast<const bf16x8*>(p); }
     static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
     }
@@ -48,6 +61,44 @@ template <> struct MM<__bf16> {
         frag z;
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
+        return z;
+    }
+};
+
+// hi / lo split of one f32 (round-to-nearest-even bf16, v_cvt_pk_bf16_f32)
+MMVAE_DEV __bf16 bf_hi(float v) { return (__bf16)v; }
+MMVAE_DEV __bf16 bf_lo(float v, __bf16 hi) { return (__bf16)(v - (float)hi); }
+
+template <> struct MM<X3> {
+    static constexpr int KSTEP = 32, EPL = 8;
+    struct frag {
+        bf16x8 h, l;
+    };
+    static MMVAE_DEV frag load(const __bf16* p, int64_t plane) {
+        return frag{*reinterpret_cast<const bf16x8*>(p), *reinterpret_cast<const bf16x8*>(p + plane)};
+    }
+    static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+    }
+    // 8 consecutive f32 (16-byte aligned) -> split fragment
+    static MMVAE_DEV frag load_f32(const float* p) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        frag f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            f.h[i] = bf_hi(v[i]);
+            f.l[i] = bf_lo(v[i], f.h[i]);
+        }
+        return f;
+    }
+    static MMVAE_DEV frag zero() {
+        frag z;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z.h[i] = z.l[i] = (__bf16)0.f;
         return z;
     }
 };

@@ -19,9 +19,11 @@ namespace mmvae {
 // =======================================================================================
 struct EncBwdLds {
     int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, bytes;
-    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc) {
-        o_lt = KP * 64 * esz;
-        o_raw = o_lt + 64 * LS * esz;
+    // wsz: element size of the staged W image (f32 in the x3 mode: W only feeds a VALU dot);
+    // planes: operand planes of the log1p tile (x3: hi + lo)
+    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes) {
+        o_lt = KP * 64 * wsz;
+        o_raw = o_lt + planes * 64 * LS * esz;
         o_part = o_raw + 64 * 68 * 4;
         o_scal = o_part + 4 * 64 * 4;
         o_wave = o_scal + nsc * 64 * 4;
@@ -30,15 +32,24 @@ struct EncBwdLds {
     }
 };
 
-template <class T, int KP, bool H1, bool RAW>
+// staged encoder weight of the backward's VALU dot: the GEMM element type, f32 in the x3 mode
+template <class P> struct WEnc { typedef typename Elem<P>::type type; };
+template <> struct WEnc<X3> { typedef float type; };
+
+template <class P, int KP, bool H1, bool RAW>
 MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                             const int32_t* __restrict__ toff, const float* __restrict__ lat,
-                            const T* __restrict__ dhT, const T* __restrict__ WeP,
+                            const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
+                            const typename WEnc<P>::type* __restrict__ WeP,
                             const Dims& d, float* __restrict__ slabE, const int bid) {
-    using M = MM<T>;
+    using T = typename Elem<P>::type;
+    using WT = typename WEnc<P>::type;
+    using M = MM<P>;
     using Fr = typename M::frag;
+    constexpr bool X = IsX3<P>::value;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // log1p tile row (gene) stride, elements
-    constexpr int RB = 64 * (int)sizeof(T);        // staged W_enc row (one latent, 64 genes)
+    constexpr int LT = 64 * LS;                    // elements of one log1p tile plane
+    constexpr int RB = 64 * (int)sizeof(WT);       // staged W_enc row (one latent, 64 genes)
     constexpr int HN = H1 ? 1 : HMAX;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -48,7 +59,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     const int S = d.tpsE + 1;
     const int H = H1 ? 1 : d.H;
     const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
-    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN);
+    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1);
     char* wst = smem;
     T* lt = reinterpret_cast<T*>(smem + L.o_lt);          // [64 genes][LS]  log1p(x)
     float* raw = reinterpret_cast<float*>(smem + L.o_raw);  // [64 genes][68] x
@@ -57,15 +68,15 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_wave + w * L.wave_bytes);  // [S] tile offsets
     // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
     RegStage<KP, RB> wreg;
-    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(T); };
-    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
+    auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(WT); };
+    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(WT));
     const int lb = w;  // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
     constexpr int KSB = 64 / M::KSTEP;
     Fr afr[KSB];
 #pragma unroll
     for (int s = 0; s < KSB; ++s)  // unconditional (clamped) loads; blocks past KP zeroed below
         afr[s] = M::load(&dhT[(int64_t)(16 * min(lb, KP / 16 - 1) + (lane & 15)) * d.Bpad + rb * 64 + s * M::KSTEP +
-                              (lane >> 4) * M::EPL]);
+                              (lane >> 4) * M::EPL], dplane);
 
     const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
     fill_toffl(toffl, S, t0, d.NT, toff, wbk, lane);
@@ -81,14 +92,16 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     auto zero_cols = [&]() {
         constexpr int CB = 16 * (int)sizeof(T) / 16;
 #pragma unroll
-        for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(lt + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
+        for (int pl = 0; pl < (X ? 2 : 1); ++pl)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) reinterpret_cast<uint4*>(lt + pl * LT + lane * LS + 16 * w)[c] = uint4{0, 0, 0, 0};
         if (RAW)
 #pragma unroll
             for (int c = 0; c < 4; ++c) reinterpret_cast<uint4*>(raw + lane * 68 + 16 * w)[c] = uint4{0, 0, 0, 0};
     };
     auto scatter = [&](const ListEntries& le) {
         le.visit(ents, lane, [&](int r, int gl, float x) {
-            lt[gl * LS + 16 * w + r] = to_t<T>(log1p_cnt<T>(x));
+            put_op<P>(lt, gl * LS + 16 * w + r, LT, log1p_cnt<P>(x));
             if (RAW) raw[gl * 68 + 16 * w + r] = x;
         });
     };
@@ -111,7 +124,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     lds_barrier();
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
-        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
+        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(WT));
         // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
         if (RAW) {
             const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
@@ -138,7 +151,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
                 f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KSB; ++s) {
-                    const Fr bx = *reinterpret_cast<const Fr*>(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                    const Fr bx = M::load(&lt[(16 * gb + (lane & 15)) * LS + s * M::KSTEP + (lane >> 4) * M::EPL], LT);
                     acc = M::mma(afr[s], bx, acc);
                 }
                 const int gl = 16 * gb + (lane & 15);
@@ -146,7 +159,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * lb + 4 * (lane >> 4) + r;
-                    v = fmaf(static_cast<float>(*reinterpret_cast<const T*>(wst + swz_off<RB>(k, gl * (int)sizeof(T)))), acc[r], v);
+                    v = fmaf(static_cast<float>(*reinterpret_cast<const WT*>(wst + swz_off<RB>(k, gl * (int)sizeof(WT)))), acc[r], v);
                 }
                 v = sum_rowgroups(v);
                 if (lane < 16) part[w * 64 + gl] = v;
@@ -171,10 +184,12 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     }
 }
 
-template <class T, int KP>
+template <class P, int KP>
 inline size_t enc_bwd_lds(const Dims& d) {
+    using T = typename Elem<P>::type;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX)).bytes;
+    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX),
+                             (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1).bytes;
 }
 
 }  // namespace mmvae

@@ -7,7 +7,10 @@
 #include <string>
 #include <vector>
 
+#include <type_traits>
+
 #include "../../include/mmvae_capi.h"
+#include "common.hpp"
 
 namespace mmvae {
 
@@ -199,9 +202,25 @@ hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float bet
 hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
-hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart);
+hipError_t enc_forward_launch(Engine* e, const Dims& d, float* hpart);
 hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const float* Wne, float* rowdots);
-hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab);
+
+// Instantiate f(operand mode, latent padding) for the handle's dtype and KP: the mode is float
+// (exact f32 MFMA), __bf16 (bf16 operands) or X3 (split-bf16, fp32-accurate products).
+template <class F>
+hipError_t dispatch_mode(const Engine* e, F&& f) {
+    using K32 = std::integral_constant<int, 32>;
+    using K64 = std::integral_constant<int, 64>;
+    const int dt = e->cfg.dtype;
+    if (e->KP == 32) {
+        if (dt == MMVAE_DTYPE_BF16) return f(__bf16{}, K32{});
+        if (dt == MMVAE_DTYPE_BF16X3) return f(X3{}, K32{});
+        return f(float{}, K32{});
+    }
+    if (dt == MMVAE_DTYPE_BF16) return f(__bf16{}, K64{});
+    if (dt == MMVAE_DTYPE_BF16X3) return f(X3{}, K64{});
+    return f(float{}, K64{});
+}
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);

@@ -86,8 +86,8 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
     for (int kk = 0; kk < 8; ++kk) {
         const int k = blockIdx.y * 8 + kk;
         const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
-        if (in) {
-            if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+        if (in) {  // bf16 image: hi plane, and the x3 mode's lo plane KP * DP elements after it
+            if (WeS_b) put_op<X3>(WeS_b, (int)((int64_t)k * d.DP + g), d.KP * d.DP, ws);
             else WeS_f[(int64_t)k * d.DP + g] = ws;
         }
         mp[kk] = xmv * ws;  // x_mean_g / sd_g * W_enc[k, g]
@@ -105,16 +105,21 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // dots of depth / nu_enc, nb.hh:448, 498, are taken by k_batch_lists, which visits every entry
 // with its row known.)
 // =======================================================================================
-template <class T, int KP>
+template <class P, int KP>
 __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
-                                                 const int32_t* __restrict__ toff, const T* __restrict__ WeS, Dims d,
+                                                 const int32_t* __restrict__ toff,
+                                                 const typename Elem<P>::type* __restrict__ WeS, int64_t wplane, Dims d,
                                                  float* __restrict__ hpart) {
-    using M = MM<T>;
+    using T = typename Elem<P>::type;
+    using M = MM<P>;
     using Fr = typename M::frag;
+    constexpr bool X = IsX3<P>::value;
+    constexpr int NPL = X ? 2 : 1;                 // operand planes (x3: hi + lo)
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;   // x tile row stride (elements): conflict-free
     constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
     constexpr int STB = KP * RB;
-    constexpr int XB = 2 * 16 * XS * (int)sizeof(T);  // per wave: two x tiles
+    constexpr int XT = 16 * XS;                    // elements of one x tile plane
+    constexpr int XB = 2 * NPL * XT * (int)sizeof(T);  // per wave: two x tiles [hi 0][hi 1][lo 0][lo 1]
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t t_entry = (d.dbg & 32) ? stamp_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -122,22 +127,28 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const EncLds L(KP, (int)sizeof(T), S, XB, 0);
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL);
     char* wst = smem;
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
     int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_toff) + w * S;
 
-    RegStage<KP, RB> wreg;
+    DualStage<KP, RB, 256, X> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
     // prologue loads with no dependence on the lists go out first (W tile t0)
-    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T));
+    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
     const int wbk = row0 >> 4;
     fill_toffl(toffl, S, t0, d.NT, toff, wbk, lane);
     const int64_t segw = seg[wbk];
-    for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xt)[i] = uint4{0, 0, 0, 0};
+    auto zero_tile = [&](T* x0) {
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+            for (int i = lane; i < XT * (int)sizeof(T) / 16; i += 64)
+                reinterpret_cast<uint4*>(x0 + pl * 2 * XT)[i] = uint4{0, 0, 0, 0};
+    };
+    zero_tile(xt);
     wave_sync();
     auto scatter = [&](const ListEntries& le, T* dst) {
-        le.visit(ents, lane, [&](int r, int gl, float x) { dst[r * XS + gl] = to_t<T>(log1p_cnt<T>(x)); });
+        le.visit(ents, lane, [&](int r, int gl, float x) { put_op<P>(dst, r * XS + gl, 2 * XT, log1p_cnt<P>(x)); });
     };
 
     f32x4 acc[KP / 16];
@@ -152,7 +163,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
         first.fetch(ents, segw, toffl, 0, lane);
 #pragma unroll
         for (int i = 0; i < EDEPTH; ++i) q[i].fetch(ents, segw, toffl, min(1 + i, nt - 1), lane);
-        wreg.store(wst);
+        wreg.store(wst, 2 * STB);
         scatter(first, xt);
     }
     lds_barrier();
@@ -168,22 +179,23 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0, buf = tl & 1;
         // unconditional (clamped) prefetch of the next weight tile: counted vmcnt waits
-        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T));
-        const T* xb = xt + buf * 16 * XS;
+        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
+        const T* xb = xt + buf * XT;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
-            const Fr a = *reinterpret_cast<const Fr*>(&xb[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+            const Fr a = M::load(&xb[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL], 2 * XT);
 #pragma unroll
             for (int lb = 0; lb < KP / 16; ++lb) {
-                const Fr bw = *reinterpret_cast<const Fr*>(
-                    wst + buf * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                const Fr bw = M::load(reinterpret_cast<const T*>(
+                    wst + buf * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                    2 * STB / (int)sizeof(T));
                 acc[lb] = M::mma(a, bw, acc[lb]);
             }
         }
         lap(sa);
-        T* xn = xt + (buf ^ 1) * 16 * XS;
+        T* xn = xt + (buf ^ 1) * XT;
         if (t + 1 < t1) {
-            for (int i = lane; i < 16 * XS * (int)sizeof(T) / 16; i += 64) reinterpret_cast<uint4*>(xn)[i] = uint4{0, 0, 0, 0};
+            zero_tile(xn);
             wave_sync();
             scatter(q[0], xn);
         }
@@ -192,7 +204,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
 #pragma unroll
         for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
         q[EDEPTH - 1].fetch(ents, segw, toffl, min(tl + 1 + EDEPTH, nt - 1), lane);
-        if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB);
+        if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB, 2 * STB);
         lap(sc);
         lds_barrier();
         lap(sd);
@@ -347,7 +359,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         if (k < d.KP) {
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
-            zb[(int64_t)b * d.KP + k] = (__bf16)zz;
+            put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
         }
         // ---- overdispersion latent (lanes r < R) ----
         const float* rx = &sRX[4 * w + c][0];  // [0] = depth pre-activation, [1 + h] = nu_enc_h
@@ -428,6 +440,8 @@ struct DecPtrs {
     const uint2* ents;     // per-step batch entry lists (batch.hip)
     const int64_t* seg;    // [Bpad/16 + 1]
     const int32_t* toff;   // [Bpad/16][NT+1]
+    int64_t zplane;        // x3 mode: element offset of the lo plane of zb
+    int64_t wplane;        // x3 mode: element offset of the lo planes of WdP / WdT
 };
 
 // Passes A and C: each tile's decoder rows + gene records are staged ONCE per workgroup into
@@ -435,14 +449,18 @@ struct DecPtrs {
 // owns 32 rows (two 16-row MFMA blocks), so every W fragment read from LDS feeds two MFMAs.
 // Workgroup = 128 rows x one gene split.
 static constexpr int AC_RPW = 2;  // 16-row MFMA blocks per wave
-template <class T, int KP, int PASS, int CM>
+template <class P, int KP, int PASS, int CM>
 MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
-    using M = MM<T>;
+    using T = typename Elem<P>::type;
+    using M = MM<P>;
     using Fr = typename M::frag;
+    constexpr bool X = IsX3<P>::value;
+    constexpr int NPL = X ? 2 : 1;
     constexpr int KS = KP / M::KSTEP;
     constexpr bool BF = sizeof(T) == 2;
     constexpr int RB = KP * (int)sizeof(T);  // bytes per staged gene row
-    constexpr int STB = 64 * RB + 1024;      // one stage buffer: W tile + grec tile
+    constexpr int WIMG = 64 * RB;            // one W image plane
+    constexpr int STB = NPL * WIMG + 1024;   // one stage buffer: W tile (hi [+ lo]) + grec tile
     constexpr int J = AC_RPW;
     constexpr int WR = 16 * J;               // rows per wave
     constexpr float L2E = 1.4426950408889634f;
@@ -477,7 +495,8 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     for (int j = 0; j < J; ++j)
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            zfr[j][s] = M::load(&Z[(int64_t)(row0 + 16 * j + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+            zfr[j][s] = M::load(&Z[(int64_t)(row0 + 16 * j + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL],
+                                Q.zplane);
     float lse2[J][4], wE[J][4], crow[J][4][CM], mrun[J][4], srun[J][4];
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -496,15 +515,16 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     // Register-staged decoder tiles, two in flight: tile t + 2 is loaded while tile t is
     // computed from LDS, tile t + 1 (loaded an iteration earlier) is written to the other LDS
     // buffer at the end — one LDS barrier per tile, no vmcnt(0) drain of a fresh DMA.
-    RegStage<64, RB> wrA, wrB;
+    using WStage = DualStage<64, RB, 256, X>;
+    WStage wrA, wrB;
     float4 grA = float4{0.f, 0.f, 0.f, 0.f}, grB = grA;
-    auto ld = [&](RegStage<64, RB>& R, float4& G, int t) {
-        R.load(WdPc + (int64_t)64 * t * RB, RB);
+    auto ld = [&](WStage& R, float4& G, int t) {
+        R.load(WdPc + (int64_t)64 * t * RB, RB, Q.wplane * (int64_t)sizeof(T));
         if (threadIdx.x < 64) G = grec[64 * t + threadIdx.x];
     };
-    auto st = [&](const RegStage<64, RB>& R, const float4& G, int buf) {
-        R.store(stg + buf * STB);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(stg + buf * STB + 64 * RB)[threadIdx.x] = G;
+    auto st = [&](const WStage& R, const float4& G, int buf) {
+        R.store(stg + buf * STB, WIMG);
+        if (threadIdx.x < 64) reinterpret_cast<float4*>(stg + buf * STB + NPL * WIMG)[threadIdx.x] = G;
     };
     // diagnostic (MMVAE_DBG & 256): per-wave phase cycles into slabC (outputs invalid)
     const bool stamps = (d.dbg & 256) != 0;
@@ -516,7 +536,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             tp_ = tn;
         }
     };
-    auto tile = [&](int t, RegStage<64, RB>& hold, float4& ghold, RegStage<64, RB>& nxt, float4& gnxt) {
+    auto tile = [&](int t, WStage& hold, float4& ghold, WStage& nxt, float4& gnxt) {
         const int buf = (t - t0) & 1;
         ld(nxt, gnxt, min(t + 2, t1 - 1));  // unconditional (clamped): counted waits
         const char* sb = stg + buf * STB;
@@ -531,7 +551,8 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 for (int j = 0; j < J; ++j) acc[gb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KS; ++s) {
-                    const Fr bw = *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                    const Fr bw = M::load(reinterpret_cast<const T*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                                          WIMG / (int)sizeof(T));
 #pragma unroll
                     for (int j = 0; j < J; ++j) acc[gb][j] = M::mma(zfr[j][s], bw, acc[gb][j]);
                 }
@@ -540,7 +561,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 #pragma unroll
             for (int gb = 0; gb < 4; ++gb) {
                 const int gl = 16 * gb + (lane & 15);
-                const float4 g4 = reinterpret_cast<const float4*>(sb + 64 * RB)[gl];
+                const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
                 b2[gb] = g4.x * L2E;  // padded genes: -inf
                 w2[gb][0] = g4.z * L2E;
 #pragma unroll
@@ -575,11 +596,12 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             for (int j = 0; j < J; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                const Fr bw = *reinterpret_cast<const Fr*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                const Fr bw = M::load(reinterpret_cast<const T*>(sb + swz_off<RB>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                                      WIMG / (int)sizeof(T));
 #pragma unroll
                 for (int j = 0; j < J; ++j) acc[j] = M::mma(zfr[j][s], bw, acc[j]);
             }
-            const float4 g4 = reinterpret_cast<const float4*>(sb + 64 * RB)[gl];
+            const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
             float wcd[CM];
             wcd[0] = g4.z;
 #pragma unroll
@@ -678,10 +700,10 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 }
 
 // distinct kernel names per pass (profiles): A = log-sum-exp, C = the E_b P column term
-template <class T, int KP, int CM>
-__global__ __launch_bounds__(256, 2) void k_dec_lse(DecPtrs Q, Dims d) { dec_ac_body<T, KP, 0, CM>(Q, d); }
-template <class T, int KP, int CM>
-__global__ __launch_bounds__(256, 2) void k_dec_tail(DecPtrs Q, Dims d) { dec_ac_body<T, KP, 2, CM>(Q, d); }
+template <class P, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_dec_lse(DecPtrs Q, Dims d) { dec_ac_body<P, KP, 0, CM>(Q, d); }
+template <class P, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_dec_tail(DecPtrs Q, Dims d) { dec_ac_body<P, KP, 2, CM>(Q, d); }
 
 // =======================================================================================
 // k_dec_nb<T, KP, CM, RM> — decoder pass B: softmax + NB likelihood + every gradient term
@@ -708,6 +730,7 @@ template <> struct CorrPair<float> {
     static MMVAE_DEV type pack(float a, float b) { return float2{a, b}; }
     static MMVAE_DEV void unpack(type v, float& a, float& b) { a = v.x; b = v.y; }
 };
+template <> struct CorrPair<X3> : CorrPair<float> {};  // x3 mode: f32 corrections
 template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to bf16
     typedef uint32_t type;
     static MMVAE_DEV type pack(float a, float b) {
@@ -725,21 +748,32 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
 // the same barriers (two co-resident 4-wave workgroups drift apart under the oldest-first
 // issue arbitration and the younger one finishes alone at half occupancy), and the staged
 // decoder tiles serve 128 rows instead of 64.  NW = 4 (64 rows, two workgroups per CU) otherwise.
+// x3 mode (ALIAS): the dz GEMM's pq operand (hi + lo planes, 4 bytes per element) lives inside
+// the wave's correction tile, laid out by 16-gene block: block gb of the correction tile is
+// [16 rows][16 genes] f32 pairs (2 KB), its first 1 KB holds pq's [16][16] hi plane then lo
+// plane.  The epilogue reads all of a block's corrections before it writes that block's pq, and
+// the tile is re-zeroed after the dz GEMM has read pq — saving the separate 4.6 KB pq tile per
+// wave that would not fit 8 waves of x3 images in 160 KB.
 struct DecNBLds {
-    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q2, o_cc, o_toff, o_rsc, bytes;
-    int sw, st, sp;  // per-buffer strides: W tile, WdT tile (bytes), column partials (floats)
-    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW) {
-        const int nbuf = NW == 8 ? 2 : 1;  // double-buffered stage + partials: one barrier per tile
-        sw = 64 * KP * esz;
-        st = KP * 64 * esz;
+    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
+    int sw, st, sp;     // per-buffer strides: W tile, WdT tile (bytes, all planes), column partials (floats)
+    int swp, stp;       // one plane of the W / WdT images (bytes)
+    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes) {
+        const bool alias = planes == 2;
+        swp = 64 * KP * esz;
+        stp = KP * 64 * esz;
+        sw = planes * swp;
+        st = planes * stp;
         sp = ((NW * nq * 64 * 4 + 15) / 16) * 4;
         o_gst = nbuf * sw;
         o_tst = o_gst + nbuf * 1024;
         o_part = o_tst + nbuf * st;
         o_wave = o_part + nbuf * sp * 4;
         const int QS = 64 + (esz == 2 ? 8 : 4);
-        o_q2 = 16 * QS * esz;
+        o_q1 = 0;
+        o_q2 = alias ? 0 : 16 * QS * esz;
         o_cc = o_q2 + 16 * 68 * 4;
+        if (alias) o_q1 = o_cc;
         o_toff = o_cc + 16 * 64 * csz;
         o_rsc = o_toff + ((S * 4 + 15) / 16) * 16;
         wave_bytes = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
@@ -747,16 +781,23 @@ struct DecNBLds {
     }
 };
 
-template <class T, int KP, int CM, int RM, int NW>
+template <class P, int KP, int CM, int RM, int NW, bool DB>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
-    using M = MM<T>;
+    using T = typename Elem<P>::type;
+    using M = MM<P>;
     using Fr = typename M::frag;
-    using CP = CorrPair<T>;
+    using CP = CorrPair<P>;
     typedef typename CP::type CT;
+    constexpr bool X = IsX3<P>::value;  // x3: split operands, pq aliased into the correction tile
+    constexpr int NPL = X ? 2 : 1;
     constexpr int KS = KP / M::KSTEP;   // k-steps of the logit GEMM
     constexpr int GK = 64 / M::KSTEP;   // k-steps of the dz GEMM over a 64-gene tile
     constexpr bool BF = sizeof(T) == 2;
     constexpr int QS = 64 + (BF ? 8 : 4);
+    // pq (dz GEMM operand) element (r, g) and its lo-plane offset; the correction tile's (r, g)
+    auto q1i = [](int r, int g) { return X ? ((g >> 4) * 1024 + r * 16 + (g & 15)) : r * QS + g; };
+    constexpr int Q1PL = 256;
+    auto cci = [](int r, int g) { return X ? ((g >> 4) * 256 + r * 16 + (g & 15)) : r * 64 + g; };
     constexpr int PS = 68;
     constexpr int NRS = 3 + RM + CM;    // row scalars: d, w, valid, znu[R], c[C]
     constexpr int RBW = KP * (int)sizeof(T);  // staged decoder row (one gene)
@@ -771,13 +812,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW);
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
     float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][nq][64]
     char* wp = smem + L.o_wave + w * L.wave_bytes;
-    T* q1 = reinterpret_cast<T*>(wp);
+    T* q1 = reinterpret_cast<T*>(wp + L.o_q1);
     float* q2 = reinterpret_cast<float*>(wp + L.o_q2);
     CT* cc = reinterpret_cast<CT*>(wp + L.o_cc);
     int32_t* toffl = reinterpret_cast<int32_t*>(wp + L.o_toff);
@@ -791,19 +832,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     Fr zfr[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL], Q.zplane);
     // ---- staging of the decoder tile, its gene records and the WdT tile ----
-    RegStage<64, RBW, NTH> wreg;
-    RegStage<KP, RBT, NTH> treg;
+    DualStage<64, RBW, NTH, X> wreg;
+    DualStage<KP, RBT, NTH, X> treg;
     float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
-        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
-        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
+        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
     auto stage_store = [&](int b_) {
-        wreg.store(wst + b_ * L.sw);
-        treg.store(tst + b_ * L.st);
+        wreg.store(wst + b_ * L.sw, L.swp);
+        treg.store(tst + b_ * L.st, L.stp);
         if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
@@ -904,7 +946,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
         stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
-        constexpr bool DB = NW == 8;
         const int buf = DB ? (tl & 1) : 0;
         const char* wsb = wst + buf * L.sw;
         const char* tsb = tst + buf * L.st;
@@ -917,7 +958,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wsb + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+                acc = M::mma(zfr[s], M::load(reinterpret_cast<const T*>(wsb + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), L.swp / (int)sizeof(T)), acc);
             const float4 g4 = gsb[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -958,7 +999,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             lossacc += x * (flog(sv) - flog(mu)) + lgd;                 // nb.hh:527
             const float dq = x * rsv - x * frcp(mu);
             const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
-            cc[r * 64 + gl] = CP::pack(p * dq, ddu);
+            cc[cci(r, gl)] = CP::pack(p * dq, ddu);
         });
         wave_sync();
         lap(1);
@@ -989,6 +1030,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                 for (int c = 0; c < 1 + CM; ++c) cs1[c] = splat2(0.f);
 #pragma unroll
                 for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
+                // the block's corrections first (x3: this block's pq overwrites them below)
+                CT ccv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ccv[r] = cc[cci(4 * (lane >> 4) + r, gl)];
+                if constexpr (X) asm volatile("" ::: "memory");
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
                     const int rl = 4 * (lane >> 4) + 2 * h;
@@ -1007,8 +1053,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                         lossd2 = fma2(nup, lg2, lossd2);
                     }
                     float cpa, cda, cpb, cdb;
-                    CP::unpack(cc[rl * 64 + gl], cpa, cda);
-                    CP::unpack(cc[(rl + 1) * 64 + gl], cpb, cdb);
+                    CP::unpack(ccv[2 * h], cpa, cda);
+                    CP::unpack(ccv[2 * h + 1], cpb, cdb);
                     const f2 pq = fma2(p, qv, f2{cpa, cpb});                     // qv = n dL/dmu' - 1 at x = 0
                     const f2 du = fma2(fma2(lg2, splat2(LN2), qv), sgm, f2{cda, cdb});
                     Eacc2[h] += pq;
@@ -1021,8 +1067,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                         csduz[qq] = fma2(du, znu2[h][qq], csduz[qq]);
                         dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                     }
-                    q1[rl * QS + gl] = to_t<T>(pq.x);
-                    q1[(rl + 1) * QS + gl] = to_t<T>(pq.y);
+                    put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
+                    put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);
                 }
                 float* pw = pb + w * nq * 64 + gl;
                 if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
@@ -1053,22 +1099,28 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             else epilogue(std::true_type{});
         }
         wave_sync();
-        for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        if constexpr (!X)
+            for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         lap(3);
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
         if (!(d.dbg & 4))
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
-                const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                const Fr a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
                 const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = *reinterpret_cast<const Fr*>(
-                        tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                    const Fr bw = M::load(reinterpret_cast<const T*>(
+                        tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                        L.stp / (int)sizeof(T));
                     dzA[lb] = M::mma(a1, bw, dzA[lb]);
                     dzP[lb] = M::mma(a2, bw, dzP[lb]);
                 }
             }
+        if constexpr (X) {  // pq consumed: re-zero the correction tile it aliased
+            wave_sync();
+            for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        }
         lap(4);
         // ---- 5. combine the waves' column partials -> slab (fixed order) ----
         // double-buffered (NW = 8): the next tile's stage goes into the other buffer before the
@@ -1320,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                 const float v = pass ? acc[r] : 0.f;
                 dh[(int64_t)b * KP + j] = v;
                 dhT_f[(int64_t)j * d.Bpad + b] = v;
-                dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)v;
+                put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, v);  // hi plane (+ the x3 lo plane)
                 rdhs += v;
             }
         }
@@ -1381,14 +1433,6 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
             o[7] = (float)wave_place();
         }
     }
-}
-
-template <class T, int KP, bool H1, bool RAW>
-__global__ __launch_bounds__(256) void k_enc_bwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
-                                                 const int32_t* __restrict__ toff, const float* __restrict__ lat,
-                                                 const T* __restrict__ dhT, const T* __restrict__ WeP,
-                                                 Dims d, float* __restrict__ slabE) {
-    enc_bwd_body<T, KP, H1, RAW>(ents, seg, toff, lat, dhT, WeP, d, slabE, (int)blockIdx.x);
 }
 
 // =======================================================================================
@@ -1465,17 +1509,18 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
 // k_enc_bwd and k_grad_small in ONE launch: both need only k_latent_bwd's outputs, so the small-
 // gradient blocks (appended after the encoder blocks) run beside the encoder tail instead of as
 // a separate kernel on the chain
-template <class T, int KP, bool H1>
+template <class P, int KP, bool H1>
 __global__ __launch_bounds__(256) void k_enc_bwd_small(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                        const int32_t* __restrict__ toff, const float* __restrict__ lat,
-                                                       const T* __restrict__ dhT, const T* __restrict__ WeP, Dims d,
+                                                       const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
+                                                       const typename WEnc<P>::type* __restrict__ WeP, Dims d,
                                                        float* __restrict__ slabE, int nenc, const float* __restrict__ small,
                                                        int nwg, NBGrads G, float* __restrict__ smallg,
                                                        const float* __restrict__ lossp, int nlossp,
                                                        const float* __restrict__ klpart, int nkl, float* __restrict__ out,
                                                        double* __restrict__ sqpart) {
     const int bid = (int)blockIdx.x;
-    if (bid < nenc) enc_bwd_body<T, KP, H1, true>(ents, seg, toff, lat, dhT, WeP, d, slabE, bid);
+    if (bid < nenc) enc_bwd_body<P, KP, H1, true>(ents, seg, toff, lat, dhT, dplane, WeP, d, slabE, bid);
     else grad_small_body(d, small, nwg, G, smallg, lossp, nlossp, klpart, nkl, out, 1, sqpart, bid - nenc);
 }
 
@@ -1681,12 +1726,14 @@ __global__ void k_pack_frozen(const float* We, const float* Wd, int D, int DP, i
     const bool v = (k < K) && (g < D);
     const float we = v ? We[(int64_t)k * D + g] : 0.f;
     const float wd = v ? Wd[(int64_t)g * K + k] : 0.f;
+    // bf16 images carry the x3 mode's lo planes KP * DP elements after the hi planes
+    const int64_t pl = (int64_t)KP * DP;
     WeP_f[i] = we;
-    WeP_b[i] = (__bf16)we;
+    put_op<X3>(WeP_b, (int)i, (int)pl, we);
     WdT_f[i] = wd;
-    WdT_b[i] = (__bf16)wd;
+    put_op<X3>(WdT_b, (int)i, (int)pl, wd);
     WdP_f[(int64_t)g * KP + k] = wd;
-    WdP_b[(int64_t)g * KP + k] = (__bf16)wd;
+    put_op<X3>(WdP_b, (int)((int64_t)g * KP + k), (int)pl, wd);
 }
 
 hipError_t nb_prepare_frozen(Engine* e) {
@@ -1700,25 +1747,35 @@ hipError_t nb_prepare_frozen(Engine* e) {
     return hipGetLastError();
 }
 
-// Per-row finalisation between decoder passes (one thread per row):
-//   MODE 0: combine pass A's per-split (max, sum-exp) -> log-sum-exp in log2 units
-//   MODE 1: E_b = sum over pass-B splits, stored as w_b E_b for pass C
-static size_t dec_lds(const Dims& d, int pass, bool bf16) {
+// LDS of decoder passes A / C: double-buffered W stage (all planes) + grec tile
+static size_t dec_lds(const Dims& d, int pass, int esz, int planes) {
     const int nq = 1 + d.C;
-    size_t s = 2 * ((size_t)64 * d.KP * (bf16 ? 2 : 4) + 1024);  // double-buffered W + grec stage
+    size_t s = 2 * ((size_t)planes * 64 * d.KP * esz + 1024);
     if (pass == 2) s += (size_t)2 * 4 * nq * 64 * 4;
     return s;
 }
 
-template <class T, int KP>
+template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
+    using T = typename Elem<P>::type;
+    constexpr int NPL = IsX3<P>::value ? 2 : 1;
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * 16 * XS * (int)sizeof(T), 0).bytes;
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * NPL * 16 * XS * (int)sizeof(T), 0, NPL).bytes;
 }
-template <class T, int KP>
-static void enc_fwd_run(Engine* e, const Dims& d, const void* WeS, float* hpart, hipStream_t st) {
-    hipLaunchKernelGGL((k_enc_fwd<T, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<T, KP>(d)), st, e->d_ents,
-                       e->d_seg, e->d_toff, (const T*)WeS, d, hpart);
+// the encoder operand images of mode P: bf16 planes (bf16, x3) or f32
+template <class P> static const typename Elem<P>::type* op_img(const float* f, const __bf16* b) {
+    if constexpr (sizeof(typename Elem<P>::type) == 2) return b;
+    else return f;
+}
+template <class P, int KP>
+static void enc_fwd_run(Engine* e, const Dims& d, float* hpart, hipStream_t st) {
+    hipLaunchKernelGGL((k_enc_fwd<P, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
+                       e->d_seg, e->d_toff, op_img<P>(e->d_WeS_f, e->d_WeS_b), (int64_t)e->KP * e->DP, d, hpart);
+}
+// encoder backward operands: dh^T planes and the staged W (f32 in the x3 mode)
+template <class P> static const typename WEnc<P>::type* enc_w(Engine* e) {
+    if constexpr (std::is_same<typename WEnc<P>::type, __bf16>::value) return e->d_WeP_b;
+    else return e->d_WeP_f;
 }
 
 static bool getenv_is(const char* name, const char* value) {
@@ -1726,29 +1783,12 @@ static bool getenv_is(const char* name, const char* value) {
     return v && std::strcmp(v, value) == 0;
 }
 
-template <class T, int KP>
-static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
-                                uint64_t step_id, int64_t row_offset) {
-    const bool bf = sizeof(T) == 2;
-    hipStream_t st = e->stream;
-    const int nrb = d.nrb;
-    float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
-    {
-        ScopedTimer tm(e, "k_enc_fwd");
-        enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
-    }
-    {
-        ScopedTimer tm(e, "k_latent_fwd");
-        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr,
-                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, step_id,
-                           row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
-    }
+static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     DecPtrs Q;
     Q.lat = e->d_lat;
     Q.zf = e->d_zf;
     Q.zb = e->d_zb;
-    Q.gene = gene;
+    Q.gene = e->d_gene;
     Q.Wcd = P.Wcd;
     Q.Wnd = P.Wnd;
     Q.covar = e->d_covar;
@@ -1769,29 +1809,60 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     Q.slabB = e->d_slabB;
     Q.slabC = e->d_slabC;
     Q.lossp = e->d_lossp;
+    Q.zplane = (int64_t)d.Bpad * d.KP;
+    Q.wplane = (int64_t)e->KP * e->DP;
+    return Q;
+}
+
+template <class PM, int KP>
+static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
+                                uint64_t step_id, int64_t row_offset) {
+    using T = typename Elem<PM>::type;
+    constexpr bool X = IsX3<PM>::value;
+    constexpr int NPL = X ? 2 : 1;
+    const bool bf = sizeof(T) == 2;  // bf16 planes (bf16 and x3 modes)
+    hipStream_t st = e->stream;
+    const int nrb = d.nrb;
+    float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
+    {
+        ScopedTimer tm(e, "k_enc_fwd");
+        enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
+    }
+    {
+        ScopedTimer tm(e, "k_latent_fwd");
+        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
+                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr,
+                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, step_id,
+                           row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
+    }
+    const DecPtrs Q = dec_ptrs(e, d, P, bf);
     const bool small_cr = (d.C == 1 && d.R == 1);
-    // pass B: 16 NW rows per workgroup (NW = 8 where the LDS carve fits, MMVAE_DEC_NW=4 forces 4)
+    // pass B: 16 NW rows per workgroup.  bf16: NW = 8 with double-buffered stages (one barrier
+    // per tile); x3: NW = 8 single-buffered (the hi + lo images of double buffers exceed the
+    // 160 KB LDS); f32 or MMVAE_DEC_NW=4: NW = 4 (64 rows, two workgroups per CU)
     const int nqB = (1 + d.C) + 1 + d.R;
-    const int csz = bf ? 4 : 8;
-    const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8).bytes;
-    const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !getenv_is("MMVAE_DEC_NW", "4")) ? 8 : 4;
+    const int csz = (bf && !X) ? 4 : 8;
+    const bool nw4 = getenv_is("MMVAE_DEC_NW", "4");
+    const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL).bytes;
+    const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !nw4) ? 8 : 4;
     const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
     const dim3 gdecA(nrb / 2 * d.nsA);  // passes A / C: 128 rows per workgroup
+    const size_t ldsA = dec_lds(d, 0, (int)sizeof(T), NPL), ldsC = dec_lds(d, 2, (int)sizeof(T), NPL);
     {
         ScopedTimer tm(e, "k_dec_lse");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec_lse<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 0, bf), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
+        else hipLaunchKernelGGL((k_dec_lse<PM, KP, CMAX>), gdecA, dim3(256), ldsA, st, Q, d);
     }
     {
         ScopedTimer tm(e, "k_dec_nb");
         if (nwB == 8) {
-            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1, 8>), gdecB, dim3(512), ldsB8, st, Q, d);
+            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PM, KP, 1, 1, 8, !X>), gdecB, dim3(512), ldsB8, st, Q, d);
         } else if (small_cr)
-            hipLaunchKernelGGL((k_dec_nb<T, KP, 1, 1, 4>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PM, KP, 1, 1, 4, false>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL).bytes, st, Q, d);
         else
-            hipLaunchKernelGGL((k_dec_nb<T, KP, CMAX, RMAX, 4>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PM, KP, CMAX, RMAX, 4, false>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL).bytes, st, Q, d);
     }
     NBGrads G = nb_grads(e);
     if (!update) {
@@ -1802,8 +1873,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<T, KP, 1>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
-        else hipLaunchKernelGGL((k_dec_tail<T, KP, CMAX>), gdecA, dim3(256), dec_lds(d, 2, bf), st, Q, d);
+        if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<PM, KP, 1>), gdecA, dim3(256), ldsC, st, Q, d);
+        else hipLaunchKernelGGL((k_dec_tail<PM, KP, CMAX>), gdecA, dim3(256), ldsC, st, Q, d);
     }
     const bool split = split_grads(e);
     const bool small_genes = d.C == 1 && d.R == 1 && d.H == 1;
@@ -1835,17 +1906,18 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         // encoder backward + the small-parameter gradients / loss in one launch
         ScopedTimer tm(e, "k_enc_bwd");
-        const T* WeT = bf ? (const T*)e->d_WeP_b : (const T*)e->d_WeP_f;
-        const T* dhT = bf ? (const T*)e->d_dhT_b : (const T*)e->d_dhT_f;
+        const auto* WeT = enc_w<PM>(e);
+        const T* dhT = op_img<PM>(e->d_dhT_f, e->d_dhT_b);
+        const int64_t dpl = (int64_t)KP * d.Bpad;
         const int nenc = nrb * d.nsE;
         if (d.H == 1)
-            hipLaunchKernelGGL((k_enc_bwd_small<T, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE, nenc, e->d_small,
+            hipLaunchKernelGGL((k_enc_bwd_small<PM, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st,
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
         else
-            hipLaunchKernelGGL((k_enc_bwd_small<T, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, WeT, d, e->d_slabE, nenc, e->d_small,
+            hipLaunchKernelGGL((k_enc_bwd_small<PM, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st,
+                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
     }
@@ -1885,7 +1957,7 @@ hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
     }
     const Dims d = nb_dims(e, B, n_total, beta);
     const NBPtrs P = nb_ptrs(e);
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
+    const bool bf = e->cfg.dtype != MMVAE_DTYPE_F32;  // bf16 planes (bf16, x3)
     ScopedTimer tm(e, "k_prep");
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, e->stream, P, d, e->d_gene, e->d_WeP_f,
                        e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec);
@@ -1900,18 +1972,15 @@ hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta
     }
     const Dims d = nb_dims(e, B, n_total, beta);
     const NBPtrs P = nb_ptrs(e);
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
-    if (e->KP == 32) return bf ? nb_launch_all<__bf16, 32>(e, d, P, update, use_eps, step_id, row_offset)
-                               : nb_launch_all<float, 32>(e, d, P, update, use_eps, step_id, row_offset);
-    return bf ? nb_launch_all<__bf16, 64>(e, d, P, update, use_eps, step_id, row_offset)
-              : nb_launch_all<float, 64>(e, d, P, update, use_eps, step_id, row_offset);
+    return dispatch_mode(e, [&](auto p, auto kp) {
+        return nb_launch_all<decltype(p), decltype(kp)::value>(e, d, P, update, use_eps, step_id, row_offset);
+    });
 }
 
-template <class T, int KP>
+template <class PM, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
-    const bool bf = sizeof(T) == 2;
     hipStream_t st = e->stream;
-    enc_fwd_run<T, KP>(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart, st);
+    enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, (uint64_t)0,
                        (int64_t)0, e->d_lat,
@@ -1926,36 +1995,17 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
     }
     const Dims d = nb_dims(e, B, B, 1.f);
     const NBPtrs P = nb_ptrs(e);
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
-    if (e->KP == 32) return bf ? nb_encode_t<__bf16, 32>(e, d, P, d_mean, d_lnvar)
-                               : nb_encode_t<float, 32>(e, d, P, d_mean, d_lnvar);
-    return bf ? nb_encode_t<__bf16, 64>(e, d, P, d_mean, d_lnvar) : nb_encode_t<float, 64>(e, d, P, d_mean, d_lnvar);
+    return dispatch_mode(e, [&](auto p, auto kp) {
+        return nb_encode_t<decltype(p), decltype(kp)::value>(e, d, P, d_mean, d_lnvar);
+    });
 }
 
 // ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
-template <class T, int KP>
-static void enc_fwd_go(Engine* e, const Dims& d, const void* WeS, float* hpart) {
-    enc_fwd_run<T, KP>(e, d, WeS, hpart, e->stream);
-}
-template <class T, int KP>
-static void enc_bwd_go(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
-    hipLaunchKernelGGL((k_enc_bwd<T, KP, true, false>), dim3(d.nrb * d.nsE), dim3(256), (enc_bwd_lds<T, KP>(d)),
-                       e->stream, e->d_ents, e->d_seg, e->d_toff, e->d_lat, (const T*)dhT,
-                       (const T*)WeP, d, slab);
-}
-
-hipError_t enc_forward_launch(Engine* e, const Dims& d, const void* WeS, float* hpart) {
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
-    if (e->KP == 32) bf ? enc_fwd_go<__bf16, 32>(e, d, WeS, hpart) : enc_fwd_go<float, 32>(e, d, WeS, hpart);
-    else bf ? enc_fwd_go<__bf16, 64>(e, d, WeS, hpart) : enc_fwd_go<float, 64>(e, d, WeS, hpart);
-    return hipGetLastError();
-}
-
-hipError_t enc_backward_launch(Engine* e, const Dims& d, const void* dhT, const void* WeP, float* slab) {
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
-    if (e->KP == 32) bf ? enc_bwd_go<__bf16, 32>(e, d, dhT, WeP, slab) : enc_bwd_go<float, 32>(e, d, dhT, WeP, slab);
-    else bf ? enc_bwd_go<__bf16, 64>(e, d, dhT, WeP, slab) : enc_bwd_go<float, 64>(e, d, dhT, WeP, slab);
-    return hipGetLastError();
+hipError_t enc_forward_launch(Engine* e, const Dims& d, float* hpart) {
+    return dispatch_mode(e, [&](auto p, auto kp) {
+        enc_fwd_run<decltype(p), decltype(kp)::value>(e, d, hpart, e->stream);
+        return hipGetLastError();
+    });
 }
 
 }  // namespace mmvae

@@ -3,6 +3,8 @@
 // register-staged LDS tile copy.  Device-inline only: every __global__ kernel lives in
 // exactly one translation unit (nb_kernels.hip / vmf_kernels.hip).
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace mmvae {
@@ -104,10 +106,25 @@ MMVAE_DEV void fill_toffl(int32_t* toffl, int S, int t0, int NT, const int32_t* 
     for (int i = lane; i < S; i += 64) toffl[i] = toff[(int64_t)wb * (NT + 1) + min(t0 + i, NT)];
 }
 
-// log1p of a count: exact libm form in the f32 parity mode; for bf16 operand tiles one v_log of
-// 1 + x (x >= 0: relative error <= 6e-8 / x, far below bf16's 4e-3 for any x >= 1e-4, and
-// exact to f32 rounding for counts >= 1)
-template <class T> MMVAE_DEV float log1p_cnt(float x) { return sizeof(T) == 4 ? log1pf(x) : flog(1.f + x); }
+// log1p of a count: exact libm form in the fp32-accurate modes (f32, x3); for bf16 operand tiles
+// one v_log of 1 + x (x >= 0: relative error <= 6e-8 / x, far below bf16's 4e-3 for any
+// x >= 1e-4, and exact to f32 rounding for counts >= 1)
+template <class P> MMVAE_DEV float log1p_cnt(float x) {
+    if constexpr (std::is_same<P, __bf16>::value) return flog(1.f + x);
+    else return log1pf(x);
+}
+
+// store v into operand tile t at element idx: plain (f32 / bf16), or as the hi / lo bf16 pair of
+// the x3 mode with the lo plane `plane` elements after the hi plane
+template <class P> MMVAE_DEV void put_op(typename Elem<P>::type* t, int idx, int plane, float v) {
+    if constexpr (IsX3<P>::value) {
+        const __bf16 h = bf_hi(v);
+        t[idx] = h;
+        t[idx + plane] = bf_lo(v, h);
+    } else {
+        t[idx] = to_t<typename Elem<P>::type>(v);
+    }
+}
 
 // mvec[k] from the per-256-gene-block partials [nblk][KP] written by k_prep / k_vprep: the
 // workgroup's 256 threads each sum a quarter of the blocks of one latent (fixed order), the
@@ -266,12 +283,13 @@ MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int
         }
 }
 
-// LDS carve of k_enc_fwd (host computes the same size)
+// LDS carve of k_enc_fwd (host computes the same size); planes = 2 in the x3 mode (hi + lo
+// images of the double-buffered W stage: [hi 0][hi 1][lo 0][lo 1])
 struct EncLds {
     int o_x, o_toff, bytes;
-    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre) {
+    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1) {
         const int stb = KP * 64 * esz;
-        o_x = pre + 2 * stb;
+        o_x = pre + 2 * planes * stb;
         o_toff = o_x + 4 * xbytes_per_wave;  // [4 waves][S] tile offsets
         bytes = o_toff + ((4 * S * 4 + 15) / 16) * 16;
     }
@@ -309,6 +327,21 @@ struct RegStage {
         if constexpr (NC > 1) st1(dst, 1, v1);
         if constexpr (NC > 2) st1(dst, 2, v2);
         if constexpr (NC > 3) st1(dst, 3, v3);
+    }
+};
+
+// RegStage of an operand tile and, in the x3 mode, of its lo plane: loaded from src and
+// src + plane_bytes, stored to the LDS images dst and dst + img_bytes (same swizzle)
+template <int NR, int RB, int NTH, bool X>
+struct DualStage {
+    RegStage<NR, RB, NTH> hi, lo;
+    MMVAE_DEV void load(const char* src, int64_t ld, int64_t plane_bytes) {
+        hi.load(src, ld);
+        if constexpr (X) lo.load(src + plane_bytes, ld);
+    }
+    MMVAE_DEV void store(char* dst, int img_bytes) const {
+        hi.store(dst);
+        if constexpr (X) lo.store(dst + img_bytes);
     }
 };
 

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(1024) void k_vnorm_enc(const float* __restrict__ W,
         float v = 0.f;
         if (k < K && g < D) v = (fmaxf(W[(int64_t)k * D + g], 0.f) + 1e-4f) / nrm;
         WeP_f[(int64_t)k * DP + g] = v;
-        WeP_b[(int64_t)k * DP + g] = (__bf16)v;
+        put_op<X3>(WeP_b, k * DP + g, (int)gridDim.x * DP, v);  // lo plane KP * DP after the hi plane
     }
 }
 
@@ -91,10 +91,11 @@ __global__ void k_vpack_dec(const float* Wd, int D, int DP, int K, int KP, float
     if (i >= (int64_t)KP * DP) return;
     const int k = (int)(i / DP), g = (int)(i % DP);
     const float wd = (k < K && g < D) ? Wd[(int64_t)g * K + k] : 0.f;
+    const int pl = KP * DP;  // the x3 mode's lo planes
     WdT_f[i] = wd;
-    WdT_b[i] = (__bf16)wd;
+    put_op<X3>(WdT_b, (int)i, pl, wd);
     WdP_f[(int64_t)g * KP + k] = wd;
-    WdP_b[(int64_t)g * KP + k] = (__bf16)wd;
+    put_op<X3>(WdP_b, g * KP + k, pl, wd);
 }
 
 // =======================================================================================
@@ -132,8 +133,8 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
     for (int kk = 0; kk < 8; ++kk) {
         const int k = blockIdx.y * 8 + kk;
         const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
-        if (in) {
-            if (WeS_b) WeS_b[(int64_t)k * d.DP + g] = (__bf16)ws;
+        if (in) {  // bf16 image: hi plane, and the x3 mode's lo plane KP * DP elements after it
+            if (WeS_b) put_op<X3>(WeS_b, (int)((int64_t)k * d.DP + g), d.KP * d.DP, ws);
             else WeS_f[(int64_t)k * d.DP + g] = ws;
         }
         mp[kk] = xmv * ws;  // xmi_g W~[k][g]
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         if (k < d.KP) {
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
-            zb[(int64_t)b * d.KP + k] = (__bf16)zz;
+            put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
         }
         if (k == 0) {
             L[d.LAT_D] = inx[c];
@@ -310,6 +311,8 @@ struct VDecPtrs {
     float* rowcos;         // [Bpad] cos_b (written by split 0 of the backward pass)
     float* dzp;            // [nsD][Bpad][KP]
     float* slabB;          // [nrb][1+C][DP]
+    int64_t zplane;        // x3 mode: element offset of the lo plane of zb
+    int64_t wplane;        // x3 mode: element offset of the lo planes of WdP / WdT
 };
 
 // Per-row combine of pass 0's split sums (threads p0, p0 + np, ... of a row's np-thread group,
@@ -352,23 +355,26 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 
 struct VDecLds {
     int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, bytes;
-    MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass) {
-        o_g = 64 * KP * esz;
+    MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass, int planes = 1) {
+        o_g = planes * 64 * KP * esz;                         // W image (hi [+ lo])
         o_t = o_g + 1024;
-        o_part = o_t + (pass ? KP * 64 * esz : 0);
+        o_part = o_t + (pass ? planes * KP * 64 * esz : 0);
         o_wave = o_part + (pass ? 4 * nq * 64 * 4 : 0);
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q1 = 16 * 68 * 4;                                   // after the l tile
-        o_toff = o_q1 + (pass ? ((16 * QS * esz + 15) / 16) * 16 : 0);
+        o_toff = o_q1 + (pass ? ((planes * 16 * QS * esz + 15) / 16) * 16 : 0);
         wave_bytes = o_toff + ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
         bytes = o_wave + 4 * wave_bytes;
     }
 };
 
-template <class T, int KP, int PASS, int CM>
+template <class P, int KP, int PASS, int CM>
 MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
-    using M = MM<T>;
+    using T = typename Elem<P>::type;
+    using M = MM<P>;
     using Fr = typename M::frag;
+    constexpr bool X = IsX3<P>::value;
+    constexpr int NPL = X ? 2 : 1;
     constexpr int KS = KP / M::KSTEP;
     constexpr int GK = 64 / M::KSTEP;
     constexpr bool BF = sizeof(T) == 2;
@@ -384,7 +390,9 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C;
     const int nq = 1 + C;
-    const VDecLds L(KP, (int)sizeof(T), S, nq, PASS);
+    const VDecLds L(KP, (int)sizeof(T), S, nq, PASS, NPL);
+    constexpr int WIMG = 64 * KP * (int)sizeof(T);  // one plane of the W / WdT images
+    constexpr int QPL = 16 * QS;                     // the pq tile's lo plane (x3)
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_g);
     char* tst = smem + L.o_t;
@@ -398,17 +406,18 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
 
-    RegStage<64, RBW> wreg;
-    RegStage<KP, RBT> treg;
+    DualStage<64, RBW, 256, X> wreg;
+    DualStage<KP, RBT, 256, X> treg;
     float4 greg = float4{0.f, 0.f, 0.f, 0.f};
+    const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
-        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW);
-        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T));
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
+        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
     auto stage_store = [&]() {
-        wreg.store(wst);
-        if (PASS) treg.store(tst);
+        wreg.store(wst, WIMG);
+        if (PASS) treg.store(tst, WIMG);
         if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
@@ -427,7 +436,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     Fr zfr[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL]);
+        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL], Q.zplane);
     float crow[4][CM], ra[4], rbt[4], svv[4], sv[4], slv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -462,7 +471,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
         for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
         wave_sync();
-        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<T>(fmaxf(x, 0.f)); });
+        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<P>(fmaxf(x, 0.f)); });
         wave_sync();
         pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
 #pragma unroll
@@ -471,7 +480,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-                acc = M::mma(zfr[s], *reinterpret_cast<const Fr*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), acc);
+                acc = M::mma(zfr[s], M::load(reinterpret_cast<const T*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), WIMG / (int)sizeof(T)), acc);
             const float4 g4 = gst[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -498,7 +507,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                     cs[0] += dv;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(dv, crow[r][c], cs[1 + c]);
-                    q1[rl * QS + gl] = to_t<T>(dv * u);
+                    put_op<P>(q1, rl * QS + gl, QPL, dv * u);
                 }
             }
             if (PASS) {
@@ -521,11 +530,12 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             // dz[cell][latent] += sum_g da[cell][g] W_d[g][latent]
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
-                const Fr a1 = *reinterpret_cast<const Fr*>(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = *reinterpret_cast<const Fr*>(
-                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T)));
+                    const Fr bw = M::load(reinterpret_cast<const T*>(
+                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                        WIMG / (int)sizeof(T));
                     dz[lb] = M::mma(a1, bw, dz[lb]);
                 }
             }
@@ -567,10 +577,10 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     }
 }
 
-template <class T, int KP, int CM>
-__global__ __launch_bounds__(256, 2) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<T, KP, 0, CM>(Q, d, epsD); }
-template <class T, int KP, int CM>
-__global__ __launch_bounds__(256, 2) void k_vdec_bwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<T, KP, 1, CM>(Q, d, epsD); }
+template <class P, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 0, CM>(Q, d, epsD); }
+template <class P, int KP, int CM>
+__global__ __launch_bounds__(256, 2) void k_vdec_bwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 1, CM>(Q, d, epsD); }
 
 // =======================================================================================
 // k_vrowfin — per row (one thread): combine pass-0 splits, cos_b = <y_b, r_b>
@@ -670,7 +680,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
                 const float v = pass ? acc[r] : 0.f;
                 const float vs = v * sH[cl * 68 + 64];
                 dhT_f[(int64_t)j * d.Bpad + b] = vs;
-                dhT_b[(int64_t)j * d.Bpad + b] = (__bf16)vs;
+                put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, vs);  // hi plane (+ the x3 lo plane)
                 rdhs += v;
             }
         }
@@ -769,10 +779,11 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
 }
 
 // the encoder backward (log1p term only) and the small-gradient / loss blocks in one launch
-template <class T, int KP>
+template <class P, int KP>
 __global__ __launch_bounds__(256) void k_enc_bwd_vsmall(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                         const int32_t* __restrict__ toff, const float* __restrict__ lat,
-                                                        const T* __restrict__ dhT, const T* __restrict__ WeP, Dims d,
+                                                        const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
+                                                        const typename WEnc<P>::type* __restrict__ WeP, Dims d,
                                                         float* __restrict__ slabE, int nenc, VScal sc,
                                                         const float* __restrict__ small, int nwg, VGrads G,
                                                         float* __restrict__ smallg, const float* __restrict__ rowcos,
@@ -780,7 +791,7 @@ __global__ __launch_bounds__(256) void k_enc_bwd_vsmall(const uint2* __restrict_
                                                         const float* __restrict__ vk, float* __restrict__ out,
                                                         double* __restrict__ sqpart) {
     const int bid = (int)blockIdx.x;
-    if (bid < nenc) enc_bwd_body<T, KP, true, false>(ents, seg, toff, lat, dhT, WeP, d, slabE, bid);
+    if (bid < nenc) enc_bwd_body<P, KP, true, false>(ents, seg, toff, lat, dhT, dplane, WeP, d, slabE, bid);
     else vgrad_small_body(d, sc, small, nwg, G, smallg, rowcos, klpart, nkl, vk, out, 1, sqpart, bid - nenc);
 }
 
@@ -951,11 +962,13 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     return d;
 }
 
-template <class T, int KP>
+template <class PM, int KP>
 static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const VScal& sc, bool update,
                                  bool use_eps, uint64_t step_id, int64_t row_offset, int mode, float* out_mean,
                                  float* out_lnvar) {
-    const bool bf = sizeof(T) == 2;
+    using T = typename Elem<PM>::type;
+    constexpr int NPL = IsX3<PM>::value ? 2 : 1;
+    const bool bf = sizeof(T) == 2;  // bf16 planes (bf16, x3)
     hipStream_t st = e->stream;
     const int nrb = d.nrb;
     float* gene = e->d_gene;
@@ -966,7 +979,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_enc_fwd");
-        hipError_t er = enc_forward_launch(e, d, bf ? (const void*)e->d_WeS_b : (const void*)e->d_WeS_f, e->d_hpart);
+        hipError_t er = enc_forward_launch(e, d, e->d_hpart);
         if (er != hipSuccess) return er;
     }
     {
@@ -997,14 +1010,16 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.rowcos = e->d_rowv;
     Q.dzp = e->d_dzp;
     Q.slabB = e->d_slabB;
+    Q.zplane = (int64_t)d.Bpad * d.KP;
+    Q.wplane = (int64_t)e->KP * e->DP;
     const dim3 gdec(nrb * d.nsD);
     const int nq = 1 + d.C;
     const int S = d.tpsD + 1;
     {
         ScopedTimer tm(e, "k_vdec_fwd");
-        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else hipLaunchKernelGGL((k_vdec_fwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0, NPL).bytes;
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     VGrads G = vmf_grads(e);
     const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K;
@@ -1021,9 +1036,9 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vdec_bwd");
-        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 1).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<T, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else hipLaunchKernelGGL((k_vdec_bwd<T, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 1, NPL).bytes;
+        if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec_bwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     const bool split = split_grads(e);
     if (split) {  // covar_decoding_ gradients final: all-reduce them under the encoder backward
@@ -1047,9 +1062,11 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         // encoder backward + the small-parameter gradients / loss in one launch
         ScopedTimer tm(e, "k_enc_bwd");
         const int nenc = nrb * d.nsE;
-        hipLaunchKernelGGL((k_enc_bwd_vsmall<T, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<T, KP>(d)), st, e->d_ents,
-                           e->d_seg, e->d_toff, e->d_lat, (const T*)(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f),
-                           (const T*)(bf ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f), d, e->d_slabE, nenc, sc,
+        const T* dhT = reinterpret_cast<const T*>(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f);
+        const auto* WeT = reinterpret_cast<const typename WEnc<PM>::type*>(
+            std::is_same<typename WEnc<PM>::type, __bf16>::value ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f);
+        hipLaunchKernelGGL((k_enc_bwd_vsmall<PM, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st, e->d_ents,
+                           e->d_seg, e->d_toff, e->d_lat, dhT, (int64_t)KP * d.Bpad, WeT, d, e->d_slabE, nenc, sc,
                            e->d_small, e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk,
                            e->d_out, sqS);
     }
@@ -1074,9 +1091,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
 
 template <class... A>
 static hipError_t vmf_dispatch(Engine* e, A... a) {
-    const bool bf = e->cfg.dtype == MMVAE_DTYPE_BF16;
-    if (e->KP == 32) return bf ? vmf_launch_all<__bf16, 32>(e, a...) : vmf_launch_all<float, 32>(e, a...);
-    return bf ? vmf_launch_all<__bf16, 64>(e, a...) : vmf_launch_all<float, 64>(e, a...);
+    return dispatch_mode(e, [&](auto p, auto kp) { return vmf_launch_all<decltype(p), decltype(kp)::value>(e, a...); });
 }
 
 hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,

@@ -5,8 +5,9 @@
 // per group, and this parser keeps exactly that behaviour.  A fourth group holds the engine's
 // own options (--seed, --dtype, --device, --threads, --no_csr_cache, --verbose).
 //
-// Outputs as the reference: ${out}.scores.gz (per-epoch loss), ${out}.covar.mtx.gz when --covar
-// is absent (create_ones_like), recorder files every --recording epochs.  The dataset is loaded
+// Outputs as the reference: ${out}.scores.gz (per-epoch loss), ${out}.covar.mtx.gz (+ .index) when
+// --covar is absent (create_ones_like), ${mtx}.index when missing (BGZF inputs), recorder files
+// every --recording epochs.  The dataset is loaded
 // once into HBM; its parsed CSR is cached next to the mtx as ${mtx}.mmvae_csr (the role of the
 // reference's ${mtx}.index: a faster second open).
 // Data parallel: launched once per GPU with RANK / WORLD_SIZE / LOCAL_RANK in the environment;
@@ -194,15 +195,35 @@ const char* usage_text(int model) {
                ? "nb_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
                  "             --mean_latent 2 --overdisp_encoding 1 --overdispersion_latent 1 --kl_discount .1\n"
                  "             --kl_max 1 --kl_min .01 --recording 10 --covar C.mtx.gz]\n"
-                 "engine: [--dtype f32|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n"
+                 "engine: [--dtype f32|bf16x3|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n"
                : "vmf_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
                  "             --latent 2 --kappa_min .1 --kappa_max 10 --kl_discount .1 --kl_max 1 --kl_min .01\n"
                  "             --recording 10 --covar C.mtx.gz]\n"
-                 "engine: [--dtype f32|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n";
+                 "engine: [--dtype f32|bf16x3|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n";
 }
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// bgzf_is_bgzf (bgzf.c:581-594): gzip magic with the FEXTRA flag and a 'BC' subfield
+static bool looks_bgzf(const std::string& path) {
+    unsigned char h[18];
+    FILE* fp = std::fopen(path.c_str(), "rb");
+    if (!fp) return false;
+    const size_t n = std::fread(h, 1, 18, fp);
+    std::fclose(fp);
+    return n == 18 && h[0] == 31 && h[1] == 139 && h[2] == 8 && (h[3] & 4) && h[12] == 'B' && h[13] == 'C';
+}
+
+// nb_vae_main.cc:58-59 / 72-78: build the column index of a BGZF MatrixMarket file when it is
+// missing (non-BGZF inputs, which the reference refuses, are read without one)
+static void ensure_index(const std::string& mtx, const std::string& idx, bool verbose) {
+    if (file_exists(idx) || !looks_bgzf(mtx)) return;
+    if (mmvae_mtx_build_index(mtx.c_str(), idx.c_str()) != MMVAE_OK)
+        std::fprintf(stderr, "warning: %s\n", mmvae_host_last_error());
+    else if (verbose)
+        std::fprintf(stderr, "[mmvae] Built the file: %s\n", idx.c_str());
 }
 
 static int load_dataset(const CliOptions& o, mmvae_csr& csr) {
@@ -300,6 +321,7 @@ int run_cli(int argc, const char** argv, int model) {
         std::fprintf(stderr, "--batch_size must be divisible by WORLD_SIZE\n");
         return EXIT_FAILURE;
     }
+    if (rank == 0) ensure_index(o.mtx, o.idx, o.verbose);
     const double t0 = now_s();
     mmvae_csr csr;
     if (load_dataset(o, csr)) {
@@ -313,6 +335,7 @@ int run_cli(int argc, const char** argv, int model) {
     std::vector<float> covar;
     int64_t C = 1;
     if (file_exists(o.covar_mtx)) {
+        if (rank == 0) ensure_index(o.covar_mtx, o.covar_idx, o.verbose);
         int64_t Nc = 0;
         float* m = nullptr;
         if (mmvae_mtx_read_dense_t(o.covar_mtx.c_str(), o.threads, &Nc, &C, &m)) {
@@ -328,12 +351,19 @@ int run_cli(int argc, const char** argv, int model) {
         mmvae_free(m);
     } else if (rank == 0) {
         const std::string f = o.out + ".covar.mtx.gz";
-        if (mmvae_mtx_write_ones(f.c_str(), csr.N)) std::fprintf(stderr, "warning: %s\n", mmvae_host_last_error());
-        else if (o.verbose) std::fprintf(stderr, "[mmvae] No covariate file is given. So we use this: %s\n", f.c_str());
+        if (mmvae_mtx_write_ones(f.c_str(), csr.N)) {
+            std::fprintf(stderr, "warning: %s\n", mmvae_host_last_error());
+        } else {
+            if (o.verbose) std::fprintf(stderr, "[mmvae] No covariate file is given. So we use this: %s\n", f.c_str());
+            std::remove((f + ".index").c_str());  // a fresh ones-file gets a fresh index
+            ensure_index(f, f + ".index", o.verbose);
+        }
     }
     mmvae_cfg cfg;
     mmvae_cfg_default(&cfg, model);
-    cfg.dtype = (o.dtype == "bf16") ? MMVAE_DTYPE_BF16 : MMVAE_DTYPE_F32;
+    cfg.dtype = (o.dtype == "bf16")                        ? MMVAE_DTYPE_BF16
+                : (o.dtype == "bf16x3" || o.dtype == "x3") ? MMVAE_DTYPE_BF16X3
+                                                           : MMVAE_DTYPE_F32;
     cfg.D = csr.D;
     cfg.C = C;
     cfg.K = o.latent;

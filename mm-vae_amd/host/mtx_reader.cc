@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
+#include <cmath>
 #include <unistd.h>
 #include <cstdlib>
 #include <cstring>
@@ -94,6 +95,7 @@ static bool read_whole(const char* path, std::vector<unsigned char>& buf, std::s
 
 struct BgzfBlock {
     size_t in_off, in_len, out_off, out_len;
+    size_t file_off;  // the member's first byte (the block address of a BGZF virtual offset)
 };
 
 static uint32_t le32(const unsigned char* p) {
@@ -118,6 +120,7 @@ static bool scan_bgzf(const std::vector<unsigned char>& b, std::vector<BgzfBlock
         const size_t total = (size_t)bsize + 1, hdr = 12 + xlen;
         if (total < hdr + 8 || p + total > b.size()) return false;
         BgzfBlock blk;
+        blk.file_off = p;
         blk.in_off = p + hdr;
         blk.in_len = total - hdr - 8;
         blk.out_len = le32(&b[p + total - 4]);
@@ -548,6 +551,195 @@ int mmvae_csr_load(const char* path, mmvae_csr* c) {
         return fail(MMVAE_E_ARG, std::string("not a valid CSR cache: ") + path);
     }
     return MMVAE_OK;
+}
+
+// ---- ${mtx}.index (mmutil_index.hh:38-190) -------------------------------------------------
+// build_mmutil_index: for every column of a column-sorted BGZF MatrixMarket file, the BGZF
+// virtual offset (block address << 16 | offset in the block) of its first line, written as gzip
+// text "col voff" lines with 0-based columns (write_tuple_stream, io.hh:248-266).  Offsets are
+// the reader's bgzf_tell after the previous line (mm_column_indexer_t::eval, :66-86): a line
+// that starts at a block boundary is addressed in the next block at offset 0 (bgzf.c:626-665).
+int mmvae_mtx_build_index(const char* mtx, const char* index_file) {
+    using namespace mmvae_host;
+    if (!mtx) return fail(MMVAE_E_ARG, "build_index: null path");
+    const std::string idx = (index_file && index_file[0]) ? std::string(index_file) : std::string(mtx) + ".index";
+    std::vector<unsigned char> raw;
+    std::string err;
+    if (!read_whole(mtx, raw, err)) return fail(MMVAE_E_ARG, err);
+    std::vector<BgzfBlock> blocks;
+    if (raw.size() < 2 || raw[0] != 0x1f || raw[1] != 0x8b || !scan_bgzf(raw, blocks))
+        return fail(MMVAE_E_ARG, std::string("This file is not bgzipped: ") + mtx);
+    {
+        FILE* fe = std::fopen(idx.c_str(), "rb");  // mmutil_index.hh:152-155: an existing index is kept
+        if (fe) {
+            std::fclose(fe);
+            return MMVAE_OK;
+        }
+    }
+    const size_t total = blocks.empty() ? 0 : blocks.back().out_off + blocks.back().out_len;
+    std::vector<char> text(total);
+    std::atomic<bool> ok{true};
+    parallel_for(default_threads(0), (int64_t)blocks.size(), [&](int, int64_t a, int64_t bnd) {
+        for (int64_t i = a; i < bnd; ++i) {
+            const BgzfBlock& k = blocks[(size_t)i];
+            if (!inflate_raw(raw.data() + k.in_off, k.in_len, text.data() + k.out_off, k.out_len)) ok = false;
+        }
+    });
+    if (!ok) return fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + mtx);
+    // uncompressed offset -> virtual offset (the block holding byte u; u at a block's end maps to
+    // the next non-empty block at offset 0)
+    std::vector<size_t> starts;
+    std::vector<size_t> addr;
+    for (const auto& b : blocks)
+        if (b.out_len > 0) {
+            starts.push_back(b.out_off);
+            addr.push_back(b.file_off);
+        }
+    size_t bi = 0;
+    auto voff = [&](size_t u) -> int64_t {
+        while (bi + 1 < starts.size() && starts[bi + 1] <= u) ++bi;
+        if (starts.empty() || u >= total) return (int64_t)((raw.size() - 28) << 16);  // EOF block
+        return (int64_t)((addr[bi] << 16) | (u - starts[bi]));
+    };
+    int64_t rows = 0, cols = 0, nnz = 0;
+    bool have_header = false;
+    int64_t lineno = 0, last_col = 0, last_off = 0, first_off = 0;
+    std::vector<std::pair<int64_t, int64_t>> map;
+    size_t pos = 0;
+    while (pos < total) {
+        const char* ls = text.data() + pos;
+        const char* le = static_cast<const char*>(std::memchr(ls, '\n', total - pos));
+        const size_t end = le ? (size_t)(le - text.data()) + 1 : total;
+        const char* lend = le ? le : text.data() + total;
+        const int64_t line_start_off = last_off;
+        last_off = voff(end);  // bgzf_tell after this line
+        pos = end;
+        if (lend == ls || ls[0] == '%') continue;
+        // fields
+        int64_t f[3];
+        int nf = 0;
+        const char* p = ls;
+        while (p < lend && nf < 3) {
+            while (p < lend && is_ws(*p)) ++p;
+            const char* q = p;
+            while (q < lend && !is_ws(*q)) ++q;
+            if (q > p) f[nf++] = parse_int(p, q);
+            p = q;
+        }
+        if (!have_header) {
+            if (nf < 3) continue;
+            rows = f[0];
+            cols = f[1];
+            nnz = f[2];
+            have_header = true;
+            first_off = last_off;  // eval_after_header: tell after the size line (:56-64)
+            continue;
+        }
+        if (nf < 3) continue;
+        const int64_t col = f[1] - 1;
+        if (lineno == 0) {
+            last_col = col;
+            map.push_back({col, first_off});
+        }
+        if (col != last_col) {
+            if (col < last_col) return fail(MMVAE_E_ARG, std::string("MTX must be sorted by columns: ") + mtx);
+            map.push_back({col, line_start_off});
+            last_col = col;
+        }
+        ++lineno;
+    }
+    (void)rows;
+    (void)nnz;
+    if (!have_header) return fail(MMVAE_E_ARG, std::string("no MatrixMarket size line in ") + mtx);
+    const int64_t lastc = map.empty() ? 0 : map.back().first;
+    if (lastc != cols - 1)  // mmutil_index.hh:171-179
+        return fail(MMVAE_E_ARG, "Failed to index all the columns: " + std::to_string(lastc) + " < " +
+                                     std::to_string(cols - 1) + " (filter out empty columns)");
+    const std::string tmp = idx + ".tmp." + std::to_string((long long)getpid());
+    gzFile g = gzopen(tmp.c_str(), "wb6");
+    if (!g) return fail(MMVAE_E_ARG, "cannot write " + idx);
+    std::string line;
+    bool wok = true;
+    for (const auto& m : map) {
+        line = std::to_string((long long)m.first) + " " + std::to_string((long long)m.second) + "\n";
+        wok = wok && gzwrite(g, line.data(), (unsigned)line.size()) == (int)line.size();
+    }
+    wok = (gzclose(g) == Z_OK) && wok;
+    if (!wok || std::rename(tmp.c_str(), idx.c_str()) != 0) {
+        std::remove(tmp.c_str());
+        return fail(MMVAE_E_ARG, "cannot write " + idx);
+    }
+    return MMVAE_OK;
+}
+
+// read_mmutil_index (mmutil_index.hh:192-228): voff per column [0, max col], missing columns
+// back-filled with the next column's offset (the reference's loop stops at MaxIdx - 1)
+int mmvae_mtx_read_index(const char* index_file, int64_t** voff_out, int64_t* ncol_out) {
+    using namespace mmvae_host;
+    if (!index_file || !voff_out || !ncol_out) return fail(MMVAE_E_ARG, "read_index: null argument");
+    gzFile g = gzopen(index_file, "rb");
+    if (!g) return fail(MMVAE_E_ARG, std::string("cannot open ") + index_file);
+    std::string buf;
+    char chunk[1 << 16];
+    int r;
+    while ((r = gzread(g, chunk, sizeof(chunk))) > 0) buf.append(chunk, (size_t)r);
+    gzclose(g);
+    std::vector<std::pair<int64_t, int64_t>> pairs;
+    const char* p = buf.data();
+    const char* e = p + buf.size();
+    while (p < e) {
+        char* q;
+        const long long c = std::strtoll(p, &q, 10);
+        if (q == p) break;
+        p = q;
+        const long long v = std::strtoll(p, &q, 10);
+        if (q == p) break;
+        p = q;
+        pairs.push_back({c, v});
+    }
+    if (pairs.empty()) return fail(MMVAE_E_ARG, std::string("empty file ") + index_file);
+    int64_t mx = 0;
+    for (auto& pr : pairs) mx = std::max<int64_t>(mx, pr.first);
+    int64_t* out = static_cast<int64_t*>(std::malloc(sizeof(int64_t) * (size_t)(mx + 1)));
+    if (!out) return fail(MMVAE_E_ARG, "out of memory");
+    for (int64_t j = 0; j <= mx; ++j) out[j] = 0;  // MISSING_POS = 0 (mmutil_bgzf_util.hh:17)
+    for (auto& pr : pairs) out[pr.first] = pr.second;
+    for (int64_t j = 0; j < mx - 1; ++j)
+        if (out[j] == 0) out[j] = out[j + 1];
+    *voff_out = out;
+    *ncol_out = mx + 1;
+    return MMVAE_OK;
+}
+
+// A cell-major CSR as a genes x cells BGZF MatrixMarket file sorted by column (cell), 1-based
+// (write_matrix_market_stream, io.hh:189-227): "integer" when every value is integral
+int mmvae_mtx_write_csr(const char* path, const mmvae_csr* c) {
+    using namespace mmvae_host;
+    if (!path || !c || c->N < 1 || c->D < 1) return fail(MMVAE_E_ARG, "mtx_write_csr: bad arguments");
+    bool integral = true;
+    for (int64_t j = 0; j < c->nnz && integral; ++j) integral = c->val[j] == std::floor(c->val[j]) && std::fabs(c->val[j]) < 1e9f;
+    BgzfWriter w;
+    if (!w.open(path)) return fail(MMVAE_E_ARG, std::string("cannot write ") + path);
+    w.write(std::string("%%MatrixMarket matrix coordinate ") + (integral ? "integer" : "real") + " general\n");
+    w.write(std::to_string((long long)c->D) + " " + std::to_string((long long)c->N) + " " +
+            std::to_string((long long)c->nnz) + "\n");
+    std::string line;
+    char num[64];
+    for (int64_t i = 0; i < c->N; ++i) {
+        const std::string cs = " " + std::to_string((long long)(i + 1)) + " ";
+        for (int64_t j = c->rowptr[i]; j < c->rowptr[i + 1]; ++j) {
+            line = std::to_string((long long)c->col[j] + 1);
+            line += cs;
+            if (integral) line += std::to_string((long long)c->val[j]);
+            else {
+                std::snprintf(num, sizeof(num), "%.9g", (double)c->val[j]);
+                line += num;
+            }
+            line += '\n';
+            w.write(line);
+        }
+    }
+    return w.close() ? MMVAE_OK : fail(MMVAE_E_ARG, std::string("write failed: ") + path);
 }
 
 int mmvae_mtx_write_ones(const char* path, int64_t N) {

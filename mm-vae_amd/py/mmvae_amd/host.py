@@ -51,6 +51,10 @@ def hlib():
                                                   ctypes.POINTER(i64), ctypes.POINTER(ctypes.POINTER(ctypes.c_float))]),
         "mmvae_free": (None, [ctypes.c_void_p]),
         "mmvae_mtx_write_ones": (ctypes.c_int, [ctypes.c_char_p, i64]),
+        "mmvae_mtx_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+        "mmvae_mtx_read_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(i64)),
+                                                ctypes.POINTER(i64)]),
+        "mmvae_mtx_write_csr": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(CSR)]),
         "mmvae_host_last_error": (ctypes.c_char_p, []),
         "mmvae_train_opts_default": (None, [ctypes.POINTER(TrainOpts)]),
         "mmvae_ridx": (i64, [ctypes.c_uint64, i64, i64, i64, i64, i64]),
@@ -88,11 +92,7 @@ def mtx_read(path, threads=0):
 
 
 def csr_save(path, rowptr, col, val, D):
-    rp = np.ascontiguousarray(rowptr, np.int64)
-    cl = np.ascontiguousarray(col, np.int32)
-    vl = np.ascontiguousarray(val, np.float32)
-    c = CSR(rp.size - 1, D, cl.size, rp.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-            cl.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), vl.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    c, keep = _csr_struct(rowptr, col, val, D)
     rc = hlib().mmvae_csr_save(os.fsencode(path), ctypes.byref(c))
     if rc:
         _err("csr_save", rc)
@@ -122,6 +122,43 @@ def mtx_write_ones(path, N):
     rc = hlib().mmvae_mtx_write_ones(os.fsencode(path), N)
     if rc:
         _err("mtx_write_ones", rc)
+
+
+def _csr_struct(rowptr, col, val, D):
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    vl = np.ascontiguousarray(val, np.float32)
+    c = CSR(rp.size - 1, D, cl.size, rp.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            cl.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), vl.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return c, (rp, cl, vl)
+
+
+def mtx_write_csr(path, rowptr, col, val, D):
+    """Cell-major CSR -> genes x cells BGZF MatrixMarket, sorted by cell."""
+    c, keep = _csr_struct(rowptr, col, val, D)
+    rc = hlib().mmvae_mtx_write_csr(os.fsencode(path), ctypes.byref(c))
+    if rc:
+        _err("mtx_write_csr", rc)
+
+
+def mtx_build_index(mtx, index_file=None):
+    """build_mmutil_index (mmutil_index.hh:138-190): ${mtx}.index as gzip 'col voff' text."""
+    rc = hlib().mmvae_mtx_build_index(os.fsencode(mtx), os.fsencode(index_file) if index_file else None)
+    if rc:
+        _err("mtx_build_index", rc)
+    return index_file or mtx + ".index"
+
+
+def mtx_read_index(index_file):
+    """read_mmutil_index (mmutil_index.hh:192-228): voff per column, gaps back-filled."""
+    p = ctypes.POINTER(ctypes.c_int64)()
+    n = ctypes.c_int64()
+    rc = hlib().mmvae_mtx_read_index(os.fsencode(index_file), ctypes.byref(p), ctypes.byref(n))
+    if rc:
+        _err("mtx_read_index", rc)
+    out = np.ctypeslib.as_array(p, shape=(n.value,)).copy()
+    hlib().mmvae_free(p)
+    return out
 
 
 def ridx(seed, epoch, batch, boot, B):

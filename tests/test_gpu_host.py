@@ -145,8 +145,11 @@ def test_cli_end_to_end(tmp_path, model):
     eng.init_params(seed=3)
     s_lib = host.train(eng, batch_size=64, max_epoch=3, nboot=2, seed=3, recording=1000)
     np.testing.assert_allclose(scores, s_lib, rtol=1e-5)
-    # outputs of the reference's CLI
+    # outputs of the reference's CLI: the auto covariate file and both column indexes
+    # (nb_vae_main.cc:58-59, 68-73)
     assert os.path.exists(out + ".covar.mtx.gz")
+    assert host.mtx_read_index(mtx + ".index").size == N
+    assert host.mtx_read_index(out + ".covar.mtx.gz.index").size == N
     tag = out + "_1"   # zeropad(epoch 1, max_epoch 3)
     lat_name = ".mu" if model == "nb" else ".latent"
     m = read_gz_matrix(tag + lat_name + "_mean.gz")

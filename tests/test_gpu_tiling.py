@@ -27,23 +27,25 @@ from helpers import (assert_grads_close, dims, engine_from_fixture, eps_of, gold
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"f32": (2e-5, 2e-4), "bf16": (2e-3, 3e-2)}
+TOL = {"f32": (2e-5, 2e-4), "bf16x3": (2e-5, 2e-4), "bf16": (2e-3, 3e-2)}
 
 
 def _eps(z, tag, vmf):
     return z[f"{tag}/eps_mu"].ravel().astype(np.float32) if vmf else eps_of(z, tag)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
 @pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("path", golden_files("nb_") + golden_files("vmf_"), ids=os.path.basename)
-def test_fixture_forced_gene_splits(monkeypatch, path, split):
+def test_fixture_forced_gene_splits(monkeypatch, path, split, dtype):
     """Every fixture with 1 or 2 gene splits per kernel (each split walks many tiles): the
-    first step's loss, gradients and clip norm against the golden vectors, in f32."""
+    first step's loss, gradients and clip norm against the golden vectors, in both
+    fp32-accurate modes."""
     for v in ("MMVAE_NSPLIT_E", "MMVAE_NSPLIT_D", "MMVAE_NSPLIT_A"):
         monkeypatch.setenv(v, split)
     z = load(path)
     vmf = "vmf" in os.path.basename(path)
-    eng = engine_from_fixture(z, "f32")
+    eng = engine_from_fixture(z, dtype)
     til = eng.tiling()
     assert til["split_dec"] == min(int(split), til["NT"]) and til["split_enc"] == min(int(split), til["NT"])
     if til["NT"] >= 4:
@@ -119,22 +121,23 @@ def _run_live(model, D, K, B, dtype, N, relu=False, beta=0.8):
     return til
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3", "bf16"])
 def test_nb_bench_shape_configs1(dtype):
     """BASELINE configs[1] per step: NB, 20k genes, latent 64, 4096 cells (the bench line)."""
     til = _run_live("nb", 20000, 64, 4096, dtype, N=12000)
     assert til["tps_dec"] >= 20, til
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3", "bf16"])
 def test_vmf_bench_shape_configs2(dtype):
     """BASELINE configs[2] per step: vMF, 20k genes, latent 32, 4096 cells."""
     _run_live("vmf", 20000, 32, 4096, dtype, N=12000)
 
 
-def test_nb_configs3_per_gpu_shape_f32():
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
+def test_nb_configs3_per_gpu_shape(dtype):
     """configs[3] per GPU: 30k genes, 4096 cells per rank (the DP=8 shard of a 32k batch)."""
-    _run_live("nb", 30000, 64, 4096, "f32", N=9000)
+    _run_live("nb", 30000, 64, 4096, dtype, N=9000)
 
 
 def test_nb_configs4_per_gpu_shape_bf16():

@@ -40,10 +40,11 @@ def check_grads(got, gold, tol, atol_k, ctx):
         (ctx, float(got["ln_kappa"][0]), float(gk[0]))
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
 @pytest.mark.parametrize("path", VMF_FILES, ids=os.path.basename)
-def test_vmf_fp32_parity_trajectory(path):
+def test_vmf_fp32_parity_trajectory(path, dtype):
     z = load(path)
-    eng = engine_from_fixture(z, "f32")
+    eng = engine_from_fixture(z, dtype)
     prev = params_of(z, "init/")
     for t in range(int(z["steps"])):
         loss, norm = eng.step(z[f"s{t}/cells"], float(z[f"s{t}/beta"]), eps=eps_v(z, f"s{t}"))
@@ -58,10 +59,11 @@ def test_vmf_fp32_parity_trajectory(path):
         eng.set_params(prev)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
 @pytest.mark.parametrize("path", VMF_FILES, ids=os.path.basename)
-def test_vmf_eval_and_encode(path):
+def test_vmf_eval_and_encode(path, dtype):
     z = load(path)
-    eng = engine_from_fixture(z, "f32")
+    eng = engine_from_fixture(z, dtype)
     steps = int(z["steps"])
     eng.set_params(params_of(z, f"s{steps - 1}/param/"))
     loss = eng.eval_loss(z["eval/cells"], float(z["eval/beta"]), eps=eps_v(z, "eval"))

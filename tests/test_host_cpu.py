@@ -160,3 +160,125 @@ def test_cli_arguments_without_gpu(tmp_path, exe):
     r = subprocess.run([b, "--mtx", str(p), "--out", str(tmp_path / "o"), "--mean_encoding" if exe == "nb_vae_main"
                         else "--encoding", "10"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "hidden" in r.stderr
+
+
+# ---- ${mtx}.index (mmutil_index.hh:38-228) ----------------------------------------------------
+def _bgzf_blocks(raw):
+    """(file offset, uncompressed start, uncompressed length) of every BGZF member."""
+    out, p, u = [], 0, 0
+    while p < len(raw):
+        xlen = struct.unpack_from("<H", raw, p + 10)[0]
+        bsize = struct.unpack_from("<H", raw, p + 16)[0]
+        isize = struct.unpack_from("<I", raw, p + bsize + 1 - 4)[0]
+        out.append((p, u, isize))
+        p += bsize + 1
+        u += isize
+    return out
+
+
+def _index_restated(raw):
+    """mm_column_indexer_t restated: bgzf_tell after each line (bgzf.c:626-665: a line ending at
+    a block's end leaves the reader at the next block, offset 0)."""
+    blocks = [b for b in _bgzf_blocks(raw) if b[2] > 0]
+    text = gzip.decompress(raw)
+
+    def tell(u):
+        for fo, us, ln in blocks:
+            if us <= u < us + ln:
+                return (fo << 16) | (u - us)
+        return None
+
+    pos, last_off, header, first_off, lineno, last_col, out = 0, 0, False, 0, 0, 0, []
+    for line in text.split(b"\n")[:-1]:
+        start_off = last_off
+        pos += len(line) + 1
+        last_off = tell(pos)
+        if not line or line.startswith(b"%"):
+            continue
+        f = line.split()
+        if not header:
+            header, first_off = True, last_off
+            continue
+        col = int(f[1]) - 1
+        if lineno == 0:
+            last_col = col
+            out.append((col, first_off))
+        if col != last_col:
+            out.append((col, start_off))
+            last_col = col
+        lineno += 1
+    return out
+
+
+def _line_at(raw, voff):
+    """Seek a BGZF virtual offset and return the line found there (bgzf_seek + getline)."""
+    addr, off = voff >> 16, voff & 0xffff
+    data = b""
+    for fo, us, ln in _bgzf_blocks(raw):
+        if fo >= addr:
+            data += zlib.decompressobj(16 + 15).decompress(raw[fo:])
+            if b"\n" in data[off:]:
+                break
+    return data[off:].split(b"\n", 1)[0]
+
+
+def test_index_builder_matches_restatement_and_seeks(tmp_path, data):
+    rp, col, val, D = data
+    raw = bgzf_compress(mtx_text(rp, col, val, D))  # ~ a few BGZF blocks, column-sorted
+    p = tmp_path / "x.mtx.gz"
+    p.write_bytes(raw)
+    idx = host.mtx_build_index(str(p))
+    assert idx == str(p) + ".index"
+    pairs = [tuple(map(int, ln.split())) for ln in gzip.decompress(open(idx, "rb").read()).decode().splitlines()]
+    assert pairs == _index_restated(raw)
+    assert len(_bgzf_blocks(raw)) > 2
+    voff = host.mtx_read_index(idx)
+    N = rp.size - 1
+    assert voff.size == N
+    for j in range(N):
+        if rp[j + 1] == rp[j]:
+            continue
+        line = _line_at(raw, int(voff[j])).split()
+        assert int(line[1]) == j + 1 and int(line[0]) == col[rp[j]] + 1, (j, line)
+
+
+def test_index_of_engine_writer_and_ones_file(tmp_path, data):
+    rp, col, val, D = data
+    p = str(tmp_path / "w.mtx.gz")
+    host.mtx_write_csr(p, rp, col, val, D)
+    r2, c2, v2, D2 = host.mtx_read(p)
+    np.testing.assert_array_equal(r2, rp)
+    np.testing.assert_array_equal(c2, col)
+    raw = open(p, "rb").read()
+    host.mtx_build_index(p, p + ".idx")
+    pairs = [tuple(map(int, ln.split())) for ln in gzip.decompress(open(p + ".idx", "rb").read()).decode().splitlines()]
+    assert pairs == _index_restated(raw)
+    # the auto covariate file and its index (nb_vae_main.cc:68-73)
+    ones = str(tmp_path / "o.covar.mtx.gz")
+    host.mtx_write_ones(ones, 200000)
+    host.mtx_build_index(ones)
+    v = host.mtx_read_index(ones + ".index")
+    raw1 = open(ones, "rb").read()
+    assert v.size == 200000 and len(_bgzf_blocks(raw1)) > 3
+    for j in (0, 1, 4567, 99999, 199999):
+        assert _line_at(raw1, int(v[j])) == f"1 {j + 1} 1".encode()
+
+
+def test_index_builder_errors(tmp_path, data):
+    rp, col, val, D = data
+    plain = tmp_path / "p.mtx.gz"
+    plain.write_bytes(gzip.compress(mtx_text(rp, col, val, D)))
+    with pytest.raises(mmvae_amd.MMVAEError, match="not bgzipped"):
+        host.mtx_build_index(str(plain))
+    shuf = tmp_path / "s.mtx.gz"
+    nnz = col.size
+    shuf.write_bytes(bgzf_compress(mtx_text(rp, col, val, D, order=np.random.default_rng(0).permutation(nnz))))
+    with pytest.raises(mmvae_amd.MMVAEError, match="sorted by columns"):
+        host.mtx_build_index(str(shuf))
+    # the last column empty: the reference refuses (mmutil_index.hh:171-179)
+    rp2 = rp.copy()
+    rp2[-1] = rp2[-2]
+    short = tmp_path / "e.mtx.gz"
+    short.write_bytes(bgzf_compress(mtx_text(rp2, col[:rp2[-1]], val[:rp2[-1]], D)))
+    with pytest.raises(mmvae_amd.MMVAEError, match="Failed to index all the columns"):
+        host.mtx_build_index(str(short))
