@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/mmvae/lbessel.hh"
 #include "common.hpp"
 #include "engine.hpp"
 #include "tiles.hpp"
@@ -956,47 +957,10 @@ int mmvae_timing_reset(mmvae_h e) {
     return MMVAE_OK;
 }
 
-// ---- operators.hh scalars (host, fp32) -------------------------------------------------
-// Bit-level restatement of P. Mineiro's fasterlog / fasterlgamma (reference
-// include/utils/fastlog.h:75-85, fastgamma.h:58-60); pinned bit-exactly by tests against
-// the reference headers compiled in oracle/_ref.
-float mmvae_fasterlog(float x) {
-    uint32_t i;
-    std::memcpy(&i, &x, 4);
-    volatile float y = (float)i;
-    y = y * 8.2629582881927490e-8f;
-    return y - 87.989971088f;
-}
-
-float mmvae_fasterlgamma(float x) {
-    volatile float a = -0.0810614667f - x;
-    a = a - mmvae_fasterlog(x);
-    volatile float b = (0.5f + x) * mmvae_fasterlog(1.0f + x);
-    return a + b;
-}
-
-// operators.hh:49-101 (forward) for a scalar kappa; nu = df
-float mmvae_lbessel(float kappa, float nu) {
-    const double nud = nu;
-    const float eta = (float)((nud + 0.5) / (2. * (nud + 1.)));
-    const float lk = std::log(kappa);
-    // stuff1 = nu*log(k) + eta*k - (eta+nu)*log(2) - fasterlgamma(nu+1): ATen float ops with
-    // double scalars rounded to float
-    float s1 = (float)nud * lk;
-    s1 = s1 + eta * kappa;
-    s1 = s1 - (float)(((double)eta + nud) * std::log(2.));
-    s1 = s1 - mmvae_fasterlgamma((float)(nud + 1));
-    float s2 = kappa - 0.5f * lk;
-    s2 = s2 - (float)(0.5 * std::log(2. * M_PI));
-    return (kappa <= nu) ? s1 : s2;
-}
-
-// operators.hh:20-40: Baricz bound, independent of the upstream gradient (Q3)
-float mmvae_lbessel_grad(float kappa, float nu) {
-    const float df = nu;
-    const float lb = std::sqrt(kappa * kappa * df / (float)(df + 1.) + df * df);
-    const float ub = std::sqrt(kappa * kappa + df * df);
-    return 0.5f * (lb + ub) / kappa;
-}
+// ---- operators.hh scalars (host, fp32): include/mmvae/lbessel.hh ---------------------------
+float mmvae_fasterlog(float x) { return mmvae_math::fasterlog(x); }
+float mmvae_fasterlgamma(float x) { return mmvae_math::fasterlgamma(x); }
+float mmvae_lbessel(float kappa, float nu) { return mmvae_math::lbessel(kappa, nu); }
+float mmvae_lbessel_grad(float kappa, float nu) { return mmvae_math::lbessel_grad(kappa, nu); }
 
 }  // extern "C"

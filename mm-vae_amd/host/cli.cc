@@ -24,6 +24,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/mmvae/options.hh"
 #include "../../include/mmvae_host.h"
 #include "cli.hh"
 #include "host_common.hh"
@@ -35,145 +36,55 @@ static bool file_exists(const std::string& f) {
     return !f.empty() && stat(f.c_str(), &st) == 0;
 }
 
-static std::vector<int64_t> split_ints(const std::string& s) {
-    std::vector<int64_t> v;
-    size_t p = 0;
-    while (p <= s.size()) {
-        size_t q = s.find(',', p);
-        if (q == std::string::npos) q = s.size();
-        if (q > p) v.push_back(std::stol(s.substr(p, q - p)));
-        p = q + 1;
-    }
-    return v;
-}
-
-struct ArgvCopy {  // getopt_long permutes argv: every group parses a fresh copy
-    std::vector<std::string> store;
-    std::vector<char*> ptrs;
-    ArgvCopy(int argc, const char** argv) {
-        for (int i = 0; i < argc; ++i) store.emplace_back(argv[i]);
-        for (auto& s : store) ptrs.push_back(&s[0]);
-        ptrs.push_back(nullptr);
-    }
-};
-
-template <class F>
-static void each_opt(int argc, const char** argv, const char* shorts, const option* longs, F&& f) {
-    ArgvCopy a(argc, argv);
-    optind = 1;
-    opterr = 0;
-    while (true) {
-        const int c = getopt_long(argc, a.ptrs.data(), shorts, longs, nullptr);
-        if (c == -1) break;
-        f(c, optarg ? std::string(optarg) : std::string());
-    }
-}
-
 int parse_options(int argc, const char** argv, int model, CliOptions& o) {
-    // ---- mmvae.hh:68-209 ----
-    static const option mm_long[] = {{"mtx", required_argument, nullptr, 'M'},         {"idx", required_argument, nullptr, 'I'},
-                                     {"out", required_argument, nullptr, 'O'},         {"output", required_argument, nullptr, 'O'},
-                                     {"cov", required_argument, nullptr, 'V'},         {"covar", required_argument, nullptr, 'V'},
-                                     {"cov_idx", required_argument, nullptr, 'J'},     {"covar_idx", required_argument, nullptr, 'J'},
-                                     {"row", required_argument, nullptr, 'r'},         {"col", required_argument, nullptr, 'c'},
-                                     {"column", required_argument, nullptr, 'c'},      {"annot", required_argument, nullptr, 'a'},
-                                     {"annotation", required_argument, nullptr, 'a'},  {"batch_size", required_argument, nullptr, 'b'},
-                                     {"batch", required_argument, nullptr, 'b'},       {"kl_discount", required_argument, nullptr, 'K'},
-                                     {"kl_max", required_argument, nullptr, 'L'},      {"kl_min", required_argument, nullptr, 'l'},
-                                     {"help", no_argument, nullptr, 'h'},              {nullptr, no_argument, nullptr, 0}};
-    each_opt(argc, argv, "M:I:O:V:J:r:c:a:b:K:L:l:h?", mm_long, [&](int c, const std::string& v) {
-        switch (c) {
-            case 'M': o.mtx = v; break;
-            case 'I': o.idx = v; break;
-            case 'V': o.covar_mtx = v; break;
-            case 'J': o.covar_idx = v; break;
-            case 'O': o.out = v; break;
-            case 'r': o.row = v; break;
-            case 'c': o.col = v; break;
-            case 'a': o.annot = v; break;
-            case 'b': o.train.batch_size = std::stol(v); break;
-            case 'K': o.train.kl_discount = std::stof(v); break;
-            case 'l': o.train.kl_min = std::stof(v); break;
-            case 'L': o.train.kl_max = std::stof(v); break;
-            case 'h': o.help = true; break;
-            default: break;
-        }
-    });
-    // ---- mmvae_alg.hh:36-125 ----
-    static const option tr_long[] = {{"lr", required_argument, nullptr, 'L'},          {"learning", required_argument, nullptr, 'L'},
-                                     {"learn_rate", required_argument, nullptr, 'L'},  {"learning_rate", required_argument, nullptr, 'L'},
-                                     {"rate", required_argument, nullptr, 'L'},        {"grad_clip", required_argument, nullptr, 'G'},
-                                     {"nboot", required_argument, nullptr, 'B'},       {"boot", required_argument, nullptr, 'B'},
-                                     {"bootstrap", required_argument, nullptr, 'B'},   {"max_epoch", required_argument, nullptr, 'E'},
-                                     {"epoch", required_argument, nullptr, 'E'},       {"recording", required_argument, nullptr, 'R'},
-                                     {"help", no_argument, nullptr, 'h'},              {nullptr, no_argument, nullptr, 0}};
-    each_opt(argc, argv, "L:G:B:E:R:h", tr_long, [&](int c, const std::string& v) {
-        switch (c) {
-            case 'L': o.lr = std::stof(v); break;
-            case 'B': o.train.nboot = std::stol(v); break;
-            case 'E': o.train.max_epoch = std::stol(v); break;
-            case 'R': o.train.recording = std::stol(v); break;
-            // 'G' (--grad_clip) is parsed but never stored by the reference (Q7): clip stays 1
-            default: break;
-        }
-    });
-    // ---- nb.hh:73-194 / vmf.hh:75-186 ----
+    // the reference's three option groups through the drop-in parsers (include/mmvae/options.hh)
+    mmvae_options_t mo;
+    bool help = false;
+    o.mm_rc = parse_mmvae_options(argc, argv, mo, &help);
+    o.help = help;
+    o.mtx = mo.mtx;
+    o.idx = mo.idx;
+    o.out = mo.out;
+    o.row = mo.row;
+    o.col = mo.col;
+    o.annot = mo.annot;
+    o.covar_mtx = mo.covar_mtx;
+    o.covar_idx = mo.covar_idx;
+    o.train.batch_size = mo.batch_size;
+    o.train.kl_discount = mo.kl_discount;
+    o.train.kl_min = mo.kl_min;
+    o.train.kl_max = mo.kl_max;
+    training_options_t to;
+    parse_training_options(argc, argv, to);
+    o.lr = to.lr;
+    o.train.nboot = to.nboot;
+    o.train.max_epoch = to.max_epoch;
+    o.train.recording = to.recording;
     if (model == MMVAE_MODEL_NB) {
-        static const option nb_long[] = {{"mean_encoding", required_argument, nullptr, 'E'},
-                                         {"mean-encoding", required_argument, nullptr, 'E'},
-                                         {"mean_decoding", required_argument, nullptr, 'D'},
-                                         {"mean-decoding", required_argument, nullptr, 'D'},
-                                         {"mean_latent", required_argument, nullptr, 'L'},
-                                         {"mean-latent", required_argument, nullptr, 'L'},
-                                         {"overdisp_encoding", required_argument, nullptr, 'e'},
-                                         {"overdisp-encoding", required_argument, nullptr, 'e'},
-                                         {"overdispersion_encoding", required_argument, nullptr, 'e'},
-                                         {"overdispersion-encoding", required_argument, nullptr, 'e'},
-                                         {"overdispersion_latent", required_argument, nullptr, 'l'},
-                                         {"overdispersion-latent", required_argument, nullptr, 'l'},
-                                         {"relu", no_argument, nullptr, 'R'},
-                                         {"no_relu", no_argument, nullptr, 'r'},
-                                         {"no-relu", no_argument, nullptr, 'r'},
-                                         {"help", no_argument, nullptr, 'h'},
-                                         {nullptr, no_argument, nullptr, 0}};
-        each_opt(argc, argv, "E:D:L:e:l:rRh", nb_long, [&](int c, const std::string& v) {
-            switch (c) {
-                case 'E': o.enc_layers = split_ints(v); break;
-                case 'D': o.dec_layers = split_ints(v); break;
-                case 'L': o.latent = std::stol(v); break;
-                case 'e': o.H = std::stol(v); break;
-                case 'l': o.R = std::stol(v); break;
-                case 'r': o.relu = false; break;
-                case 'R': o.relu = true; break;
-                default: break;
-            }
-        });
+        mmvae::nb::nbvae_options_t nb;
+        parse_nbvae_options(argc, argv, nb);
+        o.enc_layers = nb.mean_encoding_layers;
+        o.dec_layers = nb.mean_decoding_layers;
+        o.latent = nb.mean_latent;
+        o.H = nb.overdispersion_encoding;
+        o.R = nb.overdispersion_latent;
+        o.relu = nb.do_relu;
     } else {
-        static const option vmf_long[] = {{"encoding", required_argument, nullptr, 'E'},  {"decoding", required_argument, nullptr, 'D'},
-                                          {"latent", required_argument, nullptr, 'L'},    {"kappa_min", required_argument, nullptr, 'k'},
-                                          {"kappa-min", required_argument, nullptr, 'k'}, {"kappa_max", required_argument, nullptr, 'K'},
-                                          {"kappa-max", required_argument, nullptr, 'K'}, {"relu", no_argument, nullptr, 'R'},
-                                          {"no_relu", no_argument, nullptr, 'r'},         {"no-relu", no_argument, nullptr, 'r'},
-                                          {"help", no_argument, nullptr, 'h'},            {nullptr, no_argument, nullptr, 0}};
-        each_opt(argc, argv, "E:D:L:k:K:Rrh", vmf_long, [&](int c, const std::string& v) {
-            switch (c) {
-                case 'E': o.enc_layers = split_ints(v); break;
-                case 'D': o.dec_layers = split_ints(v); break;
-                case 'L': o.latent = std::stol(v); break;
-                case 'k': o.kappa_min = std::stof(v); break;
-                case 'K': o.kappa_max = std::stof(v); break;
-                case 'r': o.relu = false; break;
-                case 'R': o.relu = true; break;
-                default: break;
-            }
-        });
+        mmvae::vmf::vmf_options_t vo;
+        parse_vmf_options(argc, argv, vo);
+        o.enc_layers = vo.encoding_layers;
+        o.dec_layers = vo.decoding_layers;
+        o.latent = vo.latent;
+        o.kappa_min = vo.kappa_min;
+        o.kappa_max = vo.kappa_max;
+        o.relu = vo.do_relu;
     }
     // ---- engine options (not in the reference) ----
     static const option en_long[] = {{"seed", required_argument, nullptr, 1},      {"dtype", required_argument, nullptr, 2},
                                      {"device", required_argument, nullptr, 3},    {"threads", required_argument, nullptr, 4},
                                      {"no_csr_cache", no_argument, nullptr, 5},    {"verbose", no_argument, nullptr, 6},
                                      {"quiet", no_argument, nullptr, 7},           {nullptr, no_argument, nullptr, 0}};
-    each_opt(argc, argv, "", en_long, [&](int c, const std::string& v) {
+    mmvae_opt_detail::each_opt(argc, argv, "", en_long, [&](int c, const std::string& v) {
         switch (c) {
             case 1: o.seed = std::stoull(v); break;
             case 2: o.dtype = v; break;
@@ -184,6 +95,7 @@ int parse_options(int argc, const char** argv, int model, CliOptions& o) {
             case 7: o.verbose = false; break;
             default: break;
         }
+        return false;
     });
     if (o.idx.empty()) o.idx = o.mtx + ".index";
     if (o.covar_idx.empty()) o.covar_idx = o.covar_mtx + ".index";
@@ -300,13 +212,9 @@ int run_cli(int argc, const char** argv, int model) {
         std::fputs(usage_text(model), stderr);
         return EXIT_SUCCESS;
     }
-    // mmvae.hh:199-200 and nb_vae_main.cc:51-52
-    if (!file_exists(o.mtx)) {
-        std::fprintf(stderr, "missing mtx file\n%s", usage_text(model));
-        return EXIT_FAILURE;
-    }
-    if (o.out.empty()) {
-        std::fprintf(stderr, "need output file header\n%s", usage_text(model));
+    // mmvae.hh:197-198 (the parser printed the reason) and nb_vae_main.cc:51-52
+    if (o.mm_rc != EXIT_SUCCESS) {
+        std::fputs(usage_text(model), stderr);
         return EXIT_FAILURE;
     }
     if (o.enc_layers.size() > 4 || o.dec_layers.size() > 4) {

@@ -31,6 +31,7 @@ struct CliOptions {
     bool csr_cache = true;
     bool verbose = true;
     bool help = false;
+    int mm_rc = 0;  // parse_mmvae_options' result (EXIT_FAILURE: missing mtx / out)
 };
 
 int parse_options(int argc, const char** argv, int model, CliOptions& o);
