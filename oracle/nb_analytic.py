@@ -31,13 +31,22 @@ def _lgamma(v):
 def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     """Loss and gradients of every registered parameter (pre-clip), kernel algebra.
 
-    P, FR: dicts of float64 arrays with LibTorch names (default architecture: no hidden
-    layers).  x [B,D] dense counts, c [B,C].  n_total = the global batch (DP scaling).
+    P, FR: dicts of float64 arrays with LibTorch names (frozen Sequentials with or without
+    hidden layers).  x [B,D] dense counts, c [B,C].  n_total = the global batch (DP scaling).
     """
+    from .nb_oracle import _layer_order
     B, D = x.shape
     n = float(B if n_total is None else n_total)
-    We, be = FR["mu_enc.mu_encoding.weight"], FR["mu_enc.mu_encoding.bias"]
-    Wd, bd = FR["mu_dec.mu_decoding.weight"], FR["mu_dec.mu_decoding.bias"]
+    # frozen Sequentials (nb.hh:331-379): the first encoder Linear (D -> w0) is the big GEMM of
+    # k_enc_fwd, the other hidden encoder Linears a frozen chain in k_latent_fwd (no ReLU: with
+    # hidden encoder layers --relu is the reference's construction error, Q2); the hidden decoder
+    # Linears (+ ReLU) a chain before the final big decoder GEMM (mu_decoding)
+    enc = sorted({k.rsplit(".", 1)[0] for k in FR if k.startswith("mu_enc.")}, key=_layer_order)
+    dec = sorted({k.rsplit(".", 1)[0] for k in FR if k.startswith("mu_dec.")}, key=_layer_order)
+    We, be = FR[enc[0] + ".weight"], FR[enc[0] + ".bias"]
+    Wd, bd = FR[dec[-1] + ".weight"], FR[dec[-1] + ".bias"]
+    enc_chain = [(FR[k + ".weight"], FR[k + ".bias"]) for k in enc[1:]]
+    dec_chain = [(FR[k + ".weight"], FR[k + ".bias"]) for k in dec[:-1]]
 
     # ---- k_prep: per-gene constants ----------------------------------------------------
     theta = P["ln_x_sd"][0]
@@ -51,6 +60,9 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     h = (l * inv) @ We.T - mvec + be             # == W_e x~ + b_e
     if relu:                                     # nb.hh:345-346: ReLU after mu_encoding
         h = np.maximum(h, 0.0)
+    h0 = h
+    for Wc, bc in enc_chain:                     # k_latent_fwd: frozen encoder chain
+        h = h @ Wc.T + bc
     hnu = x @ P["nu_encoding.weight"].T + P["nu_encoding.bias"]
     pre = x @ P["depth.weight"][0] + P["depth.bias"][0]
 
@@ -61,6 +73,12 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     lnvar = np.clip(a, -4, 4)
     sig = np.exp(lnvar / 2)
     z = mean + eps_mu * sig
+    zs = [z]                                     # k_latent_fwd: frozen decoder chain (ReLU with --relu)
+    for Wc, bc in dec_chain:
+        zs.append(zs[-1] @ Wc.T + bc)
+        if relu:
+            zs[-1] = np.maximum(zs[-1], 0.0)
+    zd = zs[-1]
     nmean = hnu @ P["nu_representation_mean.weight"].T + P["nu_representation_mean.bias"]
     an = hnu @ P["nu_representation_logvariance.weight"].T + P["nu_representation_logvariance.bias"]
     nlnvar = np.clip(an, -4, 4)
@@ -72,7 +90,7 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
 
     # ---- k_dec pass A: log-sum-exp per cell ---------------------------------------------
     bias = bd + P["covar_decoding.bias"] + P["mu_bias"][0]
-    logit = z @ Wd.T + c @ P["covar_decoding.weight"].T + bias
+    logit = zd @ Wd.T + c @ P["covar_decoding.weight"].T + bias
     mx = logit.max(1, keepdims=True)
     lse = mx + np.log(np.exp(logit - mx).sum(1, keepdims=True))
 
@@ -110,7 +128,11 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     G["nu_bias"] = -du.sum(0)[None, :]
 
     # ---- k_latent_bwd ------------------------------------------------------------------
-    dz = d[:, None] * Aprime - S[:, None] * Pb
+    dz = d[:, None] * Aprime - S[:, None] * Pb     # gradient at the decoder GEMM input
+    for i in range(len(dec_chain) - 1, -1, -1):  # back through the decoder chain
+        if relu:
+            dz = dz * (zs[i + 1] > 0)
+        dz = dz @ dec_chain[i][0]
     dmean = dz + (beta / n) * mean
     dlnvar = dz * eps_mu * sig / 2 + (beta / (2 * n)) * (np.exp(lnvar) - 1)
     da = dlnvar * ((a >= -4) & (a <= 4))
@@ -121,8 +143,10 @@ def nb_step_grads(P, FR, x, c, eps_mu, eps_nu, beta, n_total=None, relu=False):
     G["mu_representation_logvariance.weight"] = da.T @ h
     G["mu_representation_logvariance.bias"] = da.sum(0)
     dh = dmean @ P["mu_representation_mean.weight"] + da @ P["mu_representation_logvariance.weight"]
+    for Wc, bc in reversed(enc_chain):           # back through the encoder chain (no ReLU, Q2)
+        dh = dh @ Wc
     if relu:                                     # ReLU backward (mask of the stored output)
-        dh = dh * (h > 0)
+        dh = dh * (h0 > 0)
     dnmean = dznu + (beta / n) * nmean
     dnlnvar = dznu * eps_nu * nsig / 2 + (beta / (2 * n)) * (np.exp(nlnvar) - 1)
     dan = dnlnvar * ((an >= -4) & (an <= 4))

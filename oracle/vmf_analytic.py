@@ -52,12 +52,22 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     n = float(B if n_total is None else n_total)
     epsD = 1e-2 / D
     df = max(0.5 * D - 1.0, 0.0)
-    W = FR["z_enc.0.weight"]
-    Wd, bd = FR["z_dec.decoding.weight"], FR["z_dec.decoding.bias"]
+    from .vmf_oracle import _vlayer_order
+    # frozen Sequentials (vmf.hh:338-385): Angular encoder layers (the first, D -> w0, is the big
+    # GEMM; the rest a chain in k_vlatent_fwd, ReLU after each with --relu), hidden decoder
+    # Linears (+ ReLU) before the final big decoder GEMM
+    enc = sorted({k.rsplit(".", 1)[0] for k in FR if k.startswith("z_enc.")}, key=_vlayer_order)
+    dec = sorted({k.rsplit(".", 1)[0] for k in FR if k.startswith("z_dec.")}, key=_vlayer_order)
+    W = FR[enc[0] + ".weight"]
+    Wd, bd = FR[dec[-1] + ".weight"], FR[dec[-1] + ".bias"]
 
     # ---- k_vnorm_enc (frozen prep): W~ = normalize(relu(W) + 1e-4) --------------------------
-    Wr = np.maximum(W, 0.0) + 1e-4
-    Wt = Wr / np.maximum(np.sqrt((Wr * Wr).sum(1, keepdims=True)), 1e-12)
+    def angular_w(Wa):
+        Wr_ = np.maximum(Wa, 0.0) + 1e-4
+        return Wr_ / np.maximum(np.sqrt((Wr_ * Wr_).sum(1, keepdims=True)), 1e-12)
+    Wt = angular_w(W)
+    enc_chain = [angular_w(FR[k + ".weight"]) for k in enc[1:]]
+    dec_chain = [(FR[k + ".weight"], FR[k + ".bias"]) for k in dec[:-1]]
 
     # ---- k_vprep / k_vmvec -----------------------------------------------------------------
     th = P["ln_x_sd"][0]
@@ -76,12 +86,23 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     h = ((l * inv) @ Wt.T) / nx[:, None] - mvec
     if relu:                                          # vmf.hh:351-352: ReLU after Angular
         h = np.maximum(h, 0.0)
+    hs = [h]                                          # frozen Angular chain (ReLU with --relu)
+    for Wc in enc_chain:
+        hs.append(hs[-1] @ Wc.T)
+        if relu:
+            hs[-1] = np.maximum(hs[-1], 0.0)
+    h = hs[-1]
     mean = h @ P["representation_mean.weight"].T + P["representation_mean.bias"] \
         + c @ P["covar_encoding.weight"].T + P["covar_encoding.bias"]
     a = h @ P["representation_logvariance.weight"].T + P["representation_logvariance.bias"]
     lnvar = np.clip(a, -4, 4)
     sg = np.exp(lnvar / 2)
     z = mean + eps * sg
+    zs = [z]                                          # frozen decoder chain (ReLU with --relu)
+    for Wc, bc in dec_chain:
+        zs.append(zs[-1] @ Wc.T + bc)
+        if relu:
+            zs[-1] = np.maximum(zs[-1], 0.0)
     kl = -0.5 * np.sum(1 + lnvar - mean ** 2 - np.exp(lnvar))
 
     # ---- k_vkappa ----------------------------------------------------------------------------
@@ -93,7 +114,7 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     c2 = 0.5 * D * float(fasterlog(np.float32(2.0 * math.pi)))
 
     # ---- k_vdec<0> + k_vrowfin -----------------------------------------------------------------
-    u = np.exp(z @ Wd.T + bd)
+    u = np.exp(zs[-1] @ Wd.T + bd)
     v = u + c @ P["covar_decoding_.weight"].T + P["covar_decoding_.bias"]
     nvr = np.sqrt((v * v).sum(1))
     nv = np.maximum(nvr, 1e-12)
@@ -112,6 +133,10 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     G["covar_decoding_.bias"] = dv.sum(0)
     G["covar_decoding_.weight"] = dv.T @ c
     dz = da @ Wd
+    for i in range(len(dec_chain) - 1, -1, -1):
+        if relu:
+            dz = dz * (zs[i + 1] > 0)
+        dz = dz @ dec_chain[i][0]
 
     # ---- k_vlatent_bwd -------------------------------------------------------------------------
     bn = beta / n
@@ -125,8 +150,12 @@ def vmf_step_grads(P, FR, x, c, eps, beta, kappa_min=0.1, kappa_max=10.0, n_tota
     G["covar_encoding.weight"] = dmean.T @ c
     G["covar_encoding.bias"] = dmean.sum(0)
     dh = dmean @ P["representation_mean.weight"] + dA @ P["representation_logvariance.weight"]
+    for i in range(len(enc_chain) - 1, -1, -1):
+        if relu:
+            dh = dh * (hs[i + 1] > 0)
+        dh = dh @ enc_chain[i]
     if relu:
-        dh = dh * (h > 0)
+        dh = dh * (hs[0] > 0)
 
     # ---- k_enc_bwd (dh / nx against log1p x) + k_vgrad_genes -----------------------------------
     Gl = ((dh / nx[:, None]).T @ l * Wt).sum(0)      # sum_k W~[k,g] sum_b dh_bk l_bg / nx_b

@@ -66,23 +66,42 @@ def param_names():
             "covar_decoding_.weight", "covar_decoding_.bias"]
 
 
-def init_params(D, C=1, Z=2, kappa_min=0.1, seed=0):
-    """vmf_vae_tImpl::vmf_vae_tImpl (vmf.hh:307-389), default architecture (no hidden layers)."""
+def init_params(D, C=1, Z=2, kappa_min=0.1, seed=0, enc_layers=(), dec_layers=()):
+    """vmf_vae_tImpl::vmf_vae_tImpl (vmf.hh:307-389).  Hidden encoder layers are Angular layers
+    named encoding_l (vmf.hh:338-345); without them one unnamed Angular maps to the latent
+    ("z_enc.0", :348-355).  Hidden decoder layers are Linears decoding_l, then "decoding"."""
     g = torch.Generator().manual_seed(seed)
     p = OrderedDict()
     p["x_mean"] = torch.zeros((1, D), dtype=F32)
     p["ln_x_sd"] = torch.ones((1, D), dtype=F32)
     p["ln_kappa"] = torch.ones((1,), dtype=F32) * float(np.log(np.float32(kappa_min)))  # vmf.hh:323
     fr = OrderedDict()
-    bound = 1.0 / math.sqrt(D)   # Angular: kaiming_uniform_(a = sqrt 5), angular.hh:62
-    fr["z_enc.0.weight"] = (torch.rand((Z, D), generator=g, dtype=F32) * 2 - 1) * bound
+    d_prev = D
+    for l, dn in enumerate(enc_layers):  # Angular: kaiming_uniform_(a = sqrt 5), angular.hh:62
+        fr[f"z_enc.encoding_{l + 1}.weight"] = (torch.rand((dn, d_prev), generator=g, dtype=F32) * 2 - 1) / math.sqrt(d_prev)
+        d_prev = dn
+    if len(enc_layers) < 1:
+        fr["z_enc.0.weight"] = (torch.rand((Z, D), generator=g, dtype=F32) * 2 - 1) / math.sqrt(D)
+        d_prev = Z
     p["covar_encoding.weight"], p["covar_encoding.bias"] = _linear_init(g, Z, C)
-    p["representation_mean.weight"], p["representation_mean.bias"] = _linear_init(g, Z, Z)
-    p["representation_logvariance.weight"], p["representation_logvariance.bias"] = _linear_init(g, Z, Z)
-    fr["z_dec.decoding.weight"], fr["z_dec.decoding.bias"] = _linear_init(g, D, Z)
+    p["representation_mean.weight"], p["representation_mean.bias"] = _linear_init(g, Z, d_prev)
+    p["representation_logvariance.weight"], p["representation_logvariance.bias"] = _linear_init(g, Z, d_prev)
+    d_prev = Z
+    for l, dn in enumerate(dec_layers):
+        fr[f"z_dec.decoding_{l + 1}.weight"], fr[f"z_dec.decoding_{l + 1}.bias"] = _linear_init(g, dn, d_prev)
+        d_prev = dn
+    fr["z_dec.decoding.weight"], fr["z_dec.decoding.bias"] = _linear_init(g, D, d_prev)
     p["covar_decoding_.weight"], p["covar_decoding_.bias"] = _linear_init(g, D, C)
     assert list(p.keys()) == param_names()
     return p, fr
+
+
+def _vlayer_order(k):
+    # "z_enc.encoding_1" < "encoding_2" < ...; the unnamed "z_enc.0" / final "z_dec.decoding" last
+    tail = k.rsplit(".", 1)[1]
+    if "_" in tail and tail.rsplit("_", 1)[1].isdigit():
+        return (0, int(tail.rsplit("_", 1)[1]))
+    return (1, 0)
 
 
 class VMFModel:
@@ -91,23 +110,39 @@ class VMFModel:
         self.fr = OrderedDict((k, v.clone()) for k, v in frozen.items())
         self.kmin, self.kmax = float(np.float32(kappa_min)), float(np.float32(kappa_max))
         self.relu = relu
+        self.enc_keys = sorted({k.rsplit(".", 1)[0] for k in self.fr if k.startswith("z_enc.")}, key=_vlayer_order)
+        self.dec_keys = sorted({k.rsplit(".", 1)[0] for k in self.fr if k.startswith("z_dec.")}, key=_vlayer_order)
 
     def lin(self, name, x):
         return F.linear(x, self.p[name + ".weight"], self.p[name + ".bias"])
 
-    def angular(self, x):
+    def angular(self, x, key="z_enc.0"):
         """angular.hh:34-42: W~ = normalize(relu(W) + 1e-4, dim=1); x W~^T (no bias)."""
-        ww = F.normalize(F.relu(self.fr["z_enc.0.weight"]) + 1e-4, p=2.0, dim=1)
+        ww = F.normalize(F.relu(self.fr[key + ".weight"]) + 1e-4, p=2.0, dim=1)
         return F.linear(x, ww)
+
+    def z_enc(self, x):
+        """The Angular Sequential, a ReLU after every layer with --relu (vmf.hh:338-355)."""
+        for k in self.enc_keys:
+            x = self.angular(x, k)
+            if self.relu:
+                x = F.relu(x)
+        return x
+
+    def z_dec(self, z):
+        """Hidden Linears (+ ReLU with --relu, vmf.hh:374-381), then the final "decoding"."""
+        for i, k in enumerate(self.dec_keys):
+            z = F.linear(z, self.fr[k + ".weight"], self.fr[k + ".bias"])
+            if self.relu and i < len(self.dec_keys) - 1:
+                z = F.relu(z)
+        return z
 
     def encode(self, x, c=None):
         """vmf.hh:250-265 (with covariate) / vmf.hh:267-281 (recorder)."""
         eps = 1e-2 / float(np.float32(x.size(1)))
         xn = F.normalize(x.log1p(), p=2.0, dim=1)
         xn_std = torch.div(torch.sub(xn, self.p["x_mean"]), F.softplus(self.p["ln_x_sd"]) + eps)
-        h = self.angular(xn_std)
-        if self.relu:  # vmf.hh:351-352: z_enc = Angular, ReLU(z_dim)
-            h = F.relu(h)
+        h = self.z_enc(xn_std)
         lnvar = torch.clamp(self.lin("representation_logvariance", h), -4.0, 4.0)
         mean = self.lin("representation_mean", h)
         if c is not None:
@@ -116,7 +151,7 @@ class VMFModel:
 
     def decode(self, z, c):
         """vmf.hh:283-290."""
-        h = torch.exp(F.linear(z, self.fr["z_dec.decoding.weight"], self.fr["z_dec.decoding.bias"]))
+        h = torch.exp(self.z_dec(z))
         hc = self.lin("covar_decoding_", c)
         return F.normalize(h + hc, p=2.0, dim=1)
 

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import nb_oracle, synth, vmf_oracle  # noqa: E402
 
 NB_CASES = [
-    # name, N, D, K, C, H, R, B, steps, lib, seed[, relu]
+    # name, N, D, K, C, H, R, B, steps, lib, seed[, relu, enc_layers, dec_layers]
     ("nb_small", 40, 50, 8, 1, 1, 1, 16, 3, 200.0, 1),
     ("nb_mid", 300, 500, 16, 1, 1, 1, 64, 3, 300.0, 2),
     ("nb_generic", 60, 70, 5, 2, 2, 2, 32, 3, 150.0, 3),
@@ -28,19 +28,24 @@ NB_CASES = [
     ("nb_dups", 10, 40, 8, 1, 1, 1, 24, 2, 120.0, 5),
     ("nb_k64", 128, 256, 64, 1, 1, 1, 128, 2, 500.0, 6),
     ("nb_relu", 100, 300, 16, 1, 1, 1, 64, 3, 300.0, 7, True),
+    ("nb_hidden1", 100, 300, 16, 1, 1, 1, 64, 3, 300.0, 8, False, (24,), (20,)),
+    ("nb_hidden2", 90, 200, 8, 2, 1, 1, 48, 3, 250.0, 9, False, (48, 12), (10, 40)),
+    ("nb_hidden_relu", 90, 200, 16, 1, 1, 1, 48, 3, 250.0, 10, True, (), (32, 20)),
 ]
 
 
-def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed, relu=False):
+def make_nb(name, N, D, K, C, H, R, B, steps, lib, seed, relu=False, enc_layers=(), dec_layers=()):
     rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
     rng = np.random.default_rng(seed + 1000)
     if C == 1:
         covar = np.ones((N, 1), dtype=np.float32)  # nb_vae_main.cc:68-73 auto ones covariate
     else:
         covar = rng.standard_normal((N, C)).astype(np.float32)
-    params, frozen = nb_oracle.init_params(D, C=C, K=K, H=H, R=R, seed=seed)
+    params, frozen = nb_oracle.init_params(D, C=C, K=K, H=H, R=R, seed=seed, enc_layers=enc_layers,
+                                           dec_layers=dec_layers, relu=relu)
     tr = nb_oracle.NBTrainer(params, frozen, relu=relu)
     out = dict(N=N, D=D, K=K, C=C, H=H, R=R, B=B, steps=steps, relu=np.int32(relu),
+               enc_layers=np.array(enc_layers, np.int32), dec_layers=np.array(dec_layers, np.int32),
                rowptr=rowptr, col=col, val=val, covar=covar)
     for k, v in params.items():
         out["init/" + k] = v.numpy()
@@ -95,21 +100,24 @@ VMF_CASES = [
     ("vmf_dups", 10, 40, 8, 1, 24, 2, 120.0, 14, float(np.log(np.float32(0.7)))),
     ("vmf_z64", 100, 300, 64, 1, 64, 2, 400.0, 15, float(np.log(np.float32(9.0)))),
     ("vmf_relu", 100, 300, 16, 1, 64, 3, 300.0, 16, float(np.log(np.float32(3.0))), True),
+    ("vmf_hidden1", 100, 300, 16, 1, 64, 3, 300.0, 17, float(np.log(np.float32(3.0))), False, (24,), (20,)),
+    ("vmf_hidden_relu", 90, 200, 8, 2, 48, 3, 250.0, 18, float(np.log(np.float32(2.0))), True, (40, 12), (10, 30)),
 ]
 
 
-def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa, relu=False):
+def make_vmf(name, N, D, Z, C, B, steps, lib, seed, ln_kappa, relu=False, enc_layers=(), dec_layers=()):
     rowptr, col, val = synth.synth_csr(N, D, lib_size=lib, seed=seed)
     rng = np.random.default_rng(seed + 1000)
     if C == 1:
         covar = np.ones((N, 1), dtype=np.float32)  # vmf_vae_main.cc auto ones covariate
     else:
         covar = rng.standard_normal((N, C)).astype(np.float32)
-    params, frozen = vmf_oracle.init_params(D, C=C, Z=Z, seed=seed)
+    params, frozen = vmf_oracle.init_params(D, C=C, Z=Z, seed=seed, enc_layers=enc_layers, dec_layers=dec_layers)
     if ln_kappa is not None:
         params["ln_kappa"] = torch.tensor([ln_kappa], dtype=torch.float32)
     tr = vmf_oracle.VMFTrainer(params, frozen, relu=relu)
     out = dict(N=N, D=D, K=Z, C=C, H=1, R=1, B=B, steps=steps, model="vmf", relu=np.int32(relu),
+               enc_layers=np.array(enc_layers, np.int32), dec_layers=np.array(dec_layers, np.int32),
                rowptr=rowptr, col=col, val=val, covar=covar)
     for k, v in params.items():
         out["init/" + k] = v.numpy()

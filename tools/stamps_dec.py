@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 os.environ["MMVAE_DBG"] = "64"
 import mmvae_amd
 B, D, K = 4096, 20000, 64
-eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
+eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=os.environ.get("DTYPE", "bf16"), seed=1)
 eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 for i in range(3):
