@@ -99,37 +99,93 @@ static void add_slot(Engine* e, const std::string& n, std::vector<int64_t> shape
     e->slots.push_back(s);
 }
 
+// Frozen hidden chains (nb.hh:331-379, vmf.hh:338-385): the first encoder layer (D -> KE) and
+// the last decoder layer (KD -> D) are the big gene GEMMs; the layers between are small chain
+// layers run inside the latent kernels.  Registers the frozen slots in the reference's names.
+static void build_frozen_chains(Engine* e, bool vmf) {
+    const int64_t D = e->D, K = e->K;
+    const int ne = e->cfg.n_enc_hidden, nd = e->cfg.n_dec_hidden;
+    const std::string ep = vmf ? "z_enc.encoding_" : "mu_enc.mu_encoding_";
+    const std::string dp = vmf ? "z_dec.decoding_" : "mu_dec.mu_decoding_";
+    int nl = 0, off = 0;
+    auto chain_layer = [&](const std::string& w, const std::string& b, int in, int out) {
+        e->ch_w[nl] = w;
+        e->ch_b[nl] = b;
+        e->ch_in[nl] = in;
+        e->ch_out[nl] = out;
+        e->ch_off[nl] = off;
+        off += in * out + out;
+        ++nl;
+    };
+    // encoder: Angular layers have no bias (angular.hh:34-42)
+    if (ne == 0) {
+        const std::string n0 = vmf ? "z_enc.0" : "mu_enc.mu_encoding";
+        add_slot(e, n0 + ".weight", {K, D}, false);
+        if (!vmf) add_slot(e, n0 + ".bias", {K}, false);
+        e->fz_enc_w = n0 + ".weight";
+        e->fz_enc_b = vmf ? "" : n0 + ".bias";
+    }
+    int64_t prev = D;
+    for (int l = 0; l < ne; ++l) {
+        const int64_t wl = e->cfg.enc_hidden[l];
+        const std::string n = ep + std::to_string(l + 1);
+        add_slot(e, n + ".weight", {wl, prev}, false);
+        if (!vmf) add_slot(e, n + ".bias", {wl}, false);
+        if (l == 0) {
+            e->fz_enc_w = n + ".weight";
+            e->fz_enc_b = vmf ? "" : n + ".bias";
+        } else {
+            chain_layer(n + ".weight", vmf ? "" : n + ".bias", (int)prev, (int)wl);
+        }
+        prev = wl;
+    }
+    e->nce = nl;
+    prev = K;
+    for (int l = 0; l < nd; ++l) {
+        const int64_t wl = e->cfg.dec_hidden[l];
+        const std::string n = dp + std::to_string(l + 1);
+        add_slot(e, n + ".weight", {wl, prev}, false);
+        add_slot(e, n + ".bias", {wl}, false);
+        chain_layer(n + ".weight", n + ".bias", (int)prev, (int)wl);
+        prev = wl;
+    }
+    e->ncd = nl - e->nce;
+    const std::string nfin = vmf ? "z_dec.decoding" : "mu_dec.mu_decoding";
+    add_slot(e, nfin + ".weight", {D, prev}, false);
+    add_slot(e, nfin + ".bias", {D}, false);
+    e->fz_dec_w = nfin + ".weight";
+    e->fz_dec_b = nfin + ".bias";
+}
+
 // vmf_vae_tImpl registration order (vmf.hh:318-388); the Angular encoder and the decoder
 // Sequential are never register_module'd (Q1) and stay frozen.
 static void build_registry_vmf(Engine* e) {
-    const int64_t D = e->D, C = e->C, K = e->K;
+    const int64_t D = e->D, C = e->C, K = e->K, E = e->E;
     add_slot(e, "x_mean", {1, D}, true);
     add_slot(e, "ln_x_sd", {1, D}, true);
     add_slot(e, "ln_kappa", {1}, true);
     add_slot(e, "covar_encoding.weight", {K, C}, true);
     add_slot(e, "covar_encoding.bias", {K}, true);
-    add_slot(e, "representation_mean.weight", {K, K}, true);
+    add_slot(e, "representation_mean.weight", {K, E}, true);
     add_slot(e, "representation_mean.bias", {K}, true);
-    add_slot(e, "representation_logvariance.weight", {K, K}, true);
+    add_slot(e, "representation_logvariance.weight", {K, E}, true);
     add_slot(e, "representation_logvariance.bias", {K}, true);
     add_slot(e, "covar_decoding_.weight", {D, C}, true);
     add_slot(e, "covar_decoding_.bias", {D}, true);
-    add_slot(e, "z_enc.0.weight", {K, D}, false);
-    add_slot(e, "z_dec.decoding.weight", {D, K}, false);
-    add_slot(e, "z_dec.decoding.bias", {D}, false);
+    build_frozen_chains(e, true);
 }
 
 static void build_registry_nb(Engine* e) {
-    const int64_t D = e->D, C = e->C, K = e->K, H = e->H, R = e->R;
+    const int64_t D = e->D, C = e->C, K = e->K, H = e->H, R = e->R, E = e->E;
     add_slot(e, "x_mean", {1, D}, true);
     add_slot(e, "ln_x_sd", {1, D}, true);
     add_slot(e, "mu_bias", {1, D}, true);
     add_slot(e, "nu_bias", {1, D}, true);
     add_slot(e, "covar_encoding.weight", {K, C}, true);
     add_slot(e, "covar_encoding.bias", {K}, true);
-    add_slot(e, "mu_representation_mean.weight", {K, K}, true);
+    add_slot(e, "mu_representation_mean.weight", {K, E}, true);
     add_slot(e, "mu_representation_mean.bias", {K}, true);
-    add_slot(e, "mu_representation_logvariance.weight", {K, K}, true);
+    add_slot(e, "mu_representation_logvariance.weight", {K, E}, true);
     add_slot(e, "mu_representation_logvariance.bias", {K}, true);
     add_slot(e, "covar_decoding.weight", {D, C}, true);
     add_slot(e, "covar_decoding.bias", {D}, true);
@@ -144,10 +200,7 @@ static void build_registry_nb(Engine* e) {
     add_slot(e, "depth.weight", {1, D}, true);
     add_slot(e, "depth.bias", {1}, true);
     // frozen Sequentials (Q1: never register_module'd)
-    add_slot(e, "mu_enc.mu_encoding.weight", {K, D}, false);
-    add_slot(e, "mu_enc.mu_encoding.bias", {K}, false);
-    add_slot(e, "mu_dec.mu_decoding.weight", {D, K}, false);
-    add_slot(e, "mu_dec.mu_decoding.bias", {D}, false);
+    build_frozen_chains(e, false);
 }
 
 template <class T>
@@ -194,8 +247,12 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (cfg->model == MMVAE_MODEL_NB && cfg->relu && cfg->n_enc_hidden > 0)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "Submodule 'mu_encoding_1' already defined (reference nb.hh:334-337: "
                                             "--relu with hidden --mean_encoding layers)");
-    if (cfg->n_enc_hidden > 0 || cfg->n_dec_hidden > 0)
-        FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden encoder/decoder layers are not built in this engine yet");
+    for (int l = 0; l < cfg->n_enc_hidden; ++l)
+        if (cfg->enc_hidden[l] < 1 || cfg->enc_hidden[l] > 64)
+            FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden encoder widths must be 1..64 in this engine");
+    for (int l = 0; l < cfg->n_dec_hidden; ++l)
+        if (cfg->dec_hidden[l] < 1 || cfg->dec_hidden[l] > 64)
+            FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden decoder widths must be 1..64 in this engine");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
         FAIL((Engine*)nullptr, MMVAE_E_HIP, "no HIP device " + std::to_string(device));
@@ -208,7 +265,10 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->DP = (cfg->D + 63) / 64 * 64;
     e->NT = e->DP / 64;
     e->K = cfg->K;
-    e->KP = (cfg->K <= 32) ? 32 : 64;
+    e->KE = cfg->n_enc_hidden ? cfg->enc_hidden[0] : cfg->K;
+    e->E = cfg->n_enc_hidden ? cfg->enc_hidden[cfg->n_enc_hidden - 1] : cfg->K;
+    e->KD = cfg->n_dec_hidden ? cfg->dec_hidden[cfg->n_dec_hidden - 1] : cfg->K;
+    e->KP = (std::max(e->K, std::max(e->KE, e->KD)) <= 32) ? 32 : 64;
     e->C = cfg->C;
     e->H = cfg->H;
     e->R = cfg->R;
@@ -264,7 +324,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
 
     // latent state layout
     int64_t o = 0;
-    e->LAT_H = o; o += e->K;
+    e->LAT_H = o; o += e->KE;  // h0: the big encoder GEMM's output (post-ReLU)
     e->LAT_MEAN = o; o += e->K;
     e->LAT_A = o; o += e->K;
     e->LAT_EPS = o; o += e->K;
@@ -279,7 +339,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->lat_stride = o;
 
     const int64_t Bp = e->Bpad, DP = e->DP, KP = e->KP, nrb = e->nrb_max;
-    const int64_t SMALL = 2 * e->K * e->K + 2 * e->K + e->K * e->C + e->K + 2 * e->R * e->H + 2 * e->R + e->H + 1;
+    const int64_t SMALL = small_len((int)e->K, (int)e->E, (int)e->KE, (int)e->C,
+                                    cfg->model == MMVAE_MODEL_VMF ? 0 : (int)(2 * e->R * e->H + 2 * e->R + e->H + 1));
     HIPCHK(e, dalloc(&e->d_params, e->P_reg));
     HIPCHK(e, dalloc(&e->d_grads, e->P_reg));
     HIPCHK(e, dalloc(&e->d_m, e->P_reg));
@@ -333,8 +394,12 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_small, (int64_t)e->n_lat_wg * SMALL));
     HIPCHK(e, dalloc(&e->d_smallg, 128));
     // clip-norm partials: k_sumsq's 256 blocks, or one per gradient-kernel block (NB world 1)
-    HIPCHK(e, dalloc(&e->d_sumsq, 256 + (e->D + 31) / 32 + (2 * e->K * e->K + 4 * e->K + e->K * e->C + 2 * e->R * e->H +
-                                                          2 * e->R + e->H + 1 + 31) / 32 + 1));
+    HIPCHK(e, dalloc(&e->d_sumsq, 256 + (e->D + 31) / 32 + (SMALL + 2 * e->K + 31) / 32 + 1));
+    {
+        int64_t nch = 0;
+        for (int l = 0; l < e->nce + e->ncd; ++l) nch = std::max<int64_t>(nch, e->ch_off[l] + e->ch_in[l] * e->ch_out[l] + e->ch_out[l]);
+        HIPCHK(e, dalloc(&e->d_chain, nch));
+    }
     HIPCHK(e, dalloc(&e->d_out, 4));
     HIPCHK(e, dalloc(&e->d_rowv, Bp));
     HIPCHK(e, dalloc(&e->d_vk, 8));
@@ -356,7 +421,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar};
+                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (e->h_cells_pin) hipHostFree(e->h_cells_pin);  // one block with h_seg_pin / h_perm_pin

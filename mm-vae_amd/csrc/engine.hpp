@@ -42,7 +42,16 @@ struct Engine {
 
     // ---- shapes ----
     int64_t D = 0, DP = 0, NT = 0;  // genes, padded to 64, #64-gene tiles
-    int64_t K = 0, KP = 0;          // latent, padded (32 or 64)
+    int64_t K = 0, KP = 0;          // latent, padded (32 or 64) over K, KE, KD
+    // frozen hidden layers: KE = width of the big encoder GEMM's output (h0), E = input width of
+    // the latent heads, KD = input width of the big decoder GEMM; the small chain layers between
+    // (nce encoder layers, then ncd decoder layers) packed in d_chain (see Dims)
+    int64_t KE = 0, E = 0, KD = 0;
+    int nce = 0, ncd = 0;
+    int ch_in[8] = {}, ch_out[8] = {}, ch_off[8] = {};
+    std::string ch_w[8], ch_b[8];  // frozen slot names of every chain layer (bias "" for Angular)
+    float* d_chain = nullptr;
+    std::string fz_enc_w, fz_enc_b, fz_dec_w, fz_dec_b;  // the big frozen layers' slots
     int64_t C = 1, H = 1, R = 1;
     int64_t Bmax = 0, Bpad = 0;     // max rows, padded (pad_rows)
     int64_t nrb_max = 0;            // row blocks of 64 at Bmax
@@ -203,6 +212,9 @@ hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
 hipError_t enc_forward_launch(Engine* e, const Dims& d, float* hpart);
+// hidden-layer chain fields of Dims, and the chain buffer packing (nb_kernels.hip)
+void dims_hidden(const Engine* e, Dims& d);
+hipError_t pack_chain(Engine* e, bool angular_enc);
 hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const float* Wne, float* rowdots);
 
 // Instantiate f(operand mode, latent padding) for the handle's dtype and KP: the mode is float

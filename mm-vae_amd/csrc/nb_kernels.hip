@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
-    const int K = d.K;
+    const int K = d.K, KE = d.KE, E = d.E;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
     __shared__ float sred[4];
@@ -267,12 +267,12 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     // every global input first, waits in issue order (one memory round, plus one for the loads
     // that depend on a cell id); the per-cell loop below then only stores
     HeadsStage hst;
-    hst.issue(P.Wm, P.Wl, K);
+    hst.issue(P.Wm, P.Wl, K, E);
     const int nqx = 1 + d.H;
     float xs[4];  // raw-count dots (k_batch_lists), lanes < 1 + H
     split_sum4(rowxp, 1, (int64_t)d.Bpad * nqx, (int64_t)bw * nqx + (k < nqx ? k : 0), nqx, k < nqx, xs);
     float hs[4];  // the encoder's gene-split partials of h
-    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
     int pbv[4];
     float cmv[4], epv[4], enp[4];
 #pragma unroll
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         epv[c] = (eps_in && k < K && valid) ? eps_in[(int64_t)pbv[c] * K + k] : 0.f;
         enp[c] = (eps_in && k < d.R && valid) ? eps_in[(int64_t)d.B * K + (int64_t)pbv[c] * d.R + k] : 0.f;
     }
-    hst.store(K, sWm, sWl);
+    if (d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
     mark(1);
     {
         // raw-count dots (+ bias) -> sRX, and rowx for k_latent_bwd
@@ -307,17 +307,25 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     }
     // h = sum of the encoder's gene-split partials - mvec + bias
     const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
-    const float hb = (k < K) ? P.be[k] - mvk : 0.f;
+    const float hb = (k < KE) ? P.be[k] - mvk : 0.f;
     mark(2);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float hv = hb + hs[c];  // mu_enc Linear output; --relu appends ReLU(inplace) (nb.hh:345-346)
-        sH[(4 * w + c) * 68 + k] = (k < K) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
+        sH[(4 * w + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
     }
     __syncthreads();
+    // the frozen encoder chain (hidden mu_encoding_l, l >= 2: nb.hh:331-340) -> the heads' input
+    __shared__ float sZ[2][LAT_CELLS * 68];
+    const float* hin = sH;
+    if (d.nce > 0) {
+        hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[1], false, sWm, w, lane);
+        hst.store(K, E, sWm, sWl);
+        __syncthreads();
+    }
     // heads on f32 MFMA (nb.hh:412-416), transposed back to lane = latent through LDS
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
-    heads_fwd(sH, sWm, sWl, K, w, lane, sM, sA);
+    heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
     __syncthreads();
     mark(3);
     float mean[4], av[4];
@@ -334,7 +342,6 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         const bool valid = b < d.B;
         const int pb = pbv[c];
         float* L = lat + (int64_t)b * d.lat_stride;
-        const float h = sH[(4 * w + c) * 68 + k];
         float mn = mean[c] + cmv[c], a = av[c];
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
         if (mode == 1) {
@@ -349,14 +356,16 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         if (k < K && b < d.B)
             eps = eps_in ? epv[c] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
+        if (k < KE) L[d.LAT_H + k] = sH[(4 * w + c) * 68 + k];
         if (k < K) {
-            L[d.LAT_H + k] = h;
             L[d.LAT_MEAN + k] = mn;
             L[d.LAT_A + k] = a;
             L[d.LAT_EPS + k] = eps;
             if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
         }
-        if (k < d.KP) {
+        if (d.ncd > 0) {
+            sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
+        } else if (k < d.KP) {
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
             put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
@@ -389,6 +398,22 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         }
     }
     if (mode == 1) return;
+    if (d.ncd > 0) {
+        // the frozen decoder chain (mu_decoding_l + ReLU with --relu, nb.hh:362-379): z -> zd,
+        // the big decoder GEMM's input
+        __syncthreads();
+        // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
+        const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[1], sM, false, sWm, w, lane);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            if (k < d.KP) {
+                const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
+                zf[(int64_t)b * d.KP + k] = zz;
+                put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+            }
+        }
+    }
     mark(4);
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
@@ -1209,16 +1234,22 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                                                     const float* __restrict__ dzp, float* __restrict__ dh,
                                                     float* __restrict__ dhT_f, __bf16* __restrict__ dhT_b,
                                                     float* __restrict__ small) {
-    const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP;
-    const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
+    const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP, E = d.E, KE = d.KE;
+    const int SMALL = small_len(K, E, KE, C, 2 * R * H + 2 * R + H + 1);
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     float* sWm = lsm;                 // [K][65]
     float* sWl = sWm + 64 * 65;       // [K][65]
     float* sDM = sWl + 64 * 65;       // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;  // [cell][68] dlnvar-pre-clamp (a)
-    float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h
+    float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h0
     float* wpart = sH + LAT_CELLS * 68; // [4][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
+    // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
+    // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
+    float* sCW = wpart + 4 * NSM;
+    float* const sG0 = sCW + 64 * 65;  // gradient images sG(0), sG(1)
+    auto sG = [&](int i) { return sG0 + i * (LAT_CELLS * 68); };
+    float* cimg = sG0 + 2 * LAT_CELLS * 68;  // [nce + ncd + 1][LAT_CELLS * 68]
     // diagnostic (MMVAE_DBG & 1024): realtime stamps of the phases into slabC (outputs invalid)
     const bool rts = (d.dbg & 1024) != 0;
     uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1230,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // 4 cells per wave
     // ---- every global input first (the waits are in issue order: one memory round) ----
-    const int kk = min(k, K - 1), kr = min(k, R - 1);
+    const int kk = min(k, K - 1), kr = min(k, R - 1), ke = min(k, KE - 1);
     float vval[4], vw[4], vmean[4], va[4], veps[4], vh[4], vnm[4], van[4], ven[4], vpre[4], vrx[4][HMAX];
     int64_t vcell[4];
 #pragma unroll
@@ -1243,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         vmean[c] = L[d.LAT_MEAN + kk];
         va[c] = L[d.LAT_A + kk];
         veps[c] = L[d.LAT_EPS + kk];
-        vh[c] = L[d.LAT_H + kk];
+        vh[c] = L[d.LAT_H + ke];
         vnm[c] = L[d.LAT_NMEAN + kr];
         van[c] = L[d.LAT_AN + kr];
         ven[c] = L[d.LAT_EPSN + kr];
@@ -1253,15 +1284,42 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         for (int hh = 0; hh < HMAX; ++hh) vrx[c][hh] = (hh < H) ? rx[2 + hh] : 0.f;
     }
     HeadsStage hst;
-    hst.issue(P.Wm, P.Wl, K);
-    float dzA4[4], dzP4[4];
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < K, dzA4);
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < K, dzP4);
+    hst.issue(P.Wm, P.Wl, K, E);
+    float dzA4[4], dzP4[4];  // the decoder GEMM input's gradient terms (KD wide)
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < d.KD, dzA4);
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < d.KD, dzP4);
     float E4[4], dzn4[4];  // pass B's per-split row sums: E_b and dL/dznu_b (lanes < R)
     split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R), 2 + R, true, E4);
     split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R) + 2 + kr, 2 + R, k < R, dzn4);
-    hst.store(K, sWm, sWl);
+    hst.store(K, E, sWm, sWl);
     mark(1);
+    // with a decoder chain: dz at the latent = the chain's backward from dzd (z recomputed, the
+    // chain outputs kept for the ReLU masks)
+    const float* dzimg = nullptr;
+    if (d.ncd > 0) {
+        float* zimg = cimg + d.nce * LAT_CELLS * 68;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            const bool valid = (b < d.Bpad) && vval[c] > 0.f;
+            const float lnvar = fminf(fmaxf(va[c], -4.f), 4.f);
+            zimg[(4 * w + c) * 68 + k] = (k < K) ? vmean[c] + veps[c] * expf(lnvar / 2.f) : 0.f;
+            sG(0)[(4 * w + c) * 68 + k] = (k < d.KD && valid) ? vw[c] * (dzA4[c] - E4[c] * dzP4[c]) : 0.f;
+        }
+        __syncthreads();
+        float* outs = zimg + LAT_CELLS * 68;  // decoder chain outputs [ncd]
+        chain_run(d, d.nce, d.nce + d.ncd, zimg, outs, nullptr, true, sCW, w, lane);
+        int g = 0;
+        for (int l = d.ncd - 1; l >= 0; --l) {
+            chain_stage_w(d, d.nce + l, sCW);
+            __syncthreads();
+            const f32x4 acc = chain_bwd(d, d.nce + l, sG(g), outs + l * LAT_CELLS * 68, sCW, d.relu != 0, w, lane);
+            img_store(sG(g ^ 1), acc, w, lane);
+            __syncthreads();
+            g ^= 1;
+        }
+        dzimg = sG(g);
+    }
     mark(2);
     float* wp = wpart + w * NSM;
     float* p_dbm = wp;                 // [64]
@@ -1294,11 +1352,10 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         const bool valid = (b < d.Bpad) && vval[c] > 0.f;
         const float E = E4[c];
         const float wb = vw[c];
-        float dmean = 0.f, da = 0.f, h = 0.f;
+        float dmean = 0.f, da = 0.f;
         if (k < K) {
-            const float dz = wb * (dzA4[c] - E * dzP4[c]);
+            const float dz = dzimg ? dzimg[(4 * w + c) * 68 + k] : wb * (dzA4[c] - E * dzP4[c]);
             const float mean = vmean[c], a = va[c], eps = veps[c];
-            h = vh[c];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
             const float sig = expf(lnvar / 2.f);
             dmean = dz + bn * mean;
@@ -1311,7 +1368,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         }
         sDM[(4 * w + c) * 68 + k] = dmean;
         sDA[(4 * w + c) * 68 + k] = da;
-        sH[(4 * w + c) * 68 + k] = h;
+        sH[(4 * w + c) * 68 + k] = (k < KE) ? vh[c] : 0.f;
         rbm += dmean;
         rbl += da;
 #pragma unroll
@@ -1358,17 +1415,37 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     }
     mark(3);
     __syncthreads();
-    // ---- dh[16 cells][K] on f32 MFMA (wave w: latents 16w..16w+15) ----
+    // the heads' input: h0, or the frozen encoder chain's output (recomputed, outputs kept)
+    const float* hin = sH;
+    if (d.nce > 0) {
+        hin = chain_run(d, 0, d.nce, sH, cimg, nullptr, true, sCW, w, lane);
+    }
+    // ---- dh0[16 cells][KE] on f32 MFMA (wave w: columns 16w..16w+15) ----
     {
-        const f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, w, lane);
+        f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, E, w, lane);
+        if (d.nce > 0) {  // back through the encoder chain
+            img_store(sG(0), acc, w, lane);
+            __syncthreads();
+            int g = 0;
+            for (int l = d.nce - 1; l >= 0; --l) {
+                chain_stage_w(d, l, sCW);
+                __syncthreads();
+                acc = chain_bwd(d, l, sG(g), cimg + l * LAT_CELLS * 68, sCW, d.relu != 0, w, lane);
+                if (l > 0) {
+                    img_store(sG(g ^ 1), acc, w, lane);
+                    __syncthreads();
+                    g ^= 1;
+                }
+            }
+        }
         const int j = 16 * w + (lane & 15);
         float rdhs = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
             if (j < KP) {
-                // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
-                const bool pass = j < K && (!d.relu || sH[cl * 68 + j] > 0.f);
+                // ReLU backward: the gradient passes where the (stored, post-ReLU) h0 is > 0
+                const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
                 dh[(int64_t)b * KP + j] = v;
                 dhT_f[(int64_t)j * d.Bpad + b] = v;
@@ -1396,11 +1473,11 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells on f32 MFMA ----
     float* out = small + (int64_t)blockIdx.x * SMALL;
     mark(4);
-    heads_dW(sDM, sDA, sH, K, w, lane, out);
+    heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     mark(5);
     __syncthreads();
     // ---- the small vectors: fixed-order sum of the four waves' partials ----
-    const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + K,
+    const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + KE,
               o_bnm = o_nm + R * H, o_nl = o_bnm + R, o_bnl = o_nl + R * H, o_bne = o_bnl + R, o_bdp = o_bne + H;
     auto wsum = [&](int off) {
         return (wpart[0 * NSM + off] + wpart[1 * NSM + off]) + (wpart[2 * NSM + off] + wpart[3 * NSM + off]);
@@ -1408,9 +1485,9 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     for (int i = threadIdx.x; i < K; i += 256) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
-        out[o_dhs + i] = wsum(128 + i);
         for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
     }
+    for (int i = threadIdx.x; i < KE; i += 256) out[o_dhs + i] = wsum(128 + i);
     const int b_nm = 192 + 64 * CMAX, b_nl = b_nm + RMAX * HMAX, b_bnm = b_nl + RMAX * HMAX, b_bnl = b_bnm + RMAX,
               b_bne = b_bnl + RMAX, b_bdp = b_bne + HMAX;
     for (int i = threadIdx.x; i < R * H; i += 256) {
@@ -1442,8 +1519,8 @@ MMVAE_DEV void grad_small_body(const Dims& d, const float* __restrict__ small, i
                                float* __restrict__ smallg, const float* __restrict__ lossp, int nlossp,
                                const float* __restrict__ klpart, int nkl, float* __restrict__ out, int with_grads,
                                double* __restrict__ sqpart, const int bid) {
-    const int K = d.K, C = d.C, H = d.H, R = d.R;
-    const int SMALL = 2 * K * K + 2 * K + K * C + K + 2 * R * H + 2 * R + H + 1;
+    const int K = d.K, C = d.C, H = d.H, R = d.R, E = d.E, KE = d.KE;
+    const int SMALL = small_len(K, E, KE, C, 2 * R * H + 2 * R + H + 1);
     if (bid == 0) {
         __shared__ float sb[8];
         float lsum = 0.f, ksum = 0.f;
@@ -1464,18 +1541,18 @@ MMVAE_DEV void grad_small_body(const Dims& d, const float* __restrict__ small, i
     // store the small gradient; returns how many gradient elements received s (0: smallg)
     auto store = [&]() -> int {
     int o = i;
-    if (o < K * K) { G.Wm[o] = s; return 1; }
-    o -= K * K;
-    if (o < K * K) { G.Wl[o] = s; return 1; }
-    o -= K * K;
+    if (o < K * E) { G.Wm[o] = s; return 1; }
+    o -= K * E;
+    if (o < K * E) { G.Wl[o] = s; return 1; }
+    o -= K * E;
     if (o < K) { G.bm[o] = s; G.bce[o] = s; return 2; }
     o -= K;
     if (o < K) { G.bl[o] = s; return 1; }
     o -= K;
     if (o < K * C) { G.Wce[o] = s; return 1; }
     o -= K * C;
-    if (o < K) { smallg[o] = s; return 0; }
-    o -= K;
+    if (o < KE) { smallg[o] = s; return 0; }
+    o -= KE;
     if (o < R * H) { G.Wnm[o] = s; return 1; }
     o -= R * H;
     if (o < R) { G.bnm[o] = s; return 1; }
@@ -1545,7 +1622,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     const int C = SMALL ? 1 : d.C, R = SMALL ? 1 : d.R, H = SMALL ? 1 : d.H;
     const int nqB = (1 + C) + 1 + R, nqC = 1 + C, nqE = 2 + H;
     const int nq = nqB + nqC + nqE;
-    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
+    for (int k = threadIdx.x; k < d.KE; k += 256) cdh[k] = smallg[k];
     const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
     const int g = blockIdx.x * 32 + gi;
     float acc[NQMAX];
@@ -1597,7 +1674,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     // encoder normalisation params (nb.hh:408-410)
     float gs = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < d.K; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
+    for (int k = 0; k < d.KE; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
     const float inv = gene[g];
     put(&G.xm[g], -inv * gs);
     const float th = P.lsd[g];
@@ -1640,10 +1717,10 @@ static NBPtrs nb_ptrs(Engine* e) {
     P.bnd = e->preg("nu_decoding.bias");
     P.wdp = e->preg("depth.weight");
     P.bdp = e->preg("depth.bias");
-    P.We = e->pfrz("mu_enc.mu_encoding.weight");
-    P.be = e->pfrz("mu_enc.mu_encoding.bias");
-    P.Wd = e->pfrz("mu_dec.mu_decoding.weight");
-    P.bd = e->pfrz("mu_dec.mu_decoding.bias");
+    P.We = e->pfrz(e->fz_enc_w);
+    P.be = e->pfrz(e->fz_enc_b);
+    P.Wd = e->pfrz(e->fz_dec_w);
+    P.bd = e->pfrz(e->fz_dec_b);
     return P;
 }
 
@@ -1714,18 +1791,18 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nmv = (int)((e->DP + 255) / 256);
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
     d.relu = e->cfg.relu != 0;
+    dims_hidden(e, d);
     return d;
 }
 
-__global__ void k_pack_frozen(const float* We, const float* Wd, int D, int DP, int K, int KP,
+__global__ void k_pack_frozen(const float* We, const float* Wd, int D, int DP, int KE, int KD, int KP,
                               float* WeP_f, __bf16* WeP_b, float* WdP_f, __bf16* WdP_b, float* WdT_f,
                               __bf16* WdT_b) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)KP * DP) return;
     const int k = (int)(i / DP), g = (int)(i % DP);
-    const bool v = (k < K) && (g < D);
-    const float we = v ? We[(int64_t)k * D + g] : 0.f;
-    const float wd = v ? Wd[(int64_t)g * K + k] : 0.f;
+    const float we = (k < KE && g < D) ? We[(int64_t)k * D + g] : 0.f;   // [KE][D]
+    const float wd = (k < KD && g < D) ? Wd[(int64_t)g * KD + k] : 0.f;  // [D][KD]
     // bf16 images carry the x3 mode's lo planes KP * DP elements after the hi planes
     const int64_t pl = (int64_t)KP * DP;
     WeP_f[i] = we;
@@ -1736,13 +1813,60 @@ __global__ void k_pack_frozen(const float* We, const float* Wd, int D, int DP, i
     put_op<X3>(WdP_b, (int)((int64_t)g * KP + k), (int)pl, wd);
 }
 
+// ---- frozen hidden chains (shared with the vMF engine) ----------------------------------
+void dims_hidden(const Engine* e, Dims& d) {
+    d.KE = (int)e->KE;
+    d.E = (int)e->E;
+    d.KD = (int)e->KD;
+    d.nce = e->nce;
+    d.ncd = e->ncd;
+    for (int l = 0; l < 8; ++l) {
+        d.ch_in[l] = e->ch_in[l];
+        d.ch_out[l] = e->ch_out[l];
+        d.ch_off[l] = e->ch_off[l];
+    }
+    d.chain = e->d_chain;
+}
+
+// one chain layer into the chain buffer: W [out][in] (an Angular layer's normalize(relu(W) +
+// 1e-4) rows, angular.hh:34-42), then the bias (0 without one).  One wave per output row.
+__global__ __launch_bounds__(64) void k_chain_pack(const float* __restrict__ W, const float* __restrict__ b, int in,
+                                                   int out, int angular, float* __restrict__ dst) {
+    const int o = blockIdx.x, lane = threadIdx.x;
+    float ss = 0.f;
+    if (angular) {
+        for (int i = lane; i < in; i += 64) {
+            const float v = fmaxf(W[(int64_t)o * in + i], 0.f) + 1e-4f;
+            ss += v * v;
+        }
+        ss = wave_sum(ss);
+    }
+    const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    for (int i = lane; i < in; i += 64) {
+        const float v = W[(int64_t)o * in + i];
+        dst[(int64_t)o * in + i] = angular ? (fmaxf(v, 0.f) + 1e-4f) * inv : v;
+    }
+    if (lane == 0) dst[(int64_t)in * out + o] = b ? b[o] : 0.f;
+}
+
+hipError_t pack_chain(Engine* e, bool angular_enc) {
+    for (int l = 0; l < e->nce + e->ncd; ++l) {
+        const bool ang = angular_enc && l < e->nce;
+        hipLaunchKernelGGL(k_chain_pack, dim3((unsigned)e->ch_out[l]), dim3(64), 0, e->stream, e->pfrz(e->ch_w[l]),
+                           e->ch_b[l].empty() ? nullptr : e->pfrz(e->ch_b[l]), e->ch_in[l], e->ch_out[l], ang ? 1 : 0,
+                           e->d_chain + e->ch_off[l]);
+    }
+    return hipGetLastError();
+}
+
 hipError_t nb_prepare_frozen(Engine* e) {
     const int64_t n = e->KP * e->DP;
     ScopedTimer tm(e, "k_pack_frozen");
     hipLaunchKernelGGL(k_pack_frozen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
-                       e->pfrz("mu_enc.mu_encoding.weight"), e->pfrz("mu_dec.mu_decoding.weight"), (int)e->D,
-                       (int)e->DP, (int)e->K, (int)e->KP, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b,
-                       e->d_WdT_f, e->d_WdT_b);
+                       e->pfrz(e->fz_enc_w), e->pfrz(e->fz_dec_w), (int)e->D, (int)e->DP, (int)e->KE, (int)e->KD,
+                       (int)e->KP, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b);
+    hipError_t er = pack_chain(e, false);
+    if (er != hipSuccess) return er;
     e->frozen_dirty = false;
     return hipGetLastError();
 }
@@ -1812,6 +1936,15 @@ static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     Q.zplane = (int64_t)d.Bpad * d.KP;
     Q.wplane = (int64_t)e->KP * e->DP;
     return Q;
+}
+
+// k_latent_bwd's LDS: head weights, 3 cell images, the per-wave partials; with hidden layers
+// also the chain W stage, 2 gradient images and the recomputed chain outputs
+static size_t latent_bwd_lds(const Engine* e) {
+    const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * NSM;
+    if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
+    return f * 4;
 }
 
 template <class PM, int KP>
@@ -1891,14 +2024,13 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");
-        const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-        const size_t lds = (size_t)(2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * NSM) * 4;
+        const size_t lds = latent_bwd_lds(e);
         hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
                            e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
-    const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K + 2 * d.R * d.H + 2 * d.R + d.H + 1;
+    const int SMALL = small_len(d.K, d.E, d.KE, d.C, 2 * d.R * d.H + 2 * d.R + d.H + 1);
     const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
     const bool fuse_sq = !split && !(e->comm && e->world > 1);  // no all-reduce after these kernels
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;

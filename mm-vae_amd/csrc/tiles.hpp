@@ -26,7 +26,22 @@ struct Dims {
     int nmv;          // mvec partial blocks (256 genes each) written by the prep kernel
     int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
     int relu;         // ReLU on the frozen encoder's output h (nb.hh:345-346, vmf.hh:351-352)
+    // frozen hidden layers (nb.hh:331-379, vmf.hh:338-385): KE = rows of the big encoder GEMM
+    // (h0), E = input width of the heads, KD = input width of the big decoder GEMM (zd).  Chain
+    // layer l (encoder layers 0 .. nce-1, then decoder layers nce .. nce+ncd-1) is
+    // W [ch_out][ch_in] row-major at chain + ch_off[l], then its bias [ch_out] (zeros for an
+    // Angular layer, whose W is stored normalised: k_chain_pack).  A ReLU follows every chain
+    // layer when relu is set (NB encoder chains never have one: Q2 rejects --relu there).
+    int KE, E, KD;
+    int nce, ncd;
+    int ch_in[8], ch_out[8], ch_off[8];
+    const float* chain;
 };
+
+// Widths and the layout of the per-workgroup partials of the latent-head backward (k_latent_bwd
+// / k_vlatent_bwd -> k_grad_small): dWm [K][E] | dWl [K][E] | dbm [K] | dbl [K] | dWce [K][C] |
+// colsum dh0 [KE] | the NB overdispersion block (nb: 2RH + 2R + H + 1, vMF: 0)
+MMVAE_HOSTDEV int small_len(int K, int E, int KE, int C, int nbx) { return 2 * K * E + 2 * K + K * C + KE + nbx; }
 
 // out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c = 0..3: the split
 // partials of four cells, loads issued four splits at a time (independent, then summed)
@@ -176,15 +191,13 @@ MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL
     return t;
 }
 
-// K x K head weights (K <= 64) into LDS images [k][65]: all 2 x 16 loads of a thread issued
-// before any store (clamped, unconditional addresses — counted waits, not one round trip per
-// element)
-// The K x K head weights (Wm, Wl) into LDS [k][65]: issue() loads into registers (no wait),
-// store() writes LDS — other loads issued between the two share the same memory round.
+// The K x E head weights (Wm, Wl; K, E <= 64) into LDS [k][65]: issue() loads into registers
+// (clamped, unconditional addresses: counted waits), store() writes LDS — other loads issued
+// between the two share the same memory round.
 struct HeadsStage {
     float tm[16], tl[16];
-    MMVAE_DEV void issue(const float* __restrict__ Wm, const float* __restrict__ Wl, int K) {
-        const int KK = K * K;
+    MMVAE_DEV void issue(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, int E) {
+        const int KK = K * E;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const int i = min((int)threadIdx.x + 256 * u, KK - 1);
@@ -192,52 +205,52 @@ struct HeadsStage {
             tl[u] = Wl[i];
         }
     }
-    MMVAE_DEV void store(int K, float* sWm, float* sWl) const {
-        const int KK = K * K;
+    MMVAE_DEV void store(int K, int E, float* sWm, float* sWl) const {
+        const int KK = K * E;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const int i = (int)threadIdx.x + 256 * u;
             if (i < KK) {
-                sWm[(i / K) * 65 + i % K] = tm[u];
-                sWl[(i / K) * 65 + i % K] = tl[u];
+                sWm[(i / E) * 65 + i % E] = tm[u];
+                sWl[(i / E) * 65 + i % E] = tl[u];
             }
         }
     }
 };
-MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, float* sWm,
+MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, int E, float* sWm,
                               float* sWl) {
     HeadsStage hs;
-    hs.issue(Wm, Wl, K);
-    hs.store(K, sWm, sWl);
+    hs.issue(Wm, Wl, K, E);
+    hs.store(K, E, sWm, sWl);
 }
 
-// ---- latent-head backward products on f32 MFMA (exact f32 FMA chains) ------------------
-// LDS images of the workgroup's LAT_CELLS = 16 cells: sDM / sDA / sH [cell][68] (latents >= K
-// hold 0), the head weights sWm / sWl [k][65] (valid for k, j < K).
-// dh[cell][j] = sum_k dmean[cell][k] Wm[k][j] + da[cell][k] Wl[k][j]: wave w owns latents
+// ---- latent-head products on f32 MFMA (exact f32 FMA chains) ---------------------------
+// LDS images of the workgroup's LAT_CELLS = 16 cells: [cell][68], columns 0..63 always written
+// (0 past the width); the head weights sWm / sWl [k][65] (valid for k < K, j < E).
+// dh[cell][j] = sum_k dmean[cell][k] Wm[k][j] + da[cell][k] Wl[k][j]: wave w owns head inputs
 // j = 16 w + (lane & 15); returns the C-layout tile, acc[r] = dh[4 (lane >> 4) + r][j].
-MMVAE_DEV f32x4 heads_dh(const float* sDM, const float* sDA, const float* sWm, const float* sWl, int K, int w,
+MMVAE_DEV f32x4 heads_dh(const float* sDM, const float* sDA, const float* sWm, const float* sWl, int K, int E, int w,
                          int lane) {
     const int j = 16 * w + (lane & 15), row = lane & 15, kq = lane >> 4;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; 4 * s < K; ++s) {
         const int kk = 4 * s + kq;
-        const bool ok = kk < K && j < K;
+        const bool ok = kk < K && j < E;
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sDM[row * 68 + kk], ok ? sWm[kk * 65 + j] : 0.f, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sDA[row * 68 + kk], ok ? sWl[kk * 65 + j] : 0.f, acc, 0, 0, 0);
     }
     return acc;
 }
-// Forward heads for the 16 cells: mean_pre[cell][k] = sum_j h[cell][j] Wm[k][j] (and the
-// same with Wl): wave w owns latents k = 16 w + (lane & 15); the C-layout results are stored
-// to sM / sA [cell][68] (rows 4 (lane >> 4) + r).
-MMVAE_DEV void heads_fwd(const float* sH, const float* sWm, const float* sWl, int K, int w, int lane, float* sM,
+// Forward heads for the 16 cells: mean_pre[cell][k] = sum_j h[cell][j] Wm[k][j] (j < E, and the
+// same with Wl): wave w owns latents k = 16 w + (lane & 15); the C-layout results are stored to
+// sM / sA [cell][68] (rows 4 (lane >> 4) + r).
+MMVAE_DEV void heads_fwd(const float* sH, const float* sWm, const float* sWl, int K, int E, int w, int lane, float* sM,
                          float* sA) {
     const int kc = 16 * w + (lane & 15), row = lane & 15, jq = lane >> 4;
     f32x4 am = f32x4{0.f, 0.f, 0.f, 0.f}, al = am;
-    for (int s = 0; 4 * s < K; ++s) {
+    for (int s = 0; 4 * s < E; ++s) {
         const int jj = 4 * s + jq;
-        const bool ok = jj < K && kc < K;
+        const bool ok = jj < E && kc < K;
         const float hj = sH[row * 68 + jj];
         am = __builtin_amdgcn_mfma_f32_16x16x4f32(hj, ok ? sWm[kc * 65 + jj] : 0.f, am, 0, 0, 0);
         al = __builtin_amdgcn_mfma_f32_16x16x4f32(hj, ok ? sWl[kc * 65 + jj] : 0.f, al, 0, 0, 0);
@@ -249,9 +262,10 @@ MMVAE_DEV void heads_fwd(const float* sH, const float* sWm, const float* sWl, in
     }
 }
 
-// Per-workgroup partials of dWm = dmean^T h and dWl = da^T h over the 16 cells: wave w owns
-// rows k = 16 w .. 16 w + 15; stored [k][j] into out[0 .. K*K) and out[K*K .. 2 K*K).
-MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int K, int w, int lane,
+// Per-workgroup partials of dWm = dmean^T h and dWl = da^T h over the 16 cells (h = the heads'
+// input, E wide): wave w owns rows k = 16 w .. 16 w + 15; stored [k][j] into out[0 .. K*E) and
+// out[K*E .. 2 K*E).
+MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int K, int E, int w, int lane,
                         float* __restrict__ out) {
     const int kr = 16 * w + (lane & 15), cq = lane >> 4, jc = lane & 15;
     f32x4 am[4], al[4];
@@ -276,11 +290,76 @@ MMVAE_DEV void heads_dW(const float* sDM, const float* sDA, const float* sH, int
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int kk = 16 * w + 4 * cq + r, jj = 16 * nb + jc;
-            if (kk < K && jj < K) {
-                out[kk * K + jj] = am[nb][r];
-                out[K * K + kk * K + jj] = al[nb][r];
+            if (kk < K && jj < E) {
+                out[kk * E + jj] = am[nb][r];
+                out[K * E + kk * E + jj] = al[nb][r];
             }
         }
+}
+
+// ---- frozen hidden chains on the same LDS images (f32 MFMA) -----------------------------
+// chain layer l's W into LDS sW [out][65] (all threads; the caller syncs before use)
+MMVAE_DEV void chain_stage_w(const Dims& d, int l, float* sW) {
+    const float* W = d.chain + d.ch_off[l];
+    const int in = d.ch_in[l], n = in * d.ch_out[l];
+    for (int i = threadIdx.x; i < n; i += 256) sW[(i / in) * 65 + i % in] = W[i];
+}
+// sOut = act(sIn W^T + b) over the 16 cells: wave w owns outputs 16 w .. 16 w + 15 (all 64
+// columns of sOut written, 0 past the width)
+MMVAE_DEV void chain_fwd(const Dims& d, int l, const float* sIn, const float* sW, bool relu, int w, int lane,
+                         float* sOut) {
+    const int in = d.ch_in[l], out = d.ch_out[l];
+    const int oc = 16 * w + (lane & 15), row = lane & 15, iq = lane >> 4;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; 4 * s < in; ++s) {
+        const int ii = 4 * s + iq;
+        const bool ok = ii < in && oc < out;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sIn[row * 68 + ii], ok ? sW[oc * 65 + ii] : 0.f, acc, 0, 0, 0);
+    }
+    const float bv = oc < out ? d.chain[d.ch_off[l] + in * out + oc] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v = acc[r] + bv;
+        if (relu) v = fmaxf(v, 0.f);
+        sOut[(4 * iq + r) * 68 + oc] = oc < out ? v : 0.f;
+    }
+}
+// Backward of one chain layer: dIn = (dOut masked by out > 0 when the layer has a ReLU) W.
+// Wave w owns inputs i = 16 w + (lane & 15); returns acc[r] = dIn[4 (lane >> 4) + r][i].
+MMVAE_DEV f32x4 chain_bwd(const Dims& d, int l, const float* sDOut, const float* sOut, const float* sW, bool relu, int w,
+                          int lane) {
+    const int in = d.ch_in[l], out = d.ch_out[l];
+    const int i = 16 * w + (lane & 15), row = lane & 15, oq = lane >> 4;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; 4 * s < out; ++s) {
+        const int oo = 4 * s + oq;
+        float g = sDOut[row * 68 + oo];
+        if (relu && !(sOut[row * 68 + oo] > 0.f)) g = 0.f;
+        const bool ok = oo < out && i < in;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(g, ok ? sW[oo * 65 + i] : 0.f, acc, 0, 0, 0);
+    }
+    return acc;
+}
+// C-layout tile (wave w's 16 columns) -> LDS image
+MMVAE_DEV void img_store(float* sImg, const f32x4& acc, int w, int lane) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sImg[(4 * (lane >> 4) + r) * 68 + 16 * w + (lane & 15)] = acc[r];
+}
+// Run chain layers [l0, l1) forward from image `in`: with keep, layer l's output goes to
+// out0 + (l - l0) images (kept for the backward's ReLU masks), else ping-pong out0 / out1.  W
+// staged through sW.  Returns the final image.  All threads; ends synced.
+MMVAE_DEV const float* chain_run(const Dims& d, int l0, int l1, const float* in, float* out0, float* out1, bool keep,
+                                 float* sW, int w, int lane) {
+    const float* cur = in;
+    for (int l = l0; l < l1; ++l) {
+        chain_stage_w(d, l, sW);
+        __syncthreads();
+        float* o = keep ? out0 + (l - l0) * (LAT_CELLS * 68) : (((l - l0) & 1) ? out1 : out0);
+        chain_fwd(d, l, cur, sW, d.relu != 0, w, lane, o);
+        __syncthreads();
+        cur = o;
+    }
+    return cur;
 }
 
 // LDS carve of k_enc_fwd (host computes the same size); planes = 2 in the x3 mode (hi + lo

@@ -85,12 +85,12 @@ __global__ __launch_bounds__(1024) void k_vnorm_enc(const float* __restrict__ W,
     }
 }
 
-__global__ void k_vpack_dec(const float* Wd, int D, int DP, int K, int KP, float* WdP_f, __bf16* WdP_b, float* WdT_f,
+__global__ void k_vpack_dec(const float* Wd, int D, int DP, int KD, int KP, float* WdP_f, __bf16* WdP_b, float* WdT_f,
                             __bf16* WdT_b) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)KP * DP) return;
     const int k = (int)(i / DP), g = (int)(i % DP);
-    const float wd = (k < K && g < D) ? Wd[(int64_t)g * K + k] : 0.f;
+    const float wd = (k < KD && g < D) ? Wd[(int64_t)g * KD + k] : 0.f;  // [D][KD]
     const int pl = KP * DP;  // the x3 mode's lo planes
     WdT_f[i] = wd;
     put_op<X3>(WdT_b, (int)i, pl, wd);
@@ -158,18 +158,20 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
     uint64_t step, int64_t row_offset,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
-    const int K = d.K;
+    const int K = d.K, KE = d.KE, E = d.E;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
     __shared__ float sred[4];
-    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
+    HeadsStage hst;
+    hst.issue(P.Wm, P.Wl, K, E);
+    if (d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;
     const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
-    const float mk = (k < K) ? mvk : 0.f;
+    const float mk = (k < KE) ? mvk : 0.f;
     float inx[4], hs[4];
-    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < K, hs);
+    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
@@ -181,12 +183,20 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
             rowx[(int64_t)b * d.rowx_stride + 1] = cn.y;
         }
         const float hv = hs[c] * inx[c] - mk;  // Angular output; --relu appends ReLU (vmf.hh:351-352)
-        sH[(4 * w + c) * 68 + k] = (k < K) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
+        sH[(4 * w + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
     }
     __syncthreads();
+    // the frozen Angular chain (encoding_l, l >= 2, + ReLU with --relu: vmf.hh:338-347)
+    __shared__ float sZ[2][LAT_CELLS * 68];
+    const float* hin = sH;
+    if (d.nce > 0) {
+        hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[1], false, sWm, w, lane);
+        hst.store(K, E, sWm, sWl);
+        __syncthreads();
+    }
     // heads on f32 MFMA (vmf.hh:259-264), transposed back to lane = latent through LDS
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
-    heads_fwd(sH, sWm, sWl, K, w, lane, sM, sA);
+    heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
     __syncthreads();
     float mean[4], av[4];
     const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
@@ -202,7 +212,6 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         const int64_t cell = cells[b];  // padding rows hold the empty row N
         const bool valid = b < d.B;
         float* L = lat + (int64_t)b * d.lat_stride;
-        const float h = sH[(4 * w + c) * 68 + k];
         float mn = mean[c];
         const float a = av[c];
         if (k < K && mode == 0) {
@@ -224,14 +233,16 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         if (k < K && b < d.B)
             eps = eps_in ? eps_in[(int64_t)pb * K + k] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
+        if (k < KE) L[d.LAT_H + k] = sH[(4 * w + c) * 68 + k];
         if (k < K) {
-            L[d.LAT_H + k] = h;
             L[d.LAT_MEAN + k] = mn;
             L[d.LAT_A + k] = a;
             L[d.LAT_EPS + k] = eps;
             if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
         }
-        if (k < d.KP) {
+        if (d.ncd > 0) {
+            sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
+        } else if (k < d.KP) {
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
             put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
@@ -242,6 +253,21 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         }
     }
     if (mode == 1) return;
+    if (d.ncd > 0) {
+        // the frozen decoder chain (decoding_l + ReLU with --relu, vmf.hh:374-381): z -> zd
+        __syncthreads();
+        // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
+        const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[1], sM, false, sWm, w, lane);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            if (k < d.KP) {
+                const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
+                zf[(int64_t)b * d.KP + k] = zz;
+                put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+            }
+        }
+    }
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
@@ -612,22 +638,56 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
                                                      const float* __restrict__ covar, const float* __restrict__ lat,
                                                      const float* __restrict__ dzp, float* __restrict__ dhT_f,
                                                      __bf16* __restrict__ dhT_b, float* __restrict__ small) {
-    const int K = d.K, C = d.C, KP = d.KP;
-    const int SMALL = 2 * K * K + 2 * K + K * C + K;
+    const int K = d.K, C = d.C, KP = d.KP, E = d.E, KE = d.KE;
+    const int SMALL = small_len(K, E, KE, C, 0);
     constexpr int NSM = 3 * 64 + 64 * CMAX;
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     float* sWm = lsm;               // [K][65]
     float* sWl = sWm + 64 * 65;     // [K][65]
     float* sDM = sWl + 64 * 65;            // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;     // [cell][68] d(pre-clamp lnvar)
-    float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h
+    float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h0 (column 64: 1/||l||)
     float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [4][NSM]
-    load_heads_lds(P.Wm, P.Wl, K, sWm, sWl);
+    // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
+    // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
+    float* sCW = &wpart[4][0];
+    float* const sG0 = sCW + 64 * 65;  // gradient images sG(0), sG(1)
+    auto sG = [&](int i) { return sG0 + i * (LAT_CELLS * 68); };
+    float* cimg = sG0 + 2 * LAT_CELLS * 68;
+    load_heads_lds(P.Wm, P.Wl, K, E, sWm, sWl);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;
-    float dz4[4];
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * KP, (int64_t)bw * KP + k, KP, k < K, dz4);
+    float dz4[4];  // the decoder GEMM input's gradient (KD wide)
+    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * KP, (int64_t)bw * KP + k, KP, k < d.KD, dz4);
+    // with a decoder chain: dz at the latent = the chain's backward from dzd (z recomputed, the
+    // chain outputs kept for the ReLU masks)
+    const float* dzimg = nullptr;
+    if (d.ncd > 0) {
+        float* zimg = cimg + d.nce * LAT_CELLS * 68;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = bw + c;
+            const float* L = lat + (int64_t)b * d.lat_stride;
+            const int kk = min(k, K - 1);
+            const float lnvar = fminf(fmaxf(L[d.LAT_A + kk], -4.f), 4.f);
+            zimg[(4 * w + c) * 68 + k] = (k < K) ? L[d.LAT_MEAN + kk] + L[d.LAT_EPS + kk] * expf(lnvar / 2.f) : 0.f;
+            sG(0)[(4 * w + c) * 68 + k] = (k < d.KD && L[d.LAT_VALID] > 0.f) ? dz4[c] : 0.f;
+        }
+        __syncthreads();
+        float* outs = zimg + LAT_CELLS * 68;  // decoder chain outputs [ncd]
+        chain_run(d, d.nce, d.nce + d.ncd, zimg, outs, nullptr, true, sCW, w, lane);
+        int g = 0;
+        for (int l = d.ncd - 1; l >= 0; --l) {
+            chain_stage_w(d, d.nce + l, sCW);
+            __syncthreads();
+            const f32x4 acc = chain_bwd(d, d.nce + l, sG(g), outs + l * LAT_CELLS * 68, sCW, d.relu != 0, w, lane);
+            img_store(sG(g ^ 1), acc, w, lane);
+            __syncthreads();
+            g ^= 1;
+        }
+        dzimg = sG(g);
+    }
     const float bn = d.beta * d.inv_n;
     float rbm = 0.f, rbl = 0.f, rWce[CMAX], inx[4];
 #pragma unroll
@@ -638,11 +698,12 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         const float* L = lat + (int64_t)b * d.lat_stride;
         const bool valid = L[d.LAT_VALID] > 0.f;
         inx[c] = L[d.LAT_D];
-        float dmean = 0.f, da = 0.f, h = 0.f;
+        float dmean = 0.f, da = 0.f;
+        const float h = (k < KE) ? L[d.LAT_H + k] : 0.f;
         if (k < K) {
-            const float dz = (c == 0) ? dz4[0] : (c == 1) ? dz4[1] : (c == 2) ? dz4[2] : dz4[3];
+            const float dz = dzimg ? dzimg[(4 * w + c) * 68 + k]
+                                   : (c == 0) ? dz4[0] : (c == 1) ? dz4[1] : (c == 2) ? dz4[2] : dz4[3];
             const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
-            h = L[d.LAT_H + k];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
             const float sig = expf(lnvar / 2.f);
             dmean = dz + bn * mean;
@@ -667,8 +728,28 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
     for (int i = lane; i < NSM; i += 64) wpart[w][i] = 0.f;
     __syncthreads();
     float* wp = wpart[w];
-    {  // dh[16 cells][K] on f32 MFMA (wave w: latents 16w..16w+15), scaled by 1/||l|| for k_enc_bwd
-        const f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, w, lane);
+    // the heads' input: h0, or the Angular chain's output (recomputed, outputs kept)
+    const float* hin = sH;
+    if (d.nce > 0) {
+        hin = chain_run(d, 0, d.nce, sH, cimg, nullptr, true, sCW, w, lane);
+    }
+    {  // dh0[16 cells][KE] on f32 MFMA (wave w: columns 16w..16w+15), scaled by 1/||l|| for k_enc_bwd
+        f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, E, w, lane);
+        if (d.nce > 0) {  // back through the Angular chain
+            img_store(sG(0), acc, w, lane);
+            __syncthreads();
+            int g = 0;
+            for (int l = d.nce - 1; l >= 0; --l) {
+                chain_stage_w(d, l, sCW);
+                __syncthreads();
+                acc = chain_bwd(d, l, sG(g), cimg + l * LAT_CELLS * 68, sCW, d.relu != 0, w, lane);
+                if (l > 0) {
+                    img_store(sG(g ^ 1), acc, w, lane);
+                    __syncthreads();
+                    g ^= 1;
+                }
+            }
+        }
         const int j = 16 * w + (lane & 15);
         float rdhs = 0.f;
 #pragma unroll
@@ -676,7 +757,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
             const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
             if (j < KP) {
                 // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
-                const bool pass = j < K && (!d.relu || sH[cl * 68 + j] > 0.f);
+                const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
                 const float vs = v * sH[cl * 68 + 64];
                 dhT_f[(int64_t)j * d.Bpad + b] = vs;
@@ -692,18 +773,23 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
 #pragma unroll
     for (int q = 0; q < CMAX; ++q) wp[192 + k * CMAX + q] = rWce[q];
     float* out = small + (int64_t)blockIdx.x * SMALL;
-    heads_dW(sDM, sDA, sH, K, w, lane, out);
+    heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     __syncthreads();
-    const int o_bm = 2 * K * K, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
+    const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
     auto wsum = [&](int off) { return (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]); };
     for (int i = threadIdx.x; i < K; i += 256) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
-        out[o_dhs + i] = wsum(128 + i);
         for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
     }
+    for (int i = threadIdx.x; i < KE; i += 256) out[o_dhs + i] = wsum(128 + i);
 }
-static constexpr size_t VLAT_BWD_LDS = (size_t)(2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * (3 * 64 + 64 * CMAX)) * 4;
+// k_vlatent_bwd's LDS (+ the chain W stage, 2 gradient images and the chain outputs with hidden layers)
+static size_t vlat_bwd_lds(const Engine* e) {
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * (3 * 64 + 64 * CMAX);
+    if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
+    return f * 4;
+}
 
 // =======================================================================================
 // k_vgrad_small — block 0: the loss (vmf.hh:429-439) and the ln_kappa gradient
@@ -717,8 +803,8 @@ MMVAE_DEV void vgrad_small_body(const Dims& d, const VScal& sc, const float* __r
                                 const VGrads& G, float* __restrict__ smallg, const float* __restrict__ rowcos,
                                 const float* __restrict__ klpart, int nkl, const float* __restrict__ vk,
                                 float* __restrict__ out, int with_grads, double* __restrict__ sqpart, const int bid) {
-    const int K = d.K, C = d.C;
-    const int SMALL = 2 * K * K + 2 * K + K * C + K;
+    const int K = d.K, C = d.C, E = d.E, KE = d.KE;
+    const int SMALL = small_len(K, E, KE, C, 0);
     if (bid == 0) {
         __shared__ float sb[8];
         float cs = 0.f, ks = 0.f;
@@ -749,10 +835,10 @@ MMVAE_DEV void vgrad_small_body(const Dims& d, const VScal& sc, const float* __r
     // store the small gradient; returns how many gradient elements received s (0: smallg)
     auto store = [&]() -> int {
         int o = i;
-        if (o < K * K) { G.Wm[o] = s; return 1; }
-        o -= K * K;
-        if (o < K * K) { G.Wl[o] = s; return 1; }
-        o -= K * K;
+        if (o < K * E) { G.Wm[o] = s; return 1; }
+        o -= K * E;
+        if (o < K * E) { G.Wl[o] = s; return 1; }
+        o -= K * E;
         if (o < K) { G.bm[o] = s; G.bce[o] = s; return 2; }
         o -= K;
         if (o < K) { G.bl[o] = s; return 1; }
@@ -809,7 +895,7 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
     __shared__ float cdh[64];
     __shared__ float red[NPART - 1][32][NQMAX + 1];
     const int C = d.C, nqB = 1 + C, nq = nqB + 1;
-    for (int k = threadIdx.x; k < d.K; k += 256) cdh[k] = smallg[k];
+    for (int k = threadIdx.x; k < d.KE; k += 256) cdh[k] = smallg[k];
     const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
     const int g = blockIdx.x * 32 + gi;
     float acc[NQMAX];
@@ -843,7 +929,7 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
         if (PART != 1) {
             const float Gl = acc[nqB];
             float gs = 0.f;
-            for (int k = 0; k < d.K; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
+            for (int k = 0; k < d.KE; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
             const float inv = gene[g];
             put(&G.xm[g], -inv * gs);
             put(&G.lsd[g], -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]));
@@ -871,9 +957,9 @@ static VPtrs vmf_ptrs(Engine* e) {
     P.bl = e->preg("representation_logvariance.bias");
     P.Wcd = e->preg("covar_decoding_.weight");
     P.bcd = e->preg("covar_decoding_.bias");
-    P.We = e->pfrz("z_enc.0.weight");
-    P.Wd = e->pfrz("z_dec.decoding.weight");
-    P.bd = e->pfrz("z_dec.decoding.bias");
+    P.We = e->pfrz(e->fz_enc_w);
+    P.Wd = e->pfrz(e->fz_dec_w);
+    P.bd = e->pfrz(e->fz_dec_b);
     return P;
 }
 
@@ -916,12 +1002,14 @@ static VScal vmf_scal(Engine* e) {
 
 hipError_t vmf_prepare_frozen(Engine* e) {
     ScopedTimer tm(e, "k_vpack_frozen");
-    hipLaunchKernelGGL(k_vnorm_enc, dim3((unsigned)e->KP), dim3(1024), 0, e->stream, e->pfrz("z_enc.0.weight"),
-                       (int)e->D, (int)e->DP, (int)e->K, e->d_WeP_f, e->d_WeP_b);
+    hipLaunchKernelGGL(k_vnorm_enc, dim3((unsigned)e->KP), dim3(1024), 0, e->stream, e->pfrz(e->fz_enc_w),
+                       (int)e->D, (int)e->DP, (int)e->KE, e->d_WeP_f, e->d_WeP_b);
     const int64_t n = e->KP * e->DP;
     hipLaunchKernelGGL(k_vpack_dec, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
-                       e->pfrz("z_dec.decoding.weight"), (int)e->D, (int)e->DP, (int)e->K, (int)e->KP, e->d_WdP_f,
+                       e->pfrz(e->fz_dec_w), (int)e->D, (int)e->DP, (int)e->KD, (int)e->KP, e->d_WdP_f,
                        e->d_WdP_b, e->d_WdT_f, e->d_WdT_b);
+    hipError_t er = pack_chain(e, true);
+    if (er != hipSuccess) return er;
     e->frozen_dirty = false;
     return hipGetLastError();
 }
@@ -959,6 +1047,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nmv = (int)((e->DP + 255) / 256);
     d.dbg = 0;
     d.relu = e->cfg.relu != 0;
+    dims_hidden(e, d);
     return d;
 }
 
@@ -1022,7 +1111,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     VGrads G = vmf_grads(e);
-    const int SMALL = 2 * d.K * d.K + 2 * d.K + d.K * d.C + d.K;
+    const int SMALL = small_len(d.K, d.E, d.KE, d.C, 0);
     if (!update) {  // eval: cos_b for the loss (the update path derives it inside k_vdec_bwd)
         {
             ScopedTimer tm(e, "k_vrowfin");
@@ -1050,7 +1139,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");
-        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), VLAT_BWD_LDS, st, P, d, e->d_cells, e->d_covar, e->d_lat,
+        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), vlat_bwd_lds(e), st, P, d, e->d_cells, e->d_covar, e->d_lat,
                            e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials

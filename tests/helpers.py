@@ -36,12 +36,18 @@ def relu_of(z):
     return bool(int(z["relu"])) if "relu" in z else False
 
 
+def hidden_of(z):
+    """(enc_layers, dec_layers) of a fixture: the frozen hidden widths (--mean_encoding ...)."""
+    return tuple(int(v) for v in z.get("enc_layers", ())), tuple(int(v) for v in z.get("dec_layers", ()))
+
+
 def engine_from_fixture(z, dtype="f32"):
     from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
     d = dims(z)
     model = MODEL_VMF if model_of(z) == "vmf" else MODEL_NB
+    enc, dec = hidden_of(z)
     eng = Engine(D=d["D"], K=d["K"], C=d["C"], H=d["H"], R=d["R"], max_batch=max(d["B"], 64), dtype=dtype,
-                 model=model, relu=relu_of(z))
+                 model=model, relu=relu_of(z), enc_hidden=enc, dec_hidden=dec)
     eng.upload_csr(z["rowptr"], z["col"], z["val"], covar=z["covar"])
     eng.set_params(params_of(z, "init/"))
     eng.set_params(params_of(z, "frozen/"))

@@ -64,3 +64,16 @@ def test_create_without_gpu_fails_cleanly():
         pytest.skip("GPU present")
     with pytest.raises(mmvae_amd.MMVAEError):
         mmvae_amd.Engine(D=10, K=2)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    # nb.hh:334-337: --relu with hidden --mean_encoding layers is the reference's construction error (Q2)
+    (dict(relu=True, enc_hidden=(16,)), "mu_encoding_1"),
+    (dict(enc_hidden=(100,)), "hidden encoder widths must be 1..64"),
+    (dict(dec_hidden=(8, 0)), "hidden decoder widths must be 1..64"),
+    (dict(enc_hidden=(8,) * 5), "at most 4"),
+])
+def test_hidden_layer_cfg_validated_before_any_device(kw, msg):
+    """cfg checks of mmvae_create run before the device is touched: the same error here and on a GPU box."""
+    with pytest.raises(mmvae_amd.MMVAEError, match=msg):
+        mmvae_amd.Engine(D=10, K=4, **kw)

@@ -158,8 +158,8 @@ def test_cli_arguments_without_gpu(tmp_path, exe):
     p = tmp_path / "x.mtx"
     p.write_text("%%MatrixMarket matrix coordinate integer general\n3 2 2\n1 1 4\n3 2 1\n")
     r = subprocess.run([b, "--mtx", str(p), "--out", str(tmp_path / "o"), "--mean_encoding" if exe == "nb_vae_main"
-                        else "--encoding", "10"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 1 and "hidden" in r.stderr
+                        else "--encoding", "100"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "hidden encoder widths must be 1..64" in r.stderr  # checked before any device
 
 
 # ---- ${mtx}.index (mmutil_index.hh:38-228) ----------------------------------------------------
