@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary lines, loop and loader")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--kernel-steps", type=int, default=10)
     return ap.parse_args()
 
@@ -104,11 +105,12 @@ def host_cpu():
     return model, (len(cores) or None)
 
 
-def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234):
+def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234, graph=True):
     eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dtype, device=device, seed=seed,
                            model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
     nnz = eng.synth_csr(cells, lib_size=lib, seed=2024)
     eng.init_params(seed=7)
+    eng.graph(graph)  # one hipGraph per step (world 1; steps with a communicator run eagerly)
     return eng, nnz
 
 
@@ -333,7 +335,8 @@ def main():
         args.latent = 32 if args.model == "vmf" else 64
     B, D, K, Ncells = args.batch, args.genes, args.latent, args.cells
     t_setup = time.perf_counter()
-    eng, nnz = make_engine(mmvae_amd, args.model, D, K, B, args.dtype, Ncells, args.lib_size, local)
+    eng, nnz = make_engine(mmvae_amd, args.model, D, K, B, args.dtype, Ncells, args.lib_size, local,
+                           graph=not args.no_graph)
     t_setup = time.perf_counter() - t_setup
     if world > 1:
         obj = [mmvae_amd.Engine.comm_unique_id() if rank == 0 else None]
@@ -385,7 +388,8 @@ def main():
         "config": {"workload": f"{mname}-VAE ELBO step (fwd+bwd+clip+Adam), {Ncells} cells x {D} genes, latent {K}, "
                                f"batch {B}/GPU",
                    "global_batch": B * world, "genes": D, "latent": K, "cells": Ncells,
-                   "nnz_per_cell": round(npc, 1), "parallelism": f"dp{world}"},
+                   "nnz_per_cell": round(npc, 1), "parallelism": f"dp{world}",
+                   "step_graph": (not args.no_graph) and world == 1},
         "roofline": roofline(args.model, args.dtype, D, K, B, npc, per_kernel),
         "composite": composite(args.model, args.dtype, D, K, B, npc, P_reg, ms),
         "device_ms_per_step": round(step_dev_ms, 4),

@@ -185,6 +185,15 @@ int mmvae_debug_copy(mmvae_h h, int32_t which, float* host, int64_t n);
  * out[0] = 64-gene tiles NT, out[1..3] = gene splits of the encoders / decoder pass B /
  * decoder passes A and C (each split walks ceil(NT / splits) tiles). */
 int mmvae_tiling_info(mmvae_h h, int32_t* out4);
+/* Step graphs (the reference's per-batch step, mmvae_alg.hh:254-333, as one hipGraph): with
+ * on != 0, mmvae_run / mmvae_step / mmvae_eval capture their device work (staging copy, kernels,
+ * loss readback) once per launch shape (batch size, n_total, beta, update, injected eps) and
+ * replay it; the step's variable scalars (Philox step / row offset, Adam's bias corrections)
+ * travel in the staged copy.  Results are identical to eager launches.  Not used while kernel
+ * timing is on or a communicator with world > 1 is attached (those steps run eagerly).
+ * graph_stats: captures and replays so far. */
+int mmvae_graph_enable(mmvae_h h, int32_t on);
+int mmvae_graph_stats(mmvae_h h, int64_t* captures, int64_t* replays);
 
 /* ---- operators.hh (vMF observation model scalars) ----------------------------------
  * lbessel(kappa, nu): piecewise log I_nu(kappa) approximation (operators.hh:49-101) with

@@ -208,6 +208,19 @@ static hipError_t dalloc(T** p, int64_t n) {
     return hipMalloc(p, sizeof(T) * (size_t)(n > 0 ? n : 1));
 }
 
+// point the current-slot views at pinned staging slot s
+static void use_slot(Engine* e, int s) {
+    const int64_t Bp = e->Bpad;
+    auto& sl = e->slots2[s];
+    e->cur_slot = s;
+    e->h_cells_pin = sl.block;
+    e->h_seg_pin = sl.block + Bp;
+    e->h_perm_pin = reinterpret_cast<int32_t*>(e->h_seg_pin + Bp / 16 + 1);
+    e->h_ss = reinterpret_cast<StepScalars*>(e->h_perm_pin + Bp);
+    e->h_eps_pin = sl.eps;
+    e->ev_staged = sl.ev;
+}
+
 extern "C" {
 
 void mmvae_cfg_default(mmvae_cfg* c, int32_t model) {
@@ -362,16 +375,20 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // per-step host->device staging in ONE pinned block and ONE device block, so a step issues a
     // single H2D copy (each copy is a ~4.5 us blit on the stream):  cells int64 [Bp] |
     // list segments int64 [Bp/16 + 1] | balancing permutation int32 [Bp]
-    e->stage_bytes = sizeof(int64_t) * (size_t)(Bp + Bp / 16 + 1) + sizeof(int32_t) * (size_t)Bp;
+    e->stage_bytes = sizeof(int64_t) * (size_t)(Bp + Bp / 16 + 1) + sizeof(int32_t) * (size_t)Bp + sizeof(StepScalars);
     HIPCHK(e, hipMalloc((void**)&e->d_cells, e->stage_bytes));
-    HIPCHK(e, hipHostMalloc((void**)&e->h_cells_pin, e->stage_bytes));
     e->d_seg = e->d_cells + Bp;
-    e->h_seg_pin = e->h_cells_pin + Bp;
     e->d_perm = reinterpret_cast<int32_t*>(e->d_seg + Bp / 16 + 1);
-    e->h_perm_pin = reinterpret_cast<int32_t*>(e->h_seg_pin + Bp / 16 + 1);
+    e->d_ss = reinterpret_cast<const StepScalars*>(e->d_perm + Bp);  // 8-aligned: Bp % 128 == 0
+    for (auto& sl : e->slots2) {
+        HIPCHK(e, hipHostMalloc((void**)&sl.block, e->stage_bytes));
+        std::memset(sl.block, 0, e->stage_bytes);
+        HIPCHK(e, hipHostMalloc((void**)&sl.eps, sizeof(float) * Bp * (e->K + e->R)));
+        HIPCHK(e, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    }
+    use_slot(e, 0);
     HIPCHK(e, hipMalloc(&e->d_toff, sizeof(int32_t) * (Bp / 16) * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
-    HIPCHK(e, hipHostMalloc((void**)&e->h_eps_pin, sizeof(float) * Bp * (e->K + e->R)));
     HIPCHK(e, dalloc(&e->d_gene, 10 * DP));
     HIPCHK(e, dalloc(&e->d_mvec, ((DP + 255) / 256) * KP));  // per-256-gene-block partials of mvec
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
@@ -404,8 +421,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_rowv, Bp));
     HIPCHK(e, dalloc(&e->d_vk, 8));
     HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4));
-    HIPCHK(e, hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming));
-    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    for (auto& sl : e->slots2) HIPCHK(e, hipEventRecord(sl.ev, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     *out = e;
     return MMVAE_OK;
@@ -415,6 +431,12 @@ int mmvae_destroy(mmvae_h e) {
     if (!e) return MMVAE_OK;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
+    for (auto& sl : e->slots2) {
+        for (auto& g : sl.graphs) hipGraphExecDestroy(g.second);
+        if (sl.block) hipHostFree(sl.block);
+        if (sl.eps) hipHostFree(sl.eps);
+        if (sl.ev) hipEventDestroy(sl.ev);
+    }
     if (e->comm) ncclCommDestroy(e->comm);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
@@ -424,17 +446,14 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain};
     for (void* b : bufs)
         if (b) hipFree(b);
-    if (e->h_cells_pin) hipHostFree(e->h_cells_pin);  // one block with h_seg_pin / h_perm_pin
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block
         if (b) hipFree(b);
-    if (e->h_eps_pin) hipHostFree(e->h_eps_pin);
     if (e->h_out_pin) hipHostFree(e->h_out_pin);
     for (auto ev : e->event_pool) hipEventDestroy(ev);
     for (auto& p : e->pending) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
     }
-    if (e->ev_staged) hipEventDestroy(e->ev_staged);
     for (auto ev : e->ev_bucket)
         if (ev) hipEventDestroy(ev);
     if (e->ev_comm_done) hipEventDestroy(e->ev_comm_done);
@@ -447,6 +466,7 @@ int mmvae_destroy(mmvae_h e) {
 int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
                      int64_t D, const float* covar) {
     if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
+    ++e->graph_gen;  // dataset buffers are replaced: step graphs are re-captured
     if (D != e->D) FAIL(e, MMVAE_E_ARG, "upload_csr: D does not match the model's data_dim");
     if (rowptr[0] != 0) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr[0] must be 0");
     for (int64_t i = 0; i < N; ++i) {
@@ -505,6 +525,7 @@ int mmvae_dataset_size(mmvae_h e, int64_t* N, int64_t* D) {
 int mmvae_synth_csr(mmvae_h e, int64_t N, double lib_size, uint64_t seed, int64_t* nnz_out) {
     if (!e || N < 1 || lib_size <= 0) FAIL(e, MMVAE_E_ARG, "synth_csr: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
+    ++e->graph_gen;
     HIPCHK(e, synth_dataset(e, N, lib_size, seed, nnz_out));
     return MMVAE_OK;
 }
@@ -683,8 +704,12 @@ static hipError_t build_lists(Engine* e, int64_t B) {
                              e->preg("nu_encoding.weight"), e->d_rowxp);
 }
 
+// host half of a step's staging: rows (+ balancing permutation, list segments) into the pinned
+// block; the one H2D copy of the block is issued by the caller (stage_copy), inside a step graph
+// when one is used
 static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
-    // wait until the previous step's H2D copies have consumed the pinned staging buffers
+    // the other pinned slot: wait until the step staged from it two steps ago is done with it
+    use_slot(e, e->cur_slot ^ 1);
     HIPCHK(e, hipEventSynchronize(e->ev_staged));
     for (int64_t j = 0; j < B; ++j) {
         int64_t r = j;
@@ -726,9 +751,47 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         HIPCHK(e, hipMalloc(&e->d_ents, sizeof(uint2) * e->ent_cap));
         HIPCHK(e, hipMemset(e->d_ents, 0, sizeof(uint2) * e->ent_cap));
     }
-    // cells | segments | permutation: one copy (the pinned block is reused only after ev_staged)
-    HIPCHK(e, hipMemcpyAsync(e->d_cells, e->h_cells_pin, e->stage_bytes, hipMemcpyHostToDevice, e->stream));
     return MMVAE_OK;
+}
+
+// cells | segments | permutation | step scalars: one copy (the pinned block is reused only after
+// ev_staged)
+static hipError_t stage_copy(Engine* e) {
+    return hipMemcpyAsync(e->d_cells, e->h_cells_pin, e->stage_bytes, hipMemcpyHostToDevice, e->stream);
+}
+
+// the device work of one step / eval, in stream order (eager, or captured into a step graph)
+static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
+    const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
+    HIPCHK(e, stage_copy(e));
+    if (a->eps) {
+        const int64_t ne = a->B * (e->K + (vmf ? 0 : e->R));
+        HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
+    }
+    e->grads_reduced = false;
+    e->sq_parts = 0;
+    if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
+    HIPCHK(e, build_lists(e, a->B));
+    if (vmf) HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
+    else HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
+    if (a->update) {
+        if (e->comm && e->world > 1 && !e->grads_reduced) {
+            ScopedTimer tm(e, "allreduce_grads");
+            if (ncclAllReduce(e->d_grads, e->d_grads, (size_t)e->P_reg, ncclFloat, ncclSum, e->comm, e->stream) !=
+                ncclSuccess)
+                FAIL(e, MMVAE_E_COMM, "ncclAllReduce failed");
+        }
+        HIPCHK(e, opt_clip_adam(e));
+    }
+    HIPCHK(e, hipMemcpyAsync(e->h_out_pin, e->d_out, sizeof(float) * 2, hipMemcpyDeviceToHost, e->stream));
+    return MMVAE_OK;
+}
+
+static void graph_drop(Engine* e) {
+    for (auto& sl : e->slots2) {
+        for (auto& g : sl.graphs) hipGraphExecDestroy(g.second);
+        sl.graphs.clear();
+    }
 }
 
 int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* total_norm_out) {
@@ -740,34 +803,65 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     int rc = stage_rows(e, a->cell_ids, a->ridx, a->B, /*balance=*/true);
     if (rc) return rc;
     const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
-    if (a->eps) {
-        const int64_t ne = a->B * (e->K + (vmf ? 0 : e->R));
-        std::memcpy(e->h_eps_pin, a->eps, sizeof(float) * ne);
-        HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
-    }
-    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
-    e->grads_reduced = false;
-    e->sq_parts = 0;
-    if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
-    HIPCHK(e, build_lists(e, a->B));
-    if (vmf)
-        HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
-                                       a->row_offset));
-    else
-        HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr, a->step_id,
-                                      a->row_offset));
-    if (a->update) {
-        if (e->comm && e->world > 1 && !e->grads_reduced) {
-            ScopedTimer tm(e, "allreduce_grads");
-            if (ncclAllReduce(e->d_grads, e->d_grads, (size_t)e->P_reg, ncclFloat, ncclSum, e->comm, e->stream) !=
-                ncclSuccess)
-                FAIL(e, MMVAE_E_COMM, "ncclAllReduce failed");
+    if (a->eps) std::memcpy(e->h_eps_pin, a->eps, sizeof(float) * a->B * (e->K + (vmf ? 0 : e->R)));
+    // the step's scalars travel in the staged block (the kernels read them from there)
+    e->h_ss->step_id = (int64_t)a->step_id;
+    e->h_ss->row_offset = a->row_offset;
+    if (a->update) adam_scalars(e, e->adam_step + 1, e->h_ss);
+    // frozen operands are repacked eagerly, never inside a step graph
+    if (e->frozen_dirty) HIPCHK(e, vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
+    // one hipGraph per step: captured on the first step of a launch shape,
+    // replayed while the shape holds; not with timers, diagnostics or a communicator (the RCCL
+    // calls stay eager)
+    static const bool dbg_env = std::getenv("MMVAE_DBG") != nullptr;
+    const bool use_graph = e->graph_on && !e->timing && !dbg_env && !(e->comm && e->world > 1);
+    if (use_graph) {
+        GraphKey k;
+        k.B = a->B;
+        k.n_total = n_total;
+        std::memcpy(&k.beta_bits, &a->beta, 4);
+        k.update = a->update != 0;
+        k.use_eps = a->eps != nullptr;
+        k.perm = e->perm_active;
+        k.ents = e->d_ents;
+        k.gen = e->graph_gen;
+        Engine::StageSlot& sl = e->slots2[e->cur_slot];
+        hipGraphExec_t gx = nullptr;
+        for (auto& g : sl.graphs)
+            if (g.first == k) gx = g.second;
+        if (!gx) {
+            constexpr size_t MAX_GRAPHS = 4;  // per slot; the oldest is dropped
+            if (sl.graphs.size() >= MAX_GRAPHS) {
+                hipGraphExecDestroy(sl.graphs.front().second);
+                sl.graphs.erase(sl.graphs.begin());
+            }
+            HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+            const int crc = enqueue_run(e, a, n_total);
+            hipGraph_t g = nullptr;
+            const hipError_t ce = hipStreamEndCapture(e->stream, &g);
+            if (crc) {
+                if (g) hipGraphDestroy(g);
+                return crc;
+            }
+            HIPCHK(e, ce);
+            const hipError_t ie = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            HIPCHK(e, ie);
+            sl.graphs.emplace_back(k, gx);
+            ++e->graph_captures;
         }
-        HIPCHK(e, opt_clip_adam(e));
+        HIPCHK(e, hipGraphLaunch(gx, e->stream));
+        ++e->graph_replays;
+    } else {
+        rc = enqueue_run(e, a, n_total);
+        if (rc) return rc;
+    }
+    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));  // this slot's block is free after this step
+    if (a->update) {
+        e->adam_step += 1;
         e->have_grads = true;
     }
     if (loss_out || total_norm_out) {
-        HIPCHK(e, hipMemcpyAsync(e->h_out_pin, e->d_out, sizeof(float) * 2, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (loss_out) *loss_out = e->h_out_pin[0];
         if (total_norm_out) *total_norm_out = a->update ? (double)e->h_out_pin[1] : 0.0;
@@ -808,6 +902,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
+    HIPCHK(e, stage_copy(e));
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
     if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));
     HIPCHK(e, build_lists(e, B));
@@ -847,6 +942,7 @@ static void build_buckets(Engine* e);
 int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (!e || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
+    ++e->graph_gen;  // rank-dependent launches (the vMF rank-0 term, bucket split) are re-captured
     if (!id128) {
         // local decomposition mode (tests): this handle computes rank `rank`'s shard of a
         // world-`world` step (rank-0-only terms included) but reduces nothing — the caller sums
@@ -1000,6 +1096,22 @@ int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     const float* src = which == 0 ? e->d_hpart : which == 1 ? e->d_dzp : e->d_slabC;
     HIPCHK(e, hipMemcpy(host, src, sizeof(float) * n, hipMemcpyDeviceToHost));
+    return MMVAE_OK;
+}
+
+int mmvae_graph_enable(mmvae_h e, int32_t on) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "graph_enable: null");
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->graph_on = on != 0;
+    if (!e->graph_on) graph_drop(e);
+    return MMVAE_OK;
+}
+
+int mmvae_graph_stats(mmvae_h e, int64_t* captures, int64_t* replays) {
+    if (!e || !captures || !replays) FAIL(e, MMVAE_E_ARG, "graph_stats: null");
+    *captures = e->graph_captures;
+    *replays = e->graph_replays;
     return MMVAE_OK;
 }
 

@@ -27,6 +27,28 @@ struct ParamSlot {
     bool registered = true;
 };
 
+// Per-step scalars staged with the batch (in the same H2D copy) and read by the kernels, so a
+// captured step graph replays unchanged with each step's values: the Philox noise key (step,
+// global row offset) and Adam's bias-corrected rates (optim/adam.cpp).
+struct StepScalars {
+    int64_t step_id, row_offset;
+    float lr_bc1, inv_sqrt_bc2;
+    int64_t pad;
+};
+
+// launch shape of a captured step graph: replayed while every field matches
+struct GraphKey {
+    int64_t B = -1, n_total = 0;
+    uint32_t beta_bits = 0;
+    int update = 0, use_eps = 0, perm = 0;
+    const void* ents = nullptr;
+    uint64_t gen = 0;
+    bool operator==(const GraphKey& o) const {
+        return B == o.B && n_total == o.n_total && beta_bits == o.beta_bits && update == o.update &&
+               use_eps == o.use_eps && perm == o.perm && ents == o.ents && gen == o.gen;
+    }
+};
+
 struct TimerRec {
     std::string name;
     double total_ms = 0;
@@ -89,6 +111,8 @@ struct Engine {
     int64_t* h_cells_pin = nullptr;  // pinned staging
     int32_t* h_perm_pin = nullptr;   // pinned: original batch position of every (balanced) row
     int32_t* d_perm = nullptr;       // [Bpad]
+    StepScalars* h_ss = nullptr;     // pinned: this step's scalars (end of the staging block)
+    const StepScalars* d_ss = nullptr;
     bool perm_active = false;        // the last staged batch was reordered (noise keyed by d_perm)
     std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing, lists)
     // per-step batch entry lists (batch.hip)
@@ -135,7 +159,20 @@ struct Engine {
     int nsplit_a = 1;                // D-split of decoder passes A / C
     int n_lat_wg = 1;                // latent kernels' workgroups
     int64_t klp_off = 0;             // offset of KL partials inside d_lossp
-    hipEvent_t ev_staged = nullptr;  // last H2D copy out of the pinned staging buffers
+    hipEvent_t ev_staged = nullptr;  // the current slot's: its last step is done with the pinned block
+    // double-buffered pinned staging: the host fills slot s while the step staged from slot s ^ 1
+    // runs; h_cells_pin / h_seg_pin / h_perm_pin / h_ss / h_eps_pin / ev_staged view the current
+    // slot.  A step graph copies from its slot's block, so each slot has its own graph.
+    struct StageSlot {
+        int64_t* block = nullptr;  // cells | seg | perm | StepScalars
+        float* eps = nullptr;
+        hipEvent_t ev = nullptr;
+        // captured step graphs of this slot by launch shape (the training loop alternates an eval
+        // forward and bootstrap updates, and the last batch of an epoch is ragged)
+        std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;
+    };
+    StageSlot slots2[2];
+    int cur_slot = 0;
     float* d_tmp = nullptr;          // encode outputs
     float* d_tmp_ar = nullptr;       // host-value all-reduce staging
     int64_t n_tmp_ar = 0;
@@ -153,6 +190,11 @@ struct Engine {
     bool grads_reduced = false;
     uint64_t auto_step = 0;  // Philox step counter of mmvae_step / mmvae_eval
     size_t stage_bytes = 0;  // the per-step H2D staging block (cells | seg | perm)  // set by a model step that already all-reduced its buckets
+
+    // ---- step graphs (A17: one hipGraph per step, mmvae_graph_enable) ----
+    bool graph_on = false;
+    uint64_t graph_gen = 0;          // bumped when a buffer a step graph points at is replaced
+    int64_t graph_captures = 0, graph_replays = 0;
 
     // ---- timing ----
     bool timing = false;
@@ -201,13 +243,11 @@ bool split_grads(const Engine* e);
 // all-reduce gradient bucket b on the comm stream after the work queued so far on e->stream;
 // bucket 1 also makes e->stream wait for both buckets.  No-op without a communicator.
 hipError_t comm_bucket(Engine* e, int b);
-hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
-                               bool use_eps, uint64_t step_id, int64_t row_offset);
+hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // vMF launchers (vmf_kernels.hip)
 hipError_t vmf_prepare_frozen(Engine* e);
-hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update,
-                                bool use_eps, uint64_t step_id, int64_t row_offset);
+hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps);
 hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // encoder kernels shared by both models (nb_kernels.hip)
 struct Dims;
@@ -235,6 +275,7 @@ hipError_t dispatch_mode(const Engine* e, F&& f) {
 }
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
+void adam_scalars(const Engine* e, int64_t t, StepScalars* ss);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
 hipError_t build_dataset_index(Engine* e);
 

@@ -246,10 +246,12 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowxp,
     float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
-    uint64_t step, int64_t row_offset,
+    const StepScalars* __restrict__ ss,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K, KE = d.KE, E = d.E;
+    const uint64_t step = (uint64_t)ss->step_id;  // the noise key (staged with the batch)
+    const int64_t row_offset = ss->row_offset;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
     __shared__ float sred[4];
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         }
         if (d.ncd > 0) {
             sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
-        } else if (k < d.KP) {
+        } else if (k < d.KP && b < d.Bpad) {  // rows past this batch's padded size: none
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
             put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int b = bw + c;
-            if (k < d.KP) {
+            if (k < d.KP && b < d.Bpad) {
                 const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
                 zf[(int64_t)b * d.KP + k] = zz;
                 put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
@@ -1443,7 +1445,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
-            if (j < KP) {
+            if (j < KP && b < d.Bpad) {  // [KP][Bpad] images: rows past this batch's padded size write nothing
                 // ReLU backward: the gradient passes where the (stored, post-ReLU) h0 is > 0
                 const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
@@ -1948,8 +1950,7 @@ static size_t latent_bwd_lds(const Engine* e) {
 }
 
 template <class PM, int KP>
-static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps,
-                                uint64_t step_id, int64_t row_offset) {
+static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps) {
     using T = typename Elem<PM>::type;
     constexpr bool X = IsX3<PM>::value;
     constexpr int NPL = X ? 2 : 1;
@@ -1965,8 +1966,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         ScopedTimer tm(e, "k_latent_fwd");
         hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                            e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr,
-                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, step_id,
-                           row_offset, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
+                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, e->d_ss, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
     }
     const DecPtrs Q = dec_ptrs(e, d, P, bf);
     const bool small_cr = (d.C == 1 && d.R == 1);
@@ -2096,8 +2096,7 @@ hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
     return hipGetLastError();
 }
 
-hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,
-                               uint64_t step_id, int64_t row_offset) {
+hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps) {
     if (e->frozen_dirty) {
         hipError_t er = nb_prepare_frozen(e);
         if (er != hipSuccess) return er;
@@ -2105,7 +2104,7 @@ hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta
     const Dims d = nb_dims(e, B, n_total, beta);
     const NBPtrs P = nb_ptrs(e);
     return dispatch_mode(e, [&](auto p, auto kp) {
-        return nb_launch_all<decltype(p), decltype(kp)::value>(e, d, P, update, use_eps, step_id, row_offset);
+        return nb_launch_all<decltype(p), decltype(kp)::value>(e, d, P, update, use_eps);
     });
 }
 
@@ -2114,8 +2113,8 @@ static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* 
     hipStream_t st = e->stream;
     enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, (uint64_t)0,
-                       (int64_t)0, e->d_lat,
+                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, e->d_ss,
+                       e->d_lat,
                        e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
     return hipGetLastError();
 }

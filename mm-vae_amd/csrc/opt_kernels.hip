@@ -25,8 +25,9 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ g, int6
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, int64_t n,
                                               const double* __restrict__ part, int nparts, float max_norm,
-                                              float lr_bc1, float inv_sqrt_bc2, float b1, float b2, float wd,
+                                              const StepScalars* __restrict__ ss, float b1, float b2, float wd,
                                               float eps, float* __restrict__ out) {
+    const float lr_bc1 = ss->lr_bc1, inv_sqrt_bc2 = ss->inv_sqrt_bc2;  // this step's (staged with the batch)
     __shared__ float s_coef;
     __shared__ double sb[4];
     double tp = 0.0;
@@ -57,11 +58,17 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
     }
 }
 
+// Adam's bias-corrected rates of optimiser step t (optim/adam.cpp), into the staged scalars
+void adam_scalars(const Engine* e, int64_t t, StepScalars* ss) {
+    const double bc1 = 1.0 - std::pow(0.9, (double)t);
+    const double bc2 = 1.0 - std::pow(0.999, (double)t);
+    ss->lr_bc1 = (float)(e->cfg.lr / bc1);
+    ss->inv_sqrt_bc2 = (float)(1.0 / std::sqrt(bc2));
+}
+
+// the staged scalars of the step hold adam_scalars(adam_step) (mmvae_run)
 hipError_t opt_clip_adam(Engine* e) {
-    e->adam_step += 1;
     const double b1 = 0.9, b2 = 0.999;
-    const double bc1 = 1.0 - std::pow(b1, (double)e->adam_step);
-    const double bc2 = 1.0 - std::pow(b2, (double)e->adam_step);
     const int64_t n = e->P_reg;
     // the NB world-1 step leaves its own partials (gradient kernels, one per block); otherwise
     // (vMF, or gradients all-reduced after the gradient kernels) k_sumsq computes them
@@ -74,8 +81,8 @@ hipError_t opt_clip_adam(Engine* e) {
     {
         ScopedTimer tm(e, "k_adam");
         hipLaunchKernelGGL(k_adam, dim3(SUMSQ_BLOCKS), dim3(256), 0, e->stream, e->d_params, e->d_grads, e->d_m,
-                           e->d_v, n, e->d_sumsq, nparts, e->cfg.grad_clip, (float)(e->cfg.lr / bc1),
-                           (float)(1.0 / std::sqrt(bc2)), (float)b1, (float)b2, e->cfg.weight_decay, 1e-8f,
+                           e->d_v, n, e->d_sumsq, nparts, e->cfg.grad_clip, e->d_ss, (float)b1, (float)b2,
+                           e->cfg.weight_decay, 1e-8f,
                            e->d_out);
     }
     return hipGetLastError();

@@ -155,10 +155,12 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
     VPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float2* __restrict__ cellnorm,
     float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
-    uint64_t step, int64_t row_offset,
+    const StepScalars* __restrict__ ss,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
     const int K = d.K, KE = d.KE, E = d.E;
+    const uint64_t step = (uint64_t)ss->step_id;  // the noise key (staged with the batch)
+    const int64_t row_offset = ss->row_offset;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
     __shared__ float sred[4];
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         }
         if (d.ncd > 0) {
             sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
-        } else if (k < d.KP) {
+        } else if (k < d.KP && b < d.Bpad) {  // rows past this batch's padded size: none
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
             put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int b = bw + c;
-            if (k < d.KP) {
+            if (k < d.KP && b < d.Bpad) {
                 const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
                 zf[(int64_t)b * d.KP + k] = zz;
                 put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
@@ -755,7 +757,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int cl = 4 * (lane >> 4) + r, b = blockIdx.x * LAT_CELLS + cl;
-            if (j < KP) {
+            if (j < KP && b < d.Bpad) {  // [KP][Bpad] images: rows past this batch's padded size write nothing
                 // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
                 const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
@@ -1053,7 +1055,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
 
 template <class PM, int KP>
 static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const VScal& sc, bool update,
-                                 bool use_eps, uint64_t step_id, int64_t row_offset, int mode, float* out_mean,
+                                 bool use_eps, int mode, float* out_mean,
                                  float* out_lnvar) {
     using T = typename Elem<PM>::type;
     constexpr int NPL = IsX3<PM>::value ? 2 : 1;
@@ -1075,7 +1077,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         ScopedTimer tm(e, "k_vlatent_fwd");
         hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
                            e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr,
-                           (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, step_id, row_offset,
+                           (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, e->d_ss,
                            e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
     }
     if (mode == 1) return hipGetLastError();
@@ -1183,14 +1185,13 @@ static hipError_t vmf_dispatch(Engine* e, A... a) {
     return dispatch_mode(e, [&](auto p, auto kp) { return vmf_launch_all<decltype(p), decltype(kp)::value>(e, a...); });
 }
 
-hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps,
-                                uint64_t step_id, int64_t row_offset) {
+hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps) {
     if (e->frozen_dirty) {
         hipError_t er = vmf_prepare_frozen(e);
         if (er != hipSuccess) return er;
     }
     const Dims d = vmf_dims(e, B, n_total, beta);
-    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), update, use_eps, step_id, row_offset, 0, (float*)nullptr,
+    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), update, use_eps, 0, (float*)nullptr,
                         (float*)nullptr);
 }
 
@@ -1200,7 +1201,7 @@ hipError_t vmf_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
         if (er != hipSuccess) return er;
     }
     const Dims d = vmf_dims(e, B, B, 1.f);
-    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), false, false, (uint64_t)0, (int64_t)0, 1, d_mean, d_lnvar);
+    return vmf_dispatch(e, d, vmf_ptrs(e), vmf_scal(e), false, false, 1, d_mean, d_lnvar);
 }
 
 }  // namespace mmvae

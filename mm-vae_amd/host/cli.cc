@@ -295,6 +295,8 @@ int run_cli(int argc, const char** argv, int model) {
     int rc = mmvae_upload_csr(h, csr.rowptr, csr.col, csr.val, csr.N, csr.D, covar.empty() ? nullptr : covar.data());
     mmvae_csr_free(&csr);
     if (!rc) rc = mmvae_init_params(h, o.seed);
+    // one hipGraph per step shape (single-rank runs; with a communicator the steps stay eager)
+    if (!rc && !std::getenv("MMVAE_NO_GRAPH")) rc = mmvae_graph_enable(h, 1);
     RcclIdCleanup id_cleanup;
     id_cleanup.path = rccl_id_path(o);
     id_cleanup.armed = world > 1 && rank == 0;

@@ -86,6 +86,8 @@ def lib():
         "mmvae_timing_reset": (ctypes.c_int, [h]),
         "mmvae_debug_copy": (ctypes.c_int, [h, i32, f32p, i64]),
         "mmvae_tiling_info": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
+        "mmvae_graph_enable": (ctypes.c_int, [h, i32]),
+        "mmvae_graph_stats": (ctypes.c_int, [h, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "mmvae_lbessel": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_lbessel_grad": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_fasterlog": (ctypes.c_float, [ctypes.c_float]),
@@ -297,6 +299,15 @@ class Engine:
         for k in ("enc", "dec", "ac"):
             out["tps_" + k] = -(-NT // out["split_" + k])
         return out
+
+    def graph(self, on=True):
+        """Capture / replay each step's device work as one hipGraph (mmvae_graph_enable)."""
+        self._chk(lib().mmvae_graph_enable(self._h, 1 if on else 0), "graph_enable")
+
+    def graph_stats(self):
+        c, r = ctypes.c_int64(), ctypes.c_int64()
+        self._chk(lib().mmvae_graph_stats(self._h, ctypes.byref(c), ctypes.byref(r)), "graph_stats")
+        return {"captures": c.value, "replays": r.value}
 
     # ---- timing ----
     def timing(self, on=True):
