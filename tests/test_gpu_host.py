@@ -168,3 +168,68 @@ def test_cli_end_to_end(tmp_path, model):
     host.train(eng2, batch_size=64, max_epoch=2, nboot=2, seed=3, recording=1000)
     em, _ = eng2.encode(np.arange(256, 300))
     np.testing.assert_allclose(m[256:300], em, rtol=2e-3, atol=2e-4)
+
+
+def test_philox_restatement_matches_engine_noise():
+    """oracle/philox.py == the engine's Philox noise (B = 50: no row balancing, staged order =
+    batch order), to the device transcendentals' ~1e-6."""
+    from oracle import philox
+    z = load(golden_files("nb_mid")[0])
+    eng = mmvae_amd.Engine(D=int(z["D"]), K=8, max_batch=64, dtype="f32", seed=1234567)
+    eng.upload_csr(z["rowptr"], z["col"], z["val"])
+    eng.init_params(seed=1)
+    eng.eval_loss(np.arange(50), 1.0, step_id=77, row_offset=1000, n_total=5000)
+    import ctypes
+    got = np.zeros(50 * 8, np.float32)
+    assert mmvae_amd.lib().mmvae_debug_copy(eng._h, 3, got.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), got.size) == 0
+    got = got.reshape(50, 8)
+    want, _ = philox.nb_step_noise(1234567, 77, 50, 8, row_offset=1000)
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
+
+
+def test_cli_configs0_against_oracle_loop(tmp_path):
+    """BASELINE configs[0]: nb_vae_main on a synthetic 1000 x 500 MatrixMarket file, latent 8,
+    batch 100, 3 epochs x 2 bootstrap updates — the CLI's per-epoch scores against the oracle's
+    loop (the reference's op sequence on ATen CPU, oracle/nb_oracle.py) from the same initial
+    parameters, with the same bootstrap indices and the engine's Philox noise restated in numpy
+    (oracle/philox.py)."""
+    from oracle import philox
+    N, D, K, B, E, NB, SEED = 1000, 500, 8, 100, 3, 2, 5
+    rp, col, val = synth.synth_csr(N, D, lib_size=1500.0, seed=21)
+    mtx = str(tmp_path / "c0.mtx.gz")
+    write_bgzf_mtx(mtx, rp, col, val, D)
+    out = str(tmp_path / "run")
+    exe = os.path.join(host.BIN_DIR, "nb_vae_main")
+    r = subprocess.run([exe, "--mtx", mtx, "--out", out, "--mean_latent", str(K), "--batch_size", str(B),
+                        "--max_epoch", str(E), "--nboot", str(NB), "--recording", "1000", "--seed", str(SEED)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    s_cli = np.array([float(s) for s in gzip.open(out + ".scores.gz", "rt").read().split()])
+    # the CLI's initial parameters: mmvae_init_params(seed) on the same cfg
+    eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="f32", seed=SEED)
+    eng.upload_csr(rp, col, val)
+    eng.init_params(seed=SEED)
+    p0 = eng.params()
+    shp, fshp = nb_oracle.init_params(D, C=1, K=K)  # the reference's tensor shapes
+    params = {k: torch.from_numpy(p0[k].reshape(v.shape).copy()) for k, v in shp.items()}
+    frozen = {k: torch.from_numpy(p0[k].reshape(v.shape).copy()) for k, v in fshp.items()}
+    tr = nb_oracle.NBTrainer(params, frozen)
+    nbatch = (N + B - 1) // B
+    fwd, s_orc = 0, []
+    for ep in range(E):
+        beta = kl_beta(ep)
+        tot = np.float32(0)
+        for b in range(nbatch):
+            batch = (b * B + np.arange(B)) % N
+            x = torch.from_numpy(synth.densify(rp, col, val, batch, D))
+            c = torch.ones((B, 1), dtype=torch.float32)  # the CLI's automatic ones covariate
+            m, n = philox.nb_step_noise(SEED, fwd, B, K)
+            fwd += 1
+            tot = np.float32(tot + np.float32(tr.eval_loss(x, c, torch.from_numpy(m), torch.from_numpy(n), beta)) * B)
+            for boot in range(NB):
+                rr = torch.from_numpy(host.ridx(SEED, ep, b, boot, B))
+                m, n = philox.nb_step_noise(SEED, fwd, B, K)
+                fwd += 1
+                tr.step(x[rr], c[rr], torch.from_numpy(m), torch.from_numpy(n), beta)
+        s_orc.append(float(tot / np.float32(B * nbatch)))
+    np.testing.assert_allclose(s_cli, s_orc, rtol=1e-4)
