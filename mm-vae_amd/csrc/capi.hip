@@ -376,12 +376,14 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // single H2D copy (each copy is a ~4.5 us blit on the stream):  cells int64 [Bp] |
     // list segments int64 [Bp/16 + 1] | balancing permutation int32 [Bp]
     e->stage_bytes = sizeof(int64_t) * (size_t)(Bp + Bp / 16 + 1) + sizeof(int32_t) * (size_t)Bp + sizeof(StepScalars);
+    e->stage_bytes = (e->stage_bytes + 15) / 16 * 16;  // copied in 16-byte chunks (StageCopy)
     HIPCHK(e, hipMalloc((void**)&e->d_cells, e->stage_bytes));
     e->d_seg = e->d_cells + Bp;
     e->d_perm = reinterpret_cast<int32_t*>(e->d_seg + Bp / 16 + 1);
     e->d_ss = reinterpret_cast<const StepScalars*>(e->d_perm + Bp);  // 8-aligned: Bp % 128 == 0
     for (auto& sl : e->slots2) {
-        HIPCHK(e, hipHostMalloc((void**)&sl.block, e->stage_bytes));
+        // device-accessible, coherent: the step's prep kernel reads it directly (StageCopy)
+        HIPCHK(e, hipHostMalloc((void**)&sl.block, e->stage_bytes, hipHostMallocMapped | hipHostMallocCoherent));
         std::memset(sl.block, 0, e->stage_bytes);
         HIPCHK(e, hipHostMalloc((void**)&sl.eps, sizeof(float) * Bp * (e->K + e->R)));
         HIPCHK(e, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
@@ -417,10 +419,11 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         for (int l = 0; l < e->nce + e->ncd; ++l) nch = std::max<int64_t>(nch, e->ch_off[l] + e->ch_in[l] * e->ch_out[l] + e->ch_out[l]);
         HIPCHK(e, dalloc(&e->d_chain, nch));
     }
-    HIPCHK(e, dalloc(&e->d_out, 4));
     HIPCHK(e, dalloc(&e->d_rowv, Bp));
     HIPCHK(e, dalloc(&e->d_vk, 8));
-    HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4));
+    // loss / total norm: written by the kernels straight into mapped pinned memory (no readback copy)
+    HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(e, hipHostGetDevicePointer((void**)&e->d_out, e->h_out_pin, 0));
     for (auto& sl : e->slots2) HIPCHK(e, hipEventRecord(sl.ev, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     *out = e;
@@ -443,7 +446,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_out, e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain};
+                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block
@@ -754,23 +757,30 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
     return MMVAE_OK;
 }
 
-// cells | segments | permutation | step scalars: one copy (the pinned block is reused only after
-// ev_staged)
-static hipError_t stage_copy(Engine* e) {
-    return hipMemcpyAsync(e->d_cells, e->h_cells_pin, e->stage_bytes, hipMemcpyHostToDevice, e->stream);
+}  // extern "C"
+
+namespace mmvae {
+// cells | segments | permutation | step scalars: copied from the current slot's mapped pinned
+// block by the step's prep kernel (k_prep / k_vprep, StageCopy; the block is reused only after
+// its slot's event)
+StageCopy stage_copy_args(Engine* e) {
+    return StageCopy{reinterpret_cast<const uint4*>(e->h_cells_pin), reinterpret_cast<uint4*>(e->d_cells),
+                     (int)(e->stage_bytes / 16)};
 }
+}  // namespace mmvae
+
+extern "C" {
 
 // the device work of one step / eval, in stream order (eager, or captured into a step graph)
 static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
     const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
-    HIPCHK(e, stage_copy(e));
     if (a->eps) {
         const int64_t ne = a->B * (e->K + (vmf ? 0 : e->R));
         HIPCHK(e, hipMemcpyAsync(e->d_eps, e->h_eps_pin, sizeof(float) * ne, hipMemcpyHostToDevice, e->stream));
     }
     e->grads_reduced = false;
     e->sq_parts = 0;
-    if (!vmf) HIPCHK(e, nb_prep(e, a->B, n_total, a->beta));
+    HIPCHK(e, vmf ? vmf_prep(e, a->B, n_total, a->beta) : nb_prep(e, a->B, n_total, a->beta));  // + staged copy
     HIPCHK(e, build_lists(e, a->B));
     if (vmf) HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
     else HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
@@ -783,8 +793,7 @@ static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
         }
         HIPCHK(e, opt_clip_adam(e));
     }
-    HIPCHK(e, hipMemcpyAsync(e->h_out_pin, e->d_out, sizeof(float) * 2, hipMemcpyDeviceToHost, e->stream));
-    return MMVAE_OK;
+    return MMVAE_OK;  // loss and norm land in the mapped h_out_pin (d_out)
 }
 
 static void graph_drop(Engine* e) {
@@ -902,9 +911,9 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
-    HIPCHK(e, stage_copy(e));
+    if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));  // + the staged copy
+    else HIPCHK(e, vmf_prep(e, B, B, 1.f));
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
-    if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));
     HIPCHK(e, build_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));

@@ -18,17 +18,18 @@ namespace mmvae {
 // row block's slab in a fixed order — no atomics.  Single-buffered tiles, two barriers per tile.
 // =======================================================================================
 struct EncBwdLds {
-    int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, bytes;
+    int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, o_tab, bytes;
     // wsz: element size of the staged W image (f32 in the x3 mode: W only feeds a VALU dot);
     // planes: operand planes of the log1p tile (x3: hi + lo)
-    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes) {
+    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes, int tab_bytes) {
         o_lt = KP * 64 * wsz;
         o_raw = o_lt + planes * 64 * LS * esz;
         o_part = o_raw + 64 * 68 * 4;
         o_scal = o_part + 4 * 64 * 4;
         o_wave = o_scal + nsc * 64 * 4;
         wave_bytes = ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
-        bytes = o_wave + 4 * wave_bytes;
+        o_tab = o_wave + 4 * wave_bytes;  // log1p table (Log1pTab)
+        bytes = o_tab + tab_bytes;
     }
 };
 
@@ -59,7 +60,9 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     const int S = d.tpsE + 1;
     const int H = H1 ? 1 : d.H;
     const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
-    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1);
+    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1, Log1pTab<P>::BYTES);
+    uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
+    Log1pTab<P>::fill(ltab);
     char* wst = smem;
     T* lt = reinterpret_cast<T*>(smem + L.o_lt);          // [64 genes][LS]  log1p(x)
     float* raw = reinterpret_cast<float*>(smem + L.o_raw);  // [64 genes][68] x
@@ -101,7 +104,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     };
     auto scatter = [&](const ListEntries& le) {
         le.visit(ents, lane, [&](int r, int gl, float x) {
-            put_op<P>(lt, gl * LS + 16 * w + r, LT, log1p_cnt<P>(x));
+            Log1pTab<P>::put(ltab, lt, gl * LS + 16 * w + r, LT, x);
             if (RAW) raw[gl * 68 + 16 * w + r] = x;
         });
     };
@@ -118,7 +121,8 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
         nxt.fetch(ents, segw, toffl, min(1, nt - 1), lane);
         wreg.store(wst);
         zero_cols();
-        wave_sync();
+        if constexpr (Log1pTab<P>::ON) __syncthreads();  // the table
+        else wave_sync();
         scatter(first);
     }
     lds_barrier();
@@ -189,7 +193,7 @@ inline size_t enc_bwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;
     return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX),
-                             (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1).bytes;
+                             (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1, Log1pTab<P>::BYTES).bytes;
 }
 
 }  // namespace mmvae

@@ -237,6 +237,10 @@ struct ScopedTimer {
 // NB launchers (nb_kernels.hip)
 hipError_t nb_prepare_frozen(Engine* e);
 hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta);
+hipError_t vmf_prep(Engine* e, int64_t B, int64_t n_total, float beta);
+// the staged block's copy for the prep kernel (nullptr src: already on the device)
+struct StageCopy;
+StageCopy stage_copy_args(Engine* e);
 // split gradient finalisation + bucketed all-reduce (capi.hip): true when the step runs the
 // decoder-side / encoder-side gradient kernels separately (world > 1, or MMVAE_SPLIT_GRADS=1)
 bool split_grads(const Engine* e);

@@ -52,7 +52,8 @@ struct NBGrads {
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, const float* __restrict__ WeP_f,
                                               float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b,
-                                              float* __restrict__ mvecp) {
+                                              float* __restrict__ mvecp, StageCopy scp) {
+    stage_copy_part(scp);
     // grid (genes / 256, KP / 8): every y-slice packs 8 latent rows of the scaled encoder weight
     // and writes its block's partial of mvec (mvec_partial; summed by k_latent_fwd)
     const int g0 = blockIdx.x * 256 + threadIdx.x;
@@ -127,8 +128,10 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL);
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Log1pTab<P>::BYTES);
     char* wst = smem;
+    uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
+    Log1pTab<P>::fill(ltab);
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
     int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_toff) + w * S;
 
@@ -146,9 +149,10 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
                 reinterpret_cast<uint4*>(x0 + pl * 2 * XT)[i] = uint4{0, 0, 0, 0};
     };
     zero_tile(xt);
-    wave_sync();
+    if constexpr (Log1pTab<P>::ON) __syncthreads();  // the table
+    else wave_sync();
     auto scatter = [&](const ListEntries& le, T* dst) {
-        le.visit(ents, lane, [&](int r, int gl, float x) { put_op<P>(dst, r * XS + gl, 2 * XT, log1p_cnt<P>(x)); });
+        le.visit(ents, lane, [&](int r, int gl, float x) { Log1pTab<P>::put(ltab, dst, r * XS + gl, 2 * XT, x); });
     };
 
     f32x4 acc[KP / 16];
@@ -1886,7 +1890,8 @@ static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int NPL = IsX3<P>::value ? 2 : 1;
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * NPL * 16 * XS * (int)sizeof(T), 0, NPL).bytes;
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
+                          Log1pTab<P>::BYTES).bytes;
 }
 // the encoder operand images of mode P: bf16 planes (bf16, x3) or f32
 template <class P> static const typename Elem<P>::type* op_img(const float* f, const __bf16* b) {
@@ -2092,7 +2097,7 @@ hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
     const bool bf = e->cfg.dtype != MMVAE_DTYPE_F32;  // bf16 planes (bf16, x3)
     ScopedTimer tm(e, "k_prep");
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, e->stream, P, d, e->d_gene, e->d_WeP_f,
-                       e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec);
+                       e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, stage_copy_args(e));
     return hipGetLastError();
 }
 

@@ -43,6 +43,19 @@ struct Dims {
 // colsum dh0 [KE] | the NB overdispersion block (nb: 2RH + 2R + H + 1, vMF: 0)
 MMVAE_HOSTDEV int small_len(int K, int E, int KE, int C, int nbx) { return 2 * K * E + 2 * K + K * C + KE + nbx; }
 
+// The step's staged block (cells | segments | permutation | step scalars, pinned host memory)
+// copied into device memory by the prep kernel's y = 0 blocks: the first kernel of a step reads
+// it straight from the mapped host block, instead of a separate copy launch.
+struct StageCopy {
+    const uint4* src;  // pinned host block (device-accessible)
+    uint4* dst;
+    int n16;           // 16-byte chunks
+};
+MMVAE_DEV void stage_copy_part(const StageCopy& sc) {
+    if (blockIdx.y != 0 || !sc.src) return;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < sc.n16; i += gridDim.x * 256) sc.dst[i] = sc.src[i];
+}
+
 // out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c = 0..3: the split
 // partials of four cells, loads issued four splits at a time (independent, then summed)
 MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, int64_t off, int64_t cstride, bool on,
@@ -128,6 +141,55 @@ template <class P> MMVAE_DEV float log1p_cnt(float x) {
     if constexpr (std::is_same<P, __bf16>::value) return flog(1.f + x);
     else return log1pf(x);
 }
+
+// log1p of the integer counts 0 .. LTAB - 1 for the fp32-accurate modes' scatters (x3, f32):
+// staged once per workgroup into LDS as the operand image of each value — x3: the hi / lo bf16
+// pair packed in one word, f32: the float — so an entry is one LDS read instead of log1pf plus
+// the split.  Other counts (non-integer, >= LTAB) take log1pf.  The bf16 mode keeps one v_log.
+static constexpr int LTAB = 1024;
+template <class P> struct Log1pTab {
+    static constexpr bool ON = !std::is_same<P, __bf16>::value;
+    static constexpr int BYTES = ON ? LTAB * 4 : 0;
+    MMVAE_DEV static void fill(uint32_t* tab) {
+        if constexpr (ON)
+            for (int i = threadIdx.x; i < LTAB; i += 256) {
+                const float v = log1pf((float)i);
+                if constexpr (IsX3<P>::value) {
+                    const __bf16 h = bf_hi(v), l = bf_lo(v, h);
+                    tab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+                } else {
+                    tab[i] = __float_as_uint(v);
+                }
+            }
+    }
+    // operand image of log1p(x) into tile t at idx (x3: lo plane `plane` elements after)
+    template <class T>
+    MMVAE_DEV static void put(const uint32_t* tab, T* t, int idx, int plane, float x) {
+        if constexpr (!ON) {
+            t[idx] = to_t<T>(flog(1.f + x));
+        } else {
+            const int xi = (int)x;
+            if (x == (float)xi && (unsigned)xi < (unsigned)LTAB) {
+                const uint32_t v = tab[xi];
+                if constexpr (IsX3<P>::value) {
+                    t[idx] = __builtin_bit_cast(__bf16, (uint16_t)(v & 0xffffu));
+                    t[idx + plane] = __builtin_bit_cast(__bf16, (uint16_t)(v >> 16));
+                } else {
+                    t[idx] = __uint_as_float(v);
+                }
+            } else {
+                const float v = log1pf(x);
+                if constexpr (IsX3<P>::value) {
+                    const __bf16 h = bf_hi(v);
+                    t[idx] = h;
+                    t[idx + plane] = bf_lo(v, h);
+                } else {
+                    t[idx] = v;
+                }
+            }
+        }
+    }
+};
 
 // store v into operand tile t at element idx: plain (f32 / bf16), or as the hi / lo bf16 pair of
 // the x3 mode with the lo plane `plane` elements after the hi plane
@@ -365,12 +427,13 @@ MMVAE_DEV const float* chain_run(const Dims& d, int l0, int l1, const float* in,
 // LDS carve of k_enc_fwd (host computes the same size); planes = 2 in the x3 mode (hi + lo
 // images of the double-buffered W stage: [hi 0][hi 1][lo 0][lo 1])
 struct EncLds {
-    int o_x, o_toff, bytes;
-    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1) {
+    int o_x, o_toff, o_tab, bytes;
+    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1, int tab_bytes = 0) {
         const int stb = KP * 64 * esz;
         o_x = pre + 2 * planes * stb;
         o_toff = o_x + 4 * xbytes_per_wave;  // [4 waves][S] tile offsets
-        bytes = o_toff + ((4 * S * 4 + 15) / 16) * 16;
+        o_tab = o_toff + ((4 * S * 4 + 15) / 16) * 16;  // log1p table (Log1pTab)
+        bytes = o_tab + tab_bytes;
     }
 };
 

@@ -111,7 +111,8 @@ MMVAE_DEV void vkappa_body(const VPtrs& P, const VScal& s, float* __restrict__ v
 __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, float* __restrict__ gene,
                                                const float* __restrict__ WeP_f, float* __restrict__ WeS_f,
                                                __bf16* __restrict__ WeS_b, float* __restrict__ mvecp, VScal sc,
-                                               float* __restrict__ vk) {
+                                               float* __restrict__ vk, StageCopy scp) {
+    stage_copy_part(scp);
     if (blockIdx.x == gridDim.x - 1) {
         if (blockIdx.y == 0) vkappa_body(P, sc, vk);
         return;
@@ -1062,12 +1063,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     const bool bf = sizeof(T) == 2;  // bf16 planes (bf16, x3)
     hipStream_t st = e->stream;
     const int nrb = d.nrb;
-    float* gene = e->d_gene;
-    {
-        ScopedTimer tm(e, "k_vprep");
-        hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256 + 1, d.KP / 8), dim3(256), 0, st, P, d, sc.epsD, gene,
-                           e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, sc, e->d_vk);
-    }
+    float* gene = e->d_gene;  // k_vprep ran before the batch lists (vmf_prep)
     {
         ScopedTimer tm(e, "k_enc_fwd");
         hipError_t er = enc_forward_launch(e, d, e->d_hpart);
@@ -1183,6 +1179,23 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
 template <class... A>
 static hipError_t vmf_dispatch(Engine* e, A... a) {
     return dispatch_mode(e, [&](auto p, auto kp) { return vmf_launch_all<decltype(p), decltype(kp)::value>(e, a...); });
+}
+
+// k_vprep (+ the staged block's copy): launched ahead of the batch lists
+hipError_t vmf_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
+    if (e->frozen_dirty) {
+        hipError_t er = vmf_prepare_frozen(e);
+        if (er != hipSuccess) return er;
+    }
+    const Dims d = vmf_dims(e, B, n_total, beta);
+    const VPtrs P = vmf_ptrs(e);
+    const VScal sc = vmf_scal(e);
+    const bool bf = e->cfg.dtype != MMVAE_DTYPE_F32;  // bf16 planes (bf16, x3)
+    ScopedTimer tm(e, "k_vprep");
+    hipLaunchKernelGGL(k_vprep, dim3((d.DP + 255) / 256 + 1, d.KP / 8), dim3(256), 0, e->stream, P, d, sc.epsD,
+                       e->d_gene, e->d_WeP_f, e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, sc, e->d_vk,
+                       stage_copy_args(e));
+    return hipGetLastError();
 }
 
 hipError_t vmf_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps) {

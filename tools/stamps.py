@@ -5,18 +5,18 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 os.environ["MMVAE_DBG"] = "32"
 import mmvae_amd
 B, D, K = 4096, 20000, 64
-eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
+eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=os.environ.get("DTYPE", "bf16"), seed=1)
 eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 for i in range(3):
     eng.eval_loss(np.arange(B), 1.0, step_id=i)
-nse = int(os.environ.get("NSE", "12"))
+nse = eng.tiling()["split_enc"]
 nwg = (B // 64) * nse
 buf = np.zeros(nwg * 4 * 8, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 0, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
 st = buf.reshape(-1, 8)
-ntile = (313 + nse - 1) // nse
+ntile = eng.tiling()["tps_enc"]
 m = st.mean(0)
 print("waves", st.shape[0], "per tile: MFMA+wait %.0f  zero+scatter %.0f  fetch+stage %.0f  barrier %.0f" % tuple(m[:4] / ntile))
 print("prologue+tail %.0f cycles, wave wall %.0f mean / %.0f max cycles" % (m[4], m[6], st[:, 6].max()))
