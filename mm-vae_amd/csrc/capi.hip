@@ -322,6 +322,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     e->nsplit_e = pick_split(bf_ops ? 4 : 2);
+    // encoder backward: bf16 ~37 KB LDS (4 per CU); x3 / f32 keep W in registers, ~43 KB (3 per CU)
+    e->nsplit_b = pick_split(bf_ops ? 4 : 3);
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
     auto env_split = [&](const char* name, int& v) {
         if (const char* ev = std::getenv(name)) {
@@ -330,6 +332,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         }
     };
     env_split("MMVAE_NSPLIT_E", e->nsplit_e);
+    if (std::getenv("MMVAE_NSPLIT_E")) e->nsplit_b = e->nsplit_e;  // a forced encoder split covers both
+    env_split("MMVAE_NSPLIT_B", e->nsplit_b);
     env_split("MMVAE_NSPLIT_D", e->nsplit_d);
     env_split("MMVAE_NSPLIT_A", e->nsplit_a);
     e->n_lat_wg = (int)(e->Bpad / LAT_CELLS);  // latent kernels: 16 cells per workgroup

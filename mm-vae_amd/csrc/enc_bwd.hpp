@@ -21,8 +21,9 @@ struct EncBwdLds {
     int o_lt, o_raw, o_part, o_scal, o_wave, wave_bytes, o_tab, bytes;
     // wsz: element size of the staged W image (f32 in the x3 mode: W only feeds a VALU dot);
     // planes: operand planes of the log1p tile (x3: hi + lo)
+    // wsz 4 (f32 / x3): W stays in registers, no LDS image
     MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes, int tab_bytes) {
-        o_lt = KP * 64 * wsz;
+        o_lt = wsz == 4 ? 0 : KP * 64 * wsz;
         o_raw = o_lt + planes * 64 * LS * esz;
         o_part = o_raw + 64 * 68 * 4;
         o_scal = o_part + 4 * 64 * 4;
@@ -51,13 +52,16 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;   // log1p tile row (gene) stride, elements
     constexpr int LT = 64 * LS;                    // elements of one log1p tile plane
     constexpr int RB = 64 * (int)sizeof(WT);       // staged W_enc row (one latent, 64 genes)
+    // f32 W (x3 / f32 modes): each lane's 16 W values of a tile live in registers, loaded a tile
+    // ahead from HBM / L2 (no 16 KB LDS image: one more workgroup per CU); bf16 W: LDS image
+    constexpr bool WREG = sizeof(WT) == 4;
     constexpr int HN = H1 ? 1 : HMAX;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = bid % d.nsE, rb = bid / d.nsE;
+    const int sp = bid % d.nsB, rb = bid / d.nsB;
     const int row0 = rb * 64 + 16 * w;
-    const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
-    const int S = d.tpsE + 1;
+    const int t0 = sp * d.tpsB, t1 = min(d.NT, t0 + d.tpsB);
+    const int S = d.tpsB + 1;
     const int H = H1 ? 1 : d.H;
     const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
     const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1, Log1pTab<P>::BYTES);
@@ -72,8 +76,18 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(WT); };
-    wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(WT));
     const int lb = w;  // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
+    float wr[4][4], wn[4][4];  // WREG: W[16 lb + 4 (lane >> 4) + r][64 t + 16 gb + (lane & 15)], this / next tile
+    auto wload = [&](float (&dst)[4][4], int t) {
+        const int kb = 16 * min(lb, KP / 16 - 1) + 4 * (lane >> 4);
+#pragma unroll
+        for (int gb = 0; gb < 4; ++gb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                dst[gb][r] = static_cast<float>(WeP[(int64_t)(kb + r) * d.DP + 64 * t + 16 * gb + (lane & 15)]);
+    };
+    if constexpr (WREG) wload(wr, min(t0, d.NT - 1));
+    else wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(WT));
     constexpr int KSB = 64 / M::KSTEP;
     Fr afr[KSB];
 #pragma unroll
@@ -119,7 +133,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
         ListEntries first;
         first.fetch(ents, segw, toffl, 0, lane);
         nxt.fetch(ents, segw, toffl, min(1, nt - 1), lane);
-        wreg.store(wst);
+        if constexpr (!WREG) wreg.store(wst);
         zero_cols();
         if constexpr (Log1pTab<P>::ON) __syncthreads();  // the table
         else wave_sync();
@@ -128,7 +142,8 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     lds_barrier();
     for (int t = t0; t < t1; ++t) {
         const int tl = t - t0;
-        wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(WT));
+        if constexpr (WREG) wload(wn, min(t + 1, t1 - 1));
+        else wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(WT));
         // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
         if (RAW) {
             const int gl = 16 * w + (lane & 15), q4 = lane >> 4;
@@ -163,7 +178,9 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * lb + 4 * (lane >> 4) + r;
-                    v = fmaf(static_cast<float>(*reinterpret_cast<const WT*>(wst + swz_off<RB>(k, gl * (int)sizeof(WT)))), acc[r], v);
+                    const float wv = WREG ? wr[gb][r]
+                                          : static_cast<float>(*reinterpret_cast<const WT*>(wst + swz_off<RB>(k, gl * (int)sizeof(WT))));
+                    v = fmaf(wv, acc[r], v);
                 }
                 v = sum_rowgroups(v);
                 if (lane < 16) part[w * 64 + gl] = v;
@@ -181,8 +198,13 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
             zero_cols();
             wave_sync();
             scatter(nxt);
-            wreg.store(wst);
+            if constexpr (!WREG) wreg.store(wst);
         }
+        if constexpr (WREG)
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) wr[gb][r] = wn[gb][r];
         nxt.fetch(ents, segw, toffl, min(tl + 2, nt - 1), lane);
         lds_barrier();
     }
@@ -192,7 +214,7 @@ template <class P, int KP>
 inline size_t enc_bwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsE + 1, LS, 1 + (d.H == 1 ? 1 : HMAX),
+    return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsB + 1, LS, 1 + (d.H == 1 ? 1 : HMAX),
                              (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1, Log1pTab<P>::BYTES).bytes;
 }
 

@@ -156,6 +156,7 @@ struct Engine {
     float* h_out_pin = nullptr;
 
     int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder pass-B grids
+    int nsplit_b = 1;                // D-split of the encoder backward
     int nsplit_a = 1;                // D-split of decoder passes A / C
     int n_lat_wg = 1;                // latent kernels' workgroups
     int64_t klp_off = 0;             // offset of KL partials inside d_lossp

@@ -1772,6 +1772,8 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nrb = d.Bpad / 64;
     d.nsE = e->nsplit_e;
     d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
+    d.nsB = e->nsplit_b;
+    d.tpsB = (int)((e->NT + d.nsB - 1) / d.nsB);
     d.nsD = e->nsplit_d;
     d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
     d.nsA = e->nsplit_a;
@@ -2046,7 +2048,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         const auto* WeT = enc_w<PM>(e);
         const T* dhT = op_img<PM>(e->d_dhT_f, e->d_dhT_b);
         const int64_t dpl = (int64_t)KP * d.Bpad;
-        const int nenc = nrb * d.nsE;
+        const int nenc = nrb * d.nsB;
         if (d.H == 1)
             hipLaunchKernelGGL((k_enc_bwd_small<PM, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st,
                                e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,

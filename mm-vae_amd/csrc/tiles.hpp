@@ -15,7 +15,8 @@ static constexpr int LAT_CELLS = 16;  // cells per 256-thread workgroup of the l
 struct Dims {
     int D, DP, NT, K, KP, C, H, R;
     int B, Bpad, nrb;
-    int nsE, tpsE;  // encoder splits, tiles per split
+    int nsE, tpsE;  // encoder (forward) splits, tiles per split
+    int nsB, tpsB;  // encoder backward splits
     int nsD, tpsD;  // decoder pass-B splits
     int nsA, tpsA;  // decoder passes A / C splits
     float inv_n, beta;

@@ -1032,6 +1032,8 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nrb = d.Bpad / 64;
     d.nsE = e->nsplit_e;
     d.tpsE = (int)((e->NT + d.nsE - 1) / d.nsE);
+    d.nsB = e->nsplit_b;
+    d.tpsB = (int)((e->NT + d.nsB - 1) / d.nsB);
     d.nsD = e->nsplit_d;
     d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
     d.nsA = e->nsplit_a;
@@ -1148,7 +1150,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         // encoder backward + the small-parameter gradients / loss in one launch
         ScopedTimer tm(e, "k_enc_bwd");
-        const int nenc = nrb * d.nsE;
+        const int nenc = nrb * d.nsB;
         const T* dhT = reinterpret_cast<const T*>(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f);
         const auto* WeT = reinterpret_cast<const typename WEnc<PM>::type*>(
             std::is_same<typename WEnc<PM>::type, __bf16>::value ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f);
