@@ -47,7 +47,7 @@ VALU_PER_ELEM = {"nb": 60, "vmf": 13}
 # dominant kernel per model: (name, GEMM flops per element / latent)
 DOMINANT = {"nb": ("k_dec_nb", 6), "vmf": ("k_vdec_bwd", 4)}
 # bf16 MFMA passes per algorithmic product
-MFMA_PASSES = {"bf16": 1, "bf16x3": 3, "f32": 1}
+MFMA_PASSES = {"bf16": 1, "bf16x3": 3, "f32": 1, "fp8": 1}
 METRIC = "cells/sec (ELBO step) NB-VAE 20k genes at 1/2/4/8 MI355X; ELBO parity"
 
 
@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--model", default="nb", choices=["nb", "vmf"])
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "bf16", "f32", "fp8"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--genes", type=int, default=20000)
     ap.add_argument("--cells", type=int, default=1000000)
@@ -165,7 +165,7 @@ def roofline(model, dtype, D, K, B, nnz_per_cell, per_kernel):
     dom, fpe = DOMINANT[model]
     t = per_kernel[dom] * 1e-3
     q_ops = float(Q_PER_ELEM[model]) * B * D
-    esz = {"bf16": 2, "bf16x3": 4, "f32": 4}[dtype]
+    esz = {"bf16": 2, "bf16x3": 4, "f32": 4, "fp8": 2}[dtype]
     KP = 32 if K <= 32 else 64
     alg_bytes = 8.0 * nnz_per_cell * B + 2 * ((D + 63) // 64 * 64) * KP * esz
     flops = float(fpe) * D * K * B
@@ -192,7 +192,7 @@ def composite(model, dtype, D, K, B, nnz_per_cell, P_reg, ms_per_step):
     Bytes = 16 nnz + (4 D K esz + 28 P_reg) / B."""
     F = 8.0 * D * K * MFMA_PASSES[dtype]
     peak = PEAK_F32_MFMA if dtype == "f32" else PEAK_BF16
-    esz = {"bf16": 2, "bf16x3": 4, "f32": 4}[dtype]
+    esz = {"bf16": 2, "bf16x3": 4, "f32": 4, "fp8": 2}[dtype]
     byts = 16.0 * nnz_per_cell + (4.0 * D * K * esz + 28.0 * P_reg) / B
     Q = float(Q_PER_ELEM[model]) * D
     terms = {"mfma_ns": F / peak * 1e9, "hbm_ns": byts / PEAK_HBM * 1e9, "valu_q_ns": Q / PEAK_Q * 1e9}
@@ -383,7 +383,10 @@ def main():
         "precision": ("ELBO-parity mode: GEMM operands as bf16 hi + lo planes, products lo*hi + hi*lo + hi*hi "
                       "accumulated in fp32, fp32 epilogue / reductions / Adam; loss within 2e-5 and gradients within "
                       "2e-4 of the fp32 oracle at this shape (tests/test_gpu_tiling.py)") if args.dtype == "bf16x3" else
-                     ("exact f32 MFMA" if args.dtype == "f32" else "bf16 GEMM operands, fp32 accumulate (loss ~2e-3)"),
+                     ("exact f32 MFMA" if args.dtype == "f32" else
+                      "fp8 e4m3 decoder logit GEMM (power-of-two scaled W_dec), bf16 encoder / dz GEMMs, fp32 accumulate "
+                      "(loss <= 2.1e-3 of the oracle, profiles/r2_fp8_accuracy.json)" if args.dtype == "fp8" else
+                      "bf16 GEMM operands, fp32 accumulate (loss ~2e-3)"),
         "data": "synthetic (seeded device-side generator, SURVEY §8(d) count distribution), random-init weights",
         "config": {"workload": f"{mname}-VAE ELBO step (fwd+bwd+clip+Adam), {Ncells} cells x {D} genes, latent {K}, "
                                f"batch {B}/GPU",

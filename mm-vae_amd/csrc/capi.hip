@@ -251,8 +251,11 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
         cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
-    if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16 && cfg->dtype != MMVAE_DTYPE_BF16X3)
-        FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32, BF16 or BF16X3");
+    if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16 && cfg->dtype != MMVAE_DTYPE_BF16X3 &&
+        cfg->dtype != MMVAE_DTYPE_FP8)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32, BF16, BF16X3 or FP8");
+    if (cfg->dtype == MMVAE_DTYPE_FP8 && cfg->model != MMVAE_MODEL_NB)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "the fp8 mode is built for the NB decoder (BASELINE configs[4])");
     if (cfg->n_enc_hidden < 0 || cfg->n_enc_hidden > 4 || cfg->n_dec_hidden < 0 || cfg->n_dec_hidden > 4)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "at most 4 hidden encoder / decoder layers");
     // nb.hh:334-337 pushes a hidden encoder Linear and its ReLU under the same name: LibTorch
@@ -316,7 +319,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // images and f32 four-byte elements, so both fit half as many (NB pass B: bf16 and x3 run one
     // 8-wave workgroup per CU = 2 units; f32 one 4-wave workgroup)
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
-    const bool bf_ops = cfg->dtype == MMVAE_DTYPE_BF16;
+    const bool bf_ops = cfg->dtype == MMVAE_DTYPE_BF16 || cfg->dtype == MMVAE_DTYPE_FP8;  // fp8: bf16 encoders / dz
     const int dec_cu = vmf_model ? (bf_ops ? 4 : 2) : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
     e->nsplit_d = pick_split(dec_cu);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
@@ -373,6 +376,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_WdP_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WdP_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WdT_f, KP * DP));
+    if (cfg->dtype == MMVAE_DTYPE_FP8) HIPCHK(e, dalloc(&e->d_WdP8, KP * DP));
     HIPCHK(e, dalloc(&e->d_WdT_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WeS_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WeS_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
@@ -450,7 +454,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain};
+                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block

@@ -103,6 +103,38 @@ template <> struct MM<X3> {
     }
 };
 
+// fp8 e4m3 operands (BASELINE configs[4]: the decoder logit GEMM z W_dec^T of passes A, B, C):
+// v_mfma_f32_16x16x32_fp8_fp8, 8 e4m3 values per lane (one 64-bit register pair), f32
+// accumulate.  z is converted from f32 as the fragment is loaded; W_dec is stored pre-scaled by a
+// power of two (amax -> the top of the e4m3 range, k_pack_w8) and the accumulator is unscaled.
+struct F8 {};
+template <> struct Elem<F8> { typedef uint8_t type; };
+template <> struct MM<F8> {
+    static constexpr int KSTEP = 32, EPL = 8;
+    typedef long frag;
+    static MMVAE_DEV frag load(const uint8_t* p) { return *reinterpret_cast<const long*>(p); }
+    static MMVAE_DEV frag load(const uint8_t* p, int64_t) { return *reinterpret_cast<const long*>(p); }
+    static MMVAE_DEV f32x4 mma(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+    }
+    // 8 consecutive f32 (16-byte aligned) -> one e4m3 fragment (v_cvt_pk_fp8_f32, RNE)
+    static MMVAE_DEV frag load_f32(const float* p) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a.x, a.y, 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(a.z, a.w, lo, true);
+        int hi = __builtin_amdgcn_cvt_pk_fp8_f32(b.x, b.y, 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(b.z, b.w, hi, true);
+        return (long)(uint32_t)lo | ((long)(uint32_t)hi << 32);
+    }
+    static MMVAE_DEV frag zero() { return 0; }
+};
+template <class P> struct IsF8 { static constexpr bool value = false; };
+template <> struct IsF8<F8> { static constexpr bool value = true; };
+// policies of the GEMMs that stay bf16 in the fp8 mode (encoder, dz): the mode's own otherwise
+template <class P> struct Bf16If8 { typedef P type; };
+template <> struct Bf16If8<F8> { typedef __bf16 type; };
+
 // ---------------------------------------------------------------------------------------
 // LDS-DMA staging (global_load_lds_dwordx4): the LDS destination is wave-uniform base +
 // 16 * lane, so tiles are staged lane-linear and the bank swizzle is applied on the SOURCE

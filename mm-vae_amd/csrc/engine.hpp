@@ -103,6 +103,8 @@ struct Engine {
     __bf16* d_WeP_b = nullptr;
     float* d_WdP_f = nullptr;   // [DP][KP] decoder weight (gene-major)
     __bf16* d_WdP_b = nullptr;
+    uint8_t* d_WdP8 = nullptr;  // [DP][KP] decoder weight x wscale, e4m3 (fp8 mode)
+    float wscale = 1.f;         // power-of-two scale of d_WdP8
     float* d_WdT_f = nullptr;   // [KP][DP] decoder weight transposed
     __bf16* d_WdT_b = nullptr;
 
@@ -264,15 +266,24 @@ hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const flo
 
 // Instantiate f(operand mode, latent padding) for the handle's dtype and KP: the mode is float
 // (exact f32 MFMA), __bf16 (bf16 operands) or X3 (split-bf16, fp32-accurate products).
-template <class F>
+// (F8 = the fp8 mode, NB only; WITH_F8 = false maps it to bf16 for code that has no fp8 variant.)
+template <bool WITH_F8 = true, class F>
 hipError_t dispatch_mode(const Engine* e, F&& f) {
     using K32 = std::integral_constant<int, 32>;
     using K64 = std::integral_constant<int, 64>;
     const int dt = e->cfg.dtype;
     if (e->KP == 32) {
+        if (dt == MMVAE_DTYPE_FP8) {
+            if constexpr (WITH_F8) return f(F8{}, K32{});
+            else return f(__bf16{}, K32{});
+        }
         if (dt == MMVAE_DTYPE_BF16) return f(__bf16{}, K32{});
         if (dt == MMVAE_DTYPE_BF16X3) return f(X3{}, K32{});
         return f(float{}, K32{});
+    }
+    if (dt == MMVAE_DTYPE_FP8) {
+        if constexpr (WITH_F8) return f(F8{}, K64{});
+        else return f(__bf16{}, K64{});
     }
     if (dt == MMVAE_DTYPE_BF16) return f(__bf16{}, K64{});
     if (dt == MMVAE_DTYPE_BF16X3) return f(X3{}, K64{});

@@ -486,6 +486,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     using M = MM<P>;
     using Fr = typename M::frag;
     constexpr bool X = IsX3<P>::value;
+    constexpr bool F8M = IsF8<P>::value;     // fp8 logits: z from f32, W_dec pre-scaled e4m3
     constexpr int NPL = X ? 2 : 1;
     constexpr int KS = KP / M::KSTEP;
     constexpr bool BF = sizeof(T) == 2;
@@ -525,9 +526,12 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 #pragma unroll
     for (int j = 0; j < J; ++j)
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-            zfr[j][s] = M::load(&Z[(int64_t)(row0 + 16 * j + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL],
-                                Q.zplane);
+        for (int s = 0; s < KS; ++s) {
+            const int64_t zo = (int64_t)(row0 + 16 * j + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL;
+            if constexpr (F8M) zfr[j][s] = M::load_f32(Q.zf + zo);
+            else zfr[j][s] = M::load(&Z[zo], Q.zplane);
+        }
+    const float ainv = F8M ? d.inv_wscale : 1.f;  // logit accumulator unscale (fp8 W_dec)
     float lse2[J][4], wE[J][4], crow[J][4][CM], mrun[J][4], srun[J][4];
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -609,7 +613,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                         float v = b2[gb];
 #pragma unroll
                         for (int c = 0; c < CM; ++c) v = fmaf(crow[j][r][c], w2[gb][c], v);
-                        l2[gb] = fmaf(acc[gb][j][r], L2E, v);
+                        l2[gb] = fmaf(acc[gb][j][r], L2E * ainv, v);
                     }
                     const float mn = fmaxf(mrun[j][r], fmaxf(fmaxf(l2[0], l2[1]), fmaxf(l2[2], l2[3])));
                     float sacc = srun[j][r] * fexp2(mrun[j][r] - mn);
@@ -645,7 +649,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 for (int j = 0; j < J; ++j)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        float lg = acc[j][r] + g4.x;
+                        float lg = fmaf(acc[j][r], ainv, g4.x);
 #pragma unroll
                         for (int c = 0; c < CM; ++c) lg = fmaf(crow[j][r][c], wcd[c], lg);
                         const float wp = wE[j][r] * fexp2(fmaf(lg, L2E, -lse2[j][r]));
@@ -789,9 +793,10 @@ struct DecNBLds {
     int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
     int sw, st, sp;     // per-buffer strides: W tile, WdT tile (bytes, all planes), column partials (floats)
     int swp, stp;       // one plane of the W / WdT images (bytes)
-    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes) {
+    // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'
+    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes, int eszw) {
         const bool alias = planes == 2;
-        swp = 64 * KP * esz;
+        swp = 64 * KP * eszw;
         stp = KP * 64 * esz;
         sw = planes * swp;
         st = planes * stp;
@@ -812,16 +817,20 @@ struct DecNBLds {
     }
 };
 
-template <class P, int KP, int CM, int RM, int NW, bool DB>
+// PL: the logit GEMM's operand policy (P, or F8 in the fp8 mode with P = bf16 for the dz GEMM)
+template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
     using Fr = typename M::frag;
+    using TL = typename Elem<PL>::type;
+    using ML = MM<PL>;
+    constexpr bool F8M = IsF8<PL>::value;
+    constexpr int KSL = KP / ML::KSTEP;  // k-steps of the logit GEMM
     using CP = CorrPair<P>;
     typedef typename CP::type CT;
     constexpr bool X = IsX3<P>::value;  // x3: split operands, pq aliased into the correction tile
     constexpr int NPL = X ? 2 : 1;
-    constexpr int KS = KP / M::KSTEP;   // k-steps of the logit GEMM
     constexpr int GK = 64 / M::KSTEP;   // k-steps of the dz GEMM over a 64-gene tile
     constexpr bool BF = sizeof(T) == 2;
     constexpr int QS = 64 + (BF ? 8 : 4);
@@ -831,7 +840,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     auto cci = [](int r, int g) { return X ? ((g >> 4) * 256 + r * 16 + (g & 15)) : r * 64 + g; };
     constexpr int PS = 68;
     constexpr int NRS = 3 + RM + CM;    // row scalars: d, w, valid, znu[R], c[C]
-    constexpr int RBW = KP * (int)sizeof(T);  // staged decoder row (one gene)
+    constexpr int RBW = KP * (int)sizeof(TL);  // staged decoder row (one gene)
     constexpr int RBT = 64 * (int)sizeof(T);  // staged WdT row (one latent, 64 genes)
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -843,7 +852,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL);
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL));
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
@@ -860,10 +869,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);  // (bias, cn, Wcd0, Wnd0)
 
     // ---- per-row state (lane holds rows 4(lane>>4)+r of the wave's 16) ----
-    Fr zfr[KS];
+    typename ML::frag zfr[KSL];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-        zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL], Q.zplane);
+    for (int s = 0; s < KSL; ++s) {
+        const int64_t zo = (int64_t)(row0 + (lane & 15)) * KP + s * ML::KSTEP + (lane >> 4) * ML::EPL;
+        if constexpr (F8M) zfr[s] = ML::load_f32(Q.zf + zo);
+        else zfr[s] = M::load(&Z[zo], Q.zplane);
+    }
+    const float ainv = F8M ? d.inv_wscale : 1.f;  // logit accumulator unscale (fp8 W_dec)
     // ---- staging of the decoder tile, its gene records and the WdT tile ----
     DualStage<64, RBW, NTH, X> wreg;
     DualStage<KP, RBT, NTH, X> treg;
@@ -988,8 +1001,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             const int gl = 16 * gb + (lane & 15);
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                acc = M::mma(zfr[s], M::load(reinterpret_cast<const T*>(wsb + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), L.swp / (int)sizeof(T)), acc);
+            for (int s = 0; s < KSL; ++s)
+                acc = ML::mma(zfr[s], ML::load(reinterpret_cast<const TL*>(wsb + swz_off<RBW>(gl, (s * ML::KSTEP + (lane >> 4) * ML::EPL) * (int)sizeof(TL))), L.swp / (int)sizeof(TL)), acc);
             const float4 g4 = gsb[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -997,7 +1010,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float lg = acc[r] + g4.x;
+                float lg = fmaf(acc[r], ainv, g4.x);
 #pragma unroll
                 for (int c = 0; c < CM; ++c) lg = fmaf(crow2[r >> 1][c][r & 1], wcd[c], lg);
                 q2[(4 * (lane >> 4) + r) * PS + gl] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
@@ -1799,6 +1812,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nmv = (int)((e->DP + 255) / 256);
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
     d.relu = e->cfg.relu != 0;
+    d.inv_wscale = 1.f / e->wscale;
     dims_hidden(e, d);
     return d;
 }
@@ -1867,8 +1881,35 @@ hipError_t pack_chain(Engine* e, bool angular_enc) {
     return hipGetLastError();
 }
 
+// fp8 mode: [DP][KP] e4m3 image of scale * W_dec[g][k] (0 past D / KD), two elements per thread
+__global__ __launch_bounds__(256) void k_pack_w8(const float* __restrict__ Wd, int D, int DP, int KD, int KP,
+                                                 float scale, uint8_t* __restrict__ WdP8) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (i >= (int64_t)DP * KP) return;
+    const int g = (int)(i / KP), k = (int)(i % KP);
+    const float a = (g < D && k < KD) ? Wd[(int64_t)g * KD + k] * scale : 0.f;
+    const float b = (g < D && k + 1 < KD) ? Wd[(int64_t)g * KD + k + 1] * scale : 0.f;
+    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    WdP8[i] = (uint8_t)(v & 0xff);
+    WdP8[i + 1] = (uint8_t)((v >> 8) & 0xff);
+}
+
 hipError_t nb_prepare_frozen(Engine* e) {
     const int64_t n = e->KP * e->DP;
+    if (e->cfg.dtype == MMVAE_DTYPE_FP8) {
+        // power-of-two scale putting amax(W_dec) at the top of the e4m3 range (448): host amax of
+        // the frozen tensor (repacked only when it changes)
+        std::vector<float> w((size_t)(e->D * e->KD));
+        hipError_t er = hipMemcpyAsync(w.data(), e->pfrz(e->fz_dec_w), sizeof(float) * w.size(), hipMemcpyDeviceToHost,
+                                       e->stream);
+        if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+        if (er != hipSuccess) return er;
+        float amax = 0.f;
+        for (float v : w) amax = std::max(amax, std::fabs(v));
+        e->wscale = amax > 0.f ? std::exp2(std::floor(std::log2(448.f / amax))) : 1.f;
+        hipLaunchKernelGGL(k_pack_w8, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, e->stream,
+                           e->pfrz(e->fz_dec_w), (int)e->D, (int)e->DP, (int)e->KD, (int)e->KP, e->wscale, e->d_WdP8);
+    }
     ScopedTimer tm(e, "k_pack_frozen");
     hipLaunchKernelGGL(k_pack_frozen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
                        e->pfrz(e->fz_enc_w), e->pfrz(e->fz_dec_w), (int)e->D, (int)e->DP, (int)e->KE, (int)e->KD,
@@ -1933,7 +1974,7 @@ static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     Q.ents = e->d_ents;
     Q.seg = e->d_seg;
     Q.toff = e->d_toff;
-    Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
+    Q.WdP = e->cfg.dtype == MMVAE_DTYPE_FP8 ? (const void*)e->d_WdP8 : bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
     Q.WdT = bf ? (const void*)e->d_WdT_b : (const void*)e->d_WdT_f;
     Q.lsep = e->d_lsep;
     Q.rowfin = e->d_rowfin;
@@ -1958,8 +1999,11 @@ static size_t latent_bwd_lds(const Engine* e) {
 
 template <class PM, int KP>
 static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool update, bool use_eps) {
-    using T = typename Elem<PM>::type;
-    constexpr bool X = IsX3<PM>::value;
+    // PB: the encoder / dz GEMM policy (bf16 in the fp8 mode), PM: the logit GEMM's
+    using PB = typename Bf16If8<PM>::type;
+    using T = typename Elem<PB>::type;
+    using TL = typename Elem<PM>::type;
+    constexpr bool X = IsX3<PB>::value;
     constexpr int NPL = X ? 2 : 1;
     const bool bf = sizeof(T) == 2;  // bf16 planes (bf16 and x3 modes)
     hipStream_t st = e->stream;
@@ -1967,7 +2011,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
     {
         ScopedTimer tm(e, "k_enc_fwd");
-        enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
+        enc_fwd_run<PB, KP>(e, d, e->d_hpart, st);
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
@@ -1983,11 +2027,11 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const int nqB = (1 + d.C) + 1 + d.R;
     const int csz = (bf && !X) ? 4 : 8;
     const bool nw4 = getenv_is("MMVAE_DEC_NW", "4");
-    const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL).bytes;
+    const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL, (int)sizeof(TL)).bytes;
     const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !nw4) ? 8 : 4;
     const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
     const dim3 gdecA(nrb / 2 * d.nsA);  // passes A / C: 128 rows per workgroup
-    const size_t ldsA = dec_lds(d, 0, (int)sizeof(T), NPL), ldsC = dec_lds(d, 2, (int)sizeof(T), NPL);
+    const size_t ldsA = dec_lds(d, 0, (int)sizeof(TL), NPL), ldsC = dec_lds(d, 2, (int)sizeof(TL), NPL);
     {
         ScopedTimer tm(e, "k_dec_lse");
         if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
@@ -1996,13 +2040,13 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         ScopedTimer tm(e, "k_dec_nb");
         if (nwB == 8) {
-            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PM, KP, 1, 1, 8, !X>), gdecB, dim3(512), ldsB8, st, Q, d);
+            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM>), gdecB, dim3(512), ldsB8, st, Q, d);
         } else if (small_cr)
-            hipLaunchKernelGGL((k_dec_nb<PM, KP, 1, 1, 4, false>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL)).bytes, st, Q, d);
         else
-            hipLaunchKernelGGL((k_dec_nb<PM, KP, CMAX, RMAX, 4, false>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PB, KP, CMAX, RMAX, 4, false, PM>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL, (int)sizeof(TL)).bytes, st, Q, d);
     }
     NBGrads G = nb_grads(e);
     if (!update) {
@@ -2045,17 +2089,17 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     {
         // encoder backward + the small-parameter gradients / loss in one launch
         ScopedTimer tm(e, "k_enc_bwd");
-        const auto* WeT = enc_w<PM>(e);
-        const T* dhT = op_img<PM>(e->d_dhT_f, e->d_dhT_b);
+        const auto* WeT = enc_w<PB>(e);
+        const T* dhT = op_img<PB>(e->d_dhT_f, e->d_dhT_b);
         const int64_t dpl = (int64_t)KP * d.Bpad;
         const int nenc = nrb * d.nsB;
         if (d.H == 1)
-            hipLaunchKernelGGL((k_enc_bwd_small<PM, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st,
+            hipLaunchKernelGGL((k_enc_bwd_small<PB, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PB, KP>(d)), st,
                                e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
         else
-            hipLaunchKernelGGL((k_enc_bwd_small<PM, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st,
+            hipLaunchKernelGGL((k_enc_bwd_small<PB, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PB, KP>(d)), st,
                                e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
@@ -2118,7 +2162,7 @@ hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta
 template <class PM, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     hipStream_t st = e->stream;
-    enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
+    enc_fwd_run<typename Bf16If8<PM>::type, KP>(e, d, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, e->d_ss,
                        e->d_lat,
@@ -2140,7 +2184,7 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
 
 // ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
 hipError_t enc_forward_launch(Engine* e, const Dims& d, float* hpart) {
-    return dispatch_mode(e, [&](auto p, auto kp) {
+    return dispatch_mode<false>(e, [&](auto p, auto kp) {
         enc_fwd_run<decltype(p), decltype(kp)::value>(e, d, hpart, e->stream);
         return hipGetLastError();
     });

@@ -27,6 +27,7 @@ struct Dims {
     int nmv;          // mvec partial blocks (256 genes each) written by the prep kernel
     int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
     int relu;         // ReLU on the frozen encoder's output h (nb.hh:345-346, vmf.hh:351-352)
+    float inv_wscale; // fp8 mode: 1 / the power-of-two scale of the e4m3 decoder weight (else 1)
     // frozen hidden layers (nb.hh:331-379, vmf.hh:338-385): KE = rows of the big encoder GEMM
     // (h0), E = input width of the heads, KD = input width of the big decoder GEMM (zd).  Chain
     // layer l (encoder layers 0 .. nce-1, then decoder layers nce .. nce+ncd-1) is

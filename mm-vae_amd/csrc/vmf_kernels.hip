@@ -1052,6 +1052,7 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nmv = (int)((e->DP + 255) / 256);
     d.dbg = 0;
     d.relu = e->cfg.relu != 0;
+    d.inv_wscale = 1.f;
     dims_hidden(e, d);
     return d;
 }
@@ -1180,7 +1181,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
 
 template <class... A>
 static hipError_t vmf_dispatch(Engine* e, A... a) {
-    return dispatch_mode(e, [&](auto p, auto kp) { return vmf_launch_all<decltype(p), decltype(kp)::value>(e, a...); });
+    return dispatch_mode<false>(e, [&](auto p, auto kp) { return vmf_launch_all<decltype(p), decltype(kp)::value>(e, a...); });
 }
 
 // k_vprep (+ the staged block's copy): launched ahead of the batch lists

@@ -17,9 +17,9 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmmvae.so"
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "include", "mmvae_capi.h"))
 
 MODEL_NB, MODEL_VMF = 0, 1
-DTYPE_F32, DTYPE_BF16, DTYPE_BF16X3 = 0, 1, 2
+DTYPE_F32, DTYPE_BF16, DTYPE_BF16X3, DTYPE_FP8 = 0, 1, 2, 3
 _DTYPES = {"f32": DTYPE_F32, "fp32": DTYPE_F32, "float32": DTYPE_F32, "bf16": DTYPE_BF16,
-           "bf16x3": DTYPE_BF16X3, "x3": DTYPE_BF16X3}
+           "bf16x3": DTYPE_BF16X3, "x3": DTYPE_BF16X3, "fp8": DTYPE_FP8, "e4m3": DTYPE_FP8}
 
 
 class MMVAEError(RuntimeError):
