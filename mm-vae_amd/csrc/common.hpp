@@ -269,7 +269,7 @@ MMVAE_DEV float dsoftplus(float u) { return (u > 20.f) ? 1.f : 1.f / (1.f + expf
 // Gamma-function terms of the NB likelihood for a count x > 0 and overdispersion nup > 0:
 //   lgd = lgamma(nup) + lgamma(x + 1) - lgamma(nup + x)      (nb.hh:522-523)
 //   dgd = digamma(nup) - digamma(nup + x)                    (its d/d nup)
-// Counts 1..4 (the bulk of single-cell data) use the exact finite product / sum with one log
+// Counts 1..8 (the bulk of single-cell data) use the exact finite product / sum with one log
 // and one reciprocal.  Everything else shifts each argument below 8 up by 8 (branch free:
 // P = v(v+1)..(v+7) and S = P'/P = sum 1/(v+i) by the product rule) and evaluates Stirling's
 // series and the digamma asymptotic series at z >= 8 (truncation < 1e-9 relative), sharing
@@ -302,10 +302,11 @@ MMVAE_DEV GammaAt gamma_at(float v, bool need_dg) {
 }
 
 MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
-    if (x <= 4.f && x == floorf(x)) {
+    // counts up to 8: P <= (nup + 7)^8 <= ~1e32 for the clamped nup <= 1e4 + 1e-4, x! <= 40320 exact
+    if (x <= 8.f && x == floorf(x)) {
         float P = 1.f, Pd = 0.f, F = 1.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const bool on = (float)i < x;
             const float a = on ? nup + (float)i : 1.f;
             Pd = on ? fmaf(Pd, a, P) : Pd;
