@@ -132,6 +132,41 @@ static bool scan_bgzf(const std::vector<unsigned char>& b, std::vector<BgzfBlock
     return true;
 }
 
+// The whole BGZF blocks at the front of b[0, n): false if b does not start a BGZF block; the
+// bytes of a trailing partial block are left (consumed = bytes of the whole blocks)
+static bool scan_bgzf_window(const unsigned char* b, size_t n, std::vector<BgzfBlock>& blocks, size_t& consumed) {
+    size_t p = 0, out = 0;
+    blocks.clear();
+    while (p + 18 <= n) {
+        if (b[p] != 31 || b[p + 1] != 139 || b[p + 2] != 8 || !(b[p + 3] & 4)) return false;
+        const size_t xlen = b[p + 10] | (b[p + 11] << 8);
+        size_t q = p + 12;
+        const size_t qe = q + xlen;
+        if (qe > n) break;
+        long bsize = -1;
+        while (q + 4 <= qe) {
+            const int slen = b[q + 2] | (b[q + 3] << 8);
+            if (b[q] == 'B' && b[q + 1] == 'C' && slen == 2 && q + 6 <= n) bsize = b[q + 4] | (b[q + 5] << 8);
+            q += 4 + (size_t)slen;
+        }
+        if (bsize < 0) return false;
+        const size_t total = (size_t)bsize + 1, hdr = 12 + xlen;
+        if (total < hdr + 8) return false;
+        if (p + total > n) break;
+        BgzfBlock blk;
+        blk.file_off = p;
+        blk.in_off = p + hdr;
+        blk.in_len = total - hdr - 8;
+        blk.out_len = le32(&b[p + total - 4]);
+        blk.out_off = out;
+        out += blk.out_len;
+        blocks.push_back(blk);
+        p += total;
+    }
+    consumed = p;
+    return true;
+}
+
 static bool inflate_raw(const unsigned char* in, size_t in_len, char* out, size_t out_len) {
     z_stream s;
     std::memset(&s, 0, sizeof(s));
@@ -352,6 +387,10 @@ int read_triplets(const char* path, int threads, int64_t& D, int64_t& N, std::ve
     return MMVAE_OK;
 }
 
+static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, std::vector<int32_t>& col,
+                      std::vector<float>& val, mmvae_csr* out);
+static int stream_sorted_csr(const char* path, int threads, mmvae_csr* out);
+
 }  // namespace mmvae_host
 
 using namespace mmvae_host;
@@ -377,6 +416,10 @@ int mmvae_mtx_read(const char* path, int threads, mmvae_csr* out) {
     if (!path || !out) return fail(MMVAE_E_ARG, "mtx_read: null argument");
     std::memset(out, 0, sizeof(*out));
     threads = default_threads(threads);
+    {
+        const int src = stream_sorted_csr(path, threads, out);  // column-sorted BGZF: streamed
+        if (src != 1) return src;
+    }
     int64_t D, N;
     std::vector<Chunk> chunks;
     int rc = read_triplets(path, threads, D, N, chunks);
@@ -423,6 +466,16 @@ int mmvae_mtx_read(const char* path, int threads, mmvae_csr* out) {
             std::vector<float>().swap(ch.val);
         }
     });
+    return finish_csr(threads, N, D, rp, col, val, out);
+}
+
+}  // extern "C"
+
+namespace mmvae_host {
+// rows strictly increasing in gene (stable sort + keep-last dedupe where needed), then copied out
+static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, std::vector<int32_t>& col,
+                      std::vector<float>& val, mmvae_csr* out) {
+    const int64_t nnz_all = rp[(size_t)N];
     // rows must be strictly increasing in gene: stable sort + keep-last dedupe where needed
     std::vector<int64_t> newlen((size_t)N);
     std::atomic<bool> compact{false};
@@ -483,6 +536,129 @@ int mmvae_mtx_read(const char* path, int threads, mmvae_csr* out) {
     std::memcpy(out->val, val.data(), sizeof(float) * (size_t)nnz);
     return MMVAE_OK;
 }
+
+
+// Streaming load of a column-sorted BGZF MatrixMarket file (the mmutil convention: entries grouped
+// by column = cell, as write_matrix_market_stream and 10x-style matrix.mtx.gz files are): windows
+// of whole BGZF blocks (64 MB compressed, MMVAE_MTX_WINDOW bytes to override) are inflated in
+// parallel and parsed straight into the cell-major CSR — file order is CSR order — so neither the
+// whole text (~12 B per entry) nor a triplet copy is ever held: peak memory ~ the CSR plus one
+// window.  Returns 1 (the caller takes the whole-file path) for input that is not BGZF or whose
+// columns are not sorted.
+static int stream_sorted_csr(const char* path, int threads, mmvae_csr* out) {
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot open ") + path + ": " + std::strerror(errno));
+    size_t WIN = (size_t)64 << 20;
+    if (const char* ev = std::getenv("MMVAE_MTX_WINDOW")) WIN = std::max<size_t>((size_t)std::atoll(ev), 4096);
+    std::vector<unsigned char> cbuf;
+    size_t have = 0;
+    std::string carry;  // a partial last line
+    bool header = false, first = true;
+    int64_t D = 0, N = 0, nnz_hdr = 0, last_cell = -1;
+    std::vector<int64_t> rp;
+    std::vector<int32_t> col;
+    std::vector<float> val;
+    std::vector<BgzfBlock> blocks;
+    std::vector<char> text;
+    int rc = MMVAE_OK;
+    // complete lines [p, e): the header first, then the entries appended in file order
+    auto lines = [&](const char* p, const char* e) -> int {
+        while (!header && p < e) {
+            const char* le = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+            if (!le) le = e;
+            if (*p != '%' && le > p) {
+                std::vector<char> h(p, le);
+                h.push_back('\n');
+                size_t pos;
+                if (!parse_header(h, pos, D, N, nnz_hdr)) return fail(MMVAE_E_ARG, std::string("no MatrixMarket size line in ") + path);
+                if (N >= INT32_MAX || D >= INT32_MAX) return fail(MMVAE_E_ARG, "matrix dimensions exceed int32");
+                header = true;
+                rp.assign((size_t)N + 1, 0);
+                col.reserve((size_t)std::max<int64_t>(nnz_hdr, 0));
+                val.reserve((size_t)std::max<int64_t>(nnz_hdr, 0));
+            }
+            p = le + 1;
+        }
+        if (p >= e) return MMVAE_OK;
+        const size_t body = (size_t)(e - p);
+        const int nch = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * 2, body / (1 << 16) + 1));
+        std::vector<const char*> cut(nch + 1);
+        cut[0] = p;
+        cut[nch] = e;
+        for (int k = 1; k < nch; ++k) {
+            const char* c = std::max(p + body * k / nch, cut[k - 1]);
+            while (c < e && c[-1] != '\n') ++c;
+            cut[k] = c;
+        }
+        std::vector<Chunk> ch(nch);
+        parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
+            for (int64_t k = a; k < b; ++k) parse_chunk(cut[k], cut[k + 1], D, N, ch[(size_t)k]);
+        });
+        for (auto& c : ch) {
+            if (!c.err.empty()) return fail(MMVAE_E_ARG, std::string(path) + ": " + c.err);
+            for (size_t i = 0; i < c.cell.size(); ++i) {
+                if (c.cell[i] < last_cell) return 1;  // not column-sorted: the whole-file path
+                last_cell = c.cell[i];
+                rp[(size_t)last_cell + 1]++;
+                col.push_back(c.gene[i]);
+                val.push_back(c.val[i]);
+            }
+        }
+        return MMVAE_OK;
+    };
+    for (bool eof = false; !eof && rc == MMVAE_OK;) {
+        cbuf.resize(have + WIN);
+        const size_t r = std::fread(cbuf.data() + have, 1, WIN, fp);
+        have += r;
+        eof = r == 0;
+        size_t used = 0;
+        if (!scan_bgzf_window(cbuf.data(), have, blocks, used)) {
+            rc = first ? 1 : fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + path);
+            break;
+        }
+        first = false;
+        if (eof && used != have) {
+            rc = fail(MMVAE_E_ARG, std::string("truncated BGZF block at the end of ") + path);
+            break;
+        }
+        if (blocks.empty()) continue;
+        const size_t total = blocks.back().out_off + blocks.back().out_len;
+        text.resize(carry.size() + total);
+        std::memcpy(text.data(), carry.data(), carry.size());
+        std::atomic<bool> ok{true};
+        parallel_for(threads, (int64_t)blocks.size(), [&](int, int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                const BgzfBlock& k = blocks[(size_t)i];
+                if (!inflate_raw(cbuf.data() + k.in_off, k.in_len, text.data() + carry.size() + k.out_off, k.out_len))
+                    ok = false;
+            }
+        });
+        if (!ok) {
+            rc = fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + path);
+            break;
+        }
+        size_t nl = text.size();
+        while (nl > 0 && text[nl - 1] != '\n') --nl;  // the last complete line ends at nl
+        carry.assign(text.data() + nl, text.size() - nl);
+        rc = lines(text.data(), text.data() + nl);
+        std::memmove(cbuf.data(), cbuf.data() + used, have - used);
+        have -= used;
+    }
+    std::fclose(fp);
+    if (rc == MMVAE_OK && !carry.empty()) {
+        carry.push_back('\n');
+        rc = lines(carry.data(), carry.data() + carry.size());
+    }
+    if (rc != MMVAE_OK) return rc;
+    if (!header) return 1;
+    for (int64_t i = 0; i < N; ++i) rp[(size_t)i + 1] += rp[(size_t)i];
+    std::vector<char>().swap(text);
+    std::vector<unsigned char>().swap(cbuf);
+    return finish_csr(threads, N, D, rp, col, val, out);
+}
+}  // namespace mmvae_host
+
+extern "C" {
 
 int mmvae_mtx_read_dense_t(const char* path, int threads, int64_t* N_out, int64_t* C_out, float** out) {
     if (!path || !N_out || !C_out || !out) return fail(MMVAE_E_ARG, "mtx_read_dense_t: null argument");

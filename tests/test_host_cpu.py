@@ -71,6 +71,34 @@ def test_mtx_read_formats(tmp_path, data, fmt):
     check(str(p), rp, col, val, D)
 
 
+@pytest.mark.parametrize("window", ["4096", "70001", "67108864"])
+def test_mtx_read_streamed_windows(tmp_path, data, monkeypatch, window):
+    """Column-sorted BGZF input streams window by window straight into the CSR (no whole-text
+    buffer): small windows split BGZF blocks and lines at arbitrary points; a mid-file comment and
+    short lines; genes shuffled and duplicated inside cells (sorted, last one kept)."""
+    rp, col, val, D = data
+    monkeypatch.setenv("MMVAE_MTX_WINDOW", window)
+    t = mtx_text(rp, col, val, D, extra=["% mid comment", "7 9", ""])
+    p = tmp_path / "w.mtx.gz"
+    p.write_bytes(bgzf_compress(t))
+    check(str(p), rp, col, val, D)
+    # cells stay grouped, genes inside each cell reversed + one duplicate (the last must win)
+    N = rp.size - 1
+    lines = ["%%MatrixMarket matrix coordinate real general", f"{D} {N} 0"]
+    for c in range(N):
+        s0, s1 = rp[c], rp[c + 1]
+        for j in range(s1 - 1, s0 - 1, -1):
+            lines.append(f"{col[j] + 1} {c + 1} {val[j] + 100:g}")
+        if s1 > s0:
+            lines.append(f"{col[s0] + 1} {c + 1} 0.5")       # duplicate of the first gene, appended last
+            lines.extend(f"{col[j] + 1} {c + 1} {val[j]:g}" for j in range(s0, s1) if j != s0)
+    q = tmp_path / "u.mtx.gz"
+    q.write_bytes(bgzf_compress(("\n".join(lines) + "\n").encode()))
+    want_v = val.astype(np.float32).copy()
+    want_v[rp[:-1][np.diff(rp) > 0]] = 0.5
+    check(str(q), rp, col, want_v, D)
+
+
 def test_mtx_read_shuffled_comments_short_lines(tmp_path, data):
     rp, col, val, D = data
     order = np.random.default_rng(0).permutation(rp[-1])
