@@ -7,6 +7,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mmvae/lbessel.hh"
@@ -474,18 +475,66 @@ int mmvae_destroy(mmvae_h e) {
     return MMVAE_OK;
 }
 
+}  // extern "C"
+
+// Host -> device copy of a large pageable array through two pinned 32 MB chunks: the host copies
+// chunk k + 1 into one while the DMA of chunk k reads the other (pageable hipMemcpy stages
+// serially, at a fraction of the link rate).  Synchronous on return.
+static hipError_t upload_chunked(Engine* e, void* dst, const void* src, size_t bytes) {
+    constexpr size_t CH = (size_t)32 << 20;
+    if (bytes <= CH) return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    char* pin[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipError_t er = hipSuccess;
+    for (int i = 0; i < 2 && er == hipSuccess; ++i) {
+        er = hipHostMalloc((void**)&pin[i], CH);
+        if (er == hipSuccess) er = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    }
+    for (size_t off = 0, k = 0; off < bytes && er == hipSuccess; off += CH, ++k) {
+        const int b = (int)(k & 1);
+        const size_t n = std::min(CH, bytes - off);
+        if (k >= 2) er = hipEventSynchronize(ev[b]);  // this pinned chunk's previous DMA is done
+        if (er != hipSuccess) break;
+        std::memcpy(pin[b], static_cast<const char*>(src) + off, n);
+        er = hipMemcpyAsync(static_cast<char*>(dst) + off, pin[b], n, hipMemcpyHostToDevice, e->stream);
+        if (er == hipSuccess) er = hipEventRecord(ev[b], e->stream);
+    }
+    const hipError_t es = hipStreamSynchronize(e->stream);
+    for (int i = 0; i < 2; ++i) {
+        if (pin[i]) hipHostFree(pin[i]);
+        if (ev[i]) hipEventDestroy(ev[i]);
+    }
+    return er != hipSuccess ? er : es;
+}
+
+extern "C" {
+
 int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
                      int64_t D, const float* covar) {
     if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
     ++e->graph_gen;  // dataset buffers are replaced: step graphs are re-captured
     if (D != e->D) FAIL(e, MMVAE_E_ARG, "upload_csr: D does not match the model's data_dim");
     if (rowptr[0] != 0) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr[0] must be 0");
-    for (int64_t i = 0; i < N; ++i) {
-        if (rowptr[i + 1] < rowptr[i]) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr not monotone");
-        for (int64_t j = rowptr[i]; j < rowptr[i + 1]; ++j) {
-            if (col[j] < 0 || col[j] >= D) FAIL(e, MMVAE_E_ARG, "upload_csr: gene index out of range");
-            if (j > rowptr[i] && col[j] <= col[j - 1])
-                FAIL(e, MMVAE_E_ARG, "upload_csr: gene indices must be strictly increasing within a row");
+    // row validation on host threads (the first bad row of each thread's range is reported)
+    {
+        const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(16, N / 4096));
+        std::vector<int> bad((size_t)nth, 0);  // 1 monotone, 2 range, 3 order
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t] {
+                for (int64_t i = N * t / nth; i < N * (t + 1) / nth && !bad[(size_t)t]; ++i) {
+                    if (rowptr[i + 1] < rowptr[i]) { bad[(size_t)t] = 1; break; }
+                    for (int64_t j = rowptr[i]; j < rowptr[i + 1]; ++j) {
+                        if (col[j] < 0 || col[j] >= D) { bad[(size_t)t] = 2; break; }
+                        if (j > rowptr[i] && col[j] <= col[j - 1]) { bad[(size_t)t] = 3; break; }
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int b : bad) {
+            if (b == 1) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr not monotone");
+            if (b == 2) FAIL(e, MMVAE_E_ARG, "upload_csr: gene index out of range");
+            if (b == 3) FAIL(e, MMVAE_E_ARG, "upload_csr: gene indices must be strictly increasing within a row");
         }
     }
     const int64_t nnz = rowptr[N];
@@ -509,8 +558,8 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice));
     HIPCHK(e, hipMemcpy(e->d_rowptr + N + 1, rowptr + N, sizeof(int64_t), hipMemcpyHostToDevice));
     if (nnz > 0) {
-        HIPCHK(e, hipMemcpy(e->d_col, col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
-        HIPCHK(e, hipMemcpy(e->d_val, val, sizeof(float) * nnz, hipMemcpyHostToDevice));
+        HIPCHK(e, upload_chunked(e, e->d_col, col, sizeof(int32_t) * nnz));
+        HIPCHK(e, upload_chunked(e, e->d_val, val, sizeof(float) * nnz));
     }
     if (covar) {
         HIPCHK(e, hipMemcpy(e->d_covar, covar, sizeof(float) * N * e->C, hipMemcpyHostToDevice));

@@ -233,3 +233,21 @@ def test_cli_configs0_against_oracle_loop(tmp_path):
                 tr.step(x[rr], c[rr], torch.from_numpy(m), torch.from_numpy(n), beta)
         s_orc.append(float(tot / np.float32(B * nbatch)))
     np.testing.assert_allclose(s_cli, s_orc, rtol=1e-4)
+
+
+def test_large_upload_roundtrip_chunked():
+    """A CSR above the 32 MB pinned-chunk size (col and val 60 MB each) uploads through the
+    double-buffered pinned path and reads back exactly (rows spread over the whole range)."""
+    rng = np.random.default_rng(3)
+    N, D, per = 30000, 4000, 500
+    rp = np.arange(N + 1, dtype=np.int64) * per
+    col = np.sort(rng.random((N, D)).argsort(axis=1)[:, :per], axis=1).astype(np.int32).ravel()
+    val = rng.integers(1, 50, rp[-1]).astype(np.float32)
+    eng = mmvae_amd.Engine(D=D, K=8, max_batch=64, dtype="bf16")
+    eng.upload_csr(rp, col, val)
+    rows = np.array([0, 1, 777, 15000, 29998, 29999], dtype=np.int64)
+    grp, gcol, gval = eng.get_rows(rows)
+    want_c = np.concatenate([col[rp[r]:rp[r + 1]] for r in rows])
+    want_v = np.concatenate([val[rp[r]:rp[r + 1]] for r in rows])
+    np.testing.assert_array_equal(gcol, want_c)
+    np.testing.assert_array_equal(gval, want_v)
