@@ -1171,7 +1171,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
         // tile's single barrier; buffer b is rewritten only after the next barrier, which every
         // wave reaches after its combine reads of b
         if (DB && t + 1 < t1) stage_store(buf ^ 1);
-        lds_barrier();
+        if (!(d.dbg & 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
+        if (!(d.dbg & 16384))                 // 16384: diagnostic, slab stores skipped
         for (int i = threadIdx.x; i < (NW / 4) * nq * 64; i += NTH) {  // per 64-row slab block h
             const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
             const float* ph = pb + 4 * h * nq * 64;
