@@ -793,21 +793,24 @@ struct DecNBLds {
     int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
     int sw, st, sp;     // per-buffer strides: W tile, WdT tile (bytes, all planes), column partials (floats)
     int swp, stp;       // one plane of the W / WdT images (bytes)
-    // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'
-    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes, int eszw) {
-        const bool alias = planes == 2;
+    // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'.
+    // loss: the eval instance (no WdT stage, column partials, correction or pq tiles)
+    MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes, int eszw,
+                           bool loss = false) {
+        const bool alias = planes == 2 && !loss;
         swp = 64 * KP * eszw;
-        stp = KP * 64 * esz;
+        stp = loss ? 0 : KP * 64 * esz;
         sw = planes * swp;
         st = planes * stp;
-        sp = ((NW * nq * 64 * 4 + 15) / 16) * 4;
+        sp = loss ? ((16 * NW * 4 + 15) / 16) * 4 : ((NW * nq * 64 * 4 + 15) / 16) * 4;
+        if (loss) csz = 0;
         o_gst = nbuf * sw;
         o_tst = o_gst + nbuf * 1024;
         o_part = o_tst + nbuf * st;
         o_wave = o_part + nbuf * sp * 4;
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q1 = 0;
-        o_q2 = alias ? 0 : 16 * QS * esz;
+        o_q2 = (alias || loss) ? 0 : 16 * QS * esz;
         o_cc = o_q2 + 16 * 68 * 4;
         if (alias) o_q1 = o_cc;
         o_toff = o_cc + 16 * 64 * csz;
@@ -818,8 +821,11 @@ struct DecNBLds {
 };
 
 // PL: the logit GEMM's operand policy (P, or F8 in the fp8 mode with P = bf16 for the dz GEMM)
-template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
+// LOSS: the eval pass (mmvae_run update = 0) — the ELBO's likelihood terms only: the same
+// arithmetic for the loss, without the corrections, column partials, dz GEMMs and WdT stage
+// (the 8-wave loss instance fits two workgroups per CU: 128 VGPRs, ~60 KB of LDS in bf16)
+template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false>
+__global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
     using Fr = typename M::frag;
@@ -852,7 +858,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL));
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
@@ -884,12 +890,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
         wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
-        treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
+        if constexpr (!LOSS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
     auto stage_store = [&](int b_) {
         wreg.store(wst + b_ * L.sw, L.swp);
-        treg.store(tst + b_ * L.st, L.stp);
+        if constexpr (!LOSS) treg.store(tst + b_ * L.st, L.stp);
         if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
@@ -966,7 +972,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
         for (int q = 0; q < RM; ++q) rs[3 + q] = (q < R) ? Lr[d.LAT_ZNU + q] : 0.f;
         for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C) ? Q.covar[cell * C + c] : 0.f;
     }
-    for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+    if constexpr (!LOSS)
+        for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
 
     wave_sync();  // toffl
     ListEntries pend;
@@ -1043,7 +1050,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             lossacc += x * (flog(sv) - flog(mu)) + lgd;                 // nb.hh:527
             const float dq = x * rsv - x * frcp(mu);
             const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
-            cc[cci(r, gl)] = CP::pack(p * dq, ddu);
+            if constexpr (!LOSS) cc[cci(r, gl)] = CP::pack(p * dq, ddu);
         });
         wave_sync();
         lap(1);
@@ -1077,7 +1084,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                 // the block's corrections first (x3: this block's pq overwrites them below)
                 CT ccv[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) ccv[r] = cc[cci(4 * (lane >> 4) + r, gl)];
+                for (int r = 0; r < 4; ++r)
+                    if constexpr (!LOSS) ccv[r] = cc[cci(4 * (lane >> 4) + r, gl)];
                 if constexpr (X) asm volatile("" ::: "memory");
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
@@ -1096,6 +1104,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                     } else {
                         lossd2 = fma2(nup, lg2, lossd2);
                     }
+                    if constexpr (LOSS) continue;
                     float cpa, cda, cpb, cdb;
                     CP::unpack(ccv[2 * h], cpa, cda);
                     CP::unpack(ccv[2 * h + 1], cpb, cdb);
@@ -1114,6 +1123,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                     put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
                     put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);
                 }
+                if constexpr (LOSS) continue;
                 float* pw = pb + w * nq * 64 + gl;
                 if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
                     pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
@@ -1143,11 +1153,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
             else epilogue(std::true_type{});
         }
         wave_sync();
-        if constexpr (!X)
+        if constexpr (!X && !LOSS)
             for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         lap(3);
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
-        if (!(d.dbg & 4))
+        if (!LOSS && !(d.dbg & 4))
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
                 const Fr a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
@@ -1161,7 +1171,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
                     dzP[lb] = M::mma(a2, bw, dzP[lb]);
                 }
             }
-        if constexpr (X) {  // pq consumed: re-zero the correction tile it aliased
+        if constexpr (X && !LOSS) {  // pq consumed: re-zero the correction tile it aliased
             wave_sync();
             for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         }
@@ -1172,7 +1182,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
         // wave reaches after its combine reads of b
         if (DB && t + 1 < t1) stage_store(buf ^ 1);
         if (!(d.dbg & 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
-        if (!(d.dbg & 16384))                 // 16384: diagnostic, slab stores skipped
+        if (!LOSS && !(d.dbg & 16384))        // 16384: diagnostic, slab stores skipped
         for (int i = threadIdx.x; i < (NW / 4) * nq * 64; i += NTH) {  // per 64-row slab block h
             const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
             const float* ph = pb + 4 * h * nq * 64;
@@ -1201,7 +1211,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     }
     // ---- per-row outputs ----
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4 && !LOSS; ++r) {
         float E = Eacc2[r >> 1][r & 1];
         float dz2[RM];
 #pragma unroll
@@ -2038,16 +2048,25 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
         else hipLaunchKernelGGL((k_dec_lse<PM, KP, CMAX>), gdecA, dim3(256), ldsA, st, Q, d);
     }
-    {
-        ScopedTimer tm(e, "k_dec_nb");
+    auto launch_b = [&](auto loss_c) {
+        constexpr bool LS = decltype(loss_c)::value;
         if (nwB == 8) {
-            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM>), gdecB, dim3(512), ldsB8, st, Q, d);
+            const size_t lds = LS ? DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL, (int)sizeof(TL), true).bytes
+                                  : ldsB8;
+            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM, LS>), gdecB, dim3(512), lds, st, Q, d);
         } else if (small_cr)
-            hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL)).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM, LS>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL), LS).bytes, st, Q, d);
         else
-            hipLaunchKernelGGL((k_dec_nb<PB, KP, CMAX, RMAX, 4, false, PM>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL, (int)sizeof(TL)).bytes, st, Q, d);
+            hipLaunchKernelGGL((k_dec_nb<PB, KP, CMAX, RMAX, 4, false, PM, LS>), gdecB, dim3(256),
+                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL, (int)sizeof(TL), LS).bytes, st, Q, d);
+    };
+    {
+        // eval (update = 0): the loss-only instance (MMVAE_EVAL_FULL=1: the full pass, diagnostic)
+        ScopedTimer tm(e, update ? "k_dec_nb" : "k_dec_nb_loss");
+        static const bool eval_full = getenv_is("MMVAE_EVAL_FULL", "1");
+        if (update || eval_full) launch_b(std::false_type{});
+        else launch_b(std::true_type{});
     }
     NBGrads G = nb_grads(e);
     if (!update) {
