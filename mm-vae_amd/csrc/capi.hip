@@ -321,7 +321,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // 8-wave workgroup per CU = 2 units; f32 one 4-wave workgroup)
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
     const bool bf_ops = cfg->dtype == MMVAE_DTYPE_BF16 || cfg->dtype == MMVAE_DTYPE_FP8;  // fp8: bf16 encoders / dz
-    const int dec_cu = vmf_model ? (bf_ops ? 4 : 2) : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
+    // vMF x3 at K <= 32: ~48 KB of LDS per decoder workgroup (no WdT image): 3 per CU
+    const int dec_cu = vmf_model ? (bf_ops ? 4 : (cfg->dtype == MMVAE_DTYPE_BF16X3 && e->KP == 32 ? 3 : 2))
+                                 : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
     e->nsplit_d = pick_split(dec_cu);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));

@@ -179,6 +179,32 @@ template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
     return row * RB + ((((byte >> 4) ^ ((row >> 1) & (NCH - 1)))) << 4) + (byte & 15);
 }
 
+// MFMA 16x16x32 B fragment of a k-by-column block read TRANSPOSED from a swizzled row-major
+// [rows][RB-byte] 16-bit image (the image another GEMM reads row-wise with ds_read_b128):
+// k = rows r0 + 8 (lane >> 4) .. + 7, column c0 + (lane & 15).  Two ds_read_b64_tr_b16: per
+// 16-lane group, lane 4q + p addresses row q of a 4-row block at columns 4p .. 4p + 3 and lane i
+// receives column i of the 4 rows (cdna_hip_programming.md T10).  The 8-byte pieces stay whole
+// under swz_off's 16-byte chunk XOR.  EXEC must be all ones.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0) {
+    const int lane = threadIdx.x & 63;
+    const int row = r0 + 8 * (lane >> 4) + ((lane >> 2) & 3);
+    const int byte = (c0 + 4 * (lane & 3)) * 2;
+    typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + swz_off<RB>(row, byte)));
+    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + swz_off<RB>(row + 4, byte)));
+    return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+template <class P, int RB> struct TrFrag;
+template <int RB> struct TrFrag<__bf16, RB> {
+    static MMVAE_DEV bf16x8 load(const char* img, int r0, int c0, int) { return tr_frag<RB>(img, r0, c0); }
+};
+template <int RB> struct TrFrag<X3, RB> {  // hi and lo planes, plane_bytes apart
+    static MMVAE_DEV MM<X3>::frag load(const char* img, int r0, int c0, int plane_bytes) {
+        return MM<X3>::frag{tr_frag<RB>(img, r0, c0), tr_frag<RB>(img + plane_bytes, r0, c0)};
+    }
+};
+
 template <class T> MMVAE_DEV T to_t(float v);
 template <> MMVAE_DEV float to_t<float>(float v) { return v; }
 template <> MMVAE_DEV __bf16 to_t<__bf16>(float v) { return (__bf16)v; }

@@ -382,12 +382,15 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
     }
 }
 
+// trw (16-bit operands): pass 1 reads the dz GEMM's B operand transposed from the W image, so
+// no WdT image is staged (x3 at K <= 32: 3 workgroups per CU instead of 2)
 struct VDecLds {
     int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, bytes;
     MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass, int planes = 1) {
+        const bool trw = esz == 2;
         o_g = planes * 64 * KP * esz;                         // W image (hi [+ lo])
         o_t = o_g + 1024;
-        o_part = o_t + (pass ? planes * KP * 64 * esz : 0);
+        o_part = o_t + (pass && !trw ? planes * KP * 64 * esz : 0);
         o_wave = o_part + (pass ? 4 * nq * 64 * 4 : 0);
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q1 = 16 * 68 * 4;                                   // after the l tile
@@ -411,6 +414,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     constexpr int LS = 68;
     constexpr int RBW = KP * (int)sizeof(T);
     constexpr int RBT = 64 * (int)sizeof(T);
+    constexpr bool TRW = BF;  // dz B operand read transposed from the W image (VDecLds)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
@@ -441,12 +445,12 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
         wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
-        if (PASS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
+        if (PASS && !TRW) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
     auto stage_store = [&]() {
         wreg.store(wst, WIMG);
-        if (PASS) treg.store(tst, WIMG);
+        if (PASS && !TRW) treg.store(tst, WIMG);
         if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
@@ -562,9 +566,12 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                 const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = M::load(reinterpret_cast<const T*>(
-                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
-                        WIMG / (int)sizeof(T));
+                    Fr bw;
+                    if constexpr (TRW) bw = TrFrag<P, RBW>::load(wst, s * M::KSTEP, 16 * lb, WIMG);
+                    else
+                        bw = M::load(reinterpret_cast<const T*>(
+                            tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                            WIMG / (int)sizeof(T));
                     dz[lb] = M::mma(a1, bw, dz[lb]);
                 }
             }
