@@ -106,7 +106,10 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // dots of depth / nu_enc, nb.hh:448, 498, are taken by k_batch_lists, which visits every entry
 // with its row known.)
 // =======================================================================================
-template <class P, int KP>
+// SB (x3 / f32): single-buffered x tile and W stage — the wave's scatter into its x tile follows
+// its own MFMA operand reads of the tile (one wave's LDS operations complete in order), and the
+// W stage is rewritten between two barriers — so x3 fits 4 workgroups per CU (39 KB) instead of 2.
+template <class P, int KP, bool SB = false>
 __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                  const int32_t* __restrict__ toff,
                                                  const typename Elem<P>::type* __restrict__ WeS, int64_t wplane, Dims d,
@@ -120,7 +123,10 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
     constexpr int STB = KP * RB;
     constexpr int XT = 16 * XS;                    // elements of one x tile plane
-    constexpr int XB = 2 * NPL * XT * (int)sizeof(T);  // per wave: two x tiles [hi 0][hi 1][lo 0][lo 1]
+    constexpr int NB = SB ? 1 : 2;                 // x tiles / W stages
+    constexpr int XB = NB * NPL * XT * (int)sizeof(T);  // per wave: x tiles [hi 0][hi 1][lo 0][lo 1]
+    constexpr int XPL = NB * XT;                   // x plane stride (elements)
+    using Tab = Log1pTab<P, SB ? 512 : LTAB>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t t_entry = (d.dbg & 32) ? stamp_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -128,10 +134,10 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Log1pTab<P>::BYTES);
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Tab::BYTES, NB);
     char* wst = smem;
     uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
-    Log1pTab<P>::fill(ltab);
+    Tab::fill(ltab);
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
     int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_toff) + w * S;
 
@@ -146,13 +152,13 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl)
             for (int i = lane; i < XT * (int)sizeof(T) / 16; i += 64)
-                reinterpret_cast<uint4*>(x0 + pl * 2 * XT)[i] = uint4{0, 0, 0, 0};
+                reinterpret_cast<uint4*>(x0 + pl * XPL)[i] = uint4{0, 0, 0, 0};
     };
     zero_tile(xt);
-    if constexpr (Log1pTab<P>::ON) __syncthreads();  // the table
+    if constexpr (Tab::ON) __syncthreads();  // the table
     else wave_sync();
     auto scatter = [&](const ListEntries& le, T* dst) {
-        le.visit(ents, lane, [&](int r, int gl, float x) { Log1pTab<P>::put(ltab, dst, r * XS + gl, 2 * XT, x); });
+        le.visit(ents, lane, [&](int r, int gl, float x) { Tab::put(ltab, dst, r * XS + gl, XPL, x); });
     };
 
     f32x4 acc[KP / 16];
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
         first.fetch(ents, segw, toffl, 0, lane);
 #pragma unroll
         for (int i = 0; i < EDEPTH; ++i) q[i].fetch(ents, segw, toffl, min(1 + i, nt - 1), lane);
-        wreg.store(wst, 2 * STB);
+        wreg.store(wst, NB * STB);
         scatter(first, xt);
     }
     lds_barrier();
@@ -181,23 +187,23 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
         }
     };
     for (int t = t0; t < t1; ++t) {
-        const int tl = t - t0, buf = tl & 1;
+        const int tl = t - t0, buf = SB ? 0 : (tl & 1);
         // unconditional (clamped) prefetch of the next weight tile: counted vmcnt waits
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
         const T* xb = xt + buf * XT;
 #pragma unroll
         for (int s = 0; s < 64 / M::KSTEP; ++s) {
-            const Fr a = M::load(&xb[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL], 2 * XT);
+            const Fr a = M::load(&xb[(lane & 15) * XS + s * M::KSTEP + (lane >> 4) * M::EPL], XPL);
 #pragma unroll
             for (int lb = 0; lb < KP / 16; ++lb) {
                 const Fr bw = M::load(reinterpret_cast<const T*>(
                     wst + buf * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
-                    2 * STB / (int)sizeof(T));
+                    NB * STB / (int)sizeof(T));
                 acc[lb] = M::mma(a, bw, acc[lb]);
             }
         }
         lap(sa);
-        T* xn = xt + (buf ^ 1) * XT;
+        T* xn = xt + (SB ? 0 : (buf ^ 1)) * XT;
         if (t + 1 < t1) {
             zero_tile(xn);
             wave_sync();
@@ -208,7 +214,12 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
 #pragma unroll
         for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
         q[EDEPTH - 1].fetch(ents, segw, toffl, min(tl + 1 + EDEPTH, nt - 1), lane);
-        if (t + 1 < t1) wreg.store(wst + (buf ^ 1) * STB, 2 * STB);
+        if constexpr (SB) {
+            lds_barrier();  // every wave's reads of this W stage done
+            if (t + 1 < t1) wreg.store(wst, STB);
+        } else if (t + 1 < t1) {
+            wreg.store(wst + (buf ^ 1) * STB, 2 * STB);
+        }
         lap(sc);
         lds_barrier();
         lap(sd);
@@ -1939,13 +1950,17 @@ static size_t dec_lds(const Dims& d, int pass, int esz, int planes) {
     return s;
 }
 
+// the single-buffered encoder forward in the split-element modes (x3, f32)
+template <class P> struct EncSB { static constexpr bool value = !std::is_same<P, __bf16>::value; };
 template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int NPL = IsX3<P>::value ? 2 : 1;
     constexpr int XS = sizeof(T) == 2 ? 80 : 68;
-    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, 2 * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
-                          Log1pTab<P>::BYTES).bytes;
+    constexpr bool SB = EncSB<P>::value;
+    constexpr int NB = SB ? 1 : 2;
+    return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, NB * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
+                          Log1pTab<P, SB ? 512 : LTAB>::BYTES, NB).bytes;
 }
 // the encoder operand images of mode P: bf16 planes (bf16, x3) or f32
 template <class P> static const typename Elem<P>::type* op_img(const float* f, const __bf16* b) {
@@ -1954,7 +1969,7 @@ template <class P> static const typename Elem<P>::type* op_img(const float* f, c
 }
 template <class P, int KP>
 static void enc_fwd_run(Engine* e, const Dims& d, float* hpart, hipStream_t st) {
-    hipLaunchKernelGGL((k_enc_fwd<P, KP>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
+    hipLaunchKernelGGL((k_enc_fwd<P, KP, EncSB<P>::value>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
                        e->d_seg, e->d_toff, op_img<P>(e->d_WeS_f, e->d_WeS_b), (int64_t)e->KP * e->DP, d, hpart);
 }
 // encoder backward operands: dh^T planes and the staged W (f32 in the x3 mode)

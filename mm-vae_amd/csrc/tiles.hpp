@@ -149,12 +149,12 @@ template <class P> MMVAE_DEV float log1p_cnt(float x) {
 // pair packed in one word, f32: the float — so an entry is one LDS read instead of log1pf plus
 // the split.  Other counts (non-integer, >= LTAB) take log1pf.  The bf16 mode keeps one v_log.
 static constexpr int LTAB = 1024;
-template <class P> struct Log1pTab {
+template <class P, int N = LTAB> struct Log1pTab {
     static constexpr bool ON = !std::is_same<P, __bf16>::value;
-    static constexpr int BYTES = ON ? LTAB * 4 : 0;
+    static constexpr int BYTES = ON ? N * 4 : 0;
     MMVAE_DEV static void fill(uint32_t* tab) {
         if constexpr (ON)
-            for (int i = threadIdx.x; i < LTAB; i += 256) {
+            for (int i = threadIdx.x; i < N; i += 256) {
                 const float v = log1pf((float)i);
                 if constexpr (IsX3<P>::value) {
                     const __bf16 h = bf_hi(v), l = bf_lo(v, h);
@@ -171,7 +171,7 @@ template <class P> struct Log1pTab {
             t[idx] = to_t<T>(flog(1.f + x));
         } else {
             const int xi = (int)x;
-            if (x == (float)xi && (unsigned)xi < (unsigned)LTAB) {
+            if (x == (float)xi && (unsigned)xi < (unsigned)N) {
                 const uint32_t v = tab[xi];
                 if constexpr (IsX3<P>::value) {
                     t[idx] = __builtin_bit_cast(__bf16, (uint16_t)(v & 0xffffu));
@@ -430,9 +430,10 @@ MMVAE_DEV const float* chain_run(const Dims& d, int l0, int l1, const float* in,
 // images of the double-buffered W stage: [hi 0][hi 1][lo 0][lo 1])
 struct EncLds {
     int o_x, o_toff, o_tab, bytes;
-    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1, int tab_bytes = 0) {
+    MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1, int tab_bytes = 0,
+                         int nbuf = 2) {
         const int stb = KP * 64 * esz;
-        o_x = pre + 2 * planes * stb;
+        o_x = pre + nbuf * planes * stb;
         o_toff = o_x + 4 * xbytes_per_wave;  // [4 waves][S] tile offsets
         o_tab = o_toff + ((4 * S * 4 + 15) / 16) * 16;  // log1p table (Log1pTab)
         bytes = o_tab + tab_bytes;
