@@ -327,8 +327,8 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->nsplit_d = pick_split(dec_cu);
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
-    // encoder forward: bf16 ~37 KB (double-buffered), x3 ~39 KB single-buffered: 4 per CU; f32 3
-    e->nsplit_e = pick_split(cfg->dtype == MMVAE_DTYPE_F32 ? 3 : 4);
+    // encoder forward: bf16 ~37 KB (double-buffered), x3 ~39 KB single-buffered: 4 per CU; f32 2
+    e->nsplit_e = pick_split(cfg->dtype == MMVAE_DTYPE_F32 ? 2 : 4);
     // encoder backward: bf16 ~37 KB LDS (4 per CU); x3 / f32 keep W in registers, ~43 KB (3 per CU)
     e->nsplit_b = pick_split(bf_ops ? 4 : 3);
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A

@@ -327,12 +327,15 @@ MMVAE_DEV GammaAt gamma_at(float v, bool need_dg) {
     return o;
 }
 
+// NF: the largest count on the finite-product path (8; 4 in the f32 mode, whose pass B already
+// spills at 256 VGPRs and runs slower with the longer product)
+template <int NF = 8>
 MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
     // counts up to 8: P <= (nup + 7)^8 <= ~1e32 for the clamped nup <= 1e4 + 1e-4, x! <= 40320 exact
-    if (x <= 8.f && x == floorf(x)) {
+    if (x <= (float)NF && x == floorf(x)) {
         float P = 1.f, Pd = 0.f, F = 1.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NF; ++i) {
             const bool on = (float)i < x;
             const float a = on ? nup + (float)i : 1.f;
             Pd = on ? fmaf(Pd, a, P) : Pd;

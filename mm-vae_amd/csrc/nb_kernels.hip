@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // dots of depth / nu_enc, nb.hh:448, 498, are taken by k_batch_lists, which visits every entry
 // with its row known.)
 // =======================================================================================
-// SB (x3 / f32): single-buffered x tile and W stage — the wave's scatter into its x tile follows
+// SB (x3): single-buffered x tile and W stage — the wave's scatter into its x tile follows
 // its own MFMA operand reads of the tile (one wave's LDS operations complete in order), and the
 // W stage is rewritten between two barriers — so x3 fits 4 workgroups per CU (39 KB) instead of 2.
 template <class P, int KP, bool SB = false>
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             const float sv = mu + nup;
             const float rsv = frcp(sv);
             float lgd, dgd;
-            nb_gamma_terms(nup, x, lgd, dgd);                           // nb.hh:522-523
+            nb_gamma_terms<std::is_same<P, float>::value ? 4 : 8>(nup, x, lgd, dgd);  // nb.hh:522-523
             lossacc += x * (flog(sv) - flog(mu)) + lgd;                 // nb.hh:527
             const float dq = x * rsv - x * frcp(mu);
             const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
@@ -1950,8 +1950,9 @@ static size_t dec_lds(const Dims& d, int pass, int esz, int planes) {
     return s;
 }
 
-// the single-buffered encoder forward in the split-element modes (x3, f32)
-template <class P> struct EncSB { static constexpr bool value = !std::is_same<P, __bf16>::value; };
+// the single-buffered encoder forward in the x3 mode (f32: 3 waves / SIMD by VGPRs either way,
+// and measured faster double-buffered at 2 workgroups per CU)
+template <class P> struct EncSB { static constexpr bool value = IsX3<P>::value; };
 template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;

@@ -594,16 +594,47 @@ static int stream_sorted_csr(const char* path, int threads, mmvae_csr* out) {
         parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
             for (int64_t k = a; k < b; ++k) parse_chunk(cut[k], cut[k + 1], D, N, ch[(size_t)k]);
         });
-        for (auto& c : ch) {
+        // chunks in file order: sortedness across chunk boundaries and the output offsets (serial,
+        // per chunk); within a chunk the check, the copy and the row counts run in parallel.  A
+        // chunk counts every entry but those of its first cell, which may continue the previous
+        // chunk's last cell: that head count is added here, so no two chunks write one counter.
+        std::vector<size_t> off(nch + 1, col.size());
+        for (int k = 0; k < nch; ++k) {
+            const Chunk& c = ch[(size_t)k];
             if (!c.err.empty()) return fail(MMVAE_E_ARG, std::string(path) + ": " + c.err);
-            for (size_t i = 0; i < c.cell.size(); ++i) {
-                if (c.cell[i] < last_cell) return 1;  // not column-sorted: the whole-file path
-                last_cell = c.cell[i];
-                rp[(size_t)last_cell + 1]++;
-                col.push_back(c.gene[i]);
-                val.push_back(c.val[i]);
+            if (!c.cell.empty()) {
+                if (c.cell.front() < last_cell) return 1;  // not column-sorted: the whole-file path
+                last_cell = c.cell.back();
             }
+            off[(size_t)k + 1] = off[(size_t)k] + c.cell.size();
         }
+        col.resize(off[(size_t)nch]);
+        val.resize(off[(size_t)nch]);
+        std::vector<int64_t> head(nch, 0);
+        std::atomic<bool> sorted{true};
+        parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
+            for (int64_t k = a; k < b; ++k) {
+                const Chunk& c = ch[(size_t)k];
+                const size_t n = c.cell.size();
+                if (!n) continue;
+                std::memcpy(col.data() + off[(size_t)k], c.gene.data(), n * sizeof(int32_t));
+                std::memcpy(val.data() + off[(size_t)k], c.val.data(), n * sizeof(float));
+                const int64_t c0 = c.cell[0];
+                int64_t h = 0;
+                for (size_t i = 0; i < n; ++i) {
+                    if (i && c.cell[i] < c.cell[i - 1]) {
+                        sorted = false;
+                        break;
+                    }
+                    if (c.cell[i] == c0) ++h;
+                    else rp[(size_t)c.cell[i] + 1]++;
+                }
+                head[(size_t)k] = h;
+            }
+        });
+        if (!sorted) return 1;
+        for (int k = 0; k < nch; ++k)
+            if (!ch[(size_t)k].cell.empty()) rp[(size_t)ch[(size_t)k].cell[0] + 1] += head[(size_t)k];
         return MMVAE_OK;
     };
     for (bool eof = false; !eof && rc == MMVAE_OK;) {
