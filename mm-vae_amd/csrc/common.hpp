@@ -195,6 +195,23 @@ template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0) {
     const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + swz_off<RB>(row + 4, byte)));
     return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
+// x3 pq operand of decoder pass B, stored per 16-gene block as [16 genes][16 rows] bf16 planes
+// (hi at +0, lo at +512 bytes; blocks 2 KB apart): the epilogue writes a lane's row pair of one
+// gene as one 32-bit word per plane, and the dz GEMM reads the MFMA A fragment (row lane & 15,
+// genes k0 + 8 (lane >> 4) .. + 7) transposed with two ds_read_b64_tr_b16 per plane.  EXEC must
+// be all ones.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+MMVAE_DEV uint32_t pk_bf16(float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)a, (__bf16)b}); }
+MMVAE_DEV int pqt_off(int g, int r) { return (g >> 4) * 2048 + (g & 15) * 32 + r * 2; }  // bytes
+MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0) {
+    const int lane = threadIdx.x & 63;
+    const int k = k0 + 8 * (lane >> 4) + ((lane >> 2) & 3), r = 4 * (lane & 3);
+    typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off(k, r)));
+    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off(k + 4, r)));
+    return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
 template <class P, int RB> struct TrFrag;
 template <int RB> struct TrFrag<__bf16, RB> {
     static MMVAE_DEV bf16x8 load(const char* img, int r0, int c0, int) { return tr_frag<RB>(img, r0, c0); }
@@ -296,7 +313,7 @@ MMVAE_DEV float dsoftplus(float u) { return (u > 20.f) ? 1.f : 1.f / (1.f + expf
 //   lgd = lgamma(nup) + lgamma(x + 1) - lgamma(nup + x)      (nb.hh:522-523)
 //   dgd = digamma(nup) - digamma(nup + x)                    (its d/d nup)
 // Counts 1..8 (the bulk of single-cell data) use the exact finite product / sum with one log
-// and one reciprocal.  Everything else shifts each argument below 8 up by 8 (branch free:
+// and one reciprocal (x! from the caller's LDS table ftab[0..8]).  Everything else shifts each argument below 8 up by 8 (branch free:
 // P = v(v+1)..(v+7) and S = P'/P = sum 1/(v+i) by the product rule) and evaluates Stirling's
 // series and the digamma asymptotic series at z >= 8 (truncation < 1e-9 relative), sharing
 // log z and 1/z between the two.
@@ -330,20 +347,19 @@ MMVAE_DEV GammaAt gamma_at(float v, bool need_dg) {
 // NF: the largest count on the finite-product path (8; 4 in the f32 mode, whose pass B already
 // spills at 256 VGPRs and runs slower with the longer product)
 template <int NF = 8>
-MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd) {
+MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd, const float* ftab) {
     // counts up to 8: P <= (nup + 7)^8 <= ~1e32 for the clamped nup <= 1e4 + 1e-4, x! <= 40320 exact
     if (x <= (float)NF && x == floorf(x)) {
-        float P = 1.f, Pd = 0.f, F = 1.f;
+        float P = 1.f, Pd = 0.f;
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
             const bool on = (float)i < x;
             const float a = on ? nup + (float)i : 1.f;
             Pd = on ? fmaf(Pd, a, P) : Pd;
             P *= a;
-            F *= on ? (float)(i + 1) : 1.f;
         }
         const float rP = frcp(P);
-        lgd = flog(F * rP);     // log(x!) - log(nup (nup+1) .. (nup+x-1))
+        lgd = flog(ftab[(int)x] * rP);  // log(x!) - log(nup (nup+1) .. (nup+x-1))
         dgd = -Pd * rP;         // -sum 1/(nup+i)
     } else {
         const GammaAt a = gamma_at(nup, true), b = gamma_at(nup + x, true), c = gamma_at(x + 1.f, false);

@@ -796,12 +796,12 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
 // decoder tiles serve 128 rows instead of 64.  NW = 4 (64 rows, two workgroups per CU) otherwise.
 // x3 mode (ALIAS): the dz GEMM's pq operand (hi + lo planes, 4 bytes per element) lives inside
 // the wave's correction tile, laid out by 16-gene block: block gb of the correction tile is
-// [16 rows][16 genes] f32 pairs (2 KB), its first 1 KB holds pq's [16][16] hi plane then lo
-// plane.  The epilogue reads all of a block's corrections before it writes that block's pq, and
+// [16 rows][16 genes] f32 pairs (2 KB), its first 1 KB holds pq's hi plane then lo plane, each
+// [16 genes][16 rows] (pqt_off: a row pair is one word; read back transposed, pqt_frag).  The epilogue reads all of a block's corrections before it writes that block's pq, and
 // the tile is re-zeroed after the dz GEMM has read pq — saving the separate 4.6 KB pq tile per
 // wave that would not fit 8 waves of x3 images in 160 KB.
 struct DecNBLds {
-    int o_gst, o_tst, o_part, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
+    int o_gst, o_tst, o_part, o_fact, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
     int sw, st, sp;     // per-buffer strides: W tile, WdT tile (bytes, all planes), column partials (floats)
     int swp, stp;       // one plane of the W / WdT images (bytes)
     // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'.
@@ -818,7 +818,8 @@ struct DecNBLds {
         o_gst = nbuf * sw;
         o_tst = o_gst + nbuf * 1024;
         o_part = o_tst + nbuf * st;
-        o_wave = o_part + nbuf * sp * 4;
+        o_fact = o_part + nbuf * sp * 4;  // x! for x = 0..8 (nb_gamma_terms)
+        o_wave = o_fact + 48;
         const int QS = 64 + (esz == 2 ? 8 : 4);
         o_q1 = 0;
         o_q2 = (alias || loss) ? 0 : 16 * QS * esz;
@@ -874,6 +875,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
     float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][nq][64]
+    float* ftab = reinterpret_cast<float*>(smem + L.o_fact);
+    if (threadIdx.x < 9) {  // published by the barrier of the row lse block below
+        float f = 1.f;
+        for (int i = 2; i <= (int)threadIdx.x; ++i) f *= (float)i;
+        ftab[threadIdx.x] = f;
+    }
     char* wp = smem + L.o_wave + w * L.wave_bytes;
     T* q1 = reinterpret_cast<T*>(wp + L.o_q1);
     float* q2 = reinterpret_cast<float*>(wp + L.o_q2);
@@ -1055,11 +1062,11 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             const bool msk = nu == spv;                                 // clamp passes the gradient
             const float nup = nu + 1e-4f;
             const float sv = mu + nup;
-            const float rsv = frcp(sv);
+            const float rsv = frcp(sv), rmu = frcp(mu);
             float lgd, dgd;
-            nb_gamma_terms<std::is_same<P, float>::value ? 4 : 8>(nup, x, lgd, dgd);  // nb.hh:522-523
-            lossacc += x * (flog(sv) - flog(mu)) + lgd;                 // nb.hh:527
-            const float dq = x * rsv - x * frcp(mu);
+            nb_gamma_terms<std::is_same<P, float>::value ? 4 : 8>(nup, x, lgd, dgd, ftab);  // nb.hh:522-523
+            lossacc += x * flog(sv * rmu) + lgd;                        // nb.hh:527: x (log(mu+nu) - log(mu))
+            const float dq = x * (rsv - rmu);
             const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
             if constexpr (!LOSS) cc[cci(r, gl)] = CP::pack(p * dq, ddu);
         });
@@ -1131,8 +1138,16 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         csduz[qq] = fma2(du, znu2[h][qq], csduz[qq]);
                         dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                     }
-                    put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
-                    put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);
+                    if constexpr (X) {  // hi / lo planes of the row pair, one word each
+                        char* qb = reinterpret_cast<char*>(q1) + pqt_off(gl, rl);
+                        const uint32_t hp = pk_bf16(pq.x, pq.y);
+                        const f2 lo = pq - f2{__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+                        *reinterpret_cast<uint32_t*>(qb) = hp;
+                        *reinterpret_cast<uint32_t*>(qb + 512) = pk_bf16(lo.x, lo.y);
+                    } else {
+                        put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
+                        put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);
+                    }
                 }
                 if constexpr (LOSS) continue;
                 float* pw = pb + w * nq * 64 + gl;
@@ -1171,7 +1186,13 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         if (!LOSS && !(d.dbg & 4))
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
-                const Fr a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
+                Fr a1;
+                if constexpr (X) {
+                    const char* qb = reinterpret_cast<const char*>(q1);
+                    a1 = Fr{pqt_frag(qb, s * M::KSTEP), pqt_frag(qb + 512, s * M::KSTEP)};
+                } else {
+                    a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
+                }
                 const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
@@ -1643,11 +1664,16 @@ __global__ __launch_bounds__(256) void k_enc_bwd_small(const uint2* __restrict__
 }
 
 // Per-gene gradients from the per-row-block column slabs of passes B, C and k_enc_bwd,
-// summed in a fixed order (deterministic).  32 genes x 8 row-block partitions per workgroup.
+// summed in a fixed order (deterministic).  64 genes x NPART row-block partitions per
+// workgroup: a thread reads 4 consecutive genes of every slab row with one 16-byte load (a
+// wave covers 1 KB of 4 row blocks per load, all of a thread's loads independent and in
+// flight together); the partitions' partial sums meet in LDS and thread g < 64 adds them in
+// partition order.
 // SMALL: the default widths C = R = H = 1 (9 slab rows per gene, all compile-time).
 // PART: 0 = every per-gene gradient; 1 = decoder side only (slabs B, C: mu_bias, nu_bias,
 // covar_decoding, nu_decoding — final after pass C, all-reduced while the encoder backward
 // runs); 2 = encoder side only (slab E: x_mean, ln_x_sd, depth, nu_encoding).
+static constexpr int GG_GENES = 64;  // genes per k_grad_genes workgroup
 template <bool SMALL, int PART>
 __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ gene,
@@ -1657,44 +1683,68 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ smallg, int nrb,
                                                     double* __restrict__ sqpart) {
     constexpr int NQMAX = SMALL ? 9 : (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
-    constexpr int NPART = 8;
+    constexpr int NQR = NQMAX + 1;         // + the column dot sum_k cdh[k] W_enc[k][g]
+    constexpr int NPART = SMALL ? 16 : 4;  // row-block partitions (LDS: NPART x NQR x 64 floats)
+    constexpr int TPP = 256 / NPART;       // threads per partition: 16 (SMALL) or 64
+    constexpr int GPT = GG_GENES / TPP;    // genes per thread: 4 or 1
     __shared__ float cdh[64];
-    __shared__ float red[NPART - 1][32][NQMAX + 1];
+    __shared__ float red[NPART][NQR][GG_GENES];
     const int C = SMALL ? 1 : d.C, R = SMALL ? 1 : d.R, H = SMALL ? 1 : d.H;
     const int nqB = (1 + C) + 1 + R, nqC = 1 + C, nqE = 2 + H;
     const int nq = nqB + nqC + nqE;
     for (int k = threadIdx.x; k < d.KE; k += 256) cdh[k] = smallg[k];
-    const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
-    const int g = blockIdx.x * 32 + gi;
-    float acc[NQMAX];
+    const int part = threadIdx.x / TPP, gq = (threadIdx.x % TPP) * GPT;
+    const int g0 = blockIdx.x * GG_GENES;  // DP is a multiple of 64: every slab read is in bounds
+    typedef float vec __attribute__((ext_vector_type(GPT)));
+    vec acc[NQMAX];
 #pragma unroll
-    for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
-    if (g < d.D) {
-#pragma unroll 2
-        for (int rb = part; rb < nrb; rb += NPART) {
-            const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
-            const float* sC = slabC + (int64_t)rb * nqC * d.DP + g;
-            const float* sE = slabE + (int64_t)rb * nqE * d.DP + g;
+    for (int q = 0; q < NQMAX; ++q) acc[q] = vec(0.f);
+    auto ld = [&](const float* p) { return *reinterpret_cast<const vec*>(p); };
+    // the encoder-side column dot's W_enc loads go out first (every thread: latent rows
+    // part, part + NPART, ... of its genes; W_enc is [KE][D], unpadded)
+    vec gs = vec(0.f);
+    if (PART != 1) {
+        __syncthreads();  // cdh
+#pragma unroll 4
+        for (int k = part; k < d.KE; k += NPART)
 #pragma unroll
-            for (int q = 0; q < NQMAX; ++q) {
-                if (q < nqB) { if (PART != 2) acc[q] += sB[(int64_t)q * d.DP]; }
-                else if (q < nqB + nqC) { if (PART != 2) acc[q] += sC[(int64_t)(q - nqB) * d.DP]; }
-                else if (q < nq) { if (PART != 1) acc[q] += sE[(int64_t)(q - nqB - nqC) * d.DP]; }
+            for (int i = 0; i < GPT; ++i) {
+                const int gg = min(g0 + gq + i, d.D - 1);
+                gs[i] = fmaf(cdh[k], P.We[(int64_t)k * d.D + gg], gs[i]);
             }
+    }
+#pragma unroll 2
+    for (int rb = part; rb < nrb; rb += NPART) {
+        const float* sB = slabB + (int64_t)rb * nqB * d.DP + g0 + gq;
+        const float* sC = slabC + (int64_t)rb * nqC * d.DP + g0 + gq;
+        const float* sE = slabE + (int64_t)rb * nqE * d.DP + g0 + gq;
+#pragma unroll
+        for (int q = 0; q < NQMAX; ++q) {
+            if (q < nqB) { if (PART != 2) acc[q] += ld(sB + (int64_t)q * d.DP); }
+            else if (q < nqB + nqC) { if (PART != 2) acc[q] += ld(sC + (int64_t)(q - nqB) * d.DP); }
+            else if (q < nq) { if (PART != 1) acc[q] += ld(sE + (int64_t)(q - nqB - nqC) * d.DP); }
         }
     }
-    if (part > 0)
 #pragma unroll
-        for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
+    for (int q = 0; q < NQMAX; ++q)
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) red[part][q][gq + i] = acc[q][i];
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) red[part][NQMAX][gq + i] = gs[i];
     __syncthreads();
     // sum of squares of every gradient element this block writes (clip norm partial, world 1)
     double sq = 0.0;
     auto put = [&](float* dst, float v) { *dst = v; sq += (double)v * v; };
-    if (part == 0 && g < d.D) {
+    const int g = g0 + (int)threadIdx.x;
+    if (threadIdx.x < GG_GENES && g < d.D) {
+    float acc[NQR];
 #pragma unroll
-    for (int pp = 0; pp < NPART - 1; ++pp)
+    for (int q = 0; q < NQR; ++q) {
+        float v = 0.f;
 #pragma unroll
-        for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
+        for (int pp = 0; pp < NPART; ++pp) v += red[pp][q][threadIdx.x];
+        acc[q] = v;
+    }
     const float* cs1 = acc;               // [1+C]
     const float du = acc[1 + C];
     const float* duz = acc + 2 + C;       // [R]
@@ -1713,9 +1763,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     }
     if (PART != 1) {
     // encoder normalisation params (nb.hh:408-410)
-    float gs = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < d.KE; ++k) gs += cdh[k] * P.We[(int64_t)k * d.D + g];
+    const float gs = acc[NQMAX];
     const float inv = gene[g];
     put(&G.xm[g], -inv * gs);
     const float th = P.lsd[g];
@@ -1723,8 +1771,8 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
     put(&G.wdp[g], raw[0]);
     for (int h = 0; h < H; ++h) put(&G.Wne[(int64_t)h * d.D + g], raw[1 + h]);
     }  // PART != 1
-    }  // part == 0 && g < D
-    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..31)
+    }  // threadIdx.x < 64 && g < D
+    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..63)
         sq = wave_sum_d(sq);
         if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
     }
@@ -2101,10 +2149,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     if (split) {  // decoder-side gene gradients final: all-reduce them under the encoder backward
         ScopedTimer tm(e, "k_grad_genes_dec");
         if (small_genes)
-            hipLaunchKernelGGL((k_grad_genes<true, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+            hipLaunchKernelGGL((k_grad_genes<true, 1>), dim3((d.D + GG_GENES - 1) / GG_GENES), dim3(256), 0, st, P, d, G, gene,
                                e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
         else
-            hipLaunchKernelGGL((k_grad_genes<false, 1>), dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene,
+            hipLaunchKernelGGL((k_grad_genes<false, 1>), dim3((d.D + GG_GENES - 1) / GG_GENES), dim3(256), 0, st, P, d, G, gene,
                                e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
         hipError_t er = comm_bucket(e, 0);
         if (er != hipSuccess) return er;
@@ -2118,7 +2166,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
     const int SMALL = small_len(d.K, d.E, d.KE, d.C, 2 * d.R * d.H + 2 * d.R + d.H + 1);
-    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
+    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + GG_GENES - 1) / GG_GENES;
     const bool fuse_sq = !split && !(e->comm && e->world > 1);  // no all-reduce after these kernels
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;

@@ -900,7 +900,7 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
                                                      const float* __restrict__ WeP_f, const float* __restrict__ slabB,
                                                      const float* __restrict__ slabE, const float* __restrict__ smallg,
                                                      int nrb, double* __restrict__ sqpart) {
-    constexpr int NQMAX = 1 + CMAX + 1;
+    constexpr int NQMAX = 1 + CMAX + 1 + 1;  // + the column dot sum_k cdh[k] W~[k][g]
     constexpr int NPART = 8;
     __shared__ float cdh[64];
     __shared__ float red[NPART - 1][32][NQMAX + 1];
@@ -911,6 +911,12 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
     float acc[NQMAX];
 #pragma unroll
     for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
+    if (PART != 1) {  // the column dot's loads first, latent rows part, part + NPART, ... per thread
+        __syncthreads();  // cdh
+        if (g < d.D)
+#pragma unroll 4
+            for (int k = part; k < d.KE; k += NPART) acc[NQMAX - 1] = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], acc[NQMAX - 1]);
+    }
     if (g < d.D) {
         for (int rb = part; rb < nrb; rb += NPART) {
             const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
@@ -938,8 +944,7 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
         }
         if (PART != 1) {
             const float Gl = acc[nqB];
-            float gs = 0.f;
-            for (int k = 0; k < d.KE; ++k) gs = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], gs);
+            const float gs = acc[NQMAX - 1];
             const float inv = gene[g];
             put(&G.xm[g], -inv * gs);
             put(&G.lsd[g], -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]));
