@@ -614,24 +614,33 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                 for (int c = 1; c < CM; ++c)
                     w2[gb][c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] * L2E : 0.f;
             }
+            // rows 2h, 2h + 1 as one packed-f32 pair
 #pragma unroll
             for (int j = 0; j < J; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float l2[4];
+                for (int h = 0; h < 2; ++h) {
+                    f2 l2[4];
 #pragma unroll
                     for (int gb = 0; gb < 4; ++gb) {
-                        float v = b2[gb];
+                        f2 v = splat2(b2[gb]);
 #pragma unroll
-                        for (int c = 0; c < CM; ++c) v = fmaf(crow[j][r][c], w2[gb][c], v);
-                        l2[gb] = fmaf(acc[gb][j][r], L2E * ainv, v);
+                        for (int c = 0; c < CM; ++c) v = fma2(f2{crow[j][2 * h][c], crow[j][2 * h + 1][c]}, splat2(w2[gb][c]), v);
+                        l2[gb] = fma2(f2{acc[gb][j][2 * h], acc[gb][j][2 * h + 1]}, splat2(L2E * ainv), v);
                     }
-                    const float mn = fmaxf(mrun[j][r], fmaxf(fmaxf(l2[0], l2[1]), fmaxf(l2[2], l2[3])));
-                    float sacc = srun[j][r] * fexp2(mrun[j][r] - mn);
+                    f2 mo = f2{mrun[j][2 * h], mrun[j][2 * h + 1]}, mn;
+                    mn.x = fmaxf(mo.x, fmaxf(fmaxf(l2[0].x, l2[1].x), fmaxf(l2[2].x, l2[3].x)));
+                    mn.y = fmaxf(mo.y, fmaxf(fmaxf(l2[0].y, l2[1].y), fmaxf(l2[2].y, l2[3].y)));
+                    const f2 dm = mo - mn;
+                    f2 sacc = f2{srun[j][2 * h], srun[j][2 * h + 1]} * f2{fexp2(dm.x), fexp2(dm.y)};
 #pragma unroll
-                    for (int gb = 0; gb < 4; ++gb) sacc += fexp2(l2[gb] - mn);
-                    srun[j][r] = sacc;
-                    mrun[j][r] = mn;
+                    for (int gb = 0; gb < 4; ++gb) {
+                        const f2 e2 = l2[gb] - mn;
+                        sacc += f2{fexp2(e2.x), fexp2(e2.y)};
+                    }
+                    srun[j][2 * h] = sacc.x;
+                    srun[j][2 * h + 1] = sacc.y;
+                    mrun[j][2 * h] = mn.x;
+                    mrun[j][2 * h + 1] = mn.y;
                 }
         } else
 #pragma unroll
@@ -652,22 +661,26 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             wcd[0] = g4.z;
 #pragma unroll
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
-            {  // pass C
-                float cs[1 + CM];
+            {  // pass C: rows 2h, 2h + 1 as one packed-f32 pair
+                f2 csp[1 + CM];
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
+                for (int c = 0; c < 1 + CM; ++c) csp[c] = splat2(0.f);
 #pragma unroll
                 for (int j = 0; j < J; ++j)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float lg = fmaf(acc[j][r], ainv, g4.x);
+                    for (int h = 0; h < 2; ++h) {
+                        f2 lg = fma2(f2{acc[j][2 * h], acc[j][2 * h + 1]}, splat2(ainv), splat2(g4.x));
 #pragma unroll
-                        for (int c = 0; c < CM; ++c) lg = fmaf(crow[j][r][c], wcd[c], lg);
-                        const float wp = wE[j][r] * fexp2(fmaf(lg, L2E, -lse2[j][r]));
-                        cs[0] += wp;
+                        for (int c = 0; c < CM; ++c) lg = fma2(f2{crow[j][2 * h][c], crow[j][2 * h + 1][c]}, splat2(wcd[c]), lg);
+                        const f2 ex = fma2(lg, splat2(L2E), -f2{lse2[j][2 * h], lse2[j][2 * h + 1]});
+                        const f2 wp = f2{wE[j][2 * h], wE[j][2 * h + 1]} * f2{fexp2(ex.x), fexp2(ex.y)};
+                        csp[0] += wp;
 #pragma unroll
-                        for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(wp, crow[j][r][c], cs[1 + c]);
+                        for (int c = 0; c < CM; ++c) csp[1 + c] = fma2(wp, f2{crow[j][2 * h][c], crow[j][2 * h + 1][c]}, csp[1 + c]);
                     }
+                float cs[1 + CM];
+#pragma unroll
+                for (int c = 0; c < 1 + CM; ++c) cs[c] = csp[c].x + csp[c].y;
                 // per-wave partial of this tile (fixed-order combine after the tile barrier)
                 float* pw = part + ((buf * 4 + w) * nq) * 64 + gl;
                 if (CM == 1) {  // nq = 2
