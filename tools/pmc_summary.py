@@ -52,8 +52,8 @@ for k in ks:
         if "FETCH_SIZE" in c:
             # gfx950: FETCH_SIZE counts 64 B per 128-B request (MI355X_MICROARCH.md) -> x2, KB -> MB
             line += f" | fetch {2 * c['FETCH_SIZE'] / 1024:7.1f} MB write {c.get('WRITE_SIZE', 0) / 1024:6.1f} MB"
-            if prefix:
-                traffic[f"{prefix}/{k.split('<')[0]}"] = (2 * c["FETCH_SIZE"] + c.get("WRITE_SIZE", 0)) * 1024.0
+            if prefix:  # instances sharing a name (e.g. pass B's loss-only one): the longest-running
+                traffic.setdefault(f"{prefix}/{k.split('<')[0]}", (2 * c["FETCH_SIZE"] + c.get("WRITE_SIZE", 0)) * 1024.0)
     print(line)
 if prefix:
     json.dump(traffic, open(os.path.join(root, f"{tag}_traffic.json"), "w"), indent=1, sort_keys=True)
