@@ -80,7 +80,10 @@ void mmvae_cfg_default(mmvae_cfg* cfg, int32_t model);
 
 /* Create an engine on HIP device `device`.  Replaces constructing nbvae_t / vmf_vae_t
  * (nb.hh:299-401, vmf.hh:307-389) plus the torch::optim::Adam of mmvae_alg.hh:234-237.
- * Parameters start at zero; load them with mmvae_set_param or mmvae_init_params. */
+ * Parameters start at zero; load them with mmvae_set_param or mmvae_init_params.
+ * Shape limits of this engine (MMVAE_E_ARG beyond them; the reference has none):
+ *   1 <= D <= 75,264 genes; 1 <= K <= 64; 1 <= C, H, R <= 8; at most 4 hidden encoder /
+ *   decoder layers, each 1..64 wide; FP8 for the NB model only. */
 int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out);
 int mmvae_destroy(mmvae_h h);
 /* Message for the last failing call on h (h may be NULL for mmvae_create failures). */

@@ -252,6 +252,11 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
         cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
+    {  // the batch-list builder keeps a 16-row block's tile pointers in LDS (batch.hip)
+        const int64_t NT = (cfg->D + 63) / 64;
+        if (4 * (NT + 1 + 16 * (NT + 1) + 16 * NT) + 8 * 1024 + 256 > 160 * 1024)
+            FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range: D above 75,264 genes (the batch lists' LDS tile index)");
+    }
     if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16 && cfg->dtype != MMVAE_DTYPE_BF16X3 &&
         cfg->dtype != MMVAE_DTYPE_FP8)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32, BF16, BF16X3 or FP8");

@@ -77,3 +77,14 @@ def test_hidden_layer_cfg_validated_before_any_device(kw, msg):
     """cfg checks of mmvae_create run before the device is touched: the same error here and on a GPU box."""
     with pytest.raises(mmvae_amd.MMVAEError, match=msg):
         mmvae_amd.Engine(D=10, K=4, **kw)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(D=75265, K=4), "D above 75,264 genes"),
+    (dict(D=10, K=65), "1<=K<=64"),
+])
+def test_shape_limits_validated_before_any_device(kw, msg):
+    """The engine's documented shape limits (include/mmvae_capi.h, mmvae_create) are MMVAE_E_ARG at
+    create time, not a failure inside the first step."""
+    with pytest.raises(mmvae_amd.MMVAEError, match=msg):
+        mmvae_amd.Engine(**kw)
