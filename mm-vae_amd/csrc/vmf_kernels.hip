@@ -895,62 +895,72 @@ __global__ __launch_bounds__(256) void k_enc_bwd_vsmall(const uint2* __restrict_
 // and x_mean / ln_x_sd through the Angular encoder (k_enc_bwd's sum_k W~ M term).
 // PART: 0 = all; 1 = covar_decoding_ only (slab B, final after k_vdec_bwd: its all-reduce overlaps
 // the encoder backward); 2 = x_mean / ln_x_sd only (slab E)
+static constexpr int VGG_GENES = 64;  // genes per k_vgrad_genes workgroup
 template <int PART>
 __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, const float* __restrict__ gene,
                                                      const float* __restrict__ WeP_f, const float* __restrict__ slabB,
                                                      const float* __restrict__ slabE, const float* __restrict__ smallg,
                                                      int nrb, double* __restrict__ sqpart) {
-    constexpr int NQMAX = 1 + CMAX + 1 + 1;  // + the column dot sum_k cdh[k] W~[k][g]
-    constexpr int NPART = 8;
+    // 64 genes x 16 row-block partitions per workgroup: a thread reads 4 consecutive genes of
+    // every slab row with one 16-byte load (all of them in flight together); the partitions'
+    // partial sums meet in LDS and thread g < 64 adds them in partition order.
+    constexpr int NQ = 1 + CMAX + 1 + 1;  // slab B [1 + C], slab E [1], the column dot sum_k cdh[k] W~[k][g]
+    constexpr int NPART = 16, GPT = 4;
     __shared__ float cdh[64];
-    __shared__ float red[NPART - 1][32][NQMAX + 1];
-    const int C = d.C, nqB = 1 + C, nq = nqB + 1;
+    __shared__ float red[NPART][NQ][VGG_GENES];
+    const int C = d.C, nqB = 1 + C;
     for (int k = threadIdx.x; k < d.KE; k += 256) cdh[k] = smallg[k];
-    const int gi = threadIdx.x & 31, part = threadIdx.x >> 5;
-    const int g = blockIdx.x * 32 + gi;
-    float acc[NQMAX];
+    const int part = threadIdx.x >> 4, gq = (threadIdx.x & 15) * GPT;
+    const int g0 = blockIdx.x * VGG_GENES;  // DP is a multiple of 64: every slab / W read is in bounds
+    f32x4 acc[NQ];
 #pragma unroll
-    for (int q = 0; q < NQMAX; ++q) acc[q] = 0.f;
-    if (PART != 1) {  // the column dot's loads first, latent rows part, part + NPART, ... per thread
+    for (int q = 0; q < NQ; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto ld = [&](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
+    if (PART != 1) {  // the column dot's loads first (latent rows part, part + NPART, ...)
         __syncthreads();  // cdh
-        if (g < d.D)
-#pragma unroll 4
-            for (int k = part; k < d.KE; k += NPART) acc[NQMAX - 1] = fmaf(cdh[k], WeP_f[(int64_t)k * d.DP + g], acc[NQMAX - 1]);
-    }
-    if (g < d.D) {
-        for (int rb = part; rb < nrb; rb += NPART) {
-            const float* sB = slabB + (int64_t)rb * nqB * d.DP + g;
+        for (int k = part; k < d.KE; k += NPART) {
+            const f32x4 wv = ld(WeP_f + (int64_t)k * d.DP + g0 + gq);
 #pragma unroll
-            for (int q = 0; q < NQMAX; ++q) {
-                if (q < nqB) { if (PART != 2) acc[q] += sB[(int64_t)q * d.DP]; }
-                else if (q < nq) { if (PART != 1) acc[q] += slabE[(int64_t)rb * d.DP + g]; }
-            }
+            for (int i = 0; i < GPT; ++i) acc[NQ - 1][i] = fmaf(cdh[k], wv[i], acc[NQ - 1][i]);
         }
     }
-    if (part > 0)
+#pragma unroll 4
+    for (int rb = part; rb < nrb; rb += NPART) {
+        const float* sB = slabB + (int64_t)rb * nqB * d.DP + g0 + gq;
 #pragma unroll
-        for (int q = 0; q < NQMAX; ++q) red[part - 1][gi][q] = acc[q];
+        for (int q = 0; q < 1 + CMAX; ++q)
+            if (PART != 2 && q < nqB) acc[q] += ld(sB + (int64_t)q * d.DP);
+        if (PART != 1) acc[NQ - 2] += ld(slabE + (int64_t)rb * d.DP + g0 + gq);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) red[part][q][gq + i] = acc[q][i];
     __syncthreads();
     double sq = 0.0;  // sum of squares of the gradient elements this block writes (clip norm)
     auto put = [&](float* dst, float v) { *dst = v; sq += (double)v * v; };
-    if (part == 0 && g < d.D) {
+    const int g = g0 + (int)threadIdx.x;
+    if (threadIdx.x < VGG_GENES && g < d.D) {
+        float t[NQ];
 #pragma unroll
-        for (int pp = 0; pp < NPART - 1; ++pp)
+        for (int q = 0; q < NQ; ++q) {
+            float v = 0.f;
 #pragma unroll
-            for (int q = 0; q < NQMAX; ++q) acc[q] += red[pp][gi][q];
+            for (int pp = 0; pp < NPART; ++pp) v += red[pp][q][threadIdx.x];
+            t[q] = v;
+        }
         if (PART != 2) {
-            put(&G.bcd[g], acc[0]);
-            for (int c = 0; c < C; ++c) put(&G.Wcd[(int64_t)g * C + c], acc[1 + c]);
+            put(&G.bcd[g], t[0]);
+            for (int c = 0; c < C; ++c) put(&G.Wcd[(int64_t)g * C + c], t[1 + c]);
         }
         if (PART != 1) {
-            const float Gl = acc[nqB];
-            const float gs = acc[NQMAX - 1];
+            const float Gl = t[NQ - 2], gs = t[NQ - 1];
             const float inv = gene[g];
             put(&G.xm[g], -inv * gs);
             put(&G.lsd[g], -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]));
         }
     }
-    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..31)
+    if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..63)
         sq = wave_sum_d(sq);
         if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
     }
@@ -1145,7 +1155,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     const bool split = split_grads(e);
     if (split) {  // covar_decoding_ gradients final: all-reduce them under the encoder backward
         ScopedTimer tm(e, "k_vgrad_genes_dec");
-        hipLaunchKernelGGL(k_vgrad_genes<1>, dim3((d.D + 31) / 32), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
+        hipLaunchKernelGGL(k_vgrad_genes<1>, dim3((d.D + VGG_GENES - 1) / VGG_GENES), dim3(256), 0, st, P, d, G, gene, e->d_WeP_f,
                            e->d_slabB, e->d_slabE, e->d_smallg, nrb, nullptr);
         hipError_t er = comm_bucket(e, 0);
         if (er != hipSuccess) return er;
@@ -1157,7 +1167,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     const bool fuse_sq = !split && !(e->comm && e->world > 1);
-    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + 31) / 32;
+    const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + VGG_GENES - 1) / VGG_GENES;
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
