@@ -195,21 +195,34 @@ template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0) {
     const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + swz_off<RB>(row + 4, byte)));
     return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
-// x3 pq operand of decoder pass B, stored per 16-gene block as [16 genes][16 rows] bf16 planes
-// (hi at +0, lo at +512 bytes; blocks 2 KB apart): the epilogue writes a lane's row pair of one
-// gene as one 32-bit word per plane, and the dz GEMM reads the MFMA A fragment (row lane & 15,
-// genes k0 + 8 (lane >> 4) .. + 7) transposed with two ds_read_b64_tr_b16 per plane.  EXEC must
-// be all ones.
+// 16-bit dz-GEMM A operand of the decoder backward passes (NB pass B pq, vMF pass 1 da), stored
+// per 16-gene block as [16 genes][16 rows] bf16 (blocks BS bytes apart; the x3 lo plane at a
+// fixed offset after the hi plane): the epilogue writes a lane's row pair of one gene as one
+// 32-bit word per plane, and the dz GEMM reads the MFMA A fragment (row lane & 15, genes
+// k0 + 8 (lane >> 4) .. + 7) transposed with two ds_read_b64_tr_b16 per plane.  EXEC must be
+// all ones.
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 MMVAE_DEV uint32_t pk_bf16(float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)a, (__bf16)b}); }
-MMVAE_DEV int pqt_off(int g, int r) { return (g >> 4) * 2048 + (g & 15) * 32 + r * 2; }  // bytes
-MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0) {
+template <int BS = 2048> MMVAE_DEV int pqt_off(int g, int r) { return (g >> 4) * BS + (g & 15) * 32 + r * 2; }  // bytes
+template <int BS = 2048> MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0) {
     const int lane = threadIdx.x & 63;
     const int k = k0 + 8 * (lane >> 4) + ((lane >> 2) & 3), r = 4 * (lane & 3);
     typedef __attribute__((address_space(3))) bf16x4 lds_v4;
-    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off(k, r)));
-    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off(k + 4, r)));
+    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off<BS>(k, r)));
+    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off<BS>(k + 4, r)));
     return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// a row pair (r, r + 1) of one gene into the transposed image: hi plane word, and for the split
+// (x3) operand the lo plane word PO bytes after it
+template <int BS, bool SPLIT> MMVAE_DEV void pqt_put(char* img, int PO, int g, int r, float a, float b) {
+    char* q = img + pqt_off<BS>(g, r);
+    const uint32_t hp = pk_bf16(a, b);
+    *reinterpret_cast<uint32_t*>(q) = hp;
+    if constexpr (SPLIT) {
+        typedef float fp2 __attribute__((ext_vector_type(2)));
+        const fp2 lo = fp2{a, b} - fp2{__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+        *reinterpret_cast<uint32_t*>(q + PO) = pk_bf16(lo.x, lo.y);
+    }
 }
 
 template <class P, int RB> struct TrFrag;

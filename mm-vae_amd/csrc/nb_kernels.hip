@@ -1152,11 +1152,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                     }
                     if constexpr (X) {  // hi / lo planes of the row pair, one word each
-                        char* qb = reinterpret_cast<char*>(q1) + pqt_off(gl, rl);
-                        const uint32_t hp = pk_bf16(pq.x, pq.y);
-                        const f2 lo = pq - f2{__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
-                        *reinterpret_cast<uint32_t*>(qb) = hp;
-                        *reinterpret_cast<uint32_t*>(qb + 512) = pk_bf16(lo.x, lo.y);
+                        pqt_put<2048, true>(reinterpret_cast<char*>(q1), 512, gl, rl, pq.x, pq.y);
                     } else {
                         put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
                         put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);

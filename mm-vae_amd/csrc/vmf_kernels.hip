@@ -470,18 +470,23 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 #pragma unroll
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL], Q.zplane);
-    float crow[4][CM], ra[4], rbt[4], svv[4], sv[4], slv[4];
+    // rows 4 (lane >> 4) + 2h + j live in component j of the pair h (packed-f32 element math)
+    f2 crow2[2][CM], ra2[2], rbt2[2], svv2[2], sv2[2], slv2[2];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+        const int h = r >> 1, j = r & 1;
         const int b = row0 + 4 * (lane >> 4) + r;
         const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
 #pragma unroll
-        for (int c = 0; c < CM; ++c) crow[r][c] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
-        ra[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r)] : 0.f;
-        rbt[r] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r) + 1] : 0.f;
-        svv[r] = 0.f;
-        sv[r] = 0.f;
-        slv[r] = 0.f;
+        for (int c = 0; c < CM; ++c) crow2[h][c][j] = (c < C) ? Q.covar[cell * C + c] : 0.f;  // row N: zeros
+        ra2[h][j] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r)] : 0.f;
+        rbt2[h][j] = PASS ? part[2 * (16 * w + 4 * (lane >> 4) + r) + 1] : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        svv2[h] = splat2(0.f);
+        sv2[h] = splat2(0.f);
+        slv2[h] = splat2(0.f);
     }
     f32x4 dz[KP / 16];
 #pragma unroll
@@ -519,30 +524,41 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             wcd[0] = g4.z;
 #pragma unroll
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
-            float cs[1 + CM];
+            f2 csp[1 + CM];
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c) cs[c] = 0.f;
+            for (int c = 0; c < 1 + CM; ++c) csp[c] = splat2(0.f);
+            constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rl = 4 * (lane >> 4) + r;
-                const float u = fexp(acc[r] + g4.x);             // exp(z_dec(z))   vmf.hh:285
-                float hc = g4.y;                                 // covar_dec(c)    vmf.hh:286
+            for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
+                const int rl = 4 * (lane >> 4) + 2 * h;
+                const f2 ex = (f2{acc[2 * h], acc[2 * h + 1]} + g4.x) * L2E;
+                const f2 u = f2{fexp2(ex.x), fexp2(ex.y)};      // exp(z_dec(z))   vmf.hh:285
+                f2 hc = splat2(g4.y);                           // covar_dec(c)    vmf.hh:286
 #pragma unroll
-                for (int c = 0; c < CM; ++c) hc = fmaf(crow[r][c], wcd[c], hc);
-                const float v = (u + hc) * g4.w;                 // padded genes: 0
-                const float l = lt[rl * LS + gl];
+                for (int c = 0; c < CM; ++c) hc = fma2(crow2[h][c], splat2(wcd[c]), hc);
+                const f2 v = (u + hc) * g4.w;                   // padded genes: 0
+                const f2 l = f2{lt[rl * LS + gl], lt[(rl + 1) * LS + gl]};
                 if (PASS == 0) {
-                    svv[r] = fmaf(v, v, svv[r]);
-                    sv[r] += v;
-                    slv[r] = fmaf(l, v, slv[r]);
+                    svv2[h] = fma2(v, v, svv2[h]);
+                    sv2[h] += v;
+                    slv2[h] = fma2(l, v, slv2[h]);
                 } else {
-                    const float dv = fmaf(ra[r], (l + epsD) * g4.w, rbt[r] * v);
-                    cs[0] += dv;
+                    const f2 dv = fma2(ra2[h], (l + epsD) * g4.w, rbt2[h] * v);
+                    csp[0] += dv;
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) cs[1 + c] = fmaf(dv, crow[r][c], cs[1 + c]);
-                    put_op<P>(q1, rl * QS + gl, QPL, dv * u);
+                    for (int c = 0; c < CM; ++c) csp[1 + c] = fma2(dv, crow2[h][c], csp[1 + c]);
+                    const f2 da = dv * u;
+                    if constexpr (BF) {
+                        pqt_put<512, X>(reinterpret_cast<char*>(q1), 2048, gl, rl, da.x, da.y);
+                    } else {
+                        put_op<P>(q1, rl * QS + gl, QPL, da.x);
+                        put_op<P>(q1, (rl + 1) * QS + gl, QPL, da.y);
+                    }
                 }
             }
+            float cs[1 + CM];
+#pragma unroll
+            for (int c = 0; c < 1 + CM; ++c) cs[c] = csp[c].x + csp[c].y;
             if (PASS) {
                 float* pw = part + w * nq * 64 + gl;
                 if (CM == 1) {  // nq = 2
@@ -563,7 +579,15 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             // dz[cell][latent] += sum_g da[cell][g] W_d[g][latent]
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
-                const Fr a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
+                Fr a1;
+                if constexpr (X) {
+                    const char* qb = reinterpret_cast<const char*>(q1);
+                    a1 = Fr{pqt_frag<512>(qb, s * M::KSTEP), pqt_frag<512>(qb + 2048, s * M::KSTEP)};
+                } else if constexpr (BF) {
+                    a1 = pqt_frag<512>(reinterpret_cast<const char*>(q1), s * M::KSTEP);
+                } else {
+                    a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
+                }
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
                     Fr bw;
@@ -592,7 +616,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     for (int r = 0; r < 4; ++r) {
         const int b = row0 + 4 * (lane >> 4) + r;
         if (PASS == 0) {
-            float a = svv[r], s1 = sv[r], s2 = slv[r];
+            float a = svv2[r >> 1][r & 1], s1 = sv2[r >> 1][r & 1], s2 = slv2[r >> 1][r & 1];
 #pragma unroll
             for (int o = 1; o < 16; o <<= 1) {
                 a += __shfl_xor(a, o, 64);
