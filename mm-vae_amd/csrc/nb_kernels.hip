@@ -1153,6 +1153,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                     }
                     if constexpr (X) {  // hi / lo planes of the row pair, one word each
                         pqt_put<2048, true>(reinterpret_cast<char*>(q1), 512, gl, rl, pq.x, pq.y);
+                    } else if constexpr (BF) {  // bf16: the separate q1 tile, compact blocks
+                        pqt_put<512, false>(reinterpret_cast<char*>(q1), 0, gl, rl, pq.x, pq.y);
                     } else {
                         put_op<P>(q1, q1i(rl, gl), Q1PL, pq.x);
                         put_op<P>(q1, q1i(rl + 1, gl), Q1PL, pq.y);
@@ -1199,6 +1201,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 if constexpr (X) {
                     const char* qb = reinterpret_cast<const char*>(q1);
                     a1 = Fr{pqt_frag(qb, s * M::KSTEP), pqt_frag(qb + 512, s * M::KSTEP)};
+                } else if constexpr (BF) {
+                    a1 = pqt_frag<512>(reinterpret_cast<const char*>(q1), s * M::KSTEP);
                 } else {
                     a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
                 }
