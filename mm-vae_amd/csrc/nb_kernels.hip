@@ -869,6 +869,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     auto q1i = [](int r, int g) { return X ? ((g >> 4) * 1024 + r * 16 + (g & 15)) : r * QS + g; };
     constexpr int Q1PL = 256;
     auto cci = [](int r, int g) { return X ? ((g >> 4) * 256 + r * 16 + (g & 15)) : r * 64 + g; };
+    // f32 corrections (x3, f32): per 16-gene block (2 KB) a p dq plane [16 genes][16 rows] and a
+    // d du plane 1 KB after it, so a lane's row pair of one gene is one 8-byte read per plane
+    // (a packed-f32 operand as stored)
+    constexpr bool PLANAR = sizeof(CT) == 8;
+    // (16-byte row quads XOR-swizzled by gene so the 16 genes of a lane group hit distinct banks)
+    auto ccp = [](int r, int g) { return (g >> 4) * 2048 + (g & 15) * 64 + (((r >> 2) ^ ((g >> 2) & 3)) << 4) + (r & 3) * 4; };
     constexpr int PS = 68;
     constexpr int NRS = 3 + RM + CM;    // row scalars: d, w, valid, znu[R], c[C]
     constexpr int RBW = KP * (int)sizeof(TL);  // staged decoder row (one gene)
@@ -1081,7 +1087,15 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             lossacc += x * flog(sv * rmu) + lgd;                        // nb.hh:527: x (log(mu+nu) - log(mu))
             const float dq = x * (rsv - rmu);
             const float ddu = msk ? (x * rsv + dgd) * sig : 0.f;
-            if constexpr (!LOSS) cc[cci(r, gl)] = CP::pack(p * dq, ddu);
+            if constexpr (!LOSS) {
+                if constexpr (PLANAR) {
+                    char* cb = reinterpret_cast<char*>(cc) + ccp(r, gl);
+                    *reinterpret_cast<float*>(cb) = p * dq;
+                    *reinterpret_cast<float*>(cb + 1024) = ddu;
+                } else {
+                    cc[cci(r, gl)] = CP::pack(p * dq, ddu);
+                }
+            }
         });
         wave_sync();
         lap(1);
@@ -1114,9 +1128,20 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
                 // the block's corrections first (x3: this block's pq overwrites them below)
                 CT ccv[4];
+                f2 cpv[2], cdv[2];
+                if constexpr (!LOSS) {
+                    if constexpr (PLANAR) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if constexpr (!LOSS) ccv[r] = cc[cci(4 * (lane >> 4) + r, gl)];
+                        for (int h = 0; h < 2; ++h) {
+                            const char* cb = reinterpret_cast<const char*>(cc) + ccp(4 * (lane >> 4) + 2 * h, gl);
+                            cpv[h] = *reinterpret_cast<const f2*>(cb);
+                            cdv[h] = *reinterpret_cast<const f2*>(cb + 1024);
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ccv[r] = cc[cci(4 * (lane >> 4) + r, gl)];
+                    }
+                }
                 if constexpr (X) asm volatile("" ::: "memory");
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
@@ -1136,11 +1161,19 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         lossd2 = fma2(nup, lg2, lossd2);
                     }
                     if constexpr (LOSS) continue;
-                    float cpa, cda, cpb, cdb;
-                    CP::unpack(ccv[2 * h], cpa, cda);
-                    CP::unpack(ccv[2 * h + 1], cpb, cdb);
-                    const f2 pq = fma2(p, qv, f2{cpa, cpb});                     // qv = n dL/dmu' - 1 at x = 0
-                    const f2 du = fma2(fma2(lg2, splat2(LN2), qv), sgm, f2{cda, cdb});
+                    f2 cpp, cdp;  // the row pair's corrections: p dq, d du
+                    if constexpr (PLANAR) {
+                        cpp = cpv[h];
+                        cdp = cdv[h];
+                    } else {
+                        float cpa, cda, cpb, cdb;
+                        CP::unpack(ccv[2 * h], cpa, cda);
+                        CP::unpack(ccv[2 * h + 1], cpb, cdb);
+                        cpp = f2{cpa, cpb};
+                        cdp = f2{cda, cdb};
+                    }
+                    const f2 pq = fma2(p, qv, cpp);                              // qv = n dL/dmu' - 1 at x = 0
+                    const f2 du = fma2(fma2(lg2, splat2(LN2), qv), sgm, cdp);
                     Eacc2[h] += pq;
                     cs1[0] = fma2(wv2[h], pq, cs1[0]);
 #pragma unroll
