@@ -170,8 +170,17 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
         const int tC = tB < NT ? chunk_end(tB) : NT;
         if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
         uint2* dst = ents + base + cb;
-        if (!(dbg & 8192))  // 8192: diagnostic, stream-out skipped (lists invalid)
-            for (int i = tid; i < cnt; i += 1024) dst[i] = stage[i];
+        if (!(dbg & 8192)) {  // 8192: diagnostic, stream-out skipped (lists invalid)
+            // 16-byte stores (two entries each) from the first 16-byte-aligned entry on
+            const int head = (cnt > 0) ? (int)((base + cb) & 1) : 0, n2 = (cnt - head) >> 1;
+            if (tid == 0 && head) dst[0] = stage[0];
+            uint4* d4 = reinterpret_cast<uint4*>(dst + head);
+            for (int i = tid; i < n2; i += 1024) {
+                const uint2 a = stage[head + 2 * i], b2 = stage[head + 2 * i + 1];
+                d4[i] = uint4{a.x, a.y, b2.x, b2.y};
+            }
+            if (tid == 0 && cnt > head && ((cnt - head) & 1)) dst[cnt - 1] = stage[cnt - 1];
+        }
         lds_barrier();  // stage reusable (the stores carry register copies)
         tA = tB;
         tB = tC;
