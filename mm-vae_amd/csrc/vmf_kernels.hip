@@ -384,8 +384,9 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 
 // trw (16-bit operands): pass 1 reads the dz GEMM's B operand transposed from the W image, so
 // no WdT image is staged (x3 at K <= 32: 3 workgroups per CU instead of 2)
+static constexpr int VTAB = 512;  // log1p table entries of the fp32-accurate modes (x3, f32)
 struct VDecLds {
-    int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, bytes;
+    int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, o_tab, bytes;
     MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass, int planes = 1) {
         const bool trw = esz == 2;
         o_g = planes * 64 * KP * esz;                         // W image (hi [+ lo])
@@ -396,7 +397,8 @@ struct VDecLds {
         o_q1 = 16 * 68 * 4;                                   // after the l tile
         o_toff = o_q1 + (pass ? ((planes * 16 * QS * esz + 15) / 16) * 16 : 0);
         wave_bytes = o_toff + ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
-        bytes = o_wave + 4 * wave_bytes;
+        o_tab = o_wave + 4 * wave_bytes;
+        bytes = o_tab + ((esz == 2 && planes == 1) ? 0 : VTAB * 4);  // the bf16 mode: one v_log, no table
     }
 };
 
@@ -438,6 +440,11 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
     const float4* grec = reinterpret_cast<const float4*>(Q.gene + 4 * d.DP);
+    // log1p of integer counts from a per-workgroup LDS table in the fp32-accurate modes (the
+    // libm log1pf per entry otherwise dominates the tile); the bf16 mode keeps one v_log
+    using VTabT = Log1pTab<typename std::conditional<BF && !X, __bf16, float>::type, VTAB>;
+    uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
+    VTabT::fill(ltab);  // published by the first barrier below
 
     DualStage<64, RBW, 256, X> wreg;
     DualStage<KP, RBT, 256, X> treg;
@@ -509,7 +516,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
         for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
         wave_sync();
-        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { lt[r * LS + gl] = log1p_cnt<P>(fmaxf(x, 0.f)); });
+        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { VTabT::put(ltab, lt, r * LS + gl, 0, fmaxf(x, 0.f)); });
         wave_sync();
         pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
 #pragma unroll
