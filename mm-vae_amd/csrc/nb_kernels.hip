@@ -869,10 +869,11 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     auto q1i = [](int r, int g) { return X ? ((g >> 4) * 1024 + r * 16 + (g & 15)) : r * QS + g; };
     constexpr int Q1PL = 256;
     auto cci = [](int r, int g) { return X ? ((g >> 4) * 256 + r * 16 + (g & 15)) : r * 64 + g; };
-    // f32 corrections (x3, f32): per 16-gene block (2 KB) a p dq plane [16 genes][16 rows] and a
-    // d du plane 1 KB after it, so a lane's row pair of one gene is one 8-byte read per plane
-    // (a packed-f32 operand as stored)
-    constexpr bool PLANAR = sizeof(CT) == 8;
+    // x3 corrections: per 16-gene block (2 KB) a p dq plane [16 genes][16 rows] and a d du plane
+    // 1 KB after it, so a lane's row pair of one gene is one 8-byte read per plane (a packed-f32
+    // operand as stored).  The f32 mode keeps (p dq, d du) pairs per element (its spilling pass B
+    // ran 6 % slower with the planes)
+    constexpr bool PLANAR = X;
     // (16-byte row quads XOR-swizzled by gene so the 16 genes of a lane group hit distinct banks)
     auto ccp = [](int r, int g) { return (g >> 4) * 2048 + (g & 15) * 64 + (((r >> 2) ^ ((g >> 2) & 3)) << 4) + (r & 3) * 4; };
     constexpr int PS = 68;
