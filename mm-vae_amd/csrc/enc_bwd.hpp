@@ -76,15 +76,22 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     // loads independent of the CSR index first: the W tile t0 and the dh^T A operand
     RegStage<KP, RB> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeP) + (int64_t)64 * t * sizeof(WT); };
-    const int lb = w;  // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
-    float wr[4][4], wn[4][4];  // WREG: W[16 lb + 4 (lane >> 4) + r][64 t + 16 gb + (lane & 15)], this / next tile
+    // M = dh^T log1p(x) by (latent block lb) x (gene blocks): with KP = 64 wave w owns latent
+    // block w and all four 16-gene blocks; with KP = 16 / 32 the waves split the gene blocks too
+    // (NGB = KP / 16 blocks each, every wave busy); KP = 48 keeps one latent block per wave
+    constexpr int NLB = KP / 16;
+    constexpr bool GSPLIT = NLB < 4 && 4 % NLB == 0;
+    constexpr int NGB = GSPLIT ? NLB : 4;   // gene blocks per wave
+    const int lb = GSPLIT ? w % NLB : w;    // A operand: dh^T rows = latents of this wave's block, k = the workgroup's 64 cells
+    const int gb0 = GSPLIT ? (w / NLB) * NGB : 0;
+    float wr[4][4], wn[4][4];  // WREG: W[16 lb + 4 (lane >> 4) + r][64 t + 16 (gb0 + i) + (lane & 15)], this / next tile
     auto wload = [&](float (&dst)[4][4], int t) {
         const int kb = 16 * min(lb, KP / 16 - 1) + 4 * (lane >> 4);
 #pragma unroll
-        for (int gb = 0; gb < 4; ++gb)
+        for (int i = 0; i < NGB; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                dst[gb][r] = static_cast<float>(WeP[(int64_t)(kb + r) * d.DP + 64 * t + 16 * gb + (lane & 15)]);
+                dst[i][r] = static_cast<float>(WeP[(int64_t)(kb + r) * d.DP + 64 * t + 16 * (gb0 + i) + (lane & 15)]);
     };
     if constexpr (WREG) wload(wr, min(t0, d.NT - 1));
     else wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(WT));
@@ -165,8 +172,14 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
         }
         // ---- M block w on MFMA, then Gl partial = sum over the block's latents of W M ----
         if (lb < KP / 16) {
+            if constexpr (GSPLIT)  // the other waves' gene blocks: zero partials from this wave
+                if (lane < 16)
 #pragma unroll
-            for (int gb = 0; gb < 4; ++gb) {
+                    for (int gb = 0; gb < 4; ++gb)
+                        if (gb < gb0 || gb >= gb0 + NGB) part[w * 64 + 16 * gb + lane] = 0.f;
+#pragma unroll
+            for (int i = 0; i < NGB; ++i) {
+                const int gb = gb0 + i;
                 f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KSB; ++s) {
@@ -178,7 +191,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * lb + 4 * (lane >> 4) + r;
-                    const float wv = WREG ? wr[gb][r]
+                    const float wv = WREG ? wr[i][r]
                                           : static_cast<float>(*reinterpret_cast<const WT*>(wst + swz_off<RB>(k, gl * (int)sizeof(WT))));
                     v = fmaf(wv, acc[r], v);
                 }
@@ -202,9 +215,9 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
         }
         if constexpr (WREG)
 #pragma unroll
-            for (int gb = 0; gb < 4; ++gb)
+            for (int i = 0; i < NGB; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) wr[gb][r] = wn[gb][r];
+                for (int r = 0; r < 4; ++r) wr[i][r] = wn[i][r];
         nxt.fetch(ents, segw, toffl, min(tl + 2, nt - 1), lane);
         lds_barrier();
     }
