@@ -20,3 +20,10 @@ ntile = eng.tiling()["tps_enc"]
 m = st.mean(0)
 print("waves", st.shape[0], "per tile: MFMA+wait %.0f  zero+scatter %.0f  fetch+stage %.0f  barrier %.0f" % tuple(m[:4] / ntile))
 print("prologue+tail %.0f cycles, wave wall %.0f mean / %.0f max cycles" % (m[4], m[6], st[:, 6].max()))
+# balance: per gene split (mean over row blocks of the workgroup's slowest wave) and per row block
+wall = st[:, 6].reshape(-1, 4).max(1)          # [wg]
+wg_sp = wall.reshape(-1, nse)                   # [rb][sp]
+print("per split (k cycles):", np.round(wg_sp.mean(0) / 1e3, 1).tolist())
+print("per row block: min %.1f mean %.1f max %.1f (k cycles)" % (wg_sp.max(1).min() / 1e3, wg_sp.max(1).mean() / 1e3, wg_sp.max(1).max() / 1e3))
+sc = st[:, 1].reshape(-1, 4).mean(1).reshape(-1, nse)  # zero+scatter cycles per wg
+print("scatter per split (k cycles):", np.round(sc.mean(0) / 1e3, 1).tolist())
