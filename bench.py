@@ -55,8 +55,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--model", default="nb", choices=["nb", "vmf"])
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "bf16", "f32", "fp8"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--genes", type=int, default=20000)
