@@ -109,8 +109,10 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // SB (x3): single-buffered x tile and W stage — the wave's scatter into its x tile follows
 // its own MFMA operand reads of the tile (one wave's LDS operations complete in order), and the
 // W stage is rewritten between two barriers — so x3 fits 4 workgroups per CU (39 KB) instead of 2.
-template <class P, int KP, bool SB = false>
-__global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+// NW waves (16 rows each) per workgroup: 8 in the x3 mode (the staged W tile serves 128 rows,
+// two workgroups per CU), 4 otherwise
+template <class P, int KP, bool SB = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                  const int32_t* __restrict__ toff,
                                                  const typename Elem<P>::type* __restrict__ WeS, int64_t wplane, Dims d,
                                                  float* __restrict__ hpart) {
@@ -131,17 +133,17 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
     const uint64_t t_entry = (d.dbg & 32) ? stamp_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
-    const int row0 = rb * 64 + 16 * w;
+    const int row0 = rb * 16 * NW + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Tab::BYTES, NB);
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Tab::BYTES, NB, NW);
     char* wst = smem;
     uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
     Tab::fill(ltab);
     T* xt = reinterpret_cast<T*>(smem + L.o_x + w * XB);
     int32_t* toffl = reinterpret_cast<int32_t*>(smem + L.o_toff) + w * S;
 
-    DualStage<KP, RB, 256, X> wreg;
+    DualStage<KP, RB, 64 * NW, X> wreg;
     auto wsrc = [&](int t) { return reinterpret_cast<const char*>(WeS) + (int64_t)64 * t * sizeof(T); };
     // prologue loads with no dependence on the lists go out first (W tile t0)
     wreg.load(wsrc(min(t0, d.NT - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void k_enc_fwd(const uint2* __restrict__ ents,
         vm_wait_all();
         __syncthreads();
         if (lane == 0) {
-            float* o = hpart + ((int64_t)blockIdx.x * 4 + w) * 8;
+            float* o = hpart + ((int64_t)blockIdx.x * NW + w) * 8;
             o[0] = (float)sa;
             o[1] = (float)sb;
             o[2] = (float)sc;
@@ -2048,6 +2050,7 @@ static size_t dec_lds(const Dims& d, int pass, int esz, int planes) {
 // the single-buffered encoder forward in the x3 mode (f32: 3 waves / SIMD by VGPRs either way,
 // and measured faster double-buffered at 2 workgroups per CU)
 template <class P> struct EncSB { static constexpr bool value = IsX3<P>::value; };
+template <class P> struct EncNW { static constexpr int value = IsX3<P>::value ? 8 : 4; };
 template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
@@ -2056,7 +2059,7 @@ static size_t enc_fwd_lds(const Dims& d) {
     constexpr bool SB = EncSB<P>::value;
     constexpr int NB = SB ? 1 : 2;
     return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, NB * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
-                          Log1pTab<P, SB ? 512 : LTAB>::BYTES, NB).bytes;
+                          Log1pTab<P, SB ? 512 : LTAB>::BYTES, NB, EncNW<P>::value).bytes;
 }
 // the encoder operand images of mode P: bf16 planes (bf16, x3) or f32
 template <class P> static const typename Elem<P>::type* op_img(const float* f, const __bf16* b) {
@@ -2065,7 +2068,9 @@ template <class P> static const typename Elem<P>::type* op_img(const float* f, c
 }
 template <class P, int KP>
 static void enc_fwd_run(Engine* e, const Dims& d, float* hpart, hipStream_t st) {
-    hipLaunchKernelGGL((k_enc_fwd<P, KP, EncSB<P>::value>), dim3(d.nrb * d.nsE), dim3(256), (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
+    constexpr int NW = EncNW<P>::value;
+    hipLaunchKernelGGL((k_enc_fwd<P, KP, EncSB<P>::value, NW>), dim3(d.nrb * 4 / NW * d.nsE), dim3(64 * NW),
+                       (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
                        e->d_seg, e->d_toff, op_img<P>(e->d_WeS_f, e->d_WeS_b), (int64_t)e->KP * e->DP, d, hpart);
 }
 // encoder backward operands: dh^T planes and the staged W (f32 in the x3 mode)

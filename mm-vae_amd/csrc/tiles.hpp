@@ -154,7 +154,7 @@ template <class P, int N = LTAB> struct Log1pTab {
     static constexpr int BYTES = ON ? N * 4 : 0;
     MMVAE_DEV static void fill(uint32_t* tab) {
         if constexpr (ON)
-            for (int i = threadIdx.x; i < N; i += 256) {
+            for (int i = threadIdx.x; i < N; i += blockDim.x) {
                 const float v = log1pf((float)i);
                 if constexpr (IsX3<P>::value) {
                     const __bf16 h = bf_hi(v), l = bf_lo(v, h);
@@ -431,11 +431,11 @@ MMVAE_DEV const float* chain_run(const Dims& d, int l0, int l1, const float* in,
 struct EncLds {
     int o_x, o_toff, o_tab, bytes;
     MMVAE_HOSTDEV EncLds(int KP, int esz, int S, int xbytes_per_wave, int pre, int planes = 1, int tab_bytes = 0,
-                         int nbuf = 2) {
+                         int nbuf = 2, int nw = 4) {
         const int stb = KP * 64 * esz;
         o_x = pre + nbuf * planes * stb;
-        o_toff = o_x + 4 * xbytes_per_wave;  // [4 waves][S] tile offsets
-        o_tab = o_toff + ((4 * S * 4 + 15) / 16) * 16;  // log1p table (Log1pTab)
+        o_toff = o_x + nw * xbytes_per_wave;  // [nw waves][S] tile offsets
+        o_tab = o_toff + ((nw * S * 4 + 15) / 16) * 16;  // log1p table (Log1pTab)
         bytes = o_tab + tab_bytes;
     }
 };
