@@ -2050,7 +2050,7 @@ static size_t dec_lds(const Dims& d, int pass, int esz, int planes) {
 // the single-buffered encoder forward in the x3 mode (f32: 3 waves / SIMD by VGPRs either way,
 // and measured faster double-buffered at 2 workgroups per CU)
 template <class P> struct EncSB { static constexpr bool value = IsX3<P>::value; };
-template <class P> struct EncNW { static constexpr int value = IsX3<P>::value ? 8 : 4; };
+template <class P> struct EncNW { static constexpr int value = sizeof(typename Elem<P>::type) == 2 ? 8 : 4; };
 template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
