@@ -188,9 +188,14 @@ int mmvae_timing_reset(mmvae_h h);
  * noise eps [Bpad][K], rows in the staged order) to the host. */
 int mmvae_debug_copy(mmvae_h h, int32_t which, float* host, int64_t n);
 /* Gene tiling of the handle's tile kernels (tests assert that a split walks many tiles):
- * out[0] = 64-gene tiles NT, out[1..3] = gene splits of the encoders / decoder pass B /
- * decoder passes A and C (each split walks ceil(NT / splits) tiles). */
-int mmvae_tiling_info(mmvae_h h, int32_t* out4);
+ * out[0] = 64-gene tiles NT, out[1..3] = gene splits of the encoder forward / decoder pass B /
+ * decoder passes A and C, out[4] = the encoder backward's (each split walks ceil(NT / splits)
+ * tiles). */
+int mmvae_tiling_info(mmvae_h h, int32_t* out5);
+/* Test hook: fill every per-step workspace buffer with the byte `byte` (parameters, optimiser
+ * state, the dataset and the frozen operand images are untouched).  A step writes everything it
+ * reads there, so results must be bit-identical whatever the workspace held before. */
+int mmvae_debug_poison(mmvae_h h, int32_t byte);
 /* Step graphs (the reference's per-batch step, mmvae_alg.hh:254-333, as one hipGraph): with
  * on != 0, mmvae_run / mmvae_step / mmvae_eval capture their device work (staging copy, kernels,
  * loss readback) once per launch shape (batch size, n_total, beta, update, injected eps) and

@@ -1195,6 +1195,58 @@ int mmvae_tiling_info(mmvae_h e, int32_t* out) {
     out[1] = e->nsplit_e;
     out[2] = e->nsplit_d;
     out[3] = e->nsplit_a;
+    out[4] = e->nsplit_b;
+    return MMVAE_OK;
+}
+
+// Fill every per-step workspace buffer with `byte` (stream-ordered).  A step must write
+// everything it reads from these buffers before reading it, so results may not depend on
+// their contents: the tests poison between steps and demand bit-identical outputs.
+// Persistent state (dataset + its index, parameters, gradients, Adam moments, frozen weights
+// and their packed operand images, the hidden-chain pack, injected noise) is left alone.
+int mmvae_debug_poison(mmvae_h e, int32_t byte) {
+    if (!e) FAIL(e, MMVAE_E_ARG, "debug_poison: null");
+    HIPCHK(e, hipSetDevice(e->device));
+    const int64_t Bp = e->Bpad, DP = e->DP, KP = e->KP, nrb = e->nrb_max;
+    const int64_t SMALL = small_len((int)e->K, (int)e->E, (int)e->KE, (int)e->C,
+                                    e->cfg.model == MMVAE_MODEL_VMF ? 0 : (int)(2 * e->R * e->H + 2 * e->R + e->H + 1));
+    const struct {
+        void* p;
+        size_t bytes;
+    } bufs[] = {
+        {e->d_cells, e->stage_bytes},
+        {e->d_ents, sizeof(uint2) * (size_t)e->ent_cap},
+        {e->d_toff, sizeof(int32_t) * (size_t)((Bp / 16) * (e->NT + 1))},
+        {e->d_gene, sizeof(float) * (size_t)(10 * DP)},
+        {e->d_mvec, sizeof(float) * (size_t)(((DP + 255) / 256) * KP)},
+        {e->d_rowx, sizeof(float) * (size_t)(Bp * (2 + e->H))},
+        {e->d_rowxp, sizeof(float) * (size_t)(e->nsplit_e * Bp * (1 + e->H))},
+        {e->d_hpart, sizeof(float) * (size_t)(e->nsplit_e * Bp * KP)},
+        {e->d_lat, sizeof(float) * (size_t)(Bp * e->lat_stride)},
+        {e->d_zf, sizeof(float) * (size_t)(Bp * KP)},
+        {e->d_zb, sizeof(__bf16) * (size_t)(2 * Bp * KP)},
+        {e->d_lsep, sizeof(float) * (size_t)(e->nsplit_a * Bp * 2)},
+        {e->d_rowB, sizeof(float) * (size_t)(e->nsplit_d * Bp * (2 + e->R))},
+        {e->d_rowfin, sizeof(float) * (size_t)(Bp * 2)},
+        {e->d_dzp, sizeof(float) * (size_t)(e->nsplit_d * Bp * 2 * KP)},
+        {e->d_dh, sizeof(float) * (size_t)(Bp * KP)},
+        {e->d_dhT_f, sizeof(float) * (size_t)(Bp * KP)},
+        {e->d_dhT_b, sizeof(__bf16) * (size_t)(2 * Bp * KP)},
+        {e->d_WeS_f, sizeof(float) * (size_t)(KP * DP)},
+        {e->d_WeS_b, sizeof(__bf16) * (size_t)(2 * KP * DP)},
+        {e->d_slabB, sizeof(float) * (size_t)(nrb * ((1 + e->C) + 1 + e->R) * DP)},
+        {e->d_slabC, sizeof(float) * (size_t)(nrb * (1 + e->C) * DP)},
+        {e->d_slabE, sizeof(float) * (size_t)(nrb * (2 + e->H) * DP)},
+        {e->d_lossp, sizeof(float) * (size_t)(e->klp_off + e->n_lat_wg)},
+        {e->d_small, sizeof(float) * (size_t)(e->n_lat_wg * SMALL)},
+        {e->d_smallg, sizeof(float) * 128},
+        {e->d_sumsq, sizeof(double) * (size_t)(256 + (e->D + 31) / 32 + (SMALL + 2 * e->K + 31) / 32 + 1)},
+        {e->d_rowv, sizeof(float) * (size_t)Bp},
+        {e->d_vk, sizeof(float) * 8},
+    };
+    for (const auto& b : bufs)
+        if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return MMVAE_OK;
 }
 

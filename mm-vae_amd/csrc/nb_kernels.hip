@@ -292,6 +292,11 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     split_sum4(rowxp, 1, (int64_t)d.Bpad * nqx, (int64_t)bw * nqx + (k < nqx ? k : 0), nqx, k < nqx, xs);
     float hs[4];  // the encoder's gene-split partials of h
     split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
+    // rows past this batch (b >= B): the handle-wide grid covers them, but the lists / encoder
+    // wrote their partials only up to pad_rows(B) — whatever the buffers hold there is dropped
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if (bw + c >= d.B) hs[c] = xs[c] = 0.f;
     int pbv[4];
     float cmv[4], epv[4], enp[4];
 #pragma unroll
@@ -1479,7 +1484,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         }
         sDM[(4 * w + c) * 68 + k] = dmean;
         sDA[(4 * w + c) * 68 + k] = da;
-        sH[(4 * w + c) * 68 + k] = (k < KE) ? vh[c] : 0.f;
+        sH[(4 * w + c) * 68 + k] = (k < KE && valid) ? vh[c] : 0.f;  // dW = dmean^T h: 0 * h must be 0
         rbm += dmean;
         rbl += da;
 #pragma unroll
@@ -2036,6 +2041,9 @@ hipError_t nb_prepare_frozen(Engine* e) {
     hipError_t er = pack_chain(e, false);
     if (er != hipSuccess) return er;
     e->frozen_dirty = false;
+    // captured step graphs hold the old operands' scalars by value (the fp8 mode's 1 / wscale in
+    // Dims): re-capture them
+    ++e->graph_gen;
     return hipGetLastError();
 }
 

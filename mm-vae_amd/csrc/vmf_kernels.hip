@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
+        if (b >= d.B) hs[c] = 0.f;  // past this batch: partials unwritten this step (NB k_latent_fwd)
         // row norms from the dataset index (row Ncells = the empty padding row)
         const float2 cn = cellnorm[cells[b]];
         inx[c] = 1.f / fmaxf(sqrtf(cn.x), 1e-12f);  // F::normalize
@@ -740,7 +741,7 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         const bool valid = L[d.LAT_VALID] > 0.f;
         inx[c] = L[d.LAT_D];
         float dmean = 0.f, da = 0.f;
-        const float h = (k < KE) ? L[d.LAT_H + k] : 0.f;
+        const float h = (k < KE && valid) ? L[d.LAT_H + k] : 0.f;  // dW = dmean^T h: 0 * h must be 0
         if (k < K) {
             const float dz = dzimg ? dzimg[(4 * w + c) * 68 + k]
                                    : (c == 0) ? dz4[0] : (c == 1) ? dz4[1] : (c == 2) ? dz4[2] : dz4[3];
@@ -1067,6 +1068,9 @@ hipError_t vmf_prepare_frozen(Engine* e) {
     hipError_t er = pack_chain(e, true);
     if (er != hipSuccess) return er;
     e->frozen_dirty = false;
+    // captured step graphs hold the old operands' scalars by value (the fp8 mode's 1 / wscale in
+    // Dims): re-capture them
+    ++e->graph_gen;
     return hipGetLastError();
 }
 

@@ -99,7 +99,20 @@ int parse_options(int argc, const char** argv, int model, CliOptions& o) {
     });
     if (o.idx.empty()) o.idx = o.mtx + ".index";
     if (o.covar_idx.empty()) o.covar_idx = o.covar_mtx + ".index";
+    if (dtype_code(o.dtype) < 0) {
+        std::fprintf(stderr, "unknown --dtype %s (f32 | bf16x3 | bf16 | fp8)\n", o.dtype.c_str());
+        return MMVAE_E_ARG;
+    }
     return MMVAE_OK;
+}
+
+// --dtype spellings (engine extension) -> MMVAE_DTYPE_*, or -1 for an unknown one
+int dtype_code(const std::string& s) {
+    if (s == "f32" || s == "fp32" || s == "float32") return MMVAE_DTYPE_F32;
+    if (s == "bf16") return MMVAE_DTYPE_BF16;
+    if (s == "bf16x3" || s == "x3") return MMVAE_DTYPE_BF16X3;
+    if (s == "fp8" || s == "e4m3") return MMVAE_DTYPE_FP8;
+    return -1;
 }
 
 const char* usage_text(int model) {
@@ -107,11 +120,12 @@ const char* usage_text(int model) {
                ? "nb_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
                  "             --mean_latent 2 --overdisp_encoding 1 --overdispersion_latent 1 --kl_discount .1\n"
                  "             --kl_max 1 --kl_min .01 --recording 10 --covar C.mtx.gz]\n"
-                 "engine: [--dtype f32|bf16x3|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n"
+                 "engine: [--dtype f32|bf16x3|bf16|fp8 --seed S --device G --threads T --no_csr_cache --verbose]\n"
                : "vmf_vae_main --mtx X.mtx.gz --out OUT [--batch_size 100 --max_epoch 101 --nboot 3 --lr 1e-3\n"
                  "             --latent 2 --kappa_min .1 --kappa_max 10 --kl_discount .1 --kl_max 1 --kl_min .01\n"
                  "             --recording 10 --covar C.mtx.gz]\n"
-                 "engine: [--dtype f32|bf16x3|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n";
+                 "engine: [--dtype f32|bf16x3|bf16 --seed S --device G --threads T --no_csr_cache --verbose]\n"
+                 "        (fp8 is built for the NB model only)\n";
 }
 
 static double now_s() {
@@ -207,7 +221,10 @@ struct RcclIdCleanup {
 
 int run_cli(int argc, const char** argv, int model) {
     CliOptions o;
-    parse_options(argc, argv, model, o);
+    if (parse_options(argc, argv, model, o) != MMVAE_OK && !o.help) {
+        std::fputs(usage_text(model), stderr);
+        return EXIT_FAILURE;
+    }
     if (o.help) {
         std::fputs(usage_text(model), stderr);
         return EXIT_SUCCESS;
@@ -269,9 +286,7 @@ int run_cli(int argc, const char** argv, int model) {
     }
     mmvae_cfg cfg;
     mmvae_cfg_default(&cfg, model);
-    cfg.dtype = (o.dtype == "bf16")                        ? MMVAE_DTYPE_BF16
-                : (o.dtype == "bf16x3" || o.dtype == "x3") ? MMVAE_DTYPE_BF16X3
-                                                           : MMVAE_DTYPE_F32;
+    cfg.dtype = dtype_code(o.dtype);
     cfg.D = csr.D;
     cfg.C = C;
     cfg.K = o.latent;

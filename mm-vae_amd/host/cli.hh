@@ -36,6 +36,8 @@ struct CliOptions {
 
 int parse_options(int argc, const char** argv, int model, CliOptions& o);
 const char* usage_text(int model);
+// --dtype spelling -> MMVAE_DTYPE_*, -1 when unknown
+int dtype_code(const std::string& s);
 int run_cli(int argc, const char** argv, int model);
 
 }  // namespace mmvae_host

@@ -86,6 +86,7 @@ def lib():
         "mmvae_timing_reset": (ctypes.c_int, [h]),
         "mmvae_debug_copy": (ctypes.c_int, [h, i32, f32p, i64]),
         "mmvae_tiling_info": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
+        "mmvae_debug_poison": (ctypes.c_int, [h, i32]),
         "mmvae_graph_enable": (ctypes.c_int, [h, i32]),
         "mmvae_graph_stats": (ctypes.c_int, [h, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "mmvae_lbessel": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
@@ -291,14 +292,18 @@ class Engine:
         self._chk(lib().mmvae_comm_init(self._h, rank, world, buf), "comm_init")
 
     def tiling(self):
-        """{'NT', 'split_enc', 'split_dec', 'split_ac'} and tiles per split (tps_*)."""
-        a = (ctypes.c_int32 * 4)()
+        """{'NT', 'split_enc', 'split_dec', 'split_ac', 'split_encb'} and tiles per split (tps_*)."""
+        a = (ctypes.c_int32 * 5)()
         self._chk(lib().mmvae_tiling_info(self._h, a), "tiling_info")
         NT = a[0]
-        out = {"NT": NT, "split_enc": a[1], "split_dec": a[2], "split_ac": a[3]}
-        for k in ("enc", "dec", "ac"):
+        out = {"NT": NT, "split_enc": a[1], "split_dec": a[2], "split_ac": a[3], "split_encb": a[4]}
+        for k in ("enc", "dec", "ac", "encb"):
             out["tps_" + k] = -(-NT // out["split_" + k])
         return out
+
+    def poison(self, byte):
+        """Fill the per-step workspace with `byte` (test hook, mmvae_debug_poison)."""
+        self._chk(lib().mmvae_debug_poison(self._h, int(byte)), "debug_poison")
 
     def graph(self, on=True):
         """Capture / replay each step's device work as one hipGraph (mmvae_graph_enable)."""

@@ -12,9 +12,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _engine(model, D, K, B, dtype, graph):
+def _engine(model, D, K, B, dtype, graph, **kw):
     from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
-    eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=9, model=MODEL_VMF if model == "vmf" else MODEL_NB)
+    eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=9, model=MODEL_VMF if model == "vmf" else MODEL_NB, **kw)
     eng.synth_csr(3000, lib_size=1500.0, seed=4)
     eng.init_params(seed=13)
     eng.graph(graph)
@@ -108,3 +108,97 @@ def test_ragged_batch_independent_of_handle_capacity(model, dtype):
     assert abs(out[0] - runs[0][0][0]) <= 1e-6 * abs(out[0])
     for k in g:
         assert rel_err(g[k], runs[0][1][k]) <= 1e-5, (k, rel_err(g[k], runs[0][1][k]))
+
+
+def _sequence(model, K, B, seed=0):
+    rng = np.random.default_rng(seed)
+    seq = [("step", rng.integers(0, 3000, B), 1.0, B, 0, None) for _ in range(2)]
+    seq.append(("step", rng.integers(0, 3000, 100), 1.0, 100, 0, None))      # ragged (padded rows)
+    seq.append(("eval", rng.integers(0, 3000, B), 0.5, B, 0, None))
+    seq.append(("step", rng.integers(0, 3000, 37), 0.5, 4 * B, 3 * B, None))  # ragged DP shard
+    eps = rng.standard_normal(B * (K + (0 if model == "vmf" else 1))).astype(np.float32)
+    seq.append(("step", rng.integers(0, 3000, B), 0.5, B, 0, eps))
+    seq.append(("step", rng.integers(0, 3000, B), 1.0, B, 0, None))
+    return seq
+
+
+HIDDEN = {"enc_hidden": (48,), "dec_hidden": (40, 24)}
+
+
+@pytest.mark.parametrize("model,dtype,arch", [("nb", "f32", {}), ("nb", "bf16x3", {}), ("nb", "bf16", {}),
+                                              ("nb", "fp8", {}), ("vmf", "f32", {}), ("vmf", "bf16x3", {}),
+                                              ("vmf", "bf16", {}), ("nb", "bf16x3", HIDDEN),
+                                              ("vmf", "bf16x3", dict(HIDDEN, relu=True))],
+                         ids=lambda v: "hidden" if isinstance(v, dict) and v else ("" if isinstance(v, dict) else v))
+def test_poisoned_workspace_bit_identical(model, dtype, arch):
+    """Every per-step workspace buffer (batch lists, tile offsets, split partials, latent
+    records, operand images, column slabs, loss / norm partials) is overwritten between steps
+    with NaN bytes (0xFF) or huge finite floats (0x7F) — mmvae_debug_poison.  A step that reads
+    a word it did not write this step (a stale padding row, an unwritten split partial) then
+    changes the result; every loss, norm and parameter must stay bit-identical to the unpoisoned
+    run, eager and graph alike.  This is the check behind the round-2 ragged-batch mismatch."""
+    D, K, B = 3000, 32, 256
+    seq = _sequence(model, K, B)
+    out = []
+    for poison, graph in ((None, False), (0xFF, False), (0x7F, True)):
+        eng = _engine(model, D, K, B, dtype, graph, **arch)
+        trace = []
+        for i, (kind, cells, beta, n_total, ro, ep) in enumerate(seq):
+            if poison is not None:
+                eng.poison(poison)
+            if kind == "eval":
+                trace.append((eng.eval_loss(cells, beta, step_id=100 + i), 0.0))
+            else:
+                trace.append(eng.step(cells, beta, n_total=n_total, row_offset=ro, step_id=100 + i, eps=ep))
+        out.append((trace, eng.params()))
+    for trace, params in out[1:]:
+        assert trace == out[0][0]
+        for k in params:
+            assert np.array_equal(params[k], out[0][1][k]), k
+
+
+@pytest.mark.parametrize("model,dtype", [("nb", "f32"), ("nb", "bf16x3"), ("nb", "bf16"), ("vmf", "bf16x3")])
+def test_repeated_ragged_step_deterministic(model, dtype):
+    """Race detector: the same ragged step (B = 100 on a 256-row handle) run eight times on one
+    handle from the same parameters and optimiser state, the workspace poisoned differently
+    before each run.  Every cross-wave / cross-workgroup sum is a fixed-order reduction of plain
+    stores, so loss, clip norm and every gradient must repeat bit for bit; an LDS or global race
+    (a read racing a write of another wave) shows up as run-to-run drift."""
+    D, K, B = 3000, 32, 256
+    eng = _engine(model, D, K, B, dtype, False)
+    cells = np.random.default_rng(7).integers(0, 3000, 100)
+    p0 = eng.params(registered_only=True)
+    ref = None
+    for rep in range(8):
+        eng.set_params(p0)
+        eng.reset_optimizer()
+        eng.poison([0x00, 0xFF, 0x7F, 0x3C][rep % 4])
+        out = eng.step(cells, 0.7, step_id=5)
+        got = (out, eng.grads())
+        if ref is None:
+            ref = got
+            continue
+        assert got[0] == ref[0], (rep, got[0], ref[0])
+        for k in ref[1]:
+            assert np.array_equal(got[1][k], ref[1][k]), (rep, k)
+
+
+def test_graph_recaptured_after_frozen_reload_fp8():
+    """Reloading a frozen decoder weight changes the fp8 mode's power-of-two W_dec scale, a
+    scalar the captured launch holds by value: the step graph must be re-captured (graph
+    generation bumped by the repack), so graph and eager handles agree after the reload."""
+    D, K, B = 3000, 32, 256
+    cells = [np.random.default_rng(s).integers(0, 3000, B) for s in range(4)]
+    res = []
+    for graph in (False, True):
+        eng = _engine("nb", D, K, B, "fp8", graph)
+        out = [eng.step(cells[0], 1.0, step_id=1), eng.step(cells[1], 1.0, step_id=2)]
+        name = "mu_dec.mu_decoding.weight"
+        n = {k: v for k, v, _ in eng.param_info()}[name]
+        eng.set_param(name, eng.get_param(name, n) * 8.0)  # amax x 8: wscale / 8
+        out += [eng.step(cells[2], 1.0, step_id=3), eng.step(cells[3], 1.0, step_id=4)]
+        res.append((out, eng.params(registered_only=True), eng.graph_stats()))
+    assert res[1][2]["captures"] >= 4, res[1][2]  # two shapes' worth before and after the reload
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k

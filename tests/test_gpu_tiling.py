@@ -27,7 +27,8 @@ from helpers import (assert_grads_close, dims, engine_from_fixture, eps_of, gold
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"f32": (2e-5, 2e-4), "bf16x3": (2e-5, 2e-4), "bf16": (2e-3, 3e-2)}
+# fp8 (decoder logit GEMM on e4m3, SURVEY §8(d): loss within 1e-2 rel, documented not parity)
+TOL = {"f32": (2e-5, 2e-4), "bf16x3": (2e-5, 2e-4), "bf16": (2e-3, 3e-2), "fp8": (1e-2, 6e-2)}
 
 
 def _eps(z, tag, vmf):
@@ -48,8 +49,9 @@ def test_fixture_forced_gene_splits(monkeypatch, path, split, dtype):
     eng = engine_from_fixture(z, dtype)
     til = eng.tiling()
     assert til["split_dec"] == min(int(split), til["NT"]) and til["split_enc"] == min(int(split), til["NT"])
+    assert til["split_encb"] == til["split_enc"], til  # MMVAE_NSPLIT_E forces the encoder backward too
     if til["NT"] >= 4:
-        assert til["tps_dec"] >= 2 and til["tps_enc"] >= 2 and til["tps_ac"] >= 2, til
+        assert til["tps_dec"] >= 2 and til["tps_enc"] >= 2 and til["tps_ac"] >= 2 and til["tps_encb"] >= 2, til
     loss, norm = eng.step(z["s0/cells"], float(z["s0/beta"]), eps=_eps(z, "s0", vmf))
     want = float(z["s0/loss"])
     assert abs(loss - want) <= 2e-5 * abs(want), (loss, want)
@@ -88,7 +90,7 @@ def _run_live(model, D, K, B, dtype, N, relu=False, beta=0.8):
     if vmf:  # kappa off its floor so its gradient is live (Q4)
         eng.set_param("ln_kappa", np.array([np.log(np.float32(4.0))], np.float32))
     til = eng.tiling()
-    assert til["tps_dec"] > 1 and til["tps_enc"] > 1 and til["tps_ac"] > 1, til
+    assert til["tps_dec"] > 1 and til["tps_enc"] > 1 and til["tps_ac"] > 1 and til["tps_encb"] > 1, til
     cells = (np.arange(B, dtype=np.int64) * 7 + 11) % N  # scattered dataset rows
     rng = np.random.default_rng(5)
     em = rng.standard_normal((B, K)).astype(np.float32)
@@ -140,9 +142,11 @@ def test_nb_configs3_per_gpu_shape(dtype):
     _run_live("nb", 30000, 64, 4096, dtype, N=9000)
 
 
-def test_nb_configs4_per_gpu_shape_bf16():
-    """configs[4] per GPU: 30k genes, 8192 cells per rank."""
-    _run_live("nb", 30000, 64, 8192, "bf16", N=9000)
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_nb_configs4_per_gpu_shape(dtype):
+    """configs[4] per GPU: 30k genes, 8192 cells per rank; fp8 is the config's named precision
+    (e4m3 MFMA), held to SURVEY §8(d)'s 1e-2 loss bar against the live oracle."""
+    _run_live("nb", 30000, 64, 8192, dtype, N=9000)
 
 
 @pytest.mark.parametrize("model", ["nb", "vmf"])
