@@ -187,7 +187,8 @@ def test_philox_restatement_matches_engine_noise():
     np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
-def test_cli_configs0_against_oracle_loop(tmp_path):
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
+def test_cli_configs0_against_oracle_loop(tmp_path, dtype):
     """BASELINE configs[0]: nb_vae_main on a synthetic 1000 x 500 MatrixMarket file, latent 8,
     batch 100, 3 epochs x 2 bootstrap updates — the CLI's per-epoch scores against the oracle's
     loop (the reference's op sequence on ATen CPU, oracle/nb_oracle.py) from the same initial
@@ -201,7 +202,8 @@ def test_cli_configs0_against_oracle_loop(tmp_path):
     out = str(tmp_path / "run")
     exe = os.path.join(host.BIN_DIR, "nb_vae_main")
     r = subprocess.run([exe, "--mtx", mtx, "--out", out, "--mean_latent", str(K), "--batch_size", str(B),
-                        "--max_epoch", str(E), "--nboot", str(NB), "--recording", "1000", "--seed", str(SEED)],
+                        "--max_epoch", str(E), "--nboot", str(NB), "--recording", "1000", "--seed", str(SEED),
+                        "--dtype", dtype],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     s_cli = np.array([float(s) for s in gzip.open(out + ".scores.gz", "rt").read().split()])
