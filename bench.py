@@ -110,7 +110,7 @@ def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234,
                            model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
     nnz = eng.synth_csr(cells, lib_size=lib, seed=2024)
     eng.init_params(seed=7)
-    eng.graph(graph)  # one hipGraph per step (world 1; steps with a communicator run eagerly)
+    eng.graph(graph)  # one hipGraph per step (with a communicator: the RCCL buckets captured too)
     return eng, nnz
 
 
@@ -409,6 +409,7 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
+    gst = eng.graph_stats()  # replays > 0: the timed steps ran as step graphs (RCCL buckets included)
     per_kernel, step_dev_ms = kernel_times(eng, batches, beta, n_total, rank * B, args.kernel_steps)
     loss, _ = eng.run(batches[0], beta, update=False, n_total=n_total, row_offset=rank * B, step_id=0)
 
@@ -443,7 +444,8 @@ def main():
                                f"batch {B}/GPU",
                    "global_batch": B * world, "genes": D, "latent": K, "cells": Ncells,
                    "nnz_per_cell": round(npc, 1), "parallelism": f"dp{world}",
-                   "step_graph": (not args.no_graph) and world == 1},
+                   "step_graph": gst["replays"] > 0 and not args.no_graph,
+                   "graph_stats": gst},
         "roofline": roofline(args.model, args.dtype, D, K, B, npc, per_kernel),
         "composite": composite(args.model, args.dtype, D, K, B, npc, P_reg, ms),
         "device_ms_per_step": round(step_dev_ms, 4),

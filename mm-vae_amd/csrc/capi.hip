@@ -885,10 +885,18 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     // frozen operands are repacked eagerly, never inside a step graph
     if (e->frozen_dirty) HIPCHK(e, vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
     // one hipGraph per step: captured on the first step of a launch shape,
-    // replayed while the shape holds; not with timers, diagnostics or a communicator (the RCCL
-    // calls stay eager)
+    // replayed while the shape holds; not with timers or diagnostics.  With a communicator the
+    // graph holds the RCCL bucket all-reduces too: comm_bucket's event fork onto the comm stream
+    // and its join back are captured with them (MMVAE_COMM_GRAPH=0 keeps those steps eager; a
+    // failed capture falls back to eager launches for the handle's lifetime)
     static const bool dbg_env = std::getenv("MMVAE_DBG") != nullptr;
-    const bool use_graph = e->graph_on && !e->timing && !dbg_env && !(e->comm && e->world > 1);
+    static const bool comm_graph_env = [] {
+        const char* v = std::getenv("MMVAE_COMM_GRAPH");
+        return !(v && v[0] == '0');
+    }();
+    const bool with_comm = e->comm && e->world > 1;
+    const bool use_graph = e->graph_on && !e->timing && !dbg_env &&
+                           (!with_comm || (comm_graph_env && !e->comm_graph_failed));
     if (use_graph) {
         GraphKey k;
         k.B = a->B;
@@ -913,19 +921,30 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
             const int crc = enqueue_run(e, a, n_total);
             hipGraph_t g = nullptr;
             const hipError_t ce = hipStreamEndCapture(e->stream, &g);
-            if (crc) {
-                if (g) hipGraphDestroy(g);
-                return crc;
+            hipError_t ie = hipSuccess;
+            if (!crc && ce == hipSuccess) ie = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
+            if (g) hipGraphDestroy(g);
+            if (with_comm && (crc || ce != hipSuccess || ie != hipSuccess)) {
+                // the communicator's calls did not capture: this step and the later ones with it
+                // run eagerly (nothing of the failed capture was executed)
+                (void)hipGetLastError();
+                e->comm_graph_failed = true;
+                gx = nullptr;
+            } else {
+                if (crc) return crc;
+                HIPCHK(e, ce);
+                HIPCHK(e, ie);
+                sl.graphs.emplace_back(k, gx);
+                ++e->graph_captures;
             }
-            HIPCHK(e, ce);
-            const hipError_t ie = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
-            hipGraphDestroy(g);
-            HIPCHK(e, ie);
-            sl.graphs.emplace_back(k, gx);
-            ++e->graph_captures;
         }
-        HIPCHK(e, hipGraphLaunch(gx, e->stream));
-        ++e->graph_replays;
+        if (gx) {
+            HIPCHK(e, hipGraphLaunch(gx, e->stream));
+            ++e->graph_replays;
+        } else {
+            rc = enqueue_run(e, a, n_total);
+            if (rc) return rc;
+        }
     } else {
         rc = enqueue_run(e, a, n_total);
         if (rc) return rc;
@@ -1039,6 +1058,7 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (r != ncclSuccess) FAIL(e, MMVAE_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     e->rank = rank;
     e->world = world;
+    e->comm_graph_failed = false;
     if (!e->comm_stream) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
         for (auto& ev : e->ev_bucket) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));

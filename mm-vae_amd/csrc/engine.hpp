@@ -196,6 +196,9 @@ struct Engine {
 
     // ---- step graphs (A17: one hipGraph per step, mmvae_graph_enable) ----
     bool graph_on = false;
+    // set when a capture with the communicator attached failed (RCCL calls not capturable in
+    // this runtime): later steps with the communicator run eagerly
+    bool comm_graph_failed = false;
     uint64_t graph_gen = 0;          // bumped when a buffer a step graph points at is replaced
     int64_t graph_captures = 0, graph_replays = 0;
 

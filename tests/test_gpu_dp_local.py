@@ -69,3 +69,34 @@ def test_vmf_baricz_term_on_rank0_only():
     kap = np.float32(3.0)
     want = lbessel_grad(float(kap), 0.5 * D - 1.0) * float(kap)
     assert abs((out[0] - out[1]) - want) <= 1e-4 * abs(want), (out, want)
+
+
+@pytest.mark.parametrize("model", ["nb", "vmf"])
+def test_local_dp_step_graphs_replay_and_match_eager(model):
+    """A17 under DP: shards of a world-2 step run as replayed step graphs (mmvae_graph_stats)
+    and give bit-identical losses and gradients to the same shards launched eagerly."""
+    D, K, B, world = 3000, 32, 512, 2
+    b = B // world
+    out = {}
+    for graph in (False, True):
+        res = []
+        for r in range(world):
+            eng = _engine(model, D, K, b, "bf16x3")
+            eng.comm_init(r, world, None)
+            eng.graph(graph)
+            for s in range(4):
+                cells = (np.arange(B, dtype=np.int64) * 7 + 11 * s) % 3000
+                l, n = eng.step(cells[r * b:(r + 1) * b], 0.7, n_total=B, row_offset=r * b, step_id=s)
+                res.append((l, n))
+            res.append(eng.grads())
+            if graph:
+                st = eng.graph_stats()
+                assert st["replays"] == 4 and st["captures"] >= 1, st
+            eng.close()
+        out[graph] = res
+    for a, c in zip(out[False], out[True]):
+        if isinstance(a, dict):
+            for k in a:
+                assert np.array_equal(a[k], c[k]), k
+        else:
+            assert a == c, (a, c)

@@ -40,7 +40,7 @@ def _batches():
     return [(np.arange(B, dtype=np.int64) * (5 + 2 * s) + 3 * s) % 3000 for s in range(STEPS)]
 
 
-def _worker(rank, model, no_overlap, uid_q, res_q, device):
+def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False):
     try:
         if no_overlap:
             os.environ["MMVAE_NO_OVERLAP"] = "1"
@@ -53,22 +53,25 @@ def _worker(rank, model, no_overlap, uid_q, res_q, device):
         b = B // 2
         eng = _engine(model, b, device)
         eng.comm_init(rank, 2, uid)
+        eng.graph(graph)  # the step graph then holds the RCCL bucket all-reduces
         out = []
         for s, cells in enumerate(_batches()):
             l, n = eng.step(cells[rank * b:(rank + 1) * b], 0.7, n_total=B, row_offset=rank * b, step_id=s)
             out.append((l, n))
+        if graph:
+            out.append(eng.graph_stats())
         res_q.put((rank, out, eng.params(registered_only=True)))
     except Exception as ex:  # reported to the parent, which fails the test
         res_q.put((rank, "error", repr(ex)))
 
 
 @pytest.mark.skipif(_ndev() < 2, reason="needs two GPUs (RCCL over xGMI)")
-@pytest.mark.parametrize("no_overlap", [False, True])
+@pytest.mark.parametrize("no_overlap,graph", [(False, False), (True, False), (False, True)])
 @pytest.mark.parametrize("model", ["nb", "vmf"])
-def test_rccl_world2_equals_world1(model, no_overlap):
+def test_rccl_world2_equals_world1(model, no_overlap, graph):
     ctx = mp.get_context("spawn")
     uid_q, res_q = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, model, no_overlap, uid_q, res_q, r)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, model, no_overlap, uid_q, res_q, r, graph)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -82,6 +85,10 @@ def test_rccl_world2_equals_world1(model, no_overlap):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+    if graph:  # every step replayed a captured graph (no eager fallback)
+        for r in (0, 1):
+            st = res[r][0].pop()
+            assert st["replays"] == STEPS, st
     # world-1 reference in this process, on device 0
     full = _engine(model, B, 0)
     for s, cells in enumerate(_batches()):
