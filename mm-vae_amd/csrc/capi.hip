@@ -1266,6 +1266,9 @@ int mmvae_debug_poison(mmvae_h e, int32_t byte) {
     };
     for (const auto& b : bufs)
         if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));
+    // and the LDS of every CU: a kernel reading LDS it did not write this launch (a tile row or
+    // a correction plane left over from another workgroup) then sees the pattern
+    HIPCHK(e, lds_poison(e, byte));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MMVAE_OK;
 }

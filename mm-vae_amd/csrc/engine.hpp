@@ -294,6 +294,8 @@ hipError_t dispatch_mode(const Engine* e, F&& f) {
 }
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
+// diagnostic: every CU's LDS filled with `byte` (mmvae_debug_poison)
+hipError_t lds_poison(Engine* e, int byte);
 void adam_scalars(const Engine* e, int64_t t, StepScalars* ss);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
 hipError_t build_dataset_index(Engine* e);

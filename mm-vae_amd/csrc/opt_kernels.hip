@@ -88,4 +88,28 @@ hipError_t opt_clip_adam(Engine* e) {
     return hipGetLastError();
 }
 
+// Diagnostic (mmvae_debug_poison): fill the whole LDS of every CU with a byte pattern.  One
+// workgroup holds the full 160 KB, so a grid of a few rounds over the 256 CUs leaves the pattern
+// in every CU's LDS for the kernels launched next.  Vector LDS stores only.
+static constexpr int LDS_POISON_BYTES = 160 * 1024;
+__global__ __launch_bounds__(256) void k_lds_poison(uint32_t word) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint4* s = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < LDS_POISON_BYTES / 16; i += 256) s[i] = uint4{word, word, word, word};
+    __syncthreads();
+}
+
+hipError_t lds_poison(Engine* e, int byte) {
+    const uint32_t b = (uint32_t)(byte & 0xff);
+    static bool attr = false;
+    if (!attr) {  // (the runtime may already allow the full LDS; a refusal is not an error here)
+        (void)hipFuncSetAttribute((const void*)k_lds_poison, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_POISON_BYTES);
+        (void)hipGetLastError();
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_lds_poison, dim3(4 * 256), dim3(256), LDS_POISON_BYTES, e->stream, b * 0x01010101u);
+    return hipGetLastError();
+}
+
 }  // namespace mmvae
