@@ -37,6 +37,8 @@ enum {
 };
 
 enum { MMVAE_MODEL_NB = 0, MMVAE_MODEL_VMF = 1 };
+/* most hidden encoder / decoder layers of a cfg (the reference takes any number) */
+#define MMVAE_MAX_HIDDEN 16
 /* Operand precision of the encoder/decoder GEMMs; every epilogue, reduction, gradient and
  * optimiser update is fp32.
  *   F32     exact f32 MFMA (v_mfma_f32_16x16x4_f32): bitwise an fp32 FMA chain.
@@ -69,10 +71,10 @@ typedef struct mmvae_cfg {
                             decoder Linear (vmf.hh:342-352, 378-379).  NB with relu and >= 1
                             hidden encoder layer is the reference's construction error (Q2,
                             nb.hh:334-337): mmvae_create returns MMVAE_E_ARG. */
-    int32_t n_enc_hidden;    /* NB --mean_encoding / vMF --encoding: hidden widths, <= 4 layers */
+    int32_t n_enc_hidden;    /* NB --mean_encoding / vMF --encoding: hidden widths, <= MMVAE_MAX_HIDDEN layers */
     int32_t n_dec_hidden;    /* NB --mean_decoding / vMF --decoding */
-    int32_t enc_hidden[4];
-    int32_t dec_hidden[4];
+    int32_t enc_hidden[MMVAE_MAX_HIDDEN];
+    int32_t dec_hidden[MMVAE_MAX_HIDDEN];
 } mmvae_cfg;
 
 /* Fill a cfg with the reference defaults (mmvae_alg.hh:19-23, nb.hh:58-61, vmf.hh:59-63). */
@@ -81,11 +83,15 @@ void mmvae_cfg_default(mmvae_cfg* cfg, int32_t model);
 /* Create an engine on HIP device `device`.  Replaces constructing nbvae_t / vmf_vae_t
  * (nb.hh:299-401, vmf.hh:307-389) plus the torch::optim::Adam of mmvae_alg.hh:234-237.
  * Parameters start at zero; load them with mmvae_set_param or mmvae_init_params.
- * Shape limits of this engine (MMVAE_E_ARG beyond them; the reference has none):
- *   1 <= D <= 75,264 genes; 1 <= K <= 64; 1 <= C, H, R <= 8; at most 4 hidden encoder /
- *   decoder layers, each 1..64 wide; FP8 for the NB model only. */
+ * Shapes: D, K, C, H, R >= 1 and at most MMVAE_MAX_HIDDEN hidden encoder / decoder layers of any
+ * width >= 1 (the reference has no limits).  Models with D <= 75,264 genes, K <= 64,
+ * C, H, R <= 8, at most 4 hidden layers per side and hidden widths <= 64 run on the fused tile
+ * kernels; any other shape runs on the wide path (a dense [B, D] batch in HBM and generic f32-MFMA
+ * GEMMs, exact f32 whatever the dtype; mmvae_path reports which).  FP8 for the NB model only. */
 int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out);
 int mmvae_destroy(mmvae_h h);
+/* Which step path the handle runs: 0 = the fused tile kernels, 1 = the wide path. */
+int mmvae_path(mmvae_h h, int32_t* wide);
 /* Message for the last failing call on h (h may be NULL for mmvae_create failures). */
 const char* mmvae_last_error(mmvae_h h);
 

@@ -249,38 +249,43 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "model must be MMVAE_MODEL_NB or MMVAE_MODEL_VMF");
     if (cfg->model == MMVAE_MODEL_VMF && !(cfg->kappa_min > 0.f && cfg->kappa_max >= cfg->kappa_min))
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "vMF needs 0 < kappa_min <= kappa_max");
-    if (cfg->D < 1 || cfg->K < 1 || cfg->K > 64 || cfg->C < 1 || cfg->C > 8 || cfg->H < 1 || cfg->H > 8 ||
-        cfg->R < 1 || cfg->R > 8 || cfg->max_batch < 1)
-        FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D>=1, 1<=K<=64, 1<=C,H,R<=8, max_batch>=1)");
-    {  // the batch-list builder keeps a 16-row block's tile pointers in LDS (batch.hip)
-        const int64_t NT = (cfg->D + 63) / 64;
-        if (4 * (NT + 1 + 16 * (NT + 1) + 16 * NT) + 8 * 1024 + 256 > 160 * 1024)
-            FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range: D above 75,264 genes (the batch lists' LDS tile index)");
-    }
+    if (cfg->D < 1 || cfg->K < 1 || cfg->C < 1 || cfg->H < 1 || cfg->R < 1 || cfg->max_batch < 1)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "cfg out of range (need D, K, C, H, R, max_batch >= 1)");
     if (cfg->dtype != MMVAE_DTYPE_F32 && cfg->dtype != MMVAE_DTYPE_BF16 && cfg->dtype != MMVAE_DTYPE_BF16X3 &&
         cfg->dtype != MMVAE_DTYPE_FP8)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "dtype must be F32, BF16, BF16X3 or FP8");
     if (cfg->dtype == MMVAE_DTYPE_FP8 && cfg->model != MMVAE_MODEL_NB)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "the fp8 mode is built for the NB decoder (BASELINE configs[4])");
-    if (cfg->n_enc_hidden < 0 || cfg->n_enc_hidden > 4 || cfg->n_dec_hidden < 0 || cfg->n_dec_hidden > 4)
-        FAIL((Engine*)nullptr, MMVAE_E_ARG, "at most 4 hidden encoder / decoder layers");
+    if (cfg->n_enc_hidden < 0 || cfg->n_enc_hidden > MMVAE_MAX_HIDDEN || cfg->n_dec_hidden < 0 ||
+        cfg->n_dec_hidden > MMVAE_MAX_HIDDEN)
+        FAIL((Engine*)nullptr, MMVAE_E_ARG, "at most 16 hidden encoder / decoder layers (MMVAE_MAX_HIDDEN)");
     // nb.hh:334-337 pushes a hidden encoder Linear and its ReLU under the same name: LibTorch
     // throws at construction, so the reference has no such model
     if (cfg->model == MMVAE_MODEL_NB && cfg->relu && cfg->n_enc_hidden > 0)
         FAIL((Engine*)nullptr, MMVAE_E_ARG, "Submodule 'mu_encoding_1' already defined (reference nb.hh:334-337: "
                                             "--relu with hidden --mean_encoding layers)");
     for (int l = 0; l < cfg->n_enc_hidden; ++l)
-        if (cfg->enc_hidden[l] < 1 || cfg->enc_hidden[l] > 64)
-            FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden encoder widths must be 1..64 in this engine");
+        if (cfg->enc_hidden[l] < 1) FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden encoder widths must be >= 1");
     for (int l = 0; l < cfg->n_dec_hidden; ++l)
-        if (cfg->dec_hidden[l] < 1 || cfg->dec_hidden[l] > 64)
-            FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden decoder widths must be 1..64 in this engine");
+        if (cfg->dec_hidden[l] < 1) FAIL((Engine*)nullptr, MMVAE_E_ARG, "hidden decoder widths must be >= 1");
+    // the fused tile kernels' shape envelope; anything else runs on the wide path (wide.hip)
+    bool wide = cfg->K > 64 || cfg->C > CMAX || cfg->H > HMAX || cfg->R > RMAX || cfg->n_enc_hidden > 4 ||
+                cfg->n_dec_hidden > 4;
+    for (int l = 0; l < cfg->n_enc_hidden; ++l) wide = wide || cfg->enc_hidden[l] > 64;
+    for (int l = 0; l < cfg->n_dec_hidden; ++l) wide = wide || cfg->dec_hidden[l] > 64;
+    {  // the batch-list builder keeps a 16-row block's tile pointers in LDS (batch.hip)
+        const int64_t NT = (cfg->D + 63) / 64;
+        if (4 * (NT + 1 + 16 * (NT + 1) + 16 * NT) + 8 * 1024 + 256 > 160 * 1024) wide = true;
+    }
+    if (const char* v = std::getenv("MMVAE_WIDE"))  // diagnostics / tests: force the wide path
+        if (v[0] == '1') wide = true;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
         FAIL((Engine*)nullptr, MMVAE_E_HIP, "no HIP device " + std::to_string(device));
     mmvae_engine* e = new mmvae_engine();
     e->cfg = *cfg;
     e->device = device;
+    e->wide = wide;
     HIPCHK(e, hipSetDevice(device));
     HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     e->D = cfg->D;
@@ -290,7 +295,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     e->KE = cfg->n_enc_hidden ? cfg->enc_hidden[0] : cfg->K;
     e->E = cfg->n_enc_hidden ? cfg->enc_hidden[cfg->n_enc_hidden - 1] : cfg->K;
     e->KD = cfg->n_dec_hidden ? cfg->dec_hidden[cfg->n_dec_hidden - 1] : cfg->K;
-    e->KP = (std::max(e->K, std::max(e->KE, e->KD)) <= 32) ? 32 : 64;
+    e->KP = (std::max(e->K, std::max(e->KE, e->KD)) <= 32) ? 32 : 64;  // (fused path only)
     e->C = cfg->C;
     e->H = cfg->H;
     e->R = cfg->R;
@@ -441,9 +446,16 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // loss / total norm: written by the kernels straight into mapped pinned memory (no readback copy)
     HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(e, hipHostGetDevicePointer((void**)&e->d_out, e->h_out_pin, 0));
+    if (e->wide) HIPCHK(e, wide_create(e));
     for (auto& sl : e->slots2) HIPCHK(e, hipEventRecord(sl.ev, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     *out = e;
+    return MMVAE_OK;
+}
+
+int mmvae_path(mmvae_h e, int32_t* wide) {
+    if (!e || !wide) FAIL(e, MMVAE_E_ARG, "path: null");
+    *wide = e->wide ? 1 : 0;
     return MMVAE_OK;
 }
 
@@ -458,6 +470,7 @@ int mmvae_destroy(mmvae_h e) {
         if (sl.ev) hipEventDestroy(sl.ev);
     }
     if (e->comm) ncclCommDestroy(e->comm);
+    wide_destroy(e);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
@@ -789,7 +802,7 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         if (c < 0 || c >= e->N) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
         e->h_cells_pin[j] = c;
     }
-    e->perm_active = balance && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == e->N &&
+    e->perm_active = balance && !e->wide && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == e->N &&
                      !std::getenv("MMVAE_NO_BALANCE");
     if (e->perm_active) {
         balance_rows(e, B);
@@ -811,7 +824,7 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         }
     }
     e->h_seg_pin[WB] = tot;
-    if (tot + 64 > e->ent_cap) {
+    if (!e->wide && tot + 64 > e->ent_cap) {  // (the wide path reads the CSR rows directly)
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (e->d_ents) hipFree(e->d_ents);
         e->d_ents = nullptr;
@@ -845,10 +858,14 @@ static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
     }
     e->grads_reduced = false;
     e->sq_parts = 0;
+    if (e->wide) {
+        HIPCHK(e, wide_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));  // + staged copy
+    } else {
     HIPCHK(e, vmf ? vmf_prep(e, a->B, n_total, a->beta) : nb_prep(e, a->B, n_total, a->beta));  // + staged copy
     HIPCHK(e, build_lists(e, a->B));
     if (vmf) HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
     else HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
+    }
     if (a->update) {
         if (e->comm && e->world > 1 && !e->grads_reduced) {
             ScopedTimer tm(e, "allreduce_grads");
@@ -883,7 +900,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     e->h_ss->row_offset = a->row_offset;
     if (a->update) adam_scalars(e, e->adam_step + 1, e->h_ss);
     // frozen operands are repacked eagerly, never inside a step graph
-    if (e->frozen_dirty) HIPCHK(e, vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
+    if (e->frozen_dirty) HIPCHK(e, e->wide ? wide_prepare_frozen(e) : vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
     // one hipGraph per step: captured on the first step of a launch shape,
     // replayed while the shape holds; not with timers or diagnostics.  With a communicator the
     // graph holds the RCCL bucket all-reduces too: comm_bucket's event fork onto the comm stream
@@ -995,6 +1012,12 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
+    if (e->wide) {
+        if (e->frozen_dirty) HIPCHK(e, wide_prepare_frozen(e));
+        if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
+        HIPCHK(e, wide_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));  // + the staged copy
+        HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    } else {
     if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));  // + the staged copy
     else HIPCHK(e, vmf_prep(e, B, B, 1.f));
     HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
@@ -1002,6 +1025,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
     else HIPCHK(e, nb_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));
+    }
     HIPCHK(e, hipMemcpyAsync(mean, e->d_tmp, sizeof(float) * B * e->K, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(lnvar, e->d_tmp + e->Bpad * e->K, sizeof(float) * B * e->K, hipMemcpyDeviceToHost,
                              e->stream));
@@ -1266,6 +1290,8 @@ int mmvae_debug_poison(mmvae_h e, int32_t byte) {
     };
     for (const auto& b : bufs)
         if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));
+    for (const auto& b : wide_poison_bufs(e))
+        if (b.first && b.second) HIPCHK(e, hipMemsetAsync(b.first, byte & 0xff, b.second, e->stream));
     // and the LDS of every CU: a kernel reading LDS it did not write this launch (a tile row or
     // a correction plane left over from another workgroup) then sees the pattern
     HIPCHK(e, lds_poison(e, byte));

@@ -70,8 +70,8 @@ struct Engine {
     // (nce encoder layers, then ncd decoder layers) packed in d_chain (see Dims)
     int64_t KE = 0, E = 0, KD = 0;
     int nce = 0, ncd = 0;
-    int ch_in[8] = {}, ch_out[8] = {}, ch_off[8] = {};
-    std::string ch_w[8], ch_b[8];  // frozen slot names of every chain layer (bias "" for Angular)
+    int ch_in[2 * MMVAE_MAX_HIDDEN] = {}, ch_out[2 * MMVAE_MAX_HIDDEN] = {}, ch_off[2 * MMVAE_MAX_HIDDEN] = {};
+    std::string ch_w[2 * MMVAE_MAX_HIDDEN], ch_b[2 * MMVAE_MAX_HIDDEN];  // frozen slot names of every chain layer (bias "" for Angular)
     float* d_chain = nullptr;
     std::string fz_enc_w, fz_enc_b, fz_dec_w, fz_dec_b;  // the big frozen layers' slots
     int64_t C = 1, H = 1, R = 1;
@@ -194,6 +194,10 @@ struct Engine {
     uint64_t auto_step = 0;  // Philox step counter of mmvae_step / mmvae_eval
     size_t stage_bytes = 0;  // the per-step H2D staging block (cells | seg | perm)  // set by a model step that already all-reduced its buckets
 
+    // ---- the wide path (wide.hip): shapes beyond the fused kernels' limits ----
+    bool wide = false;
+    struct WideState* wide_st = nullptr;
+
     // ---- step graphs (A17: one hipGraph per step, mmvae_graph_enable) ----
     bool graph_on = false;
     // set when a capture with the communicator attached failed (RCCL calls not capturable in
@@ -292,6 +296,15 @@ hipError_t dispatch_mode(const Engine* e, F&& f) {
     if (dt == MMVAE_DTYPE_BF16X3) return f(X3{}, K64{});
     return f(float{}, K64{});
 }
+// the wide path (wide.hip): dense [B, D] batch + generic f32-MFMA GEMMs for model shapes beyond
+// the fused kernels (K or a hidden width > 64, > 4 hidden layers, C / H / R > 8, D > 75,264)
+hipError_t wide_create(Engine* e);
+void wide_destroy(Engine* e);
+hipError_t wide_prepare_frozen(Engine* e);
+hipError_t wide_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps);
+hipError_t wide_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
+typedef std::vector<std::pair<void*, size_t>> wide_poison_t;
+wide_poison_t wide_poison_bufs(Engine* e);
 // optimiser (opt_kernels.hip)
 hipError_t opt_clip_adam(Engine* e);
 // diagnostic: every CU's LDS filled with `byte` (mmvae_debug_poison)

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
 }
 
 hipError_t build_dataset_index(Engine* e) {
+    if (e->wide) return hipSuccess;  // the wide path densifies straight from the CSR rows
     hipFree(e->d_rtp);
     hipFree(e->d_cellnorm);
     e->d_rtp = nullptr;

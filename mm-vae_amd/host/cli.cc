@@ -234,8 +234,8 @@ int run_cli(int argc, const char** argv, int model) {
         std::fputs(usage_text(model), stderr);
         return EXIT_FAILURE;
     }
-    if (o.enc_layers.size() > 4 || o.dec_layers.size() > 4) {
-        std::fprintf(stderr, "at most 4 hidden encoder / decoder layers\n");
+    if (o.enc_layers.size() > MMVAE_MAX_HIDDEN || o.dec_layers.size() > MMVAE_MAX_HIDDEN) {
+        std::fprintf(stderr, "at most %d hidden encoder / decoder layers\n", MMVAE_MAX_HIDDEN);
         return EXIT_FAILURE;
     }
     const int rank = std::getenv("RANK") ? std::atoi(std::getenv("RANK")) : 0;

@@ -26,13 +26,17 @@ class MMVAEError(RuntimeError):
     pass
 
 
+MAX_HIDDEN = 16  # MMVAE_MAX_HIDDEN (include/mmvae_capi.h)
+
+
 class Cfg(ctypes.Structure):
     _fields_ = [("model", ctypes.c_int32), ("dtype", ctypes.c_int32), ("D", ctypes.c_int64),
                 ("C", ctypes.c_int64), ("K", ctypes.c_int64), ("H", ctypes.c_int64), ("R", ctypes.c_int64),
                 ("max_batch", ctypes.c_int64), ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("grad_clip", ctypes.c_float), ("kappa_min", ctypes.c_float), ("kappa_max", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("relu", ctypes.c_int32), ("n_enc_hidden", ctypes.c_int32),
-                ("n_dec_hidden", ctypes.c_int32), ("enc_hidden", ctypes.c_int32 * 4), ("dec_hidden", ctypes.c_int32 * 4)]
+                ("n_dec_hidden", ctypes.c_int32), ("enc_hidden", ctypes.c_int32 * MAX_HIDDEN),
+                ("dec_hidden", ctypes.c_int32 * MAX_HIDDEN)]
 
 
 class StepArgs(ctypes.Structure):
@@ -88,6 +92,7 @@ def lib():
         "mmvae_tiling_info": (ctypes.c_int, [h, ctypes.POINTER(i32)]),
         "mmvae_debug_poison": (ctypes.c_int, [h, i32]),
         "mmvae_graph_enable": (ctypes.c_int, [h, i32]),
+        "mmvae_path": (ctypes.c_int, [h, ctypes.POINTER(ctypes.c_int32)]),
         "mmvae_graph_stats": (ctypes.c_int, [h, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "mmvae_lbessel": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
         "mmvae_lbessel_grad": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
@@ -125,8 +130,8 @@ class Engine:
         c = default_cfg(model)
         c.D, c.K, c.C, c.H, c.R, c.max_batch = D, K, C, H, R, max_batch
         c.relu = 1 if relu else 0
-        if len(enc_hidden) > 4 or len(dec_hidden) > 4:
-            raise MMVAEError("at most 4 hidden encoder / decoder layers")
+        if len(enc_hidden) > MAX_HIDDEN or len(dec_hidden) > MAX_HIDDEN:
+            raise MMVAEError(f"at most {MAX_HIDDEN} hidden encoder / decoder layers")
         c.n_enc_hidden, c.n_dec_hidden = len(enc_hidden), len(dec_hidden)
         for i, v in enumerate(enc_hidden):
             c.enc_hidden[i] = int(v)
@@ -304,6 +309,12 @@ class Engine:
     def poison(self, byte):
         """Fill the per-step workspace with `byte` (test hook, mmvae_debug_poison)."""
         self._chk(lib().mmvae_debug_poison(self._h, int(byte)), "debug_poison")
+
+    def path(self):
+        """'fused' (the tile kernels) or 'wide' (dense batch + generic GEMMs: shapes beyond them)."""
+        w = ctypes.c_int32()
+        self._chk(lib().mmvae_path(self._h, ctypes.byref(w)), "path")
+        return "wide" if w.value else "fused"
 
     def graph(self, on=True):
         """Capture / replay each step's device work as one hipGraph (mmvae_graph_enable)."""

@@ -31,6 +31,12 @@ NB_CASES = [
     ("nb_hidden1", 100, 300, 16, 1, 1, 1, 64, 3, 300.0, 8, False, (24,), (20,)),
     ("nb_hidden2", 90, 200, 8, 2, 1, 1, 48, 3, 250.0, 9, False, (48, 12), (10, 40)),
     ("nb_hidden_relu", 90, 200, 16, 1, 1, 1, 48, 3, 250.0, 10, True, (), (32, 20)),
+    # beyond the fused kernels' shape limits: the wide path (mm-vae_amd/csrc/wide.hip)
+    ("nb_wide_k128", 100, 300, 128, 1, 1, 1, 64, 3, 300.0, 21),
+    ("nb_wide_enc", 100, 300, 16, 1, 1, 1, 64, 3, 300.0, 22, False, (256, 128), (96,)),
+    ("nb_wide_chr", 60, 120, 8, 12, 10, 9, 32, 3, 150.0, 23),
+    ("nb_wide_deep", 80, 200, 8, 2, 1, 1, 48, 3, 250.0, 24, False, (40, 32, 24, 20, 16, 12), (10, 12, 14, 16, 18)),
+    ("nb_wide_relu", 80, 200, 72, 1, 1, 1, 48, 3, 250.0, 25, True, (), (100, 80)),
 ]
 
 
@@ -102,6 +108,10 @@ VMF_CASES = [
     ("vmf_relu", 100, 300, 16, 1, 64, 3, 300.0, 16, float(np.log(np.float32(3.0))), True),
     ("vmf_hidden1", 100, 300, 16, 1, 64, 3, 300.0, 17, float(np.log(np.float32(3.0))), False, (24,), (20,)),
     ("vmf_hidden_relu", 90, 200, 8, 2, 48, 3, 250.0, 18, float(np.log(np.float32(2.0))), True, (40, 12), (10, 30)),
+    # the wide path
+    ("vmf_wide_z96", 100, 300, 96, 1, 64, 3, 400.0, 31, float(np.log(np.float32(4.0)))),
+    ("vmf_wide_enc", 100, 300, 16, 1, 64, 3, 300.0, 32, float(np.log(np.float32(3.0))), True, (256, 100), (80,)),
+    ("vmf_wide_deep", 80, 200, 8, 12, 48, 3, 250.0, 33, float(np.log(np.float32(2.0))), False, (40, 32, 24, 20, 16), (10, 12, 14, 16, 18)),
 ]
 
 

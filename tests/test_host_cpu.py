@@ -186,8 +186,8 @@ def test_cli_arguments_without_gpu(tmp_path, exe):
     p = tmp_path / "x.mtx"
     p.write_text("%%MatrixMarket matrix coordinate integer general\n3 2 2\n1 1 4\n3 2 1\n")
     r = subprocess.run([b, "--mtx", str(p), "--out", str(tmp_path / "o"), "--mean_encoding" if exe == "nb_vae_main"
-                        else "--encoding", "100"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 1 and "hidden encoder widths must be 1..64" in r.stderr  # checked before any device
+                        else "--encoding", ",".join(["100"] * 17)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "at most 16 hidden" in r.stderr  # checked before any device
     r = subprocess.run([b, "--mtx", str(p), "--out", str(tmp_path / "o"), "--dtype", "bf61"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "unknown --dtype bf61" in r.stderr and "fp8" in r.stderr
