@@ -390,7 +390,11 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_WdP_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WdP_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WdT_f, KP * DP));
-    if (cfg->dtype == MMVAE_DTYPE_FP8) HIPCHK(e, dalloc(&e->d_WdP8, KP * DP));
+    if (cfg->dtype == MMVAE_DTYPE_FP8) {
+        HIPCHK(e, dalloc(&e->d_WdP8, KP * DP));
+        HIPCHK(e, dalloc(&e->d_WeS8, KP * DP));
+        HIPCHK(e, dalloc(&e->d_escale, 2));
+    }
     HIPCHK(e, dalloc(&e->d_WdT_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WeS_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WeS_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
@@ -476,7 +480,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8};
+                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8, e->d_WeS8, e->d_escale};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block
@@ -1287,6 +1291,8 @@ int mmvae_debug_poison(mmvae_h e, int32_t byte) {
         {e->d_sumsq, sizeof(double) * (size_t)(256 + (e->D + 31) / 32 + (SMALL + 2 * e->K + 31) / 32 + 1)},
         {e->d_rowv, sizeof(float) * (size_t)Bp},
         {e->d_vk, sizeof(float) * 8},
+        {e->d_WeS8, (size_t)(KP * DP)},
+        {e->d_escale, sizeof(float) * 2},
     };
     for (const auto& b : bufs)
         if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));

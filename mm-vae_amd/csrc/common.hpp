@@ -238,6 +238,10 @@ template <int RB> struct TrFrag<X3, RB> {  // hi and lo planes, plane_bytes apar
 template <class T> MMVAE_DEV T to_t(float v);
 template <> MMVAE_DEV float to_t<float>(float v) { return v; }
 template <> MMVAE_DEV __bf16 to_t<__bf16>(float v) { return (__bf16)v; }
+// one f32 -> e4m3 byte (v_cvt_pk_fp8_f32, round to nearest even)
+template <> MMVAE_DEV uint8_t to_t<uint8_t>(float v) {
+    return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+}
 
 // ---------------------------------------------------------------------------------------
 // Scalar math.  fast exp/log/rcp map to v_exp_f32 / v_log_f32 / v_rcp_f32 (quarter rate).

@@ -105,6 +105,9 @@ struct Engine {
     __bf16* d_WdP_b = nullptr;
     uint8_t* d_WdP8 = nullptr;  // [DP][KP] decoder weight x wscale, e4m3 (fp8 mode)
     float wscale = 1.f;         // power-of-two scale of d_WdP8
+    uint8_t* d_WeS8 = nullptr;  // [KP][DP] encoder weight / sd x escale, e4m3 (fp8 mode, k_prep)
+    float* d_escale = nullptr;  // [2] the step's power-of-two scale of d_WeS8 and its inverse (k_enc_scale)
+    float wemax = 0.f;          // max |W_enc| (frozen), the scale's bound
     float* d_WdT_f = nullptr;   // [KP][DP] decoder weight transposed
     __bf16* d_WdT_b = nullptr;
 

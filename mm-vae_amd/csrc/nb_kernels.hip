@@ -46,13 +46,48 @@ struct NBGrads {
 
 
 // =======================================================================================
+// k_enc_scale (fp8 mode) — the power-of-two scale of this step's e4m3 encoder image W / sd:
+// amax(W / sd) <= max|W| / min_g sd_g, so scale = 2^floor(log2(448 / bound)) keeps every
+// scaled value inside the e4m3 range (448); [0] = scale, [1] = 1 / scale (the accumulator's).
+// =======================================================================================
+__global__ __launch_bounds__(1024) void k_enc_scale(const float* __restrict__ lsd, int D, float wmax,
+                                                   float* __restrict__ escale) {
+    // min_g sd_g = softplus(min_g ln_x_sd_g) + 1e-4 (softplus is increasing): a plain min over
+    // the genes, loads issued eight at a time per thread (independent accumulators)
+    __shared__ float red[16];
+    float m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = INFINITY;
+    for (int g0 = threadIdx.x; g0 < D; g0 += 8 * 1024) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int g = g0 + i * 1024;
+            if (g < D) m[i] = fminf(m[i], lsd[g]);
+        }
+    }
+    float v = fminf(fminf(fminf(m[0], m[1]), fminf(m[2], m[3])), fminf(fminf(m[4], m[5]), fminf(m[6], m[7])));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 16; ++i) v = fminf(v, red[i]);
+        const float bound = wmax / (softplus_acc(v) + 1e-4f);
+        const float sc = bound > 0.f ? exp2f(floorf(log2f(448.f / bound))) : 1.f;
+        escale[0] = sc;
+        escale[1] = 1.f / sc;
+    }
+}
+
+// =======================================================================================
 // k_prep — per-gene constants (nb.hh:408-410 softplus(ln_x_sd)+eps, nb.hh:440 bias terms,
 // nb.hh:458 nu_dec bias - nu_bias) and the encoder's dense mean term
 // mvec[k] = sum_g x_mean_g / (softplus(ln_x_sd_g) + 1e-4) * W_enc[k, g].
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, const float* __restrict__ WeP_f,
                                               float* __restrict__ WeS_f, __bf16* __restrict__ WeS_b,
-                                              float* __restrict__ mvecp, StageCopy scp) {
+                                              float* __restrict__ mvecp, StageCopy scp, uint8_t* __restrict__ WeS8,
+                                              const float* __restrict__ escale) {
     stage_copy_part(scp);
     // grid (genes / 256, KP / 8): every y-slice packs 8 latent rows of the scaled encoder weight
     // and writes its block's partial of mvec (mvec_partial; summed by k_latent_fwd)
@@ -90,6 +125,8 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
         if (in) {  // bf16 image: hi plane, and the x3 mode's lo plane KP * DP elements after it
             if (WeS_b) put_op<X3>(WeS_b, (int)((int64_t)k * d.DP + g), d.KP * d.DP, ws);
             else WeS_f[(int64_t)k * d.DP + g] = ws;
+            // fp8 mode: the forward GEMM's e4m3 image (the bf16 one stays for the backward)
+            if (WeS8) WeS8[(int64_t)k * d.DP + g] = to_t<uint8_t>(ws * escale[0]);
         }
         mp[kk] = xmv * ws;  // x_mean_g / sd_g * W_enc[k, g]
     }
@@ -115,13 +152,13 @@ template <class P, int KP, bool SB = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                  const int32_t* __restrict__ toff,
                                                  const typename Elem<P>::type* __restrict__ WeS, int64_t wplane, Dims d,
-                                                 float* __restrict__ hpart) {
+                                                 float* __restrict__ hpart, const float* __restrict__ oscale) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
     using Fr = typename M::frag;
     constexpr bool X = IsX3<P>::value;
     constexpr int NPL = X ? 2 : 1;                 // operand planes (x3: hi + lo)
-    constexpr int XS = sizeof(T) == 2 ? 80 : 68;   // x tile row stride (elements): conflict-free
+    constexpr int XS = sizeof(T) == 4 ? 68 : 80;   // x tile row stride (elements): conflict-free
     constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
     constexpr int STB = KP * RB;
     constexpr int XT = 16 * XS;                    // elements of one x tile plane
@@ -242,11 +279,13 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
         }
         return;
     }
+    // fp8 mode: the e4m3 weight image carries the step's power-of-two scale (k_enc_scale)
+    const float osc = IsF8<P>::value ? oscale[1] : 1.f;
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            hpart[((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * KP + 16 * lb + (lane & 15)] = acc[lb][r];
+            hpart[((int64_t)sp * d.Bpad + row0 + 4 * (lane >> 4) + r) * KP + 16 * lb + (lane & 15)] = acc[lb][r] * osc;
 }
 
 // =======================================================================================
@@ -2031,6 +2070,14 @@ hipError_t nb_prepare_frozen(Engine* e) {
         float amax = 0.f;
         for (float v : w) amax = std::max(amax, std::fabs(v));
         e->wscale = amax > 0.f ? std::exp2(std::floor(std::log2(448.f / amax))) : 1.f;
+        // max |W_enc| (frozen): the bound behind the encoder image's per-step scale (k_enc_scale)
+        std::vector<float> we((size_t)(e->D * e->KE));
+        er = hipMemcpyAsync(we.data(), e->pfrz(e->fz_enc_w), sizeof(float) * we.size(), hipMemcpyDeviceToHost, e->stream);
+        if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+        if (er != hipSuccess) return er;
+        float wmax = 0.f;
+        for (float v : we) wmax = std::max(wmax, std::fabs(v));
+        e->wemax = wmax;
         hipLaunchKernelGGL(k_pack_w8, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, e->stream,
                            e->pfrz(e->fz_dec_w), (int)e->D, (int)e->DP, (int)e->KD, (int)e->KP, e->wscale, e->d_WdP8);
     }
@@ -2063,7 +2110,7 @@ template <class P, int KP>
 static size_t enc_fwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int NPL = IsX3<P>::value ? 2 : 1;
-    constexpr int XS = sizeof(T) == 2 ? 80 : 68;
+    constexpr int XS = sizeof(T) == 4 ? 68 : 80;
     constexpr bool SB = EncSB<P>::value;
     constexpr int NB = SB ? 1 : 2;
     return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, NB * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
@@ -2074,12 +2121,18 @@ template <class P> static const typename Elem<P>::type* op_img(const float* f, c
     if constexpr (sizeof(typename Elem<P>::type) == 2) return b;
     else return f;
 }
+// the encoder forward's scaled weight image: f32, bf16 planes, or the fp8 mode's e4m3 bytes
+template <class P> static const typename Elem<P>::type* enc_img(const Engine* e) {
+    if constexpr (IsF8<P>::value) return e->d_WeS8;
+    else return op_img<P>(e->d_WeS_f, e->d_WeS_b);
+}
 template <class P, int KP>
 static void enc_fwd_run(Engine* e, const Dims& d, float* hpart, hipStream_t st) {
     constexpr int NW = EncNW<P>::value;
     hipLaunchKernelGGL((k_enc_fwd<P, KP, EncSB<P>::value, NW>), dim3(d.nrb * 4 / NW * d.nsE), dim3(64 * NW),
                        (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
-                       e->d_seg, e->d_toff, op_img<P>(e->d_WeS_f, e->d_WeS_b), (int64_t)e->KP * e->DP, d, hpart);
+                       e->d_seg, e->d_toff, enc_img<P>(e), (int64_t)e->KP * e->DP, d, hpart,
+                       (const float*)e->d_escale);
 }
 // encoder backward operands: dh^T planes and the staged W (f32 in the x3 mode)
 template <class P> static const typename WEnc<P>::type* enc_w(Engine* e) {
@@ -2146,7 +2199,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
     {
         ScopedTimer tm(e, "k_enc_fwd");
-        enc_fwd_run<PB, KP>(e, d, e->d_hpart, st);
+        enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);  // fp8 mode: the e4m3 encoder GEMM (PM = F8)
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
@@ -2285,9 +2338,15 @@ hipError_t nb_prep(Engine* e, int64_t B, int64_t n_total, float beta) {
     const Dims d = nb_dims(e, B, n_total, beta);
     const NBPtrs P = nb_ptrs(e);
     const bool bf = e->cfg.dtype != MMVAE_DTYPE_F32;  // bf16 planes (bf16, x3)
+    const bool f8 = e->cfg.dtype == MMVAE_DTYPE_FP8;
+    if (f8) {
+        ScopedTimer tm(e, "k_enc_scale");
+        hipLaunchKernelGGL(k_enc_scale, dim3(1), dim3(1024), 0, e->stream, P.lsd, (int)e->D, e->wemax, e->d_escale);
+    }
     ScopedTimer tm(e, "k_prep");
     hipLaunchKernelGGL(k_prep, dim3((d.DP + 255) / 256, d.KP / 8), dim3(256), 0, e->stream, P, d, e->d_gene, e->d_WeP_f,
-                       e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, stage_copy_args(e));
+                       e->d_WeS_f, bf ? e->d_WeS_b : nullptr, e->d_mvec, stage_copy_args(e),
+                       f8 ? e->d_WeS8 : nullptr, (const float*)e->d_escale);
     return hipGetLastError();
 }
 
@@ -2306,7 +2365,7 @@ hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta
 template <class PM, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     hipStream_t st = e->stream;
-    enc_fwd_run<typename Bf16If8<PM>::type, KP>(e, d, e->d_hpart, st);
+    enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
     hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
                        e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, e->d_ss,
                        e->d_lat,
@@ -2328,6 +2387,11 @@ hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
 
 // ---- encoder kernels shared with the vMF engine (vmf_kernels.hip) ----------------------
 hipError_t enc_forward_launch(Engine* e, const Dims& d, float* hpart) {
+    if (e->cfg.dtype == MMVAE_DTYPE_FP8) {  // BASELINE configs[4]: the encoder GEMM on e4m3 too
+        if (e->KP == 32) enc_fwd_run<F8, 32>(e, d, hpart, e->stream);
+        else enc_fwd_run<F8, 64>(e, d, hpart, e->stream);
+        return hipGetLastError();
+    }
     return dispatch_mode<false>(e, [&](auto p, auto kp) {
         enc_fwd_run<decltype(p), decltype(kp)::value>(e, d, hpart, e->stream);
         return hipGetLastError();

@@ -159,6 +159,8 @@ template <class P, int N = LTAB> struct Log1pTab {
                 if constexpr (IsX3<P>::value) {
                     const __bf16 h = bf_hi(v), l = bf_lo(v, h);
                     tab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+                } else if constexpr (IsF8<P>::value) {
+                    tab[i] = (uint32_t)to_t<uint8_t>(v);  // the e4m3 operand byte
                 } else {
                     tab[i] = __float_as_uint(v);
                 }
@@ -176,6 +178,8 @@ template <class P, int N = LTAB> struct Log1pTab {
                 if constexpr (IsX3<P>::value) {
                     t[idx] = __builtin_bit_cast(__bf16, (uint16_t)(v & 0xffffu));
                     t[idx + plane] = __builtin_bit_cast(__bf16, (uint16_t)(v >> 16));
+                } else if constexpr (IsF8<P>::value) {
+                    t[idx] = (uint8_t)v;
                 } else {
                     t[idx] = __uint_as_float(v);
                 }
@@ -186,7 +190,7 @@ template <class P, int N = LTAB> struct Log1pTab {
                     t[idx] = h;
                     t[idx + plane] = bf_lo(v, h);
                 } else {
-                    t[idx] = v;
+                    t[idx] = to_t<T>(v);
                 }
             }
         }

@@ -1,7 +1,9 @@
-"""The fp8 e4m3 mode (BASELINE configs[4], -m gpu): the decoder logit GEMM z W_dec^T of all
-three decoder passes on v_mfma_f32_16x16x32_fp8_fp8 (W_dec pre-scaled by a power of two to the
-top of the e4m3 range, z rounded to e4m3 as loaded, f32 accumulate); the encoder and dz GEMMs
-stay bf16.  SURVEY §8(d) allows 1e-2 relative ELBO for fp8.  Checked against the oracle's golden
+"""The fp8 e4m3 mode (BASELINE configs[4] "fp8 MFMA encoder/decoder", -m gpu): the decoder
+logit GEMM z W_dec^T of all three decoder passes and the encoder GEMM log1p(x) (W_enc / sd)^T on
+v_mfma_f32_16x16x32_fp8_fp8 (W_dec pre-scaled by a power of two to the top of the e4m3 range; the
+encoder image W_enc / sd re-scaled every step by the power of two k_enc_scale bounds; z and
+log1p(x) rounded to e4m3 as loaded / scattered; f32 accumulate); the backward (dz, encoder
+dh^T log1p(x)) GEMMs stay bf16.  SURVEY §8(d) allows 1e-2 relative ELBO for fp8.  Checked against the oracle's golden
 steps (every NB fixture) beside the bf16 mode's error, and at the configs[4] per-GPU shape
 (D = 30000, B = 8192, latent 64) against the fp32-accurate bf16x3 mode.  The error table is
 written to gpurun_out/fp8_accuracy.json.
@@ -34,8 +36,11 @@ def test_fp8_against_oracle_fixtures(path):
         want = float(z["s0/loss"])
         row[dtype] = {"loss_rel": abs(loss - want) / abs(want), "grad_rel": _grad_err(eng.grads(), params_of(z, "s0/grad/"))}
     TABLE[os.path.basename(path)] = row
-    assert row["fp8"]["loss_rel"] <= 1e-2, row
-    assert row["fp8"]["grad_rel"] <= 0.1, row
+    assert row["fp8"]["loss_rel"] <= 1e-2, row  # fp8 ELBO within 1e-2 rel
+    # gradients: documented, not parity.  With the encoder GEMM on e4m3 a tiny model's encoder
+    # output (a few genes' 3-mantissa-bit products, e.g. nb_k1: D = 30, K = 1) can lose most of
+    # its digits; the bound here only catches a broken scale (overflow / NaN, wrong unscale)
+    assert np.isfinite(row["fp8"]["grad_rel"]) and row["fp8"]["grad_rel"] <= 1.0, row
 
 
 def test_fp8_configs4_shape_against_x3():
@@ -62,3 +67,5 @@ def test_fp8_configs4_shape_against_x3():
     with open(os.path.join(root, "gpurun_out", "fp8_accuracy.json"), "w") as f:
         json.dump(TABLE, f, indent=1)
     assert row["fp8"]["loss_rel"] <= 1e-2, row
+    # at the shape the mode is for, gradients within 5 % (norm-relative) of the parity-grade mode
+    assert row["fp8"]["grad_rel"] <= 5e-2, row
