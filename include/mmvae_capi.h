@@ -47,8 +47,9 @@ enum { MMVAE_MODEL_NB = 0, MMVAE_MODEL_VMF = 1 };
  *           as lo*hi + hi*lo + hi*hi on the bf16 MFMA (relative product error <= ~2^-16), at a
  *           fraction of the f32 MFMA's cost — the parity-grade production mode.
  *   FP8     (NB only; BASELINE configs[4]) the decoder logit GEMM z W_dec^T of all three decoder
- *           passes on the fp8 e4m3 MFMA (W_dec scaled by a power of two to the top of the e4m3
- *           range, z converted as loaded, f32 accumulate); the encoder and dz GEMMs as BF16. */
+ *           passes and the encoder GEMM log1p(x) (W_enc / sd)^T on the fp8 e4m3 MFMA (W_dec scaled
+ *           once, W_enc / sd every step, by a power of two below the e4m3 range; z and log1p(x)
+ *           converted as loaded; f32 accumulate); the backward (dz, encoder) GEMMs as BF16. */
 enum { MMVAE_DTYPE_F32 = 0, MMVAE_DTYPE_BF16 = 1, MMVAE_DTYPE_BF16X3 = 2, MMVAE_DTYPE_FP8 = 3 };
 
 typedef struct mmvae_cfg {
