@@ -8,8 +8,11 @@ B, D, K = 4096, 20000, 64
 eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=os.environ.get("DTYPE", "bf16"), seed=1)
 eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
-for i in range(3):
-    eng.eval_loss(np.arange(B), 1.0, step_id=i)
+for i in range(3):  # UPDATE=1: the training instance (outputs invalid under stamps), else the eval one
+    if os.environ.get("UPDATE") == "1":
+        eng.step(np.arange(B), 1.0, step_id=i)
+    else:
+        eng.eval_loss(np.arange(B), 1.0, step_id=i)
 nsd = int(os.environ.get("NSD", "8"))
 NW = 8  # waves per pass-B workgroup (DEC_NW)
 nwg = (B // (16 * NW)) * nsd
