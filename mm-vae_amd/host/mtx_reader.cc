@@ -770,90 +770,165 @@ int mmvae_mtx_build_index(const char* mtx, const char* index_file) {
     using namespace mmvae_host;
     if (!mtx) return fail(MMVAE_E_ARG, "build_index: null path");
     const std::string idx = (index_file && index_file[0]) ? std::string(index_file) : std::string(mtx) + ".index";
-    std::vector<unsigned char> raw;
-    std::string err;
-    if (!read_whole(mtx, raw, err)) return fail(MMVAE_E_ARG, err);
-    std::vector<BgzfBlock> blocks;
-    if (raw.size() < 2 || raw[0] != 0x1f || raw[1] != 0x8b || !scan_bgzf(raw, blocks))
-        return fail(MMVAE_E_ARG, std::string("This file is not bgzipped: ") + mtx);
+    FILE* fp = std::fopen(mtx, "rb");
+    if (!fp) return fail(MMVAE_E_ARG, std::string("cannot open ") + mtx + ": " + std::strerror(errno));
+    {
+        unsigned char magic[2] = {0, 0};
+        const bool gz = std::fread(magic, 1, 2, fp) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        std::rewind(fp);
+        if (!gz) {
+            std::fclose(fp);
+            return fail(MMVAE_E_ARG, std::string("This file is not bgzipped: ") + mtx);
+        }
+    }
     {
         FILE* fe = std::fopen(idx.c_str(), "rb");  // mmutil_index.hh:152-155: an existing index is kept
         if (fe) {
             std::fclose(fe);
+            std::fclose(fp);
             return MMVAE_OK;
         }
     }
-    const size_t total = blocks.empty() ? 0 : blocks.back().out_off + blocks.back().out_len;
-    std::vector<char> text(total);
-    std::atomic<bool> ok{true};
-    parallel_for(default_threads(0), (int64_t)blocks.size(), [&](int, int64_t a, int64_t bnd) {
-        for (int64_t i = a; i < bnd; ++i) {
-            const BgzfBlock& k = blocks[(size_t)i];
-            if (!inflate_raw(raw.data() + k.in_off, k.in_len, text.data() + k.out_off, k.out_len)) ok = false;
-        }
-    });
-    if (!ok) return fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + mtx);
-    // uncompressed offset -> virtual offset (the block holding byte u; u at a block's end maps to
-    // the next non-empty block at offset 0)
-    std::vector<size_t> starts;
-    std::vector<size_t> addr;
-    for (const auto& b : blocks)
-        if (b.out_len > 0) {
-            starts.push_back(b.out_off);
-            addr.push_back(b.file_off);
-        }
-    size_t bi = 0;
-    auto voff = [&](size_t u) -> int64_t {
-        while (bi + 1 < starts.size() && starts[bi + 1] <= u) ++bi;
-        if (starts.empty() || u >= total) return (int64_t)((raw.size() - 28) << 16);  // EOF block
-        return (int64_t)((addr[bi] << 16) | (u - starts[bi]));
-    };
+    // Streamed window by window (64 MB of whole BGZF blocks, MMVAE_MTX_WINDOW to override), like
+    // the loader: peak memory is one window and its text, never the whole inflated file.
+    size_t WIN = (size_t)64 << 20;
+    if (const char* ev = std::getenv("MMVAE_MTX_WINDOW")) WIN = std::max<size_t>((size_t)std::atoll(ev), 4096);
+    const int threads = default_threads(0);
+    std::vector<unsigned char> cbuf;
+    std::vector<BgzfBlock> blocks;
+    std::vector<char> text;
+    std::string carry;           // the partial last line of the previous window
+    size_t have = 0;
+    size_t file_base = 0;        // file offset of cbuf[0]
+    size_t ubase = 0;            // uncompressed offset of the current window's first block
     int64_t rows = 0, cols = 0, nnz = 0;
-    bool have_header = false;
+    bool have_header = false, first = true;
     int64_t lineno = 0, last_col = 0, last_off = 0, first_off = 0;
     std::vector<std::pair<int64_t, int64_t>> map;
-    size_t pos = 0;
-    while (pos < total) {
-        const char* ls = text.data() + pos;
-        const char* le = static_cast<const char*>(std::memchr(ls, '\n', total - pos));
-        const size_t end = le ? (size_t)(le - text.data()) + 1 : total;
-        const char* lend = le ? le : text.data() + total;
-        const int64_t line_start_off = last_off;
-        last_off = voff(end);  // bgzf_tell after this line
-        pos = end;
-        if (lend == ls || ls[0] == '%') continue;
-        // fields
+    int rc = MMVAE_OK;
+    for (bool eof = false; !eof && rc == MMVAE_OK;) {
+        cbuf.resize(have + WIN);
+        const size_t r = std::fread(cbuf.data() + have, 1, WIN, fp);
+        have += r;
+        eof = r == 0;
+        size_t used = 0;
+        if (!scan_bgzf_window(cbuf.data(), have, blocks, used) || (first && blocks.empty() && have > 0 && eof)) {
+            rc = fail(MMVAE_E_ARG, std::string(first ? "This file is not bgzipped: " : "corrupt BGZF block in ") + mtx);
+            break;
+        }
+        first = false;
+        if (eof && used != have) {
+            rc = fail(MMVAE_E_ARG, std::string("truncated BGZF block at the end of ") + mtx);
+            break;
+        }
+        if (blocks.empty()) continue;
+        const size_t total = blocks.back().out_off + blocks.back().out_len;
+        text.resize(carry.size() + total);
+        std::memcpy(text.data(), carry.data(), carry.size());
+        std::atomic<bool> ok{true};
+        parallel_for(threads, (int64_t)blocks.size(), [&](int, int64_t a, int64_t bnd) {
+            for (int64_t i = a; i < bnd; ++i) {
+                const BgzfBlock& k = blocks[(size_t)i];
+                if (!inflate_raw(cbuf.data() + k.in_off, k.in_len, text.data() + carry.size() + k.out_off, k.out_len))
+                    ok = false;
+            }
+        });
+        if (!ok) {
+            rc = fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + mtx);
+            break;
+        }
+        // uncompressed offset (absolute) -> virtual offset: the block holding byte u; u at a
+        // block's end maps to the next non-empty block at offset 0, past this window to the block
+        // that follows it (the EOF marker block at the end of the file)
+        std::vector<size_t> starts, addr;
+        for (const auto& b : blocks)
+            if (b.out_len > 0) {
+                starts.push_back(ubase + b.out_off);
+                addr.push_back(file_base + b.file_off);
+            }
+        const size_t wend = ubase + total;
+        const bool last_window = eof || (std::feof(fp) && used == have);
+        const size_t next_addr = last_window ? file_base + used - 28 : file_base + used;
+        size_t bi = 0;
+        auto voff = [&](size_t u) -> int64_t {
+            if (starts.empty() || u >= wend) return (int64_t)(next_addr << 16);
+            while (bi + 1 < starts.size() && starts[bi + 1] <= u) ++bi;
+            return (int64_t)((addr[bi] << 16) | (u - starts[bi]));
+        };
+        // complete lines of carry + this window's text; text index i is uncompressed offset
+        // ubase - carry.size() + i
+        const size_t tbase = ubase - carry.size();
+        size_t nl = text.size();
+        while (nl > 0 && text[nl - 1] != '\n') --nl;
+        size_t pos = 0;
+        while (pos < nl && rc == MMVAE_OK) {
+            const char* ls = text.data() + pos;
+            const char* le = static_cast<const char*>(std::memchr(ls, '\n', nl - pos));
+            const size_t end = (size_t)(le - text.data()) + 1;
+            const int64_t line_start_off = last_off;
+            last_off = voff(tbase + end);  // bgzf_tell after this line
+            pos = end;
+            if (le == ls || ls[0] == '%') continue;
+            int64_t f[3];
+            int nf = 0;
+            const char* p = ls;
+            while (p < le && nf < 3) {
+                while (p < le && is_ws(*p)) ++p;
+                const char* q = p;
+                while (q < le && !is_ws(*q)) ++q;
+                if (q > p) f[nf++] = parse_int(p, q);
+                p = q;
+            }
+            if (!have_header) {
+                if (nf < 3) continue;
+                rows = f[0];
+                cols = f[1];
+                nnz = f[2];
+                have_header = true;
+                first_off = last_off;  // eval_after_header: tell after the size line (:56-64)
+                continue;
+            }
+            if (nf < 3) continue;
+            const int64_t col = f[1] - 1;
+            if (lineno == 0) {
+                last_col = col;
+                map.push_back({col, first_off});
+            }
+            if (col != last_col) {
+                if (col < last_col) rc = fail(MMVAE_E_ARG, std::string("MTX must be sorted by columns: ") + mtx);
+                map.push_back({col, line_start_off});
+                last_col = col;
+            }
+            ++lineno;
+        }
+        carry.assign(text.data() + nl, text.size() - nl);
+        ubase = wend;
+        std::memmove(cbuf.data(), cbuf.data() + used, have - used);
+        file_base += used;
+        have -= used;
+    }
+    std::fclose(fp);
+    if (rc != MMVAE_OK) return rc;
+    if (!carry.empty()) {  // a last line without its newline (not written by bgzip'd mmutil files)
         int64_t f[3];
         int nf = 0;
-        const char* p = ls;
-        while (p < lend && nf < 3) {
-            while (p < lend && is_ws(*p)) ++p;
+        const char* p = carry.data();
+        const char* le = p + carry.size();
+        while (p < le && nf < 3) {
+            while (p < le && is_ws(*p)) ++p;
             const char* q = p;
-            while (q < lend && !is_ws(*q)) ++q;
+            while (q < le && !is_ws(*q)) ++q;
             if (q > p) f[nf++] = parse_int(p, q);
             p = q;
         }
-        if (!have_header) {
-            if (nf < 3) continue;
-            rows = f[0];
-            cols = f[1];
-            nnz = f[2];
-            have_header = true;
-            first_off = last_off;  // eval_after_header: tell after the size line (:56-64)
-            continue;
+        if (have_header && nf >= 3 && carry[0] != '%') {
+            const int64_t col = f[1] - 1;
+            if (lineno == 0) map.push_back({col, first_off});
+            else if (col != last_col) {
+                if (col < last_col) return fail(MMVAE_E_ARG, std::string("MTX must be sorted by columns: ") + mtx);
+                map.push_back({col, last_off});
+            }
         }
-        if (nf < 3) continue;
-        const int64_t col = f[1] - 1;
-        if (lineno == 0) {
-            last_col = col;
-            map.push_back({col, first_off});
-        }
-        if (col != last_col) {
-            if (col < last_col) return fail(MMVAE_E_ARG, std::string("MTX must be sorted by columns: ") + mtx);
-            map.push_back({col, line_start_off});
-            last_col = col;
-        }
-        ++lineno;
     }
     (void)rows;
     (void)nnz;

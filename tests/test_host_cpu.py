@@ -253,7 +253,12 @@ def _line_at(raw, voff):
     return data[off:].split(b"\n", 1)[0]
 
 
-def test_index_builder_matches_restatement_and_seeks(tmp_path, data):
+@pytest.mark.parametrize("window", [None, "4096", "70000"])
+def test_index_builder_matches_restatement_and_seeks(tmp_path, data, monkeypatch, window):
+    """The index is streamed window by window (MMVAE_MTX_WINDOW: a few BGZF blocks per window, so
+    lines and block boundaries straddle windows); every window size gives the restated index."""
+    if window:
+        monkeypatch.setenv("MMVAE_MTX_WINDOW", window)
     rp, col, val, D = data
     raw = bgzf_compress(mtx_text(rp, col, val, D))  # ~ a few BGZF blocks, column-sorted
     p = tmp_path / "x.mtx.gz"
@@ -287,7 +292,11 @@ def test_index_of_engine_writer_and_ones_file(tmp_path, data):
     # the auto covariate file and its index (nb_vae_main.cc:68-73)
     ones = str(tmp_path / "o.covar.mtx.gz")
     host.mtx_write_ones(ones, 200000)
-    host.mtx_build_index(ones)
+    os.environ["MMVAE_MTX_WINDOW"] = "100000"  # several windows over the ones file
+    try:
+        host.mtx_build_index(ones)
+    finally:
+        del os.environ["MMVAE_MTX_WINDOW"]
     v = host.mtx_read_index(ones + ".index")
     raw1 = open(ones, "rb").read()
     assert v.size == 200000 and len(_bgzf_blocks(raw1)) > 3
