@@ -14,6 +14,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libmmvae.so"))
+if os.environ.get("MMVAE_LIB"):  # diagnostics: an alternative in-tree build (tools/build_variant.sh)
+    LIB_PATH = os.path.abspath(os.environ["MMVAE_LIB"])
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "include", "mmvae_capi.h"))
 
 MODEL_NB, MODEL_VMF = 0, 1
