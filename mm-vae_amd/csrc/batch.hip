@@ -33,7 +33,8 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
                                                       int NT, int cap, int32_t* __restrict__ toff,
                                                       uint2* __restrict__ ents, int dbg,
                                                       const float2* __restrict__ dotw, const float* __restrict__ Wne,
-                                                      int H, int D, float* __restrict__ rowdots) {
+                                                      int H, int D, float* __restrict__ rowdots,
+                                                      const StepScalars* __restrict__ ss, int64_t* ticket_out) {
     extern __shared__ __attribute__((aligned(16))) char csm[];
     uint2* stage = reinterpret_cast<uint2*>(csm);                      // [cap]
     int32_t* tw = reinterpret_cast<int32_t*>(csm + 8 * (size_t)cap);    // [NT + 1] tile offsets
@@ -43,6 +44,9 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     __shared__ int32_t scarry;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
     const int wb = blockIdx.x, b = wb * 16 + w;
+    // the staged block is copied (the prep kernel ran before this one): release its slot to the
+    // host with one system-scope vector store of the step's ticket
+    if (wb == 0 && tid == 0) __hip_atomic_store(ticket_out, ss->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int64_t c = cells[b];
     const int64_t s = rowptr[c];
     const int rn = (int)(rowptr[c + 1] - s);  // the row's nonzeros (rt[NT])
@@ -205,7 +209,7 @@ hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const flo
     hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
                        e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
                        [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(), dotw, Wne,
-                       (int)e->H, (int)e->D, rowdots);
+                       (int)e->H, (int)e->D, rowdots, e->d_ss, e->d_ticket);
     return hipGetLastError();
 }
 

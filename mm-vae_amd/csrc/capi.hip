@@ -450,6 +450,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // loss / total norm: written by the kernels straight into mapped pinned memory (no readback copy)
     HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(e, hipHostGetDevicePointer((void**)&e->d_out, e->h_out_pin, 0));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_ticket, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(e->h_ticket, 0, 64);
+    HIPCHK(e, hipHostGetDevicePointer((void**)&e->d_ticket, e->h_ticket, 0));
     if (e->wide) HIPCHK(e, wide_create(e));
     for (auto& sl : e->slots2) HIPCHK(e, hipEventRecord(sl.ev, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -486,6 +489,7 @@ int mmvae_destroy(mmvae_h e) {
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block
         if (b) hipFree(b);
     if (e->h_out_pin) hipHostFree(e->h_out_pin);
+    if (e->h_ticket) hipHostFree(e->h_ticket);
     for (auto ev : e->event_pool) hipEventDestroy(ev);
     for (auto& p : e->pending) {
         hipEventDestroy(p.a);
@@ -792,10 +796,36 @@ static hipError_t build_lists(Engine* e, int64_t B) {
 // host half of a step's staging: rows (+ balancing permutation, list segments) into the pinned
 // block; the one H2D copy of the block is issued by the caller (stage_copy), inside a step graph
 // when one is used
+// until the device has written back staging ticket t (spin on the mapped word; a drained stream
+// also frees the slot)
+static hipError_t wait_ticket(Engine* e, int64_t t) {
+    const volatile int64_t* p = e->h_ticket;
+    for (uint32_t i = 1; *p < t; ++i) {
+        if ((i & 63) == 0) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return q;
+        }
+        __builtin_ia32_pause();
+    }
+    return hipSuccess;
+}
+
+// the slot's step: a fused-path step is tracked by its staging ticket, others by the slot's event
+static hipError_t release_slot(Engine* e, bool ticketed) {
+    auto& sl = e->slots2[e->cur_slot];
+    sl.ticket = ticketed ? e->h_ss->ticket : 0;
+    return ticketed ? hipSuccess : hipEventRecord(sl.ev, e->stream);
+}
+
 static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
     // the other pinned slot: wait until the step staged from it two steps ago is done with it
     use_slot(e, e->cur_slot ^ 1);
-    HIPCHK(e, hipEventSynchronize(e->ev_staged));
+    {
+        const auto& sl = e->slots2[e->cur_slot];
+        HIPCHK(e, sl.ticket > 0 ? wait_ticket(e, sl.ticket) : hipEventSynchronize(e->ev_staged));
+    }
+    e->h_ss->ticket = ++e->ticket_seq;  // (only the fused path's k_batch_lists writes it back)
     for (int64_t j = 0; j < B; ++j) {
         int64_t r = j;
         if (ridx) {
@@ -970,7 +1000,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         rc = enqueue_run(e, a, n_total);
         if (rc) return rc;
     }
-    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));  // this slot's block is free after this step
+    HIPCHK(e, release_slot(e, !e->wide));  // this slot's block is free after this step's copy
     if (a->update) {
         e->adam_step += 1;
         e->have_grads = true;
@@ -1020,11 +1050,11 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
         if (e->frozen_dirty) HIPCHK(e, wide_prepare_frozen(e));
         if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
         HIPCHK(e, wide_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));  // + the staged copy
-        HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+        HIPCHK(e, release_slot(e, false));
     } else {
     if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));  // + the staged copy
     else HIPCHK(e, vmf_prep(e, B, B, 1.f));
-    HIPCHK(e, hipEventRecord(e->ev_staged, e->stream));
+    HIPCHK(e, release_slot(e, true));
     HIPCHK(e, build_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
     if (e->cfg.model == MMVAE_MODEL_VMF) HIPCHK(e, vmf_encode(e, B, e->d_tmp, e->d_tmp + e->Bpad * e->K));

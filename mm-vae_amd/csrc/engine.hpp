@@ -33,7 +33,7 @@ struct ParamSlot {
 struct StepScalars {
     int64_t step_id, row_offset;
     float lr_bc1, inv_sqrt_bc2;
-    int64_t pad;
+    int64_t ticket;  // the staging ticket: k_batch_lists writes it back once the block is copied
 };
 
 // launch shape of a captured step graph: replayed while every field matches
@@ -166,6 +166,11 @@ struct Engine {
     int n_lat_wg = 1;                // latent kernels' workgroups
     int64_t klp_off = 0;             // offset of KL partials inside d_lossp
     hipEvent_t ev_staged = nullptr;  // the current slot's: its last step is done with the pinned block
+    // staging tickets (fused path): the step's k_batch_lists stores the ticket of the block it
+    // follows into h_ticket (mapped, coherent) — stream order puts it after the prep kernel's copy
+    int64_t* h_ticket = nullptr;
+    int64_t* d_ticket = nullptr;
+    int64_t ticket_seq = 0;
     // double-buffered pinned staging: the host fills slot s while the step staged from slot s ^ 1
     // runs; h_cells_pin / h_seg_pin / h_perm_pin / h_ss / h_eps_pin / ev_staged view the current
     // slot.  A step graph copies from its slot's block, so each slot has its own graph.
@@ -173,6 +178,9 @@ struct Engine {
         int64_t* block = nullptr;  // cells | seg | perm | StepScalars
         float* eps = nullptr;
         hipEvent_t ev = nullptr;
+        // > 0: the slot is free once the device has written back this ticket (*h_ticket, mapped
+        // memory, no event marker between steps); 0: free after ev (wide path, upload)
+        int64_t ticket = 0;
         // captured step graphs of this slot by launch shape (the training loop alternates an eval
         // forward and bootstrap updates, and the last batch of an epoch is ragged)
         std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;
