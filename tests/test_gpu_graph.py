@@ -202,3 +202,34 @@ def test_graph_recaptured_after_frozen_reload_fp8():
     assert res[0][0] == res[1][0]
     for k in res[0][1]:
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_pipelined_steps_equal_synced_steps(graph):
+    """Unsynced steps (the bench / training-loop pattern: the host stages step n + 1 into the other
+    pinned slot while step n runs, and reuses a slot once the device has written back its staging
+    ticket) must train exactly as steps synced one by one: a slot released too early would hand a
+    later batch's cells to an earlier step.  Eval passes and bootstrap ridx interleave as in the
+    reference loop (mmvae_alg.hh:277-311)."""
+    D, K, B, N = 20000, 64, 1024, 20000
+    rng = np.random.default_rng(3)
+    plan = []
+    for i in range(24):
+        cells = rng.integers(0, N, B)
+        if i % 4 == 0:
+            plan.append(("eval", cells, None))
+        else:
+            plan.append(("step", cells, rng.integers(0, B, B)))
+    res = []
+    for sync in (True, False):
+        from mmvae_amd import Engine
+        eng = Engine(D=D, K=K, max_batch=B, dtype="bf16x3", seed=9)
+        eng.synth_csr(N, lib_size=2000.0, seed=4)
+        eng.init_params(seed=13)
+        eng.graph(graph)
+        for i, (kind, cells, ridx) in enumerate(plan):
+            eng.run(cells, 0.7, ridx=ridx, update=kind == "step", step_id=500 + i, sync=sync)
+        eng.sync()
+        res.append(eng.params())
+    for k in res[0]:
+        assert np.array_equal(res[0][k], res[1][k]), k
