@@ -63,7 +63,7 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
             x[u] = val[s + j];
         }
     };
-    if (!(dbg & 512)) load(0, rn);
+    if (!dbg_bit(dbg, 512)) load(0, rn);
     // the row's tile pointers: all loads of a group of 8 issued before the first LDS store
     {
         const int32_t* src = rtp + c * (int64_t)(NT + 1);
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     for (int t = tid; t <= NT; t += 1024) toff[(int64_t)wb * (NT + 1) + t] = tw[t];
     for (int i = tid; i < 16 * NT; i += 1024) sbase[i] += tw[i % NT];
     __syncthreads();
-    if (dbg & 512) return;  // diagnostic: index phase only (lists invalid)
+    if (dbg_bit(dbg, 512)) return;  // diagnostic: index phase only (lists invalid)
     const int64_t base = seg[wb];
     const int32_t* sb = sbase + w * NT;
     const int32_t* rt = srt + w * (NT + 1);
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     // while the current chunk streams out
     // NB (dotw != null): the raw-count dots of depth and nu_enc (nb.hh:448, 498) ride along,
     // every entry of the row passes through this wave exactly once
-    const bool dots = dotw != nullptr && !(dbg & 4096);  // 4096: diagnostic, dots skipped
+    const bool dots = dotw != nullptr && !dbg_bit(dbg, 4096);  // 4096: diagnostic, dots skipped
     float dpre = 0.f, dhn[HMAX];
 #pragma unroll
     for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
         const int tC = tB < NT ? chunk_end(tB) : NT;
         if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
         uint2* dst = ents + base + cb;
-        if (!(dbg & 8192)) {  // 8192: diagnostic, stream-out skipped (lists invalid)
+        if (!dbg_bit(dbg, 8192)) {  // 8192: diagnostic, stream-out skipped (lists invalid)
             // 16-byte stores (two entries each) from the first 16-byte-aligned entry on
             const int head = (cnt > 0) ? (int)((base + cb) & 1) : 0, n2 = (cnt - head) >> 1;
             if (tid == 0 && head) dst[0] = stage[0];

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
     constexpr int XPL = NB * XT;                   // x plane stride (elements)
     using Tab = Log1pTab<P, SB ? 512 : LTAB>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint64_t t_entry = (d.dbg & 32) ? stamp_now() : 0;
+    const uint64_t t_entry = dbg_bit(d.dbg, 32) ? stamp_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsE, rb = blockIdx.x / d.nsE;
     const int row0 = rb * 16 * NW + 16 * w;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
         scatter(first, xt);
     }
     lds_barrier();
-    const bool stamps = (d.dbg & 32) != 0;
+    const bool stamps = dbg_bit(d.dbg, 32);
     uint64_t sa = 0, sb = 0, sc = 0, sd = 0, tp = stamps ? stamp_now() : 0;
     auto lap = [&](uint64_t& acc_) {
         if (stamps) {
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     const int k = lane;
     const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // first cell of this wave (4 cells per wave)
     // diagnostic (MMVAE_DBG & 2048): realtime stamps of the phases into P.dbg_out (outputs invalid)
-    const bool rts = (d.dbg & 2048) != 0 && mode == 0;
+    const bool rts = dbg_bit(d.dbg, 2048) && mode == 0;
     uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto mark = [&](int i_) {  // constant index at every call: rt_ stays in registers
         if (rts) rt_[i_] = realtime_now();
@@ -554,7 +554,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     constexpr int WR = 16 * J;               // rows per wave
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint64_t rt_entry = (d.dbg & 256) ? realtime_now() : 0;
+    const uint64_t rt_entry = dbg_bit(d.dbg, 256) ? realtime_now() : 0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int sp = blockIdx.x % d.nsA, rbw = blockIdx.x / d.nsA;
     const int row0 = rbw * 4 * WR + WR * w;
@@ -619,7 +619,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         if (threadIdx.x < 64) reinterpret_cast<float4*>(stg + buf * STB + NPL * WIMG)[threadIdx.x] = G;
     };
     // diagnostic (MMVAE_DBG & 256): per-wave phase cycles into slabC (outputs invalid)
-    const bool stamps = (d.dbg & 256) != 0;
+    const bool stamps = dbg_bit(d.dbg, 256);
     uint64_t st_[3] = {0, 0, 0}, tp_ = 0;
     auto lap = [&](int i_) {
         if (stamps) {
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     lds_barrier();  // the first tile's entry loads stay in flight
 
     // diagnostic (MMVAE_DBG & 64): per-wave phase cycles into dzp (outputs invalid)
-    const bool stamps = (d.dbg & 64) != 0;
+    const bool stamps = dbg_bit(d.dbg, 64);
     const uint64_t rt0 = stamps ? realtime_now() : 0;
     uint64_t st_[7] = {0, 0, 0, 0, 0, 0, 0}, tp_ = stamps ? stamp_now() : 0;
     auto lap = [&](int i_) {
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         wave_sync();
         lap(0);
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
-        if (!(d.dbg & 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
+        if (!dbg_bit(d.dbg, 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
             const float p = q2[r * PS + gl];
             const float mu = fmaf(p, rs_[0], 1e-4f);
@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 }
             }
         };
-        if (!(d.dbg & 2)) {
+        if (!dbg_bit(d.dbg, 2)) {
             if (row0 + 16 <= d.B && 64 * t + 64 <= d.D) epilogue(std::false_type{});
             else epilogue(std::true_type{});
         }
@@ -1274,7 +1274,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         lap(3);
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
-        if (!LOSS && !(d.dbg & 4))
+        if (!LOSS && !dbg_bit(d.dbg, 4))
 #pragma unroll
             for (int s = 0; s < GK; ++s) {
                 Fr a1;
@@ -1306,8 +1306,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         // tile's single barrier; buffer b is rewritten only after the next barrier, which every
         // wave reaches after its combine reads of b
         if (DB && t + 1 < t1) stage_store(buf ^ 1);
-        if (!(d.dbg & 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
-        if (!LOSS && !(d.dbg & 16384))        // 16384: diagnostic, slab stores skipped
+        if (!dbg_bit(d.dbg, 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
+        if (!LOSS && !dbg_bit(d.dbg, 16384))        // 16384: diagnostic, slab stores skipped
         for (int i = threadIdx.x; i < (NW / 4) * nq * 64; i += NTH) {  // per 64-row slab block h
             const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
             const float* ph = pb + 4 * h * nq * 64;
@@ -1406,7 +1406,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     auto sG = [&](int i) { return sG0 + i * (LAT_CELLS * 68); };
     float* cimg = sG0 + 2 * LAT_CELLS * 68;  // [nce + ncd + 1][LAT_CELLS * 68]
     // diagnostic (MMVAE_DBG & 1024): realtime stamps of the phases into slabC (outputs invalid)
-    const bool rts = (d.dbg & 1024) != 0;
+    const bool rts = dbg_bit(d.dbg, 1024);
     uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto mark = [&](int i_) {  // constant index at every call: rt_ stays in registers
         if (rts) rt_[i_] = realtime_now();
@@ -1973,7 +1973,11 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.rowx_stride = 2 + (int)e->H;
     d.Ncells = (int)e->N;
     d.nmv = (int)((e->DP + 255) / 256);
+#ifdef MMVAE_DIAG
     { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
+#else
+    d.dbg = 0;
+#endif
     d.relu = e->cfg.relu != 0;
     d.inv_wscale = 1.f / e->wscale;
     dims_hidden(e, d);

@@ -25,7 +25,7 @@ struct Dims {
     int rowx_stride;  // 2 + H : pre, lnorm2, hnu[H]
     int Ncells;       // dataset rows: row Ncells of the per-cell tile index is the empty row
     int nmv;          // mvec partial blocks (256 genes each) written by the prep kernel
-    int dbg;          // diagnostic ablation bits (MMVAE_DBG env; 0 in normal runs)
+    int dbg;          // diagnostic ablation bits (MMVAE_DBG env, diagnostic builds only; dbg_bit)
     int relu;         // ReLU on the frozen encoder's output h (nb.hh:345-346, vmf.hh:351-352)
     float inv_wscale; // fp8 mode: 1 / the power-of-two scale of the e4m3 decoder weight (else 1)
     // frozen hidden layers (nb.hh:331-379, vmf.hh:338-385): KE = rows of the big encoder GEMM
@@ -43,6 +43,14 @@ struct Dims {
 // Widths and the layout of the per-workgroup partials of the latent-head backward (k_latent_bwd
 // / k_vlatent_bwd -> k_grad_small): dWm [K][E] | dWl [K][E] | dbm [K] | dbl [K] | dWce [K][C] |
 // colsum dh0 [KE] | the NB overdispersion block (nb: 2RH + 2R + H + 1, vMF: 0)
+// Diagnostic ablation / stamp bits (MMVAE_DBG): live only in diagnostic builds (-DMMVAE_DIAG,
+// tools/build_variant.sh diag "-DMMVAE_DIAG"); product builds fold every test to false.
+#ifdef MMVAE_DIAG
+MMVAE_HOSTDEV bool dbg_bit(int dbg, int bit) { return (dbg & bit) != 0; }
+#else
+MMVAE_HOSTDEV constexpr bool dbg_bit(int, int) { return false; }
+#endif
+
 MMVAE_HOSTDEV int small_len(int K, int E, int KE, int C, int nbx) { return 2 * K * E + 2 * K + K * C + KE + nbx; }
 
 // The step's staged block (cells | segments | permutation | step scalars, pinned host memory)
