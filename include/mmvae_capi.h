@@ -208,7 +208,11 @@ int mmvae_debug_poison(mmvae_h h, int32_t byte);
  * loss readback) once per launch shape (batch size, n_total, beta, update, injected eps) and
  * replay it; the step's variable scalars (Philox step / row offset, Adam's bias corrections)
  * travel in the staged copy.  Results are identical to eager launches.  Not used while kernel
- * timing is on or a communicator with world > 1 is attached (those steps run eagerly).
+ * timing is on.  With an active communicator (world > 1, or a 1-rank one under
+ * MMVAE_FORCE_COMM=1) steps run eagerly unless MMVAE_COMM_GRAPH=1 was set at mmvae_comm_init:
+ * then the RCCL bucket all-reduces are captured into the step graph, after the ranks agree
+ * (ncclMin over every rank's capture outcome) that every one of them captured; if any rank's
+ * capture failed, all of them run that handle's communicator steps eagerly from then on.
  * graph_stats: captures and replays so far. */
 int mmvae_graph_enable(mmvae_h h, int32_t on);
 int mmvae_graph_stats(mmvae_h h, int64_t* captures, int64_t* replays);

@@ -208,7 +208,12 @@ hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const flo
     const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - 256 - tab) / 8) & ~1;  // 256: static LDS
     hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
                        e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
-                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(), dotw, Wne,
+#ifdef MMVAE_DIAG
+                       [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(),
+#else
+                       0,
+#endif
+                       dotw, Wne,
                        (int)e->H, (int)e->D, rowdots, e->d_ss, e->d_ticket);
     return hipGetLastError();
 }

@@ -385,6 +385,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, hipMemset(e->d_m, 0, sizeof(float) * e->P_reg));
     HIPCHK(e, hipMemset(e->d_v, 0, sizeof(float) * e->P_reg));
     HIPCHK(e, hipMemset(e->d_frozen, 0, sizeof(float) * e->P_frz));
+    // the fused path's operand images and per-step workspace: a wide-path handle (wide.hip) has
+    // its own dense buffers and never reads these (they grow with K, E, B and C x D)
+    if (!e->wide) {
     HIPCHK(e, dalloc(&e->d_WeP_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WeP_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WdP_f, KP * DP));
@@ -398,6 +401,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_WdT_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_WeS_f, KP * DP));
     HIPCHK(e, dalloc(&e->d_WeS_b, 2 * KP * DP));  // hi + lo planes (x3 mode)
+    }
     // per-step host->device staging in ONE pinned block and ONE device block, so a step issues a
     // single H2D copy (each copy is a ~4.5 us blit on the stream):  cells int64 [Bp] |
     // list segments int64 [Bp/16 + 1] | balancing permutation int32 [Bp]
@@ -415,8 +419,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         HIPCHK(e, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     }
     use_slot(e, 0);
-    HIPCHK(e, hipMalloc(&e->d_toff, sizeof(int32_t) * (Bp / 16) * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_eps, Bp * (e->K + e->R)));
+    if (!e->wide) {
+    HIPCHK(e, hipMalloc(&e->d_toff, sizeof(int32_t) * (Bp / 16) * (e->NT + 1)));
     HIPCHK(e, dalloc(&e->d_gene, 10 * DP));
     HIPCHK(e, dalloc(&e->d_mvec, ((DP + 255) / 256) * KP));  // per-256-gene-block partials of mvec
     HIPCHK(e, dalloc(&e->d_rowx, Bp * (2 + e->H)));
@@ -438,15 +443,16 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_lossp, e->klp_off + e->n_lat_wg));
     HIPCHK(e, dalloc(&e->d_small, (int64_t)e->n_lat_wg * SMALL));
     HIPCHK(e, dalloc(&e->d_smallg, 128));
+    }
     // clip-norm partials: k_sumsq's 256 blocks, or one per gradient-kernel block (NB world 1)
     HIPCHK(e, dalloc(&e->d_sumsq, 256 + (e->D + 31) / 32 + (SMALL + 2 * e->K + 31) / 32 + 1));
-    {
+    if (!e->wide) {
         int64_t nch = 0;
         for (int l = 0; l < e->nce + e->ncd; ++l) nch = std::max<int64_t>(nch, e->ch_off[l] + e->ch_in[l] * e->ch_out[l] + e->ch_out[l]);
         HIPCHK(e, dalloc(&e->d_chain, nch));
+        HIPCHK(e, dalloc(&e->d_rowv, Bp));
+        HIPCHK(e, dalloc(&e->d_vk, 8));
     }
-    HIPCHK(e, dalloc(&e->d_rowv, Bp));
-    HIPCHK(e, dalloc(&e->d_vk, 8));
     // loss / total norm: written by the kernels straight into mapped pinned memory (no readback copy)
     HIPCHK(e, hipHostMalloc((void**)&e->h_out_pin, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(e, hipHostGetDevicePointer((void**)&e->d_out, e->h_out_pin, 0));
@@ -483,7 +489,7 @@ int mmvae_destroy(mmvae_h e) {
                     e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
-                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8, e->d_WeS8, e->d_escale};
+                    e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8, e->d_WeS8, e->d_escale, e->d_flag};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {(void*)e->d_toff, (void*)e->d_ents})  // d_seg / d_perm live in d_cells' block
@@ -793,9 +799,14 @@ static hipError_t build_lists(Engine* e, int64_t B) {
                              e->preg("nu_encoding.weight"), e->d_rowxp);
 }
 
-// host half of a step's staging: rows (+ balancing permutation, list segments) into the pinned
-// block; the one H2D copy of the block is issued by the caller (stage_copy), inside a step graph
-// when one is used
+static inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#else
+    std::this_thread::yield();
+#endif
+}
+
 // until the device has written back staging ticket t (spin on the mapped word; a drained stream
 // also frees the slot)
 static hipError_t wait_ticket(Engine* e, int64_t t) {
@@ -806,7 +817,7 @@ static hipError_t wait_ticket(Engine* e, int64_t t) {
             if (q == hipSuccess) break;
             if (q != hipErrorNotReady) return q;
         }
-        __builtin_ia32_pause();
+        cpu_relax();
     }
     return hipSuccess;
 }
@@ -818,6 +829,9 @@ static hipError_t release_slot(Engine* e, bool ticketed) {
     return ticketed ? hipSuccess : hipEventRecord(sl.ev, e->stream);
 }
 
+// host half of a step's staging: rows (+ balancing permutation, list segments) into the pinned
+// block; the one H2D copy of the block is issued by the caller (stage_copy), inside a step graph
+// when one is used
 static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, int64_t B, bool balance = false) {
     // the other pinned slot: wait until the step staged from it two steps ago is done with it
     use_slot(e, e->cur_slot ^ 1);
@@ -901,7 +915,7 @@ static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
     else HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
     }
     if (a->update) {
-        if (e->comm && e->world > 1 && !e->grads_reduced) {
+        if (e->comm_active() && !e->grads_reduced) {
             ScopedTimer tm(e, "allreduce_grads");
             if (ncclAllReduce(e->d_grads, e->d_grads, (size_t)e->P_reg, ncclFloat, ncclSum, e->comm, e->stream) !=
                 ncclSuccess)
@@ -936,18 +950,20 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     // frozen operands are repacked eagerly, never inside a step graph
     if (e->frozen_dirty) HIPCHK(e, e->wide ? wide_prepare_frozen(e) : vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
     // one hipGraph per step: captured on the first step of a launch shape,
-    // replayed while the shape holds; not with timers or diagnostics.  With a communicator the
-    // graph holds the RCCL bucket all-reduces too: comm_bucket's event fork onto the comm stream
-    // and its join back are captured with them (MMVAE_COMM_GRAPH=0 keeps those steps eager; a
-    // failed capture falls back to eager launches for the handle's lifetime)
+    // replayed while the shape holds; not with timers or diagnostics.  Steps with an active
+    // communicator run eagerly unless MMVAE_COMM_GRAPH=1 was set at mmvae_comm_init: then the
+    // graph holds the RCCL bucket all-reduces too (comm_bucket's event fork onto the comm stream
+    // and its join back are captured with them).  Every rank takes the same capture decision
+    // (comm_capture_agree), and a failed capture falls back to eager launches for the
+    // handle's lifetime on every rank.
+#ifdef MMVAE_DIAG
     static const bool dbg_env = std::getenv("MMVAE_DBG") != nullptr;
-    static const bool comm_graph_env = [] {
-        const char* v = std::getenv("MMVAE_COMM_GRAPH");
-        return !(v && v[0] == '0');
-    }();
-    const bool with_comm = e->comm && e->world > 1;
+#else
+    constexpr bool dbg_env = false;
+#endif
+    const bool with_comm = e->comm_active();
     const bool use_graph = e->graph_on && !e->timing && !dbg_env &&
-                           (!with_comm || (comm_graph_env && !e->comm_graph_failed));
+                           (!with_comm || (e->comm_graph && !e->comm_graph_failed));
     if (use_graph) {
         GraphKey k;
         k.B = a->B;
@@ -975,10 +991,20 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
             hipError_t ie = hipSuccess;
             if (!crc && ce == hipSuccess) ie = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
             if (g) hipGraphDestroy(g);
-            if (with_comm && (crc || ce != hipSuccess || ie != hipSuccess)) {
-                // the communicator's calls did not capture: this step and the later ones with it
-                // run eagerly (nothing of the failed capture was executed)
+            bool comm_fail = false;
+            if (with_comm) {
+                // the ranks agree before any of them launches: a graph one rank captured while
+                // another fell back would pair a replayed collective with eager ones
+                const bool ok = !crc && ce == hipSuccess && ie == hipSuccess;
                 (void)hipGetLastError();
+                int agreed = 0;
+                HIPCHK(e, comm_capture_agree(e, ok, &agreed));
+                comm_fail = !agreed;
+            }
+            if (comm_fail) {
+                // the communicator's calls did not capture here or on another rank: this step and
+                // the later ones with it run eagerly (nothing of the capture was executed)
+                if (gx) hipGraphExecDestroy(gx);
                 e->comm_graph_failed = true;
                 gx = nullptr;
             } else {
@@ -1102,6 +1128,7 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
             ncclCommDestroy(e->comm);
             e->comm = nullptr;
         }
+        e->comm_force = false;
         e->rank = rank;
         e->world = world;
         return MMVAE_OK;
@@ -1116,6 +1143,8 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (r != ncclSuccess) FAIL(e, MMVAE_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     e->rank = rank;
     e->world = world;
+    e->comm_force = getenv_is("MMVAE_FORCE_COMM", "1");
+    e->comm_graph = getenv_is("MMVAE_COMM_GRAPH", "1");
     e->comm_graph_failed = false;
     if (!e->comm_stream) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
@@ -1132,7 +1161,7 @@ bool split_grads(const Engine* e) {
     // MMVAE_NO_OVERLAP=1: one all-reduce of the whole flat gradient on the main stream after the
     // backward (no comm-stream events) instead of the two overlapped buckets
     const char* no = std::getenv("MMVAE_NO_OVERLAP");
-    if (e->comm && e->world > 1) return !(no && no[0] == '1');
+    if (e->comm_active()) return !(no && no[0] == '1');
     const char* v = std::getenv("MMVAE_SPLIT_GRADS");
     return v && v[0] == '1';
 }
@@ -1164,7 +1193,15 @@ static void build_buckets(Engine* e) {
 }
 
 hipError_t comm_bucket(Engine* e, int b) {
-    if (!e->comm || e->world <= 1) return hipSuccess;
+    if (!e->comm_active()) return hipSuccess;
+    {
+        // test hook (MMVAE_TEST_COMM_CAPTURE_FAIL=1): the bucket refuses to enqueue while its
+        // stream is being captured, as a runtime whose RCCL cannot be captured would
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (getenv_is("MMVAE_TEST_COMM_CAPTURE_FAIL", "1") && hipStreamIsCapturing(e->stream, &cs) == hipSuccess &&
+            cs == hipStreamCaptureStatusActive)
+            return hipErrorStreamCaptureUnsupported;
+    }
     hipError_t er = hipEventRecord(e->ev_bucket[b], e->stream);
     if (er != hipSuccess) return er;
     er = hipStreamWaitEvent(e->comm_stream, e->ev_bucket[b], 0);
@@ -1183,12 +1220,31 @@ hipError_t comm_bucket(Engine* e, int b) {
     }
     return hipSuccess;
 }
+
+// every rank's capture outcome, min-reduced over the communicator (eager, outside any capture):
+// *agreed = 1 only when every rank captured its step graph
+hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed) {
+    if (!e->d_flag) {
+        hipError_t er = hipMalloc(&e->d_flag, sizeof(int32_t));
+        if (er != hipSuccess) return er;
+    }
+    const int32_t v = ok ? 1 : 0;
+    hipError_t er = hipMemcpyAsync(e->d_flag, &v, sizeof(v), hipMemcpyHostToDevice, e->stream);
+    if (er != hipSuccess) return er;
+    if (ncclAllReduce(e->d_flag, e->d_flag, 1, ncclInt32, ncclMin, e->comm, e->stream) != ncclSuccess)
+        return hipErrorUnknown;
+    int32_t r = 0;
+    er = hipMemcpyAsync(&r, e->d_flag, sizeof(r), hipMemcpyDeviceToHost, e->stream);
+    if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+    *agreed = r;
+    return er;
+}
 }  // namespace mmvae
 }  // extern "C++"
 
 int mmvae_comm_allreduce(mmvae_h e, float* values, int64_t n) {
     if (!e || !values || n < 0) FAIL(e, MMVAE_E_ARG, "comm_allreduce: bad arguments");
-    if (n == 0 || !e->comm || e->world <= 1) return MMVAE_OK;
+    if (n == 0 || !e->comm_active()) return MMVAE_OK;
     HIPCHK(e, hipSetDevice(e->device));
     if (!e->d_tmp_ar || e->n_tmp_ar < n) {
         if (e->d_tmp_ar) hipFree(e->d_tmp_ar);

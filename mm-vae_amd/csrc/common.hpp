@@ -447,6 +447,8 @@ MMVAE_DEV void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
     }
 }
 
+// the overdispersion noise's lanes: NU_LANE + r, disjoint from the latent lanes k < 2^31 at any K
+constexpr uint32_t NU_LANE = 0x80000000u;
 MMVAE_DEV float philox_normal(uint64_t seed, uint64_t step, uint64_t row, uint32_t k) {
     uint32_t c[4] = {(uint32_t)(k >> 1), (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)step,
                      (uint32_t)(step >> 32)};

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -13,6 +15,12 @@
 #include "common.hpp"
 
 namespace mmvae {
+
+// environment switch: `name` is set to exactly `value`
+inline bool getenv_is(const char* name, const char* value) {
+    const char* v = std::getenv(name);
+    return v && std::strcmp(v, value) == 0;
+}
 
 // Batch rows are padded to whole 128-row blocks: decoder pass B runs 128 rows per workgroup,
 // the other row-blocked kernels 64 (padding rows point at the dataset's empty row N).
@@ -189,11 +197,19 @@ struct Engine {
     int cur_slot = 0;
     float* d_tmp = nullptr;          // encode outputs
     float* d_tmp_ar = nullptr;       // host-value all-reduce staging
+    int32_t* d_flag = nullptr;       // the ranks' capture-agreement word (comm_capture_agree)
     int64_t n_tmp_ar = 0;
 
     // ---- comm ----
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    // MMVAE_FORCE_COMM=1 at mmvae_comm_init: a 1-rank communicator still runs the data-parallel
+    // exchange (buckets, flat all-reduce, their graph capture) — the one-GPU test of that path
+    bool comm_force = false;
+    // RCCL calls inside step graphs: opt in with MMVAE_COMM_GRAPH=1 (read at mmvae_comm_init)
+    bool comm_graph = false;
+    // the gradient exchange runs (a communicator of > 1 rank, or a forced 1-rank one)
+    bool comm_active() const { return comm && (world > 1 || comm_force); }
     // bucketed gradient all-reduce overlapped with the encoder backward:
     // bucket 0 = the decoder-side gene vectors (ready after decoder pass C), bucket 1 = the rest.
     // Each bucket is a list of contiguous [offset, count) ranges of the flat gradient.
@@ -268,6 +284,8 @@ bool split_grads(const Engine* e);
 // all-reduce gradient bucket b on the comm stream after the work queued so far on e->stream;
 // bucket 1 also makes e->stream wait for both buckets.  No-op without a communicator.
 hipError_t comm_bucket(Engine* e, int b);
+// min-reduce every rank's step-graph capture outcome (eager): *agreed = 1 iff all captured
+hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed);
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // vMF launchers (vmf_kernels.hip)

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
             if (b < d.B)
-                en = eps_in ? enp[c] : philox_normal(seed, step, row_offset + pb, 4096 + k);
+                en = eps_in ? enp[c] : philox_normal(seed, step, row_offset + pb, NU_LANE + k);
             const float zn = nm + en * expf(nlv / 2.f);
             L[d.LAT_NMEAN + k] = nm;
             L[d.LAT_AN + k] = an;
@@ -2144,11 +2144,6 @@ template <class P> static const typename WEnc<P>::type* enc_w(Engine* e) {
     else return e->d_WeP_f;
 }
 
-static bool getenv_is(const char* name, const char* value) {
-    const char* v = std::getenv(name);
-    return v && std::strcmp(v, value) == 0;
-}
-
 static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     DecPtrs Q;
     Q.lat = e->d_lat;
@@ -2284,7 +2279,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
     const int SMALL = small_len(d.K, d.E, d.KE, d.C, 2 * d.R * d.H + 2 * d.R + d.H + 1);
     const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + GG_GENES - 1) / GG_GENES;
-    const bool fuse_sq = !split && !(e->comm && e->world > 1);  // no all-reduce after these kernels
+    const bool fuse_sq = !split && !(e->comm_active());  // no all-reduce after these kernels
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
     {
@@ -2326,7 +2321,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     if (split) {
         hipError_t er = comm_bucket(e, 1);
         if (er != hipSuccess) return er;
-        e->grads_reduced = e->comm && e->world > 1;
+        e->grads_reduced = e->comm_active();
     } else if (fuse_sq) {
         e->sq_parts = gS + gG;
     }

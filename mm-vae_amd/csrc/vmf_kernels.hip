@@ -1201,7 +1201,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
                            e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
-    const bool fuse_sq = !split && !(e->comm && e->world > 1);
+    const bool fuse_sq = !split && !(e->comm_active());
     const int gS = 1 + (SMALL + 31) / 32, gG = (d.D + VGG_GENES - 1) / VGG_GENES;
     double* sqS = fuse_sq ? e->d_sumsq : nullptr;
     double* sqG = fuse_sq ? e->d_sumsq + gS : nullptr;
@@ -1229,7 +1229,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     if (split) {
         hipError_t er = comm_bucket(e, 1);
         if (er != hipSuccess) return er;
-        e->grads_reduced = e->comm && e->world > 1;
+        e->grads_reduced = e->comm_active();
     } else if (fuse_sq) {
         e->sq_parts = gS + gG;
     }

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void k_w_latent(WLat a) {
             const int64_t i = (int64_t)b * a.R + k;
             const float nm = a.NMr[i];
             const float nlv = fminf(fmaxf(a.NAr[i], -4.f), 4.f);
-            const float en = a.eps_in ? a.eps_in[(int64_t)a.B * a.K + i] : philox_normal(a.seed, step, grow, 4096 + k);
+            const float en = a.eps_in ? a.eps_in[(int64_t)a.B * a.K + i] : philox_normal(a.seed, step, grow, NU_LANE + k);
             a.En[i] = en;
             a.Zn[i] = nm + en * expf(nlv / 2.f);
             kl += 1.f + nlv - nm * nm - expf(nlv);

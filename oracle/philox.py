@@ -48,7 +48,12 @@ def philox_normal(seed, step, rows, ks):
 
 
 def nb_step_noise(seed, step, B, K, R=1, row_offset=0):
-    """The NB step's (eps_mu [B, K], eps_nu [B, R]): latent k keyed k, overdispersion r keyed 4096 + r
-    (nb_kernels.hip k_latent_fwd), row = row_offset + batch position."""
+    """The NB step's (eps_mu [B, K], eps_nu [B, R]): latent k keyed k, overdispersion r keyed
+    NU_LANE + r = 2^31 + r (common.hpp, nb_kernels.hip k_latent_fwd), row = row_offset + batch
+    position."""
     rows = row_offset + np.arange(B)
-    return philox_normal(seed, step, rows, np.arange(K)), philox_normal(seed, step, rows, 4096 + np.arange(R))
+    return (philox_normal(seed, step, rows, np.arange(K)),
+            philox_normal(seed, step, rows, NU_LANE + np.arange(R, dtype=np.uint64)))
+
+
+NU_LANE = 0x80000000

@@ -44,6 +44,8 @@ def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False):
     try:
         if no_overlap:
             os.environ["MMVAE_NO_OVERLAP"] = "1"
+        if graph:  # RCCL calls inside step graphs are opt-in (read at comm_init)
+            os.environ["MMVAE_COMM_GRAPH"] = "1"
         from mmvae_amd import Engine
         if rank == 0:
             uid = Engine.comm_unique_id()

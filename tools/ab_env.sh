@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an env knob: NB parity tests under the knob, then headline benches without / with it.
-# Usage: bash tools/r3_ab.sh TAG "VAR=value [VAR2=value]" [dtypes]
+# Usage: bash tools/ab_env.sh TAG "VAR=value [VAR2=value]" [dtypes]
 R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out; cd $R
 TAG=$1; KNOB=$2; DTS=${3:-"bf16x3 bf16"}
 env $KNOB timeout -k 10 400 python -u -m pytest tests/test_gpu_nb.py tests/test_gpu_tiling.py tests/test_gpu_graph.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG.test.log 2>&1
