@@ -865,11 +865,13 @@ struct DecNBLds {
     int swp, stp;       // one plane of the W / WdT images (bytes)
     // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'.
     // loss: the eval instance (no WdT stage, column partials, correction or pq tiles)
+    // no_wdt: the dz GEMM reads its W operand transposed from the logit GEMM's W image (the
+    // staggered x3 instance), so there is no WdT stage
     MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes, int eszw,
-                           bool loss = false) {
+                           bool loss = false, bool no_wdt = false) {
         const bool alias = planes == 2 && !loss;
         swp = 64 * KP * eszw;
-        stp = loss ? 0 : KP * 64 * esz;
+        stp = (loss || no_wdt) ? 0 : KP * 64 * esz;
         sw = planes * swp;
         st = planes * stp;
         sp = loss ? ((16 * NW * 4 + 15) / 16) * 4 : ((NW * nq * 64 * 4 + 15) / 16) * 4;
@@ -895,7 +897,9 @@ struct DecNBLds {
 // LOSS: the eval pass (mmvae_run update = 0) — the ELBO's likelihood terms only: the same
 // arithmetic for the loss, without the corrections, column partials, dz GEMMs and WdT stage
 // (the 8-wave loss instance fits two workgroups per CU: 128 VGPRs, ~60 KB of LDS in bf16)
-template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false>
+// SG: the staggered instance (x3, NW = 8, training): waves 4-7 run half a tile behind waves 0-3
+// (below), the W stage is double-buffered and serves the dz GEMM transposed (no WdT stage)
+template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false, bool SG = false>
 __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
@@ -936,7 +940,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const int S = d.tpsD + 1;
     const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS);
+    static_assert(!SG || (X && DB && NW == 8 && !LOSS), "the staggered pass B is the x3 training instance");
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
@@ -968,21 +973,26 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     }
     const float ainv = F8M ? d.inv_wscale : 1.f;  // logit accumulator unscale (fp8 W_dec)
     // ---- staging of the decoder tile, its gene records and the WdT tile ----
-    DualStage<64, RBW, NTH, X> wreg;
+    // SG: the stage is loaded and stored by the lagging half (waves 4-7, 256 threads) only
+    constexpr int NST = SG ? NTH / 2 : NTH;
+    const bool lag = SG && w >= NW / 2;
+    const bool stager = !SG || lag;
+    const int stid = (int)threadIdx.x & (NST - 1);
+    DualStage<64, RBW, NST, X> wreg;
     DualStage<KP, RBT, NTH, X> treg;
     float4 greg = float4{0.f, 0.f, 0.f, 0.f};
     const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
         wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
-        if constexpr (!LOSS) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
-        if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
+        if constexpr (!LOSS && !SG) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
+        if (stid < 64) greg = grec[64 * t + stid];
     };
     auto stage_store = [&](int b_) {
         wreg.store(wst + b_ * L.sw, L.swp);
-        if constexpr (!LOSS) treg.store(tst + b_ * L.st, L.stp);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + threadIdx.x] = greg;
+        if constexpr (!LOSS && !SG) treg.store(tst + b_ * L.st, L.stp);
+        if (stid < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + stid] = greg;
     };
-    stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
+    if (stager) stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
     // row log-sum-exp (log2 units) from pass A's split partials, 4 threads per row; split 0
     // also publishes it for pass C
     {
@@ -1063,7 +1073,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     ListEntries pend;
     if (t0 < t1) {
         pend.fetch(Q.ents, segw, toffl, 0, lane);
-        stage_store(0);
+        if (stager) stage_store(0);
     }
     lds_barrier();  // the first tile's entry loads stay in flight
 
@@ -1078,14 +1088,22 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             tp_ = tn;
         }
     };
-    for (int t = t0; t < t1; ++t) {
-        const int tl = t - t0;
-        stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
-        const int buf = DB ? (tl & 1) : 0;
-        const char* wsb = wst + buf * L.sw;
-        const char* tsb = tst + buf * L.st;
-        const float4* gsb = gst + 64 * buf;
-        float* pb = part + buf * L.sp;
+    // one tile's LDS stage / column-partial buffers
+    struct TileCtx {
+        int t;
+        const char *wsb, *tsb;
+        const float4* gsb;
+        float* pb;
+    };
+    auto ctx = [&](int t) {
+        const int buf = DB ? ((t - t0) & 1) : 0;
+        return TileCtx{t, wst + buf * L.sw, tst + buf * L.st, gst + 64 * buf, part + buf * L.sp};
+    };
+    // ---- phases L + S of tile c.t: logits -> p, sparse pass, next tile's entry prefetch ----
+    auto phase_ls = [&](const TileCtx& c) {
+        const int t = c.t, tl = t - t0;
+        const char* wsb = c.wsb;
+        const float4* gsb = c.gsb;
         // ---- 1. logits -> p (into the wave's LDS p tile) ----
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
@@ -1098,12 +1116,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             float wcd[CM];
             wcd[0] = g4.z;
 #pragma unroll
-            for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
+            for (int c2 = 1; c2 < CM; ++c2) wcd[c2] = (c2 < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c2] : 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float lg = fmaf(acc[r], ainv, g4.x);
 #pragma unroll
-                for (int c = 0; c < CM; ++c) lg = fmaf(crow2[r >> 1][c][r & 1], wcd[c], lg);
+                for (int c2 = 0; c2 < CM; ++c2) lg = fmaf(crow2[r >> 1][c2][r & 1], wcd[c2], lg);
                 q2[(4 * (lane >> 4) + r) * PS + gl] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
             }
         }
@@ -1149,6 +1167,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
         pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
         lap(2);
+    };
+    // ---- phases E + Z of tile c.t: dense epilogue, dz GEMM ----
+    auto phase_ez = [&](const TileCtx& c) {
+        const int t = c.t;
+        const float4* gsb = c.gsb;
+        float* pb = c.pb;
         // ---- 3. dense epilogue in the owner lanes ----
         // MASK: some of the wave's rows (last row block) or the tile's genes (last tile) are
         // padding; the common case runs without the validity products.
@@ -1170,7 +1194,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 const float gvf = gv ? 1.f : 0.f;
                 f2 cs1[1 + CM], csdu = splat2(0.f), csduz[RM];
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) cs1[c] = splat2(0.f);
+                for (int c2 = 0; c2 < 1 + CM; ++c2) cs1[c2] = splat2(0.f);
 #pragma unroll
                 for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
                 // the block's corrections first (x3: this block's pq overwrites them below)
@@ -1224,7 +1248,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                     Eacc2[h] += pq;
                     cs1[0] = fma2(wv2[h], pq, cs1[0]);
 #pragma unroll
-                    for (int c = 0; c < CM; ++c) cs1[1 + c] = fma2(wc2[h][c], pq, cs1[1 + c]);
+                    for (int c2 = 0; c2 < CM; ++c2) cs1[1 + c2] = fma2(wc2[h][c2], pq, cs1[1 + c2]);
                     csdu += du;
 #pragma unroll
                     for (int qq = 0; qq < RM; ++qq) {
@@ -1247,10 +1271,10 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                                                           csduz[0].x + csduz[0].y);
                 } else {
 #pragma unroll
-                    for (int c = 0; c < 1 + CM; ++c)
-                        if (c <= C) {
-                            const float v = sum_rowgroups(cs1[c].x + cs1[c].y);
-                            if (lane < 16) pw[c * 64] = v;
+                    for (int c2 = 0; c2 < 1 + CM; ++c2)
+                        if (c2 <= C) {
+                            const float v = sum_rowgroups(cs1[c2].x + cs1[c2].y);
+                            if (lane < 16) pw[c2 * 64] = v;
                         }
                     {
                         const float v = sum_rowgroups(csdu.x + csdu.y);
@@ -1289,9 +1313,13 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
-                    const Fr bw = M::load(reinterpret_cast<const T*>(
-                        tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
-                        L.stp / (int)sizeof(T));
+                    Fr bw;
+                    if constexpr (SG)  // transposed from the logit GEMM's W image (genes = k)
+                        bw = TrFrag<P, RBW>::load(c.wsb, s * M::KSTEP, 16 * lb, L.swp);
+                    else
+                        bw = M::load(reinterpret_cast<const T*>(
+                            c.tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                            L.stp / (int)sizeof(T));
                     dzA[lb] = M::mma(a1, bw, dzA[lb]);
                     dzP[lb] = M::mma(a2, bw, dzP[lb]);
                 }
@@ -1301,26 +1329,75 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         }
         lap(4);
-        // ---- 5. combine the waves' column partials -> slab (fixed order) ----
-        // double-buffered (NW = 8): the next tile's stage goes into the other buffer before the
-        // tile's single barrier; buffer b is rewritten only after the next barrier, which every
-        // wave reaches after its combine reads of b
-        if (DB && t + 1 < t1) stage_store(buf ^ 1);
-        if (!dbg_bit(d.dbg, 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
-        if (!LOSS && !dbg_bit(d.dbg, 16384))        // 16384: diagnostic, slab stores skipped
-        for (int i = threadIdx.x; i < (NW / 4) * nq * 64; i += NTH) {  // per 64-row slab block h
+    };
+    // ---- 5. the waves' column partials of tile c.t -> slab (fixed order), by threads
+    //      [th0, th0 + nth) ----
+    auto combine = [&](const TileCtx& c, int th0, int nth) {
+        if (LOSS || dbg_bit(d.dbg, 16384)) return;  // 16384: diagnostic, slab stores skipped
+        for (int i = (int)threadIdx.x - th0; i < (NW / 4) * nq * 64; i += nth) {  // per 64-row slab block h
             const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
-            const float* ph = pb + 4 * h * nq * 64;
+            const float* ph = c.pb + 4 * h * nq * 64;
             const float v = ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
                             ph[(3 * nq + q) * 64 + g];
-            Q.slabB[((int64_t)(rbw * (NW / 4) + h) * nq + q) * d.DP + 64 * t + g] = v;
+            Q.slabB[((int64_t)(rbw * (NW / 4) + h) * nq + q) * d.DP + 64 * c.t + g] = v;
         }
-        lap(5);
-        if (!DB) {
-            if (t + 1 < t1) stage_store(0);
-            lds_barrier();
+    };
+    if constexpr (SG) {
+        // Staggered pass B (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves w and w + 4
+        // share a SIMD, so with both halves in the same phase the logit / dz MFMAs of one wave
+        // meet the other's at the same time and the epilogue VALU likewise.  Waves 4-7 lag half a
+        // tile: between barriers B(t-1) and B(t) the lead runs L S E Z of tile t while the lag
+        // runs E Z of tile t-1 and L S of tile t.  Hazards, with the stage double-buffered:
+        //  * stage(t+1) is written by the lag after its E Z(t-1) and L S(t), before B(t): every
+        //    read of that buffer (stage(t-1)) is done — the lead's before B(t-1), the lag's
+        //    earlier in its own program;
+        //  * column partials of tile t (buffer t & 1) are complete at B(t+1) (the lag's E(t));
+        //    the lead combines them after B(t+1), before its own E(t+2) rewrites the buffer,
+        //    and the lag's E(t+2) follows B(t+2).
+        for (int t = t0; t < t1; ++t) {
+            const int tl = t - t0;
+            if (lag) {
+                stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits
+                if (t > t0) phase_ez(ctx(t - 1));
+                phase_ls(ctx(t));
+                if (t + 1 < t1) stage_store((tl + 1) & 1);
+                lds_barrier();
+            } else {
+                phase_ls(ctx(t));
+                phase_ez(ctx(t));
+                lds_barrier();
+                if (t > t0) combine(ctx(t - 1), 0, NTH / 2);
+            }
         }
-        lap(6);
+        if (t0 < t1) {
+            if (lag) {
+                phase_ez(ctx(t1 - 1));
+                lds_barrier();
+            } else {
+                lds_barrier();
+                combine(ctx(t1 - 1), 0, NTH / 2);
+            }
+        }
+    } else {
+        for (int t = t0; t < t1; ++t) {
+            const int tl = t - t0;
+            stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
+            const TileCtx c = ctx(t);
+            phase_ls(c);
+            phase_ez(c);
+            // double-buffered (NW = 8): the next tile's stage goes into the other buffer before the
+            // tile's single barrier; buffer b is rewritten only after the next barrier, which every
+            // wave reaches after its combine reads of b
+            if (DB && t + 1 < t1) stage_store((tl & 1) ^ 1);
+            if (!dbg_bit(d.dbg, 32768)) lds_barrier();  // 32768: diagnostic, barrier skipped (outputs invalid)
+            combine(c, 0, NTH);
+            lap(5);
+            if (!DB) {
+                if (t + 1 < t1) stage_store(0);
+                lds_barrier();
+            }
+            lap(6);
+        }
     }
     if (stamps) {
         vm_wait_all();
@@ -2224,11 +2301,23 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
         else hipLaunchKernelGGL((k_dec_lse<PM, KP, CMAX>), gdecA, dim3(256), ldsA, st, Q, d);
     }
+    // x3 training, MMVAE_DEC_SG=1: the staggered instance (waves 4-7 half a tile behind).
+    // Measured slower than the lock-step one (x3 k_dec_nb 264.9 vs 249.0 us at the headline
+    // shape), so it is a diagnostic variant, not the default
+    static const bool sg_on = getenv_is("MMVAE_DEC_SG", "1");
+    const size_t ldsSG = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, 2, NPL, (int)sizeof(TL), false, true).bytes;
+    const bool use_sg = X && nwB == 8 && sg_on && ldsSG <= 160 * 1024;
     auto launch_b = [&](auto loss_c) {
         constexpr bool LS = decltype(loss_c)::value;
         if (nwB == 8) {
             const size_t lds = LS ? DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL, (int)sizeof(TL), true).bytes
                                   : ldsB8;
+            if constexpr (X && !LS) {
+                if (use_sg) {
+                    hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, true, PM, false, true>), gdecB, dim3(512), ldsSG, st, Q, d);
+                    return;
+                }
+            }
             if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM, LS>), gdecB, dim3(512), lds, st, Q, d);
         } else if (small_cr)
             hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM, LS>), gdecB, dim3(256),

@@ -463,13 +463,17 @@ struct RegStage {
     static constexpr int NC = (CH + NTH - 1) / NTH;     // chunks per thread (1, 2 or 4)
     static constexpr bool PART = CH < NTH;              // fewer chunks than threads: the rest idle
     static_assert(NC >= 1 && NC <= 4 && (PART || CH % NTH == 0), "RegStage: 1..4 whole chunks per thread");
+    static_assert((NTH & (NTH - 1)) == 0, "RegStage: a power-of-two thread group");
+    // the staging threads are NTH consecutive threads of the block (a whole block, or one
+    // aligned half of it): thread index within the group
+    static MMVAE_DEV int tid() { return (int)threadIdx.x & (NTH - 1); }
     u32x4 v0, v1, v2, v3;
     MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
-        const int c = PART ? min((int)threadIdx.x, CH - 1) : (int)threadIdx.x + NTH * i;
+        const int c = PART ? min(tid(), CH - 1) : tid() + NTH * i;
         return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
     }
     MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
-        const int c = (int)threadIdx.x + NTH * i;
+        const int c = tid() + NTH * i;
         if (PART && c >= CH) return;
         *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
     }
