@@ -486,9 +486,11 @@ def main():
                                    label="BASELINE configs[3] per GPU: NB 1M x 30k, 4096 of the 32k global batch, bf16x3"))
             lines.append(secondary(mmvae_amd, "nb", 30000, 64, 8192, "fp8", 1000000, args.lib_size,
                                    label="BASELINE configs[4] per GPU: NB 1M x 30k, 8192 of the 65k global batch, fp8"))
-            # the wide path (shapes beyond the fused kernels: here --mean_latent 128), exact f32 MFMA
-            lines.append(secondary(mmvae_amd, "nb", 20000, 128, 4096, "f32", 100000, args.lib_size, steps=20,
-                                   label="wide path: NB 100k x 20k, --mean_latent 128 (dense batch + generic GEMMs)"))
+            # the wide path (shapes beyond the fused kernels: here --mean_latent 128): its GEMMs on
+            # the bf16 MFMA in the x3 (fp32-accurate) mode, and the exact f32 MFMA line beside it
+            for dt_ in ("bf16x3", "f32"):
+                lines.append(secondary(mmvae_amd, "nb", 20000, 128, 4096, dt_, 100000, args.lib_size, steps=20,
+                                       label=f"wide path: NB 100k x 20k, --mean_latent 128 (dense batch), {dt_}"))
             out["lines"] = lines
     print(json.dumps(out), flush=True)
     if world > 1:

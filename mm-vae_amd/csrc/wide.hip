@@ -7,15 +7,17 @@
 // Layout: the step's B cells are densified into HBM as a row-major [B, D] f32 block (the
 // reference's own dense batch, mmvae_io.hh:208-245; 328 MB at B = 4096, D = 20k — HBM has room),
 // and the step is the reference's op sequence (oracle/nb_oracle.py, oracle/vmf_oracle.py) on:
-//   * one generic GEMM on the exact f32 MFMA (v_mfma_f32_16x16x4_f32, 64 x 64 tiles of four
-//     waves, 16-deep k chunks staged through LDS, strided operands so every transpose of the
-//     forward / backward is a stride swap), split-K into fixed-order partials when the tile grid
-//     would not fill the 256 CUs — deterministic, like every reduction of the fused path;
-//   * fused per-row kernels (softmax + NB likelihood + its gradient in three sweeps of a row;
-//     the vMF row normalisations and their backward);
-//   * per-gene kernels (the encoder's x_mean / ln_x_sd gradients from column sums).
-// Column sums over the batch are GEMMs with a ones operand.  Every operand stays f32 (the dtype
-// of the handle is ignored: this path is parity-grade in every mode).
+//   * the big gene GEMMs (encoder / decoder, forward and both backward transposes) on the bf16
+//     MFMA in the handle's mode — x3 split operands (fp32-accurate) or bf16 — with the operands
+//     converted as they are staged (k_gemm_mf); the encoder's input normalisation applied as the
+//     raw batch is loaded; the decoder's covariate Linear and both biases in the logit GEMM's
+//     epilogue.  f32 handles and small or broadcast shapes use the exact f32 MFMA (k_gemm).
+//     Split-K partials are reduced in a fixed order — deterministic, like the fused path;
+//   * per-row kernels with the fused path's element arithmetic (NB: softmax + likelihood + its
+//     gradient in three sweeps of a row; vMF: the row normalisations and their backward), the
+//     small row Linears (depth, nu_enc, nu_dec, the covariate part) inline;
+//   * fixed-order column reductions (k_colred) for every gene-vector gradient: one read of a
+//     dense block serves all the sums over it.
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -42,23 +44,46 @@ struct GemmOp {
     float* C = nullptr;
     int64_t scm = 0, scn = 0;
     float alpha = 1.f;
-    const float* bias = nullptr;  // [N]
+    const float* bias = nullptr;   // [N]
+    const float* bias2 = nullptr;  // [N], a second bias (the decoder's mu_bias, nb.hh:437-441)
+    // rank-nc term sum_c ca[m * lca + c] * cw[n * lcw + c] (the covariate Linear of a decoder,
+    // nb.hh:436 / vmf.hh:287, folded into the logit GEMM's epilogue; nc <= 8)
+    const float* ca = nullptr;
+    const float* cw = nullptr;
+    const float* cbias = nullptr;  // that Linear's bias [N]
+    int64_t lca = 0, lcw = 0;
+    int nc = 0;
     int act = 0;                  // 1: ReLU
     int accumulate = 0;           // C += result
 };
 
 static constexpr int GT = 64, GK = 16, GLD = GT + 4;
 
-MMVAE_DEV void gemm_epilogue(const GemmOp& g, int m, int n, float acc) {
-    float v = g.alpha * acc;
-    if (g.bias) v += g.bias[n];
+// the column's constant: every bias of output column n, summed in a fixed order
+MMVAE_DEV float gemm_colc(const GemmOp& g, int n) {
+    float c = 0.f;
+    if (g.bias) c += g.bias[n];
+    if (g.bias2) c += g.bias2[n];
+    if (g.cbias) c += g.cbias[n];
+    return c;
+}
+// alpha acc + colc + the rank-nc term (cwn: column n's nc weights), ReLU, store / accumulate
+MMVAE_DEV void gemm_store(const GemmOp& g, int m, int n, float acc, float colc, const float* cwn) {
+    float v = fmaf(g.alpha, acc, colc);
+    for (int c = 0; c < g.nc; ++c) v = fmaf(g.ca[(int64_t)m * g.lca + c], cwn[c], v);
     if (g.act == 1) v = fmaxf(v, 0.f);
     float* c = g.C + (int64_t)m * g.scm + (int64_t)n * g.scn;
     *c = g.accumulate ? *c + v : v;
 }
+MMVAE_DEV void gemm_epilogue(const GemmOp& g, int m, int n, float acc) {
+    float cwn[8];
+    for (int c = 0; c < g.nc; ++c) cwn[c] = g.cw[(int64_t)n * g.lcw + c];
+    gemm_store(g, m, n, acc, gemm_colc(g, n), cwn);
+}
 
 // grid (tiles over N, tiles over M, splits); split s covers k chunks [s * cps, (s + 1) * cps)
-// and, with more than one split, stores its raw sums into ws[s][M][N] for k_gemm_reduce
+// and, with more than one split, stores its raw sums into ws[s][M][N] for k_gemm_reduce.
+// The exact f32 MFMA path (f32 handles, and every shape too small or too strided for k_gemm_mf).
 __global__ __launch_bounds__(256) void k_gemm(GemmOp g, int cps, float* __restrict__ ws) {
     __shared__ float As[GK][GLD], Bs[GK][GLD];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -141,6 +166,196 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmOp g, int S, const floa
 }
 
 // =======================================================================================
+// k_gemm_mf — the big GEMMs of the wide path on the bf16 MFMA (v_mfma_f32_16x16x32_bf16):
+// one pass on bf16 operands (bf16 / fp8 handles) or the split "x3" products (bf16x3 handles,
+// hi + lo planes, lo*hi + hi*lo + hi*hi: the fp32-accurate mode of the fused kernels).  The
+// operands stay f32 in HBM; each 64 x 32 (rows x k) slice is loaded as float4 along its
+// contiguous dimension, rounded to the bf16 planes in registers and stored into a
+// double-buffered LDS image, one barrier per 32-deep k chunk (the next chunk's loads are in
+// flight under the current chunk's MFMAs).  A slice whose k is contiguous in HBM is imaged
+// [rows][k] and read with ds_read_b128; one whose rows are contiguous is imaged [k][rows] and
+// read transposed (ds_read_b64_tr_b16, tr_frag) — so both transposes of every Linear's forward
+// and backward run from the same kernel.  Workgroup: 64 x 64 outputs, four waves of 32 x 32.
+// AT: the encoder's input transform on A (nb.hh:408-410, vmf.hh:253-257) applied as A is
+// loaded, A(m, k) = (log1p(x) rs[m] - x_mean[k]) / sd[k] from the raw dense batch x, so the
+// normalised input block is never stored.
+// =======================================================================================
+struct GemmX {
+    const float* xm = nullptr;   // x_mean [K]
+    const float* isd = nullptr;  // 1 / (softplus(ln_x_sd) + eps) [K]
+    const float* rs = nullptr;   // per-row scale of log1p(x) (vMF: 1 / |log1p(x_b)|), null: 1
+};
+
+MMVAE_DEV float enc_in(float v, float rs, float xm, float isd) { return (log1p_pos(v) * rs - xm) * isd; }
+// the same with libm log1pf (the f32 handles' input block, the ln_x_sd gradient's column sum)
+MMVAE_DEV float log1p_acc(float v) {
+    // integer counts: 1 + v is exact and v_log's error is ~1 ulp of the result; others libm
+    if (v == 0.f) return 0.f;
+    if (v >= 1.f && v < 16777216.f && v == floorf(v)) return flog(1.f + v);
+    return log1pf(v);
+}
+MMVAE_DEV float enc_in_acc(float v, float rs, float xm, float isd) { return (log1p_acc(v) * rs - xm) * isd; }
+
+template <class P>
+struct MfOperand {
+    static constexpr bool X = IsX3<P>::value;
+    // one 64-row x 32-k slice: KF (k contiguous in HBM) -> image [64][32] (64-byte rows);
+    // otherwise -> image [32][64] (128-byte rows); four f32 per thread per half
+    template <bool KF>
+    static MMVAE_DEV void load(const float* base, int64_t srow, int64_t sk, int r0, int nrow, int k0, int K, bool vec,
+                               float4 (&v)[2]) {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if constexpr (KF) {
+                const int r = (t >> 3) + 32 * i, k = k0 + (t & 7) * 4;
+                const int64_t o = (int64_t)(r0 + r) * srow + k;
+                if (r0 + r >= nrow) {
+                    v[i] = float4{0.f, 0.f, 0.f, 0.f};
+                } else if (vec && k + 3 < K) {
+                    v[i] = *reinterpret_cast<const float4*>(base + o);
+                } else {
+                    v[i].x = k < K ? base[o] : 0.f;
+                    v[i].y = k + 1 < K ? base[o + 1] : 0.f;
+                    v[i].z = k + 2 < K ? base[o + 2] : 0.f;
+                    v[i].w = k + 3 < K ? base[o + 3] : 0.f;
+                }
+            } else {
+                const int k = k0 + (t >> 4) + 16 * i, r = r0 + (t & 15) * 4;
+                const int64_t o = (int64_t)k * sk + r;
+                if (k >= K) {
+                    v[i] = float4{0.f, 0.f, 0.f, 0.f};
+                } else if (vec && r + 3 < nrow) {
+                    v[i] = *reinterpret_cast<const float4*>(base + o);
+                } else {
+                    v[i].x = r < nrow ? base[o] : 0.f;
+                    v[i].y = r + 1 < nrow ? base[o + 1] : 0.f;
+                    v[i].z = r + 2 < nrow ? base[o + 2] : 0.f;
+                    v[i].w = r + 3 < nrow ? base[o + 3] : 0.f;
+                }
+            }
+        }
+    }
+    // the slice's bf16 planes (hi [, lo at +PL bytes]) into the image
+    template <bool KF>
+    static MMVAE_DEV void store(char* img, int PL, const float4 (&v)[2]) {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int off;
+            if constexpr (KF) off = swz_off<64>((t >> 3) + 32 * i, (t & 7) * 8);
+            else off = swz_off<128>((t >> 4) + 16 * i, (t & 15) * 8);
+            const float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            const uint32_t h01 = pk_bf16(e[0], e[1]), h23 = pk_bf16(e[2], e[3]);
+            *reinterpret_cast<uint2*>(img + off) = uint2{h01, h23};
+            if constexpr (X) {
+                const uint32_t l01 = pk_bf16(e[0] - __uint_as_float(h01 << 16), e[1] - __uint_as_float(h01 & 0xffff0000u));
+                const uint32_t l23 = pk_bf16(e[2] - __uint_as_float(h23 << 16), e[3] - __uint_as_float(h23 & 0xffff0000u));
+                *reinterpret_cast<uint2*>(img + PL + off) = uint2{l01, l23};
+            }
+        }
+    }
+    // MFMA fragment of rows c0 .. c0 + 15 (lane & 15), k 8 (lane >> 4) .. + 7
+    template <bool KF>
+    static MMVAE_DEV typename MM<P>::frag frag(const char* img, int PL, int c0) {
+        const int lane = threadIdx.x & 63;
+        if constexpr (KF) {
+            const int off = swz_off<64>(c0 + (lane & 15), (lane >> 4) * 16);
+            if constexpr (X) return typename MM<P>::frag{*reinterpret_cast<const bf16x8*>(img + off),
+                                                          *reinterpret_cast<const bf16x8*>(img + PL + off)};
+            else return *reinterpret_cast<const bf16x8*>(img + off);
+        } else {
+            if constexpr (X) return typename MM<P>::frag{tr_frag<128>(img, 0, c0), tr_frag<128>(img + PL, 0, c0)};
+            else return tr_frag<128>(img, 0, c0);
+        }
+    }
+};
+
+// NT: 64 or 128 output columns per workgroup (the four waves 32 x NT / 2 each); 128 halves
+// the A re-reads of the K = D GEMMs whose N is the latent width
+template <class P, bool AKF, bool BKF, bool AT, int NT>
+__global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, float* __restrict__ ws, int vec) {
+    static_assert(!AT || AKF, "the input transform follows the k-contiguous slice layout");
+    using M = MM<P>;
+    using Op = MfOperand<P>;
+    constexpr int NPL = IsX3<P>::value ? 2 : 1;
+    constexpr int PL = 4096;                // one plane of a 64 x 32 bf16 image
+    constexpr int IMG = NPL * PL;           // one 64-row operand image
+    constexpr int NB = NT / 64;             // B images per buffer
+    constexpr int WJ = NT / 32;             // 16-column blocks per wave
+    __shared__ __attribute__((aligned(16))) char lds[2][1 + NB][IMG];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * NT;
+    const int nch = (g.K + 31) / 32;
+    const int c0 = blockIdx.z * cps, c1 = min(nch, c0 + cps);
+    float4 va[2], vb[NB][2];
+    auto load = [&](int ch) {
+        Op::template load<AKF>(g.A, g.sam, g.sak, m0, g.M, ch * 32, g.K, vec != 0, va);
+#pragma unroll
+        for (int h = 0; h < NB; ++h) Op::template load<BKF>(g.B, g.sbn, g.sbk, n0 + 64 * h, g.N, ch * 32, g.K, vec != 0, vb[h]);
+        if constexpr (AT) {  // the encoder input transform; k past K stays 0
+            const int t = threadIdx.x;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = m0 + (t >> 3) + 32 * i, k = ch * 32 + (t & 7) * 4;
+                const float rs = (x.rs && r < g.M) ? x.rs[r] : 1.f;
+                float* e = reinterpret_cast<float*>(&va[i]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) e[j] = (k + j < g.K) ? enc_in(e[j], rs, x.xm[k + j], x.isd[k + j]) : 0.f;
+            }
+        }
+    };
+    const int wm = (w >> 1) * 32, wn = (w & 1) * (NT / 2);
+    f32x4 acc[2][WJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (c0 < c1) load(c0);
+    for (int ch = c0; ch < c1; ++ch) {
+        const int buf = (ch - c0) & 1;
+        // buffer buf was last read two chunks ago, before the previous chunk's barrier
+        Op::template store<AKF>(lds[buf][0], PL, va);
+#pragma unroll
+        for (int h = 0; h < NB; ++h) Op::template store<BKF>(lds[buf][1 + h], PL, vb[h]);
+        __syncthreads();
+        if (ch + 1 < c1) load(ch + 1);  // in flight under this chunk's MFMAs
+        typename M::frag fa[2], fb[WJ];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = Op::template frag<AKF>(lds[buf][0], PL, wm + 16 * i);
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+            const int cn = wn + 16 * j;
+            fb[j] = Op::template frag<BKF>(lds[buf][1 + cn / 64], PL, cn & 63);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < WJ; ++j) acc[i][j] = M::mma(fa[i], fb[j], acc[i][j]);
+    }
+    const bool split = gridDim.z > 1;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+        const int n = n0 + wn + 16 * j + (lane & 15);
+        if (n >= g.N) continue;
+        float colc = 0.f, cwn[8];
+        if (!split) {
+            colc = gemm_colc(g, n);
+            for (int c = 0; c < g.nc; ++c) cwn[c] = g.cw[(int64_t)n * g.lcw + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+                if (m >= g.M) continue;
+                if (split) ws[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+                else gemm_store(g, m, n, acc[i][j][r], colc, cwn);
+            }
+    }
+}
+
+// =======================================================================================
 // Wide-path state (device buffers sized at create, so a step allocates nothing and can be
 // captured into a step graph)
 // =======================================================================================
@@ -154,15 +369,22 @@ struct WLayer {
 
 struct WideState {
     int64_t Bp = 0, D = 0;
-    // dense [Bpad][D] blocks
+    // dense [Bpad][D] blocks: the raw batch, logits, their gradient, the nu pre-activation /
+    // its gradient; Xn, the normalised encoder input, only on f32 handles (the bf16 / x3 GEMMs
+    // transform the raw batch as they load it)
     float *X = nullptr, *Xn = nullptr, *LG = nullptr, *G = nullptr, *U = nullptr;
-    // per-gene vectors: sdv, sigmoid(ln_x_sd), colsum scratch x2, (vMF) the eps-shifted y norm
+    float* Uin = nullptr;  // the nu pre-activation when R > RMAX (a GEMM output; U holds dL/du)
+    // per-gene vectors [5][D]: sdv, softplus'(ln_x_sd), the encoder's two column sums, 1 / sdv
     float *gvec = nullptr;
+    float* cr_part = nullptr;  // column-reduction partials (k_colred)
+    int64_t cr_cap = 0;
     float* one = nullptr;    // a device 1.0f (ones operand of the column-sum GEMMs)
     float* ws = nullptr;     // split-K partials
     int64_t ws_cap = 0;
     // covariates of the batch rows, per-row scalars
-    float *Cb = nullptr, *rowv = nullptr;  // rowv: [8][Bpad]
+    // rowv [8][Bpad]: loss, KL, depth d, depth pre-activation, its gradient, (vMF) kappa scalars,
+    // (vMF) 1 / |log1p(x_b)|, 1 / |log1p(relu(x_b)) + eps|
+    float *Cb = nullptr, *rowv = nullptr;
     // latent blocks [Bpad][K]: heads (raw mean, raw lnvar), covariate part, mean, z, eps, dz,
     // dmean, dlnvar(raw)
     float *Mr = nullptr, *Ar = nullptr, *Ce = nullptr, *Mn = nullptr, *Z = nullptr, *Ep = nullptr,
@@ -181,27 +403,90 @@ struct WideState {
 
 static hipError_t walloc(float** p, int64_t n) { return hipMalloc(p, sizeof(float) * (size_t)(n > 0 ? n : 1)); }
 
-static hipError_t gemm(Engine* e, const GemmOp& g) {
-    if (g.M <= 0 || g.N <= 0) return hipSuccess;
-    WideState* w = e->wide_st;
-    const int tm = (g.M + GT - 1) / GT, tn = (g.N + GT - 1) / GT;
-    const int nch = (g.K + GK - 1) / GK;
+// split-K count: one round of >= 512 workgroups where the tile grid is smaller, each split
+// keeping >= min_ch chunks, capped by the partial buffer
+static int split_count(const WideState* w, int64_t MN, int tiles, int nch, int min_ch) {
     int S = 1;
-    const int tiles = tm * tn;
-    if (tiles < 512 && nch >= 32) {
-        S = std::min((512 + tiles - 1) / tiles, nch / 16);
-        const int64_t cap = w->ws_cap / ((int64_t)g.M * g.N);
+    if (tiles < 512 && nch >= 2 * min_ch) {
+        S = std::min((512 + tiles - 1) / tiles, nch / min_ch);
+        const int64_t cap = w->ws_cap / MN;
         if (S > cap) S = (int)cap;
         if (S < 2) S = 1;
     }
+    return S;
+}
+
+static void launch_reduce(Engine* e, const GemmOp& g, int S) {
+    const int64_t MN = (int64_t)g.M * g.N;
+    const int nb = (int)std::min<int64_t>((MN + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, e->stream, g, S, (const float*)e->wide_st->ws);
+}
+
+template <class P, bool AT, int NT>
+static void launch_mf(Engine* e, const GemmOp& g, const GemmX& x, dim3 grid, int cps, int vec) {
+    float* ws = e->wide_st->ws;
+    const bool akf = g.sak == 1, bkf = g.sbk == 1;
+    if constexpr (AT) {
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, true, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, true, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+    } else if (akf) {
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+    } else {
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, false, true, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, false, false, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+    }
+}
+template <class P, bool AT>
+static void launch_mf_nt(Engine* e, const GemmOp& g, const GemmX& x, dim3 grid, int cps, int vec, int nt) {
+    if (nt == 128) launch_mf<P, AT, 128>(e, g, x, grid, cps, vec);
+    else launch_mf<P, AT, 64>(e, g, x, grid, cps, vec);
+}
+
+// the bf16-MFMA kernel takes the handle's non-f32 modes, operands with a unit stride on one side
+// each, and shapes big enough to fill its 64 x 64 x 32 tiles
+static bool use_mf(const Engine* e, const GemmOp& g) {
+    if (e->cfg.dtype == MMVAE_DTYPE_F32 || getenv_is("MMVAE_WIDE_F32GEMM", "1")) return false;
+    if (!(g.sak == 1 || g.sam == 1) || !(g.sbk == 1 || g.sbn == 1)) return false;
+    if (g.sam == 0 || g.sbn == 0) return false;  // broadcast operands (column sums): the f32 kernel
+    return g.M >= 32 && g.N >= 32 && g.K >= 32 && (int64_t)g.M * g.N * (int64_t)g.K >= ((int64_t)1 << 22);
+}
+
+// C = epilogue(A . B); `x` non-null: the encoder input transform on A (the f32 handles
+// materialise the normalised block instead, see enc_forward)
+static hipError_t gemm(Engine* e, const GemmOp& g, const GemmX* x = nullptr) {
+    if (g.M <= 0 || g.N <= 0) return hipSuccess;
+    WideState* w = e->wide_st;
+    const int64_t MN = (int64_t)g.M * g.N;
+    if (x || use_mf(e, g)) {
+        const int nt = g.N >= 96 ? 128 : 64;
+        const int tm = (g.M + 63) / 64, tn = (g.N + nt - 1) / nt, nch = (g.K + 31) / 32;
+        int S = split_count(w, MN, tm * tn, nch, 8);
+        const int cps = (nch + S - 1) / S;
+        S = std::max(1, (nch + cps - 1) / cps);
+        // float4 loads: 16-byte aligned bases and strides on the strided side
+        auto al = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+        const int64_t sa = g.sak == 1 ? g.sam : g.sak, sb = g.sbk == 1 ? g.sbn : g.sbk;
+        const int vec = al(g.A) && al(g.B) && sa % 4 == 0 && sb % 4 == 0;
+        const GemmX gx = x ? *x : GemmX{};
+        const dim3 grid(tn, tm, S);
+        if (e->cfg.dtype == MMVAE_DTYPE_BF16X3) {
+            if (x) launch_mf_nt<X3, true>(e, g, gx, grid, cps, vec, nt);
+            else launch_mf_nt<X3, false>(e, g, gx, grid, cps, vec, nt);
+        } else {
+            if (x) launch_mf_nt<__bf16, true>(e, g, gx, grid, cps, vec, nt);
+            else launch_mf_nt<__bf16, false>(e, g, gx, grid, cps, vec, nt);
+        }
+        if (S > 1) launch_reduce(e, g, S);
+        return hipGetLastError();
+    }
+    const int tm = (g.M + GT - 1) / GT, tn = (g.N + GT - 1) / GT;
+    const int nch = (g.K + GK - 1) / GK;
+    int S = split_count(w, MN, tm * tn, nch, 16);
     const int cps = (nch + S - 1) / S;
     S = std::max(1, (nch + cps - 1) / cps);
     hipLaunchKernelGGL(k_gemm, dim3(tn, tm, S), dim3(256), 0, e->stream, g, cps, w->ws);
-    if (S > 1) {
-        const int64_t MN = (int64_t)g.M * g.N;
-        const int nb = (int)std::min<int64_t>((MN + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, e->stream, g, S, (const float*)w->ws);
-    }
+    if (S > 1) launch_reduce(e, g, S);
     return hipGetLastError();
 }
 
@@ -256,21 +541,6 @@ __global__ __launch_bounds__(256) void k_w_stage(const uint4* __restrict__ src, 
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
 }
 
-// one workgroup per batch row: zero the row, then scatter the cell's nonzeros (mmvae_io.hh:208-245)
-__global__ __launch_bounds__(256) void k_w_densify(int D, int C, const int64_t* __restrict__ cells,
-                                                   const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                                   const float* __restrict__ val, const float* __restrict__ covar,
-                                                   float* __restrict__ X, float* __restrict__ Cb) {
-    const int b = blockIdx.x;
-    const int64_t cell = cells[b];
-    float* xr = X + (int64_t)b * D;
-    for (int g = threadIdx.x; g < D; g += 256) xr[g] = 0.f;
-    __syncthreads();
-    const int64_t r0 = rowptr[cell], r1 = rowptr[cell + 1];
-    for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) xr[col[i]] = val[i];
-    for (int c = threadIdx.x; c < C; c += 256) Cb[(int64_t)b * C + c] = covar[cell * C + c];
-}
-
 // =======================================================================================
 // Block reductions (256 threads, fixed order)
 // =======================================================================================
@@ -290,15 +560,222 @@ MMVAE_DEV float wblock_max(float v, float* red) {
     return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// digamma in double: recurrence up to 6, then the asymptotic series
-MMVAE_DEV double digamma_d(double x) {
-    double r = 0.0;
-    while (x < 6.0) {
-        r -= 1.0 / x;
-        x += 1.0;
+// =======================================================================================
+// Batch densify (mmvae_io.hh:208-245), one workgroup per batch row: the row is zeroed with
+// 16-byte stores, then the cell's nonzeros are scattered.  The same pass takes the row terms
+// that need only the nonzeros (fixed-order block sums):
+//   NB: the raw-count Linears depth(x) (nb.hh:400, 498) and nu_enc(x) (nb.hh:444-451) for
+//       H <= HMAX (bias included);
+//   vMF: 1 / |log1p(x_b)| (vmf.hh:253, F::normalize eps 1e-12) and 1 / |log1p(relu(x_b)) + eps|
+//       (vmf.hh:421-422), the zeros' eps^2 terms in closed form.
+// =======================================================================================
+struct WDens {
+    int D, C, H;
+    const int64_t* cells;
+    const int64_t* rowptr;
+    const int32_t* col;
+    const float* val;
+    const float* covar;
+    float *X, *Cb;
+    // NB row dots (null: not taken here)
+    const float *dw, *db, *Wne, *bne;
+    float *dpre, *Hn;
+    // vMF row scales (null: NB)
+    float *rs1, *rs2;
+    float epsD;
+};
+// The row is built in LDS segments of WSEG genes (zeroed, the segment's nonzeros scattered, then
+// written out with coalesced 16-byte stores), so every byte of the dense row is written once.
+static constexpr int WSEG = 4096;
+__global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
+    __shared__ __attribute__((aligned(16))) float seg[WSEG];
+    __shared__ float red[4];
+    __shared__ int64_t bnd[2];
+    const int b = blockIdx.x;
+    const int64_t cell = a.cells[b];
+    float* xr = a.X + (int64_t)b * a.D;
+    const int64_t r0 = a.rowptr[cell], r1 = a.rowptr[cell + 1];
+    const int32_t* cr = a.col;
+    // the row terms over its nonzeros
+    float dp = 0.f, hn[HMAX], n1 = 0.f, n2 = 0.f;
+#pragma unroll
+    for (int h = 0; h < HMAX; ++h) hn[h] = 0.f;
+    for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+        const int g = cr[i];
+        const float x = a.val[i];
+        if (a.dpre) {
+            dp = fmaf(x, a.dw[g], dp);
+#pragma unroll
+            for (int h = 0; h < HMAX; ++h)
+                if (h < a.H) hn[h] = fmaf(x, a.Wne[(int64_t)h * a.D + g], hn[h]);
+        }
+        if (a.rs1) {
+            const float l = log1pf(x), ly = log1pf(fmaxf(x, 0.f)) + a.epsD;
+            n1 = fmaf(l, l, n1);
+            n2 += ly * ly - a.epsD * a.epsD;
+        }
     }
-    const double f = 1.0 / (x * x);
-    return r + log(x) - 0.5 / x - f * (1.0 / 12 - f * (1.0 / 120 - f * (1.0 / 252 - f * (1.0 / 240 - f / 132))));
+    const bool v4 = (a.D & 3) == 0;
+    int64_t e = r0;  // the first entry of the current segment (genes sorted in the row)
+    for (int s0 = 0; s0 < a.D; s0 += WSEG) {
+        const int len = min(WSEG, a.D - s0);
+        // this segment's entries: [e, first entry with gene >= s0 + len)
+        if (threadIdx.x == 0) {
+            int64_t lo = e, hi = r1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (cr[mid] < s0 + len) lo = mid + 1;
+                else hi = mid;
+            }
+            bnd[0] = lo;
+        }
+        for (int i = threadIdx.x; i < WSEG / 4; i += 256) reinterpret_cast<float4*>(seg)[i] = float4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        const int64_t e1 = bnd[0];
+        for (int64_t i = e + threadIdx.x; i < e1; i += 256) seg[cr[i] - s0] = a.val[i];
+        __syncthreads();
+        if (v4) {
+            for (int i = threadIdx.x; i < len / 4; i += 256)
+                *reinterpret_cast<float4*>(xr + s0 + 4 * i) = reinterpret_cast<const float4*>(seg)[i];
+        } else {
+            for (int i = threadIdx.x; i < len; i += 256) xr[s0 + i] = seg[i];
+        }
+        e = e1;
+        __syncthreads();  // seg and bnd are rewritten by the next segment
+    }
+    for (int c = threadIdx.x; c < a.C; c += 256) a.Cb[(int64_t)b * a.C + c] = a.covar[cell * a.C + c];
+    if (a.dpre) {
+        dp = wblock_sum(dp, red);
+        if (threadIdx.x == 0) a.dpre[b] = dp + a.db[0];
+        for (int h = 0; h < a.H && h < HMAX; ++h) {
+            const float v = wblock_sum(hn[h], red);
+            if (threadIdx.x == 0) a.Hn[(int64_t)b * a.H + h] = v + a.bne[h];
+        }
+    }
+    if (a.rs1) {
+        n1 = wblock_sum(n1, red);
+        n2 = wblock_sum(n2, red);
+        if (threadIdx.x == 0) {
+            a.rs1[b] = 1.f / fmaxf(sqrtf(n1), 1e-12f);
+            a.rs2[b] = 1.f / fmaxf(sqrtf(fmaf((float)a.D * a.epsD, a.epsD, n2)), 1e-12f);
+        }
+    }
+}
+
+// =======================================================================================
+// Column reductions of a dense [M rows][N] block (the batch sums of the gene-vector gradients,
+// nb.hh:410-460 / vmf.hh:256-290 backward), fixed order, no atomics:
+//   s_j(n) = sum_m a_j(m) Y(m, n),  columns j: [a0 (null: ones)] then A1[:, j1 .. j1 + n1 - 1]
+//   XPROD: s_0 = sum_m Y(m, n), s_1 = sum_m Y(m, n) enc_in(X2(m, n)) (ln_x_sd's sum)
+// Stage 1 (k_colred): a thread owns 4 consecutive columns of one chunk of rows -> part[chunk];
+// stage 2 (k_colred_fin): the chunks summed in order into the outputs.
+// =======================================================================================
+static constexpr int CR_QMAX = 9;
+struct ColRed {
+    int M, N, Q, has0, rows_per;
+    const float* a0;
+    const float* A1;
+    int64_t la1;
+    const float* Y;
+    int64_t ly;
+    const float* X2;  // XPROD (Q = 2)
+    GemmX xf;
+    float* part;  // [chunks][Q][N]
+};
+template <bool XPROD>
+__global__ __launch_bounds__(256) void k_colred(ColRed c) {
+    constexpr int RG = 8;  // rows per group: their loads are all issued before the sums
+    const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (n >= c.N) return;
+    const int r0 = blockIdx.y * c.rows_per, r1 = min(c.M, r0 + c.rows_per);
+    const bool v4 = n + 3 < c.N && (c.ly & 3) == 0;
+    float acc[CR_QMAX][4];
+#pragma unroll
+    for (int q = 0; q < CR_QMAX; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[q][j] = 0.f;
+    float xm[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
+    if (XPROD)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (n + j < c.N) {
+                xm[j] = c.xf.xm[n + j];
+                isd[j] = c.xf.isd[n + j];
+            }
+    auto ld4 = [&](const float* base, int m, float (&v)[4]) {
+        const float* p = base + (int64_t)m * c.ly + n;
+        if (m >= r1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = 0.f;
+        } else if (v4) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (n + j < c.N) ? p[j] : 0.f;
+        }
+    };
+    for (int m0 = r0; m0 < r1; m0 += RG) {
+        float y[RG][4], x2[XPROD ? RG : 1][4];
+#pragma unroll
+        for (int i = 0; i < RG; ++i) ld4(c.Y, m0 + i, y[i]);
+        if constexpr (XPROD)
+#pragma unroll
+            for (int i = 0; i < RG; ++i) ld4(c.X2, m0 + i, x2[i]);
+#pragma unroll
+        for (int i = 0; i < RG; ++i) {
+            const int m = m0 + i;
+            if (m >= r1) continue;
+            if constexpr (XPROD) {
+                const float rs = c.xf.rs ? c.xf.rs[m] : 1.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] += y[i][j];
+                    acc[1][j] = fmaf(y[i][j], enc_in_acc(x2[i][j], rs, xm[j], isd[j]), acc[1][j]);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < CR_QMAX; ++q)
+                    if (q < c.Q) {
+                        const float a = (c.has0 && q == 0) ? (c.a0 ? c.a0[m] : 1.f) : c.A1[(int64_t)m * c.la1 + q - c.has0];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[q][j] = fmaf(a, y[i][j], acc[q][j]);
+                    }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < CR_QMAX; ++q)
+        if (q < c.Q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (n + j < c.N) c.part[((int64_t)blockIdx.y * c.Q + q) * c.N + n + j] = acc[q][j];
+}
+// outputs: column 0 -> o0[n s0] = alpha0 s (and o0b[n s0] = beta0 s); the A1 columns j ->
+// o1[j q1 + n s1] = alpha1 s (the XPROD sum: o1[n s1])
+struct ColOut {
+    float* o0 = nullptr;
+    float* o0b = nullptr;
+    int64_t s0 = 1;
+    float alpha0 = 1.f, beta0 = 1.f;
+    float* o1 = nullptr;
+    int64_t q1 = 0, s1 = 1;
+    float alpha1 = 1.f;
+};
+__global__ __launch_bounds__(256) void k_colred_fin(int N, int Q, int has0, int chunks, const float* __restrict__ part,
+                                                    ColOut o) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)N * Q) return;
+    const int q = (int)(i / N), n = (int)(i % N);
+    float s = 0.f;
+    for (int c = 0; c < chunks; ++c) s += part[((int64_t)c * Q + q) * N + n];
+    if (has0 && q == 0) {
+        o.o0[n * o.s0] = o.alpha0 * s;
+        if (o.o0b) o.o0b[n * o.s0] = o.beta0 * s;
+    } else {
+        const int j = q - has0;
+        o.o1[j * o.q1 + n * o.s1] = o.alpha1 * s;
+    }
 }
 
 // =======================================================================================
@@ -310,17 +787,19 @@ __global__ __launch_bounds__(256) void k_w_gene(int D, const float* __restrict__
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= D) return;
     const float u = lsd[g];
-    gv[g] = softplus_acc(u) + eps;
+    const float sdv = softplus_acc(u) + eps;
+    gv[g] = sdv;
     gv[D + g] = dsoftplus(u);
+    gv[4 * D + g] = 1.f / sdv;  // the encoder input transform's scale (GemmX::isd)
 }
 
-// NB encoder input: (log1p(x) - x_mean) / sdv (nb.hh:410)
-__global__ __launch_bounds__(256) void k_w_xn_nb(int64_t n, int D, const float* __restrict__ X,
-                                                 const float* __restrict__ xm, const float* __restrict__ gv,
-                                                 float* __restrict__ Xn) {
+// the normalised encoder input block of the exact-f32 handles (the bf16 / x3 GEMMs apply the
+// same enc_in transform as they load the raw batch): nb.hh:408-410, vmf.hh:253-257
+__global__ __launch_bounds__(256) void k_w_xn(int64_t n, int D, const float* __restrict__ X, GemmX x,
+                                              float* __restrict__ Xn) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const int g = (int)(i % D);
-        Xn[i] = (log1pf(X[i]) - xm[g]) / gv[g];
+        Xn[i] = enc_in_acc(X[i], x.rs ? x.rs[i / D] : 1.f, x.xm[g], x.isd[g]);
     }
 }
 
@@ -415,63 +894,195 @@ __global__ __launch_bounds__(256) void k_w_latent_bwd(WLatB a) {
     }
 }
 
-// NB likelihood row (nb.hh:433-442, 453-460, 510-531) and its gradient, one workgroup per row:
-//   sweep 1: l = logit + mu_bias (stored back), row max; sweep 2: sum exp -> lse;
-//   sweep 3: p, mu' = p d + 1e-4, nu' = clamp(softplus(u - nu_bias)) + 1e-4, the NLL terms,
-//            G = p dL/dp, U <- dL/du (x inv_n), row sums S = sum G, dd = sum p dL/dmu';
-//   sweep 4: G <- inv_n (G - p S)  (the softmax backward: dL/dlogit)
+// NB likelihood row (nb.hh:433-442, 453-460, 510-531) and its gradient, one workgroup per row,
+// with the fused path's element arithmetic (nb_kernels.hip pass B: softplus_sig, nb_gamma_terms):
+//   sweep 1: online max / sum-exp of the logits (every bias already added by the GEMM) -> lse;
+//   sweep 2: p, mu' = p d + 1e-4, u = nu_dec(z_nu) - nu_bias (inline for R <= RMAX),
+//            nu' = clamp(softplus(u)) + 1e-4, the NLL terms; G <- p dL/dmu' d,
+//            U <- dL/du / n, row sums S = sum G, dd = sum p dL/dmu', dz_nu = sum U Wnd;
+//   sweep 3: G <- (G - p S) / n  (the softmax backward: dL/dlogit).
 struct WNbRow {
-    int D;
+    int D, R;
     float inv_n;
-    float *LG, *G, *U;
-    const float *X, *mu_bias, *nu_bias, *dv, *dpre;
-    float *lossr, *ddpre;
+    const float* LG;
+    float *G, *U;
+    const float* Uin;  // u when R > RMAX (else computed from Zn)
+    const float* X;    // the dense batch (register-resident variant)
+    // the row's nonzeros straight from the dataset CSR (cells[b]'s entries)
+    const int64_t *cells, *rowptr;
+    const int32_t* col;
+    const float* val;
+    const float *Zn, *Wnd, *bnd, *nu_bias;  // u inline (Zn non-null) or from U
+    const float *dv, *dpre;
+    float *lossr, *ddpre, *dZn;
     int with_grads;
 };
+// one (cell, gene) element of the NB row at x = 0 (every gene; the x-dependent terms of the
+// nonzeros are added by nb_delta): loss term, G = p dL/dmu' d, dL/du / n (0 where the clamp
+// bites), p dL/dmu'.  The dense part shares the fused path's arithmetic (nb_dense2's terms).
+struct NbElem {
+    float ll, gp, du, pg;
+};
+struct NbCore {
+    float mu, nup, sv, rsv, lg2, sig;
+    bool pass;  // the clamp passes the gradient
+};
+MMVAE_DEV NbCore nb_core(float p, float u, float d) {
+    NbCore c;
+    c.mu = fmaf(p, d, 1e-4f);
+    const float sp = softplus_sig(u, c.sig);
+    const float nu = clamp_nu(sp);
+    c.pass = nu == sp;
+    c.nup = nu + 1e-4f;
+    c.sv = c.mu + c.nup;
+    const float rr = frcp(c.nup * c.sv);
+    c.rsv = c.nup * rr;                       // 1 / (mu + nu)
+    c.lg2 = flog2(c.sv * (c.sv * rr));        // log2((mu + nu) / nu)
+    return c;
+}
+MMVAE_DEV NbElem nb_elem(float p, float u, float d, float inv_n) {
+    constexpr float LN2 = 0.6931471805599453f;
+    const NbCore c = nb_core(p, u, d);
+    const float gmu = c.nup * c.rsv;
+    const float gnu = fmaf(c.lg2, LN2, fmaf(c.nup, c.rsv, -1.f));
+    NbElem r;
+    r.ll = c.nup * c.lg2 * LN2;                   // nb.hh:528
+    r.du = c.pass ? gnu * c.sig * inv_n : 0.f;
+    r.pg = gmu * p;
+    r.gp = r.pg * d;
+    return r;
+}
+// the x-dependent terms of a nonzero count x (nb.hh:522-527): added to the x = 0 element
+MMVAE_DEV NbElem nb_delta(float p, float u, float d, float x, float inv_n, const float* ftab) {
+    const NbCore c = nb_core(p, u, d);
+    const float rmu = frcp(c.mu);
+    float lgd, dgd;
+    nb_gamma_terms<8>(c.nup, x, lgd, dgd, ftab);  // nb.hh:522-523
+    const float dgmu = x * (c.rsv - rmu);          // x / s - x / mu
+    const float dgnu = fmaf(x, c.rsv, dgd);
+    NbElem r;
+    r.ll = x * flog(c.sv * rmu) + lgd;             // nb.hh:527
+    r.du = c.pass ? dgnu * c.sig * inv_n : 0.f;
+    r.pg = dgmu * p;
+    r.gp = r.pg * d;
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_w_nb_row(WNbRow a) {
-    __shared__ float red[4];
+    __shared__ float red[4], red2[4], ftab[9];
+    constexpr float L2E = 1.4426950408889634f;
     const int b = blockIdx.x;
     const int64_t o = (int64_t)b * a.D;
-    float* l = a.LG + o;
-    float mx = -INFINITY;
-    for (int g = threadIdx.x; g < a.D; g += 256) {
-        const float v = l[g] + a.mu_bias[g];
-        l[g] = v;
-        mx = fmaxf(mx, v);
+    const float* l = a.LG + o;
+    if (threadIdx.x < 9) {
+        float f = 1.f;
+        for (int i = 2; i <= (int)threadIdx.x; ++i) f *= (float)i;
+        ftab[threadIdx.x] = f;
     }
-    mx = wblock_max(mx, red);
-    float se = 0.f;
-    for (int g = threadIdx.x; g < a.D; g += 256) se += expf(l[g] - mx);
-    se = wblock_sum(se, red);
-    const float lse = mx + logf(se);
-    const float d = a.dv[b];
-    float lsum = 0.f, S = 0.f, dd = 0.f;
-    for (int g = threadIdx.x; g < a.D; g += 256) {
-        const float p = expf(l[g] - lse);
-        const float x = a.X[o + g];
-        const float mu = p * d + 1e-4f;
-        const float u = a.U[o + g] - a.nu_bias[g];
-        const float sp = softplus_acc(u);
-        const float nu = fminf(fmaxf(sp, 1e-4f), 1e4f);
-        const float nup = nu + 1e-4f;
-        const float s = mu + nup;
-        const float ls = logf(s), lnu = logf(nup);
-        float ll = nup * (ls - lnu);
-        float dgd = 0.f;
-        if (x != 0.f) {
-            ll += lgammaf(nup) + lgammaf(x + 1.f) - lgammaf(nup + x) + x * (ls - logf(mu));
-            dgd = (float)(digamma_d((double)nup) - digamma_d((double)nup + (double)x));
+    // float4 sweeps when rows are 16-byte aligned (D % 4 == 0): thread t takes genes 4t + 1024 i
+    const bool v4 = (a.D & 3) == 0;
+    // sweep 1 (log2 units; -1e30: a thread without genes contributes nothing)
+    float m = -1e30f, s = 0.f;
+    if (v4) {
+        for (int g = 4 * threadIdx.x; g < a.D; g += 1024) {
+            const float4 v = *reinterpret_cast<const float4*>(l + g);
+            const float v0 = v.x * L2E, v1 = v.y * L2E, v2 = v.z * L2E, v3 = v.w * L2E;
+            const float mn = fmaxf(m, fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
+            s = s * fexp2(m - mn) + ((fexp2(v0 - mn) + fexp2(v1 - mn)) + (fexp2(v2 - mn) + fexp2(v3 - mn)));
+            m = mn;
         }
-        lsum += ll;
-        if (a.with_grads) {
-            const float gmu = x / s - x / mu + nup / s;
-            const float gnu = dgd + (x + nup) / s + (ls - lnu) - 1.f;
-            const float msk = (sp >= 1e-4f && sp <= 1e4f) ? 1.f : 0.f;
-            a.U[o + g] = gnu * dsoftplus(u) * msk * a.inv_n;
-            const float gp = p * gmu * d;
-            a.G[o + g] = gp;
-            S += gp;
-            dd += gmu * p;
+    } else {
+        for (int g = threadIdx.x; g < a.D; g += 256) {
+            const float v = l[g] * L2E, mn = fmaxf(m, v);
+            s = s * fexp2(m - mn) + fexp2(v - mn);
+            m = mn;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+        const float mn = fmaxf(m, m2);
+        s = s * fexp2(m - mn) + s2 * fexp2(m2 - mn);
+        m = mn;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = m;
+        red2[threadIdx.x >> 6] = s;
+    }
+    __syncthreads();
+    float M2 = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), S2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S2 += red2[i] * fexp2(red[i] - M2);
+    const float lse2 = M2 + flog2(S2);
+    __syncthreads();  // red reused below
+    const float d = a.dv[b];
+    float zn[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) zn[r] = (a.Zn && r < a.R) ? a.Zn[(int64_t)b * a.R + r] : 0.f;
+    auto u_of = [&](int g) {
+        if (!a.Zn) return a.Uin[o + g] - a.nu_bias[g];
+        float u = a.bnd[g] - a.nu_bias[g];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            if (r < a.R) u = fmaf(zn[r], a.Wnd[(int64_t)g * a.R + r], u);
+        return u;
+    };
+    float lsum = 0.f, S = 0.f, dd = 0.f, dz[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) dz[r] = 0.f;
+    auto take = [&](int g, const NbElem& q) {
+        lsum += q.ll;
+        S += q.gp;
+        dd += q.pg;
+        if (a.Zn)
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if (r < a.R) dz[r] = fmaf(q.du, a.Wnd[(int64_t)g * a.R + r], dz[r]);
+    };
+    // sweep 2: every gene at x = 0 (no count-dependent branch: the nonzeros follow)
+    if (v4) {
+        for (int g = 4 * threadIdx.x; g < a.D; g += 1024) {
+            const float4 lv = *reinterpret_cast<const float4*>(l + g);
+            const float lgs[4] = {lv.x, lv.y, lv.z, lv.w};
+            float gps[4], dus[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const NbElem q = nb_elem(fexp2(fmaf(lgs[j], L2E, -lse2)), u_of(g + j), d, a.inv_n);
+                take(g + j, q);
+                gps[j] = q.gp;
+                dus[j] = q.du;
+            }
+            if (a.with_grads) {
+                *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
+                *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+            }
+        }
+    } else {
+        for (int g = threadIdx.x; g < a.D; g += 256) {
+            const NbElem q = nb_elem(fexp2(fmaf(l[g], L2E, -lse2)), u_of(g), d, a.inv_n);
+            take(g, q);
+            if (a.with_grads) {
+                a.U[o + g] = q.du;
+                a.G[o + g] = q.gp;
+            }
+        }
+    }
+    // the row's nonzeros (CSR, one gene at most once): their count-dependent terms, added onto
+    // the x = 0 values just stored (the barrier orders the workgroup's stores before these
+    // read-modify-writes)
+    __syncthreads();
+    {
+        const int64_t cell = a.cells[b], e0 = a.rowptr[cell], e1 = a.rowptr[cell + 1];
+        for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+            const int g = a.col[e];
+            const float x = a.val[e];
+            if (x == 0.f) continue;
+            const NbElem q = nb_delta(fexp2(fmaf(l[g], L2E, -lse2)), u_of(g), d, x, a.inv_n, ftab);
+            take(g, q);
+            if (a.with_grads) {
+                a.U[o + g] += q.du;
+                a.G[o + g] += q.gp;
+            }
         }
     }
     lsum = wblock_sum(lsum, red);
@@ -480,9 +1091,181 @@ __global__ __launch_bounds__(256) void k_w_nb_row(WNbRow a) {
     S = wblock_sum(S, red);
     dd = wblock_sum(dd, red);
     if (threadIdx.x == 0) a.ddpre[b] = dd * a.inv_n * dsoftplus(a.dpre[b]);
-    for (int g = threadIdx.x; g < a.D; g += 256) {
-        const float p = expf(l[g] - lse);
-        a.G[o + g] = a.inv_n * (a.G[o + g] - p * S);
+    if (a.Zn)
+        for (int r = 0; r < a.R && r < RMAX; ++r) {
+            const float v = wblock_sum(dz[r], red);
+            if (threadIdx.x == 0) a.dZn[(int64_t)b * a.R + r] = v;
+        }
+    // sweep 3: G <- (G - p S) / n
+    if (v4) {
+        for (int g = 4 * threadIdx.x; g < a.D; g += 1024) {
+            const float4 lv = *reinterpret_cast<const float4*>(l + g);
+            float4 gv = *reinterpret_cast<const float4*>(a.G + o + g);
+            gv.x = a.inv_n * fmaf(-fexp2(fmaf(lv.x, L2E, -lse2)), S, gv.x);
+            gv.y = a.inv_n * fmaf(-fexp2(fmaf(lv.y, L2E, -lse2)), S, gv.y);
+            gv.z = a.inv_n * fmaf(-fexp2(fmaf(lv.z, L2E, -lse2)), S, gv.z);
+            gv.w = a.inv_n * fmaf(-fexp2(fmaf(lv.w, L2E, -lse2)), S, gv.w);
+            *reinterpret_cast<float4*>(a.G + o + g) = gv;
+        }
+    } else {
+        for (int g = threadIdx.x; g < a.D; g += 256) {
+            const float p = fexp2(fmaf(l[g], L2E, -lse2));
+            a.G[o + g] = a.inv_n * fmaf(-p, S, a.G[o + g]);
+        }
+    }
+}
+
+// The LDS-resident variant for rows that fit (D % 4 == 0, 4 D bytes of LDS): 512 threads; the
+// row's logits are read once into LDS and turned into p there, and the count-dependent terms
+// come from the row's CSR entries after a branch-free x = 0 sweep of every gene — 5 passes over
+// [B, D] (logits, U, G out, G back in and out) and no per-element divergence.
+MMVAE_DEV float block_sum512(float v, float* red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
+}
+__global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
+    extern __shared__ __attribute__((aligned(16))) float prow[];  // [D]
+    __shared__ float red[8], red2[8], ftab[9];
+    constexpr float L2E = 1.4426950408889634f;
+    const int b = blockIdx.x;
+    const int64_t o = (int64_t)b * a.D;
+    if (threadIdx.x < 9) {
+        float f = 1.f;
+        for (int i = 2; i <= (int)threadIdx.x; ++i) f *= (float)i;
+        ftab[threadIdx.x] = f;
+    }
+    // sweep 1: the logits into LDS (log2 units), online max / sum-exp
+    float m = -1e30f, s = 0.f;
+    for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
+        const float4 v = *reinterpret_cast<const float4*>(a.LG + o + g);
+        const float v0 = v.x * L2E, v1 = v.y * L2E, v2 = v.z * L2E, v3 = v.w * L2E;
+        *reinterpret_cast<float4*>(prow + g) = float4{v0, v1, v2, v3};
+        const float mn = fmaxf(m, fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
+        s = s * fexp2(m - mn) + ((fexp2(v0 - mn) + fexp2(v1 - mn)) + (fexp2(v2 - mn) + fexp2(v3 - mn)));
+        m = mn;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+        const float mn = fmaxf(m, m2);
+        s = s * fexp2(m - mn) + s2 * fexp2(m2 - mn);
+        m = mn;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = m;
+        red2[threadIdx.x >> 6] = s;
+    }
+    __syncthreads();
+    float M2 = red[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) M2 = fmaxf(M2, red[i]);
+    float S2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) S2 += red2[i] * fexp2(red[i] - M2);
+    const float lse2 = M2 + flog2(S2);
+    __syncthreads();  // red reused below
+    const float d = a.dv[b];
+    float zn[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) zn[r] = (a.Zn && r < a.R) ? a.Zn[(int64_t)b * a.R + r] : 0.f;
+    float lsum = 0.f, S = 0.f, dd = 0.f, dz[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) dz[r] = 0.f;
+    auto u_of = [&](int gg) {
+        if (!a.Zn) return a.Uin[o + gg] - a.nu_bias[gg];
+        float u = a.bnd[gg] - a.nu_bias[gg];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            if (r < a.R) u = fmaf(zn[r], a.Wnd[(int64_t)gg * a.R + r], u);
+        return u;
+    };
+    auto take = [&](int gg, const NbElem& q) {
+        lsum += q.ll;
+        S += q.gp;
+        dd += q.pg;
+        if (a.Zn)
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if (r < a.R) dz[r] = fmaf(q.du, a.Wnd[(int64_t)gg * a.R + r], dz[r]);
+    };
+    // sweep 2: p (kept in LDS) and every gene's terms at x = 0 (branch free); U and G stored
+    for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
+        float4 lv = *reinterpret_cast<const float4*>(prow + g);
+        float* pl = reinterpret_cast<float*>(&lv);
+        float dus[4], gps[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float p = fexp2(pl[j] - lse2);
+            pl[j] = p;
+            const NbElem q = nb_elem(p, u_of(g + j), d, a.inv_n);
+            take(g + j, q);
+            gps[j] = q.gp;
+            dus[j] = q.du;
+        }
+        *reinterpret_cast<float4*>(prow + g) = lv;
+        if (a.with_grads) {
+            *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
+            *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+        }
+    }
+    // the row's nonzeros (CSR, each gene at most once): their count-dependent terms onto the
+    // x = 0 values (the barrier orders the block's stores and LDS p before these reads), with
+    // all of a thread's entries loaded before any is processed
+    __syncthreads();
+    {
+        constexpr int NE = 4;
+        const int64_t cell = a.cells[b], e0 = a.rowptr[cell], e1 = a.rowptr[cell + 1];
+        for (int64_t eb = e0 + threadIdx.x; eb < e1; eb += 512 * NE) {
+            int gs[NE];
+            float xs[NE], gpo[NE], duo[NE];
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                const int64_t e = eb + 512 * k;
+                gs[k] = e < e1 ? a.col[e] : 0;
+                xs[k] = e < e1 ? a.val[e] : 0.f;
+            }
+            if (a.with_grads)
+#pragma unroll
+                for (int k = 0; k < NE; ++k) {
+                    gpo[k] = xs[k] != 0.f ? a.G[o + gs[k]] : 0.f;
+                    duo[k] = xs[k] != 0.f ? a.U[o + gs[k]] : 0.f;
+                }
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                if (xs[k] == 0.f) continue;
+                const int gg = gs[k];
+                const NbElem q = nb_delta(prow[gg], u_of(gg), d, xs[k], a.inv_n, ftab);
+                take(gg, q);
+                if (a.with_grads) {
+                    a.G[o + gg] = gpo[k] + q.gp;
+                    a.U[o + gg] = duo[k] + q.du;
+                }
+            }
+        }
+    }
+    lsum = block_sum512(lsum, red);
+    if (threadIdx.x == 0) a.lossr[b] = lsum;
+    if (!a.with_grads) return;
+    S = block_sum512(S, red);
+    dd = block_sum512(dd, red);
+    if (threadIdx.x == 0) a.ddpre[b] = dd * a.inv_n * dsoftplus(a.dpre[b]);
+    if (a.Zn)
+        for (int r = 0; r < a.R && r < RMAX; ++r) {
+            const float v = block_sum512(dz[r], red);
+            if (threadIdx.x == 0) a.dZn[(int64_t)b * a.R + r] = v;
+        }
+    // sweep 3: G = (G - p S) / n (each thread re-reads the G it stored: no barrier needed)
+    for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
+        const float4 pv = *reinterpret_cast<const float4*>(prow + g);
+        float4 gv = *reinterpret_cast<const float4*>(a.G + o + g);
+        gv.x = a.inv_n * fmaf(-pv.x, S, gv.x);
+        gv.y = a.inv_n * fmaf(-pv.y, S, gv.y);
+        gv.z = a.inv_n * fmaf(-pv.z, S, gv.z);
+        gv.w = a.inv_n * fmaf(-pv.w, S, gv.w);
+        *reinterpret_cast<float4*>(a.G + o + g) = gv;
     }
 }
 
@@ -511,9 +1294,6 @@ __global__ __launch_bounds__(256) void k_w_xgrad(int D, const float* __restrict_
     glsd[g] = -s12[D + g] / sdv * gv[D + g];
 }
 
-__global__ __launch_bounds__(256) void k_w_mul(int64_t n, const float* __restrict__ a, float* __restrict__ b) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) b[i] *= a[i];
-}
 
 // ReLU backward: dY[m][n] = 0 where the layer's (post-ReLU) output Y[m][n] is 0
 __global__ __launch_bounds__(256) void k_w_relu_bwd(int64_t n, const float* __restrict__ Y, float* __restrict__ dY) {
@@ -539,58 +1319,56 @@ __global__ __launch_bounds__(256) void k_w_angular(int in, const float* __restri
     for (int i = threadIdx.x; i < in; i += 256) Wt[(int64_t)o * in + i] = (fmaxf(w[i], 0.f) + 1e-4f) / nr;
 }
 
-// vMF encoder input per row: xn = normalize(log1p(x)); x~ = (xn - x_mean) / sdv  (vmf.hh:255-257)
-// and the observed direction y = normalize(log1p(relu(x)) + eps) kept in X (vmf.hh:421-422)
-__global__ __launch_bounds__(256) void k_w_xn_vmf(int D, float epsD, float* __restrict__ X, const float* __restrict__ xm,
-                                                  const float* __restrict__ gv, float* __restrict__ Xn) {
-    __shared__ float red[4];
-    const int64_t o = (int64_t)blockIdx.x * D;
-    float s1 = 0.f, s2 = 0.f;
-    for (int g = threadIdx.x; g < D; g += 256) {
-        const float x = X[o + g];
-        const float lx = log1pf(x), ly = log1pf(fmaxf(x, 0.f)) + epsD;
-        s1 += lx * lx;
-        s2 += ly * ly;
-    }
-    s1 = wblock_sum(s1, red);
-    s2 = wblock_sum(s2, red);
-    const float n1 = fmaxf(sqrtf(s1), 1e-12f), n2 = fmaxf(sqrtf(s2), 1e-12f);
-    for (int g = threadIdx.x; g < D; g += 256) {
-        const float x = X[o + g];
-        Xn[o + g] = (log1pf(x) / n1 - xm[g]) / gv[g];
-        X[o + g] = (log1pf(fmaxf(x, 0.f)) + epsD) / n2;
-    }
-}
-
-// vMF decoder row: LG = exp(z_dec(z)) (the final Linear's output, exponentiated in place) + hc
-// (U holds c Wcd^T + bcd); r = normalize(v); cos_b = <y_b, r_b>; backward
+// vMF decoder row (vmf.hh:283-304, 419-440): h = exp(z_dec(z)) (the final Linear's output,
+// exponentiated in place in LG), v = h + hc with hc = covar_decoding_(c) (inline for C <= CMAX,
+// else read from U), r = normalize(v), y = normalize(log1p(relu(x)) + eps) from the raw batch and
+// its row scale (k_w_densify2), cos_b = <y_b, r_b>; backward:
 //   dr = -(kappa / n) y, dv = (dr - r <r, dr>) / |v|, U <- dv (covar_decoding_ grads),
-//   G <- dv * exp(.) (the final Linear's output gradient)
+//   G <- dv * h (the final Linear's output gradient)
 struct WVRow {
-    int D;
-    float inv_n;
+    int D, C;
+    float inv_n, epsD;
     float *LG, *U, *G;
-    const float* Y;
+    const float* X;
+    const float* rs2;                    // 1 / |log1p(relu(x_b)) + eps|
+    const float *Cb, *Wcd, *bcd;         // hc inline (Cb non-null) or from U
     const float* vk;  // kappa scalars (VK_KAPPA)
     float* cosr;
     int with_grads;
 };
 __global__ __launch_bounds__(256) void k_w_vmf_row(WVRow a) {
     __shared__ float red[4];
-    const int64_t o = (int64_t)blockIdx.x * a.D;
-    float ss = 0.f;
+    const int b = blockIdx.x;
+    const int64_t o = (int64_t)b * a.D;
+    float cb[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) cb[c] = (a.Cb && c < a.C) ? a.Cb[(int64_t)b * a.C + c] : 0.f;
+    auto hc = [&](int g) {
+        if (!a.Cb) return a.U[o + g];
+        float v = a.bcd[g];
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < a.C) v = fmaf(cb[c], a.Wcd[(int64_t)g * a.C + c], v);
+        return v;
+    };
+    const float ry = a.rs2[b];
+    auto yv = [&](int g) {
+        const float x = a.X[o + g];
+        return ((x > 0.f ? log1p_acc(x) : 0.f) + a.epsD) * ry;
+    };
+    float ss = 0.f, cr = 0.f;
     for (int g = threadIdx.x; g < a.D; g += 256) {
-        const float h = expf(a.LG[o + g]);
+        const float h = fexp(a.LG[o + g]);
         a.LG[o + g] = h;
-        const float v = h + a.U[o + g];
-        ss += v * v;
+        const float v = h + hc(g);
+        ss = fmaf(v, v, ss);
+        cr = fmaf(yv(g), v, cr);
     }
     ss = wblock_sum(ss, red);
-    const float nv = sqrtf(ss), nr = fmaxf(nv, 1e-12f);
-    float c = 0.f;
-    for (int g = threadIdx.x; g < a.D; g += 256) c += a.Y[o + g] * ((a.LG[o + g] + a.U[o + g]) / nr);
-    c = wblock_sum(c, red);
-    if (threadIdx.x == 0) a.cosr[blockIdx.x] = c;
+    cr = wblock_sum(cr, red);
+    const float nv = sqrtf(ss), nr = fmaxf(nv, 1e-12f), inr = 1.f / nr;
+    const float c = cr * inr;
+    if (threadIdx.x == 0) a.cosr[b] = c;
     if (!a.with_grads) return;
     const float kn = a.vk[0] * a.inv_n;
     // <r, dr> = -(kappa / n) cos;  dv = (dr - r <r, dr>) / nr while nv > eps (else dr / eps)
@@ -598,9 +1376,9 @@ __global__ __launch_bounds__(256) void k_w_vmf_row(WVRow a) {
     const bool big = nv > 1e-12f;
     for (int g = threadIdx.x; g < a.D; g += 256) {
         const float h = a.LG[o + g];
-        const float r = (h + a.U[o + g]) / nr;
-        const float dr = -kn * a.Y[o + g];
-        const float dv = big ? (dr - r * rdr) / nr : dr / nr;
+        const float r = (h + hc(g)) * inr;
+        const float dr = -kn * yv(g);
+        const float dv = (big ? fmaf(-r, rdr, dr) : dr) * inr;
         a.U[o + g] = dv;
         a.G[o + g] = dv * h;
     }
@@ -746,14 +1524,17 @@ hipError_t wide_create(Engine* e) {
     hipError_t er;
 #define WA(p, n) if ((er = walloc(&(p), (n))) != hipSuccess) return er
     WA(w->X, Bp * D);
-    WA(w->Xn, Bp * D);
+    if (e->cfg.dtype == MMVAE_DTYPE_F32) WA(w->Xn, Bp * D);
+    if (e->cfg.model == MMVAE_MODEL_NB && R > RMAX) WA(w->Uin, Bp * D);
     WA(w->LG, Bp * D);
     WA(w->G, Bp * D);
     WA(w->U, Bp * D);
-    WA(w->gvec, 4 * D);
+    WA(w->gvec, 5 * D);
     WA(w->one, 1);
     w->ws_cap = std::max<int64_t>(int64_t(8) << 20, 4 * D);
     WA(w->ws, w->ws_cap);
+    w->cr_cap = 64 * CR_QMAX * ((D + 3) / 4 * 4);
+    WA(w->cr_part, w->cr_cap);
     WA(w->Cb, Bp * C);
     WA(w->rowv, 8 * Bp);
     for (float** p : {&w->Mr, &w->Ar, &w->Ce, &w->Mn, &w->Z, &w->Ep, &w->dZ, &w->dM, &w->dA}) WA(*p, Bp * K);
@@ -786,7 +1567,7 @@ hipError_t wide_create(Engine* e) {
 void wide_destroy(Engine* e) {
     WideState* w = e->wide_st;
     if (!w) return;
-    for (float* p : {w->X, w->Xn, w->LG, w->G, w->U, w->gvec, w->one, w->ws, w->Cb, w->rowv, w->Mr, w->Ar, w->Ce,
+    for (float* p : {w->X, w->Xn, w->Uin, w->LG, w->G, w->U, w->gvec, w->one, w->ws, w->cr_part, w->Cb, w->rowv, w->Mr, w->Ar, w->Ce,
                      w->Mn, w->Z, w->Ep, w->dZ, w->dM, w->dA, w->Hn, w->dHn, w->NMr, w->NAr, w->Zn, w->En, w->dZn,
                      w->dNM, w->dNA, w->dT0, w->dT1, w->wtil, w->lossv})
         if (p) hipFree(p);
@@ -819,9 +1600,11 @@ wide_poison_t wide_poison_bufs(Engine* e) {
     WideState* w = e->wide_st;
     if (!w) return v;
     const int64_t Bp = w->Bp, D = w->D, K = e->K, C = e->C, H = e->H, R = e->R;
-    for (float* p : {w->X, w->Xn, w->LG, w->G, w->U}) v.push_back({p, sizeof(float) * (size_t)(Bp * D)});
-    v.push_back({w->gvec, sizeof(float) * (size_t)(4 * D)});
+    for (float* p : {w->X, w->Xn, w->Uin, w->LG, w->G, w->U})
+        if (p) v.push_back({p, sizeof(float) * (size_t)(Bp * D)});
+    v.push_back({w->gvec, sizeof(float) * (size_t)(5 * D)});
     v.push_back({w->ws, sizeof(float) * (size_t)w->ws_cap});
+    v.push_back({w->cr_part, sizeof(float) * (size_t)w->cr_cap});
     v.push_back({w->Cb, sizeof(float) * (size_t)(Bp * C)});
     v.push_back({w->rowv, sizeof(float) * (size_t)(8 * Bp)});
     for (float* p : {w->Mr, w->Ar, w->Ce, w->Mn, w->Z, w->Ep, w->dZ, w->dM, w->dA})
@@ -837,29 +1620,129 @@ wide_poison_t wide_poison_bufs(Engine* e) {
     return v;
 }
 
-// staged block copy + densify (shared by step, eval and encode)
+// staged block copy + densify (shared by step, eval and encode); the NB raw-count row dots and
+// the vMF row scales ride along (k_w_densify2)
 static hipError_t wide_input(Engine* e, int64_t B) {
     WideState* w = e->wide_st;
     const StageCopy sc = stage_copy_args(e);
     hipLaunchKernelGGL(k_w_stage, dim3((sc.n16 + 255) / 256), dim3(256), 0, e->stream, sc.src, sc.dst, sc.n16);
-    hipLaunchKernelGGL(k_w_densify, dim3((unsigned)B), dim3(256), 0, e->stream, (int)e->D, (int)e->C,
-                       (const int64_t*)e->d_cells, (const int64_t*)e->d_rowptr, (const int32_t*)e->d_col,
-                       (const float*)e->d_val, (const float*)e->d_covar, w->X, w->Cb);
+    WDens a;
+    std::memset(&a, 0, sizeof(a));
+    a.D = (int)e->D;
+    a.C = (int)e->C;
+    a.H = (int)e->H;
+    a.cells = e->d_cells;
+    a.rowptr = e->d_rowptr;
+    a.col = e->d_col;
+    a.val = e->d_val;
+    a.covar = e->d_covar;
+    a.X = w->X;
+    a.Cb = w->Cb;
+    if (e->cfg.model == MMVAE_MODEL_VMF) {
+        a.rs1 = w->rowv + 6 * w->Bp;
+        a.rs2 = w->rowv + 7 * w->Bp;
+        a.epsD = (float)(1e-2 / (double)(float)e->D);
+    } else {
+        a.dw = e->preg("depth.weight");
+        a.db = e->preg("depth.bias");
+        a.Wne = e->preg("nu_encoding.weight");
+        a.bne = e->preg("nu_encoding.bias");
+        a.dpre = w->rowv + 3 * w->Bp;
+        a.Hn = w->Hn;
+        if (e->H > HMAX) a.H = 0;  // (the wide nu encoder runs as a GEMM)
+    }
+    hipLaunchKernelGGL(k_w_densify2, dim3((unsigned)B), dim3(256), 0, e->stream, a);
     return hipGetLastError();
 }
 
-// the encoder chain from its input block (Xn, [B][D]) to the heads' input; returns it
-static const float* enc_forward(Engine* e, int B, const float* in, hipError_t& er) {
+// the encoder input transform of this step (GemmX): x_mean, 1 / sdv, the vMF row scale
+static GemmX enc_x(Engine* e) {
     WideState* w = e->wide_st;
-    const float* x = in;
+    GemmX x;
+    x.xm = e->preg("x_mean");
+    x.isd = w->gvec + 4 * w->D;
+    x.rs = e->cfg.model == MMVAE_MODEL_VMF ? w->rowv + 6 * w->Bp : nullptr;
+    return x;
+}
+
+// the encoder chain from the raw batch X to the heads' input; returns it.  The first Linear
+// takes enc_in(X) (nb.hh:408-410 / vmf.hh:253-257): on bf16 / x3 handles transformed inside the
+// GEMM, on f32 handles from the materialised block Xn (the exact f32 GEMM)
+static const float* enc_forward(Engine* e, int B, hipError_t& er) {
+    WideState* w = e->wide_st;
+    const GemmX gx = enc_x(e);
+    const float* x = nullptr;
     int64_t ld = e->D;
-    for (auto& L : w->enc) {
-        if ((er = linear_fwd(e, B, L.out, L.in, x, ld, L.W, L.b, L.act, L.out, L.relu ? 1 : 0)) != hipSuccess)
-            return nullptr;
+    for (size_t l = 0; l < w->enc.size(); ++l) {
+        WLayer& L = w->enc[l];
+        GemmOp g;
+        g.M = B; g.N = L.out; g.K = L.in;
+        g.sam = ld; g.sak = 1;
+        g.B = L.W; g.sbk = 1; g.sbn = L.in;
+        g.C = L.act; g.scm = L.out; g.scn = 1;
+        g.bias = L.b; g.act = L.relu ? 1 : 0;
+        if (l == 0 && e->cfg.dtype != MMVAE_DTYPE_F32) {
+            g.A = w->X;
+            er = gemm(e, g, &gx);
+        } else {
+            if (l == 0) {
+                const int64_t n = (int64_t)B * e->D;
+                hipLaunchKernelGGL(k_w_xn, dim3(grid_for(n)), dim3(256), 0, e->stream, n, (int)e->D, (const float*)w->X,
+                                   gx, w->Xn);
+                x = w->Xn;
+            }
+            g.A = x;
+            er = gemm(e, g);
+        }
+        if (er != hipSuccess) return nullptr;
         x = L.act;
         ld = L.out;
     }
     return x;
+}
+
+// column sums of Y [M][N] (row stride ly) into `o`: column 0 = a0 (null: ones) when has0, then
+// the n1 columns of A1 (row stride la1), at most CR_QMAX per launch; X2: the XPROD pair
+// (sum Y, sum Y enc_in(X2)) for the encoder's ln_x_sd gradient
+static hipError_t colred(Engine* e, int M, int N, const float* Y, int64_t ly, bool has0, const float* a0,
+                         const float* A1, int64_t la1, int n1, ColOut o, const float* X2 = nullptr,
+                         const GemmX* xf = nullptr) {
+    WideState* w = e->wide_st;
+    int done = 0;
+    for (bool first = true; first || done < n1; first = false) {
+        const int h0 = (first && has0) ? 1 : 0;
+        const int nc = X2 ? 1 : std::min(n1 - done, CR_QMAX - h0);
+        ColRed c;
+        std::memset(&c, 0, sizeof(c));
+        c.M = M;
+        c.N = N;
+        c.has0 = h0;
+        c.Q = h0 + nc;
+        c.a0 = a0;
+        c.A1 = A1 ? A1 + done : nullptr;
+        c.la1 = la1;
+        c.Y = Y;
+        c.ly = ly;
+        c.X2 = X2;
+        if (xf) c.xf = *xf;
+        c.part = w->cr_part;
+        const int64_t NQ = (int64_t)c.Q * ((N + 3) / 4 * 4);
+        int chunks = (int)std::min<int64_t>(std::max(1, M / 64), w->cr_cap / NQ);
+        chunks = std::max(1, std::min(chunks, 64));
+        c.rows_per = (M + chunks - 1) / chunks;
+        chunks = (M + c.rows_per - 1) / c.rows_per;
+        const dim3 grid((unsigned)((N + 1023) / 1024), (unsigned)chunks);
+        if (X2) hipLaunchKernelGGL(k_colred<true>, grid, dim3(256), 0, e->stream, c);
+        else hipLaunchKernelGGL(k_colred<false>, grid, dim3(256), 0, e->stream, c);
+        ColOut oc = o;
+        if (done) oc.o1 = o.o1 + done * o.q1;
+        const int64_t nq = (int64_t)N * c.Q;
+        hipLaunchKernelGGL(k_colred_fin, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, e->stream, N, c.Q, h0, chunks,
+                           (const float*)w->cr_part, oc);
+        done += nc;
+        if (X2) break;
+    }
+    return hipGetLastError();
 }
 
 // back through the encoder chain from dh [B][E] (in dT0) to dXn [B][D] (into out)
@@ -958,23 +1841,22 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     float* r_d = w->rowv + 2 * w->Bp;
     float* r_dpre = w->rowv + 3 * w->Bp;
     float* r_ddpre = w->rowv + 4 * w->Bp;
-    WCHK(wide_input(e, B));
+    // the small Linears of the row side run inline (densify, the row kernel, the logit GEMM's
+    // epilogue) up to the fused kernels' widths; wider ones as GEMMs
+    const bool h_in = H <= HMAX, r_in = R <= RMAX, c_in = C <= CMAX;
+    WCHK(wide_input(e, B));  // + depth(x), nu_enc(x) (h_in)
     hipLaunchKernelGGL(k_w_gene, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)e->preg("ln_x_sd"),
                        1e-4f, w->gvec);
-    const int64_t nBD = (int64_t)B * D;
-    hipLaunchKernelGGL(k_w_xn_nb, dim3(grid_for(nBD)), dim3(256), 0, e->stream, nBD, D, (const float*)w->X,
-                       (const float*)e->preg("x_mean"), (const float*)w->gvec, w->Xn);
     hipError_t er = hipSuccess;
-    const float* h = enc_forward(e, B, w->Xn, er);
+    const float* h = enc_forward(e, B, er);
     WCHK(er);
     WCHK(heads_fwd(e, B, h, "mu_representation_mean", "mu_representation_logvariance", true));
-    // overdispersion encoder on raw x (nb.hh:444-451), depth (nb.hh:400, 498)
-    WCHK(linear_fwd(e, B, H, D, w->X, D, e->preg("nu_encoding.weight"), e->preg("nu_encoding.bias"), w->Hn, H));
+    // overdispersion encoder on raw x (nb.hh:444-451)
+    if (!h_in) WCHK(linear_fwd(e, B, H, D, w->X, D, e->preg("nu_encoding.weight"), e->preg("nu_encoding.bias"), w->Hn, H));
     WCHK(linear_fwd(e, B, R, H, w->Hn, H, e->preg("nu_representation_mean.weight"),
                     e->preg("nu_representation_mean.bias"), w->NMr, R));
     WCHK(linear_fwd(e, B, R, H, w->Hn, H, e->preg("nu_representation_logvariance.weight"),
                     e->preg("nu_representation_logvariance.bias"), w->NAr, R));
-    WCHK(linear_fwd(e, B, 1, D, w->X, D, e->preg("depth.weight"), e->preg("depth.bias"), r_dpre, 1));
     WLat la;
     std::memset(&la, 0, sizeof(la));
     la.B = B; la.K = K; la.R = R;
@@ -986,36 +1868,78 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     la.ss = e->d_ss;
     la.seed = e->cfg.seed;
     hipLaunchKernelGGL(k_w_latent, dim3(B), dim3(256), 0, e->stream, la);
-    // decoders: logits = mu_dec(z) + covar_dec(c) (+ mu_bias in the row kernel), u = nu_dec(z_nu)
+    // logits = mu_dec(z) + covar_dec(c) + mu_bias (nb.hh:433-442) in one GEMM: the covariate
+    // Linear and both biases in its epilogue
     const float* zd = dec_hidden_fwd(e, B, er);
     WCHK(er);
     const WLayer& F = w->dec.back();
-    WCHK(linear_fwd(e, B, D, F.in, zd, F.in, F.W, F.b, w->LG, D));
-    WCHK(linear_fwd(e, B, D, C, w->Cb, C, e->preg("covar_decoding.weight"), e->preg("covar_decoding.bias"), w->LG,
-                    D, 0, 1));
-    WCHK(linear_fwd(e, B, D, R, w->Zn, R, e->preg("nu_decoding.weight"), e->preg("nu_decoding.bias"), w->U, D));
+    {
+        GemmOp g;
+        g.M = B; g.N = D; g.K = F.in;
+        g.A = zd; g.sam = F.in; g.sak = 1;
+        g.B = F.W; g.sbk = 1; g.sbn = F.in;
+        g.C = w->LG; g.scm = D; g.scn = 1;
+        g.bias = F.b;
+        g.bias2 = e->preg("mu_bias");
+        if (c_in) {
+            g.ca = w->Cb; g.lca = C;
+            g.cw = e->preg("covar_decoding.weight"); g.lcw = C;
+            g.cbias = e->preg("covar_decoding.bias");
+            g.nc = C;
+        }
+        WCHK(gemm(e, g));
+    }
+    if (!c_in)
+        WCHK(linear_fwd(e, B, D, C, w->Cb, C, e->preg("covar_decoding.weight"), e->preg("covar_decoding.bias"), w->LG,
+                        D, 0, 1));
+    // u = nu_dec(z_nu) (nb.hh:458): inline in the row kernel, or a GEMM for R > RMAX
+    if (!r_in) WCHK(linear_fwd(e, B, D, R, w->Zn, R, e->preg("nu_decoding.weight"), e->preg("nu_decoding.bias"), w->Uin, D));
     WNbRow rw;
-    rw.D = D; rw.inv_n = inv_n;
-    rw.LG = w->LG; rw.G = w->G; rw.U = w->U;
-    rw.X = w->X; rw.mu_bias = e->preg("mu_bias"); rw.nu_bias = e->preg("nu_bias");
+    std::memset(&rw, 0, sizeof(rw));
+    rw.D = D; rw.R = R; rw.inv_n = inv_n;
+    rw.LG = w->LG; rw.G = w->G; rw.U = w->U; rw.Uin = w->Uin; rw.X = w->X;
+    rw.cells = e->d_cells;
+    rw.rowptr = e->d_rowptr;
+    rw.col = e->d_col;
+    rw.val = e->d_val;
+    if (r_in) {
+        rw.Zn = w->Zn;
+        rw.Wnd = e->preg("nu_decoding.weight");
+        rw.bnd = e->preg("nu_decoding.bias");
+        rw.dZn = w->dZn;
+    }
+    rw.nu_bias = e->preg("nu_bias");
     rw.dv = r_d; rw.dpre = r_dpre; rw.lossr = r_loss; rw.ddpre = r_ddpre;
     rw.with_grads = update ? 1 : 0;
-    hipLaunchKernelGGL(k_w_nb_row, dim3(B), dim3(256), 0, e->stream, rw);
+    if (D % 4 == 0 && (size_t)D * 4 <= 150 * 1024)  // the row in LDS (2 workgroups per CU up to 20k genes)
+        hipLaunchKernelGGL(k_w_nb_row_lds, dim3(B), dim3(512), (size_t)D * 4, e->stream, rw);
+    else
+        hipLaunchKernelGGL(k_w_nb_row, dim3(B), dim3(256), 0, e->stream, rw);
     hipLaunchKernelGGL(k_w_loss, dim3(1), dim3(256), 0, e->stream, B, (const float*)r_loss, (const float*)r_kl, beta,
                        inv_n, 0.f, e->d_out);
     if (!update) return hipGetLastError();
     // ---- backward ----
-    // decoder side gene vectors: mu_bias, covar_decoding.*, nu_bias, nu_decoding.*
-    WCHK(colsum(e, B, D, w->G, D, e->greg("mu_bias")));
-    WCHK(colsum(e, B, D, w->G, D, e->greg("covar_decoding.bias")));
-    WCHK(linear_dw(e, B, D, C, w->G, D, w->Cb, C, e->greg("covar_decoding.weight")));
-    WCHK(colsum(e, B, D, w->U, D, e->greg("nu_bias"), -1.f));
-    WCHK(colsum(e, B, D, w->U, D, e->greg("nu_decoding.bias")));
-    WCHK(linear_dw(e, B, D, R, w->U, D, w->Zn, R, e->greg("nu_decoding.weight")));
-    WCHK(linear_dx(e, B, D, R, w->U, D, e->preg("nu_decoding.weight"), w->dZn, R));
-    // depth
-    WCHK(linear_dw(e, B, 1, D, r_ddpre, 1, w->X, D, e->greg("depth.weight")));
-    WCHK(colsum(e, B, 1, r_ddpre, 1, e->greg("depth.bias")));
+    // decoder-side gene vectors from the batch sums of dL/dlogit (G) and dL/du (U)
+    {
+        ColOut o;
+        o.o0 = e->greg("mu_bias");
+        o.o0b = e->greg("covar_decoding.bias");
+        o.o1 = e->greg("covar_decoding.weight");
+        o.q1 = 1;
+        o.s1 = C;
+        WCHK(colred(e, B, D, w->G, D, true, nullptr, w->Cb, C, C, o));
+    }
+    {
+        ColOut o;
+        o.o0 = e->greg("nu_decoding.bias");
+        o.o0b = e->greg("nu_bias");
+        o.beta0 = -1.f;  // u = nu_dec(z_nu) - nu_bias
+        o.o1 = e->greg("nu_decoding.weight");
+        o.q1 = 1;
+        o.s1 = R;
+        WCHK(colred(e, B, D, w->U, D, true, nullptr, w->Zn, R, R, o));
+    }
+    if (!r_in) WCHK(linear_dx(e, B, D, R, w->U, D, e->preg("nu_decoding.weight"), w->dZn, R));
     // decoder chain -> dz, then the latent
     WCHK(dec_backward(e, B));
     WLatB lb;
@@ -1032,13 +1956,26 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     WCHK(colsum(e, B, R, w->dNA, R, e->greg("nu_representation_logvariance.bias")));
     WCHK(linear_dx(e, B, R, H, w->dNM, R, e->preg("nu_representation_mean.weight"), w->dHn, H));
     WCHK(linear_dx(e, B, R, H, w->dNA, R, e->preg("nu_representation_logvariance.weight"), w->dHn, H, 1));
-    WCHK(linear_dw(e, B, H, D, w->dHn, H, w->X, D, e->greg("nu_encoding.weight")));
+    // the raw-count Linears' weights from one pass over the batch: depth (nb.hh:400) and nu_enc
+    {
+        ColOut o;
+        o.o0 = e->greg("depth.weight");
+        o.o1 = e->greg("nu_encoding.weight");
+        o.q1 = D;
+        o.s1 = 1;
+        WCHK(colred(e, B, D, w->X, D, true, r_ddpre, w->dHn, H, H, o));
+    }
+    WCHK(colsum(e, B, 1, r_ddpre, 1, e->greg("depth.bias")));
     WCHK(colsum(e, B, H, w->dHn, H, e->greg("nu_encoding.bias")));
     // encoder chain -> dXn (into G: the decoder's gradient block is consumed), x_mean / ln_x_sd
     WCHK(enc_backward(e, B, w->G));
-    WCHK(colsum(e, B, D, w->G, D, w->gvec + 2 * D));
-    hipLaunchKernelGGL(k_w_mul, dim3(grid_for(nBD)), dim3(256), 0, e->stream, nBD, (const float*)w->Xn, w->G);
-    WCHK(colsum(e, B, D, w->G, D, w->gvec + 3 * D));
+    {
+        const GemmX gx = enc_x(e);
+        ColOut o;
+        o.o0 = w->gvec + 2 * D;
+        o.o1 = w->gvec + 3 * D;
+        WCHK(colred(e, B, D, w->G, D, true, nullptr, nullptr, 0, 1, o, w->X, &gx));
+    }
     hipLaunchKernelGGL(k_w_xgrad, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)(w->gvec + 2 * D),
                        (const float*)w->gvec, e->greg("x_mean"), e->greg("ln_x_sd"));
     return hipGetLastError();
@@ -1071,15 +2008,14 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     float* r_cos = w->rowv;
     float* r_kl = w->rowv + w->Bp;
     float* vk = w->rowv + 5 * w->Bp;
+    const bool c_in = C <= CMAX;
     const WVScal sc = wvscal(e);
-    WCHK(wide_input(e, B));
+    WCHK(wide_input(e, B));  // + the row scales of log1p(x) and y
     hipLaunchKernelGGL(k_w_vkappa, dim3(1), dim3(64), 0, e->stream, (const float*)e->preg("ln_kappa"), sc, vk);
     hipLaunchKernelGGL(k_w_gene, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)e->preg("ln_x_sd"),
                        epsD, w->gvec);
-    hipLaunchKernelGGL(k_w_xn_vmf, dim3(B), dim3(256), 0, e->stream, D, epsD, w->X, (const float*)e->preg("x_mean"),
-                       (const float*)w->gvec, w->Xn);
     hipError_t er = hipSuccess;
-    const float* h = enc_forward(e, B, w->Xn, er);
+    const float* h = enc_forward(e, B, er);
     WCHK(er);
     WCHK(heads_fwd(e, B, h, "representation_mean", "representation_logvariance", true));
     WLat la;
@@ -1096,17 +2032,31 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     WCHK(er);
     const WLayer& F = w->dec.back();
     WCHK(linear_fwd(e, B, D, F.in, zd, F.in, F.W, F.b, w->LG, D));
-    WCHK(linear_fwd(e, B, D, C, w->Cb, C, e->preg("covar_decoding_.weight"), e->preg("covar_decoding_.bias"), w->U, D));
+    if (!c_in)
+        WCHK(linear_fwd(e, B, D, C, w->Cb, C, e->preg("covar_decoding_.weight"), e->preg("covar_decoding_.bias"), w->U, D));
     WVRow rw;
-    rw.D = D; rw.inv_n = inv_n;
-    rw.LG = w->LG; rw.U = w->U; rw.G = w->G; rw.Y = w->X; rw.vk = vk; rw.cosr = r_cos;
+    std::memset(&rw, 0, sizeof(rw));
+    rw.D = D; rw.C = C; rw.inv_n = inv_n; rw.epsD = epsD;
+    rw.LG = w->LG; rw.U = w->U; rw.G = w->G; rw.X = w->X; rw.rs2 = w->rowv + 7 * w->Bp;
+    if (c_in) {
+        rw.Cb = w->Cb;
+        rw.Wcd = e->preg("covar_decoding_.weight");
+        rw.bcd = e->preg("covar_decoding_.bias");
+    }
+    rw.vk = vk; rw.cosr = r_cos;
     rw.with_grads = update ? 1 : 0;
     hipLaunchKernelGGL(k_w_vmf_row, dim3(B), dim3(256), 0, e->stream, rw);
     hipLaunchKernelGGL(k_w_vloss, dim3(1), dim3(256), 0, e->stream, B, (const float*)r_cos, (const float*)r_kl,
                        (const float*)vk, sc, beta, inv_n, e->d_out, e->greg("ln_kappa"), update ? 1 : 0);
     if (!update) return hipGetLastError();
-    WCHK(colsum(e, B, D, w->U, D, e->greg("covar_decoding_.bias")));
-    WCHK(linear_dw(e, B, D, C, w->U, D, w->Cb, C, e->greg("covar_decoding_.weight")));
+    {
+        ColOut o;
+        o.o0 = e->greg("covar_decoding_.bias");
+        o.o1 = e->greg("covar_decoding_.weight");
+        o.q1 = 1;
+        o.s1 = C;
+        WCHK(colred(e, B, D, w->U, D, true, nullptr, w->Cb, C, C, o));
+    }
     WCHK(dec_backward(e, B));
     WLatB lb;
     std::memset(&lb, 0, sizeof(lb));
@@ -1116,10 +2066,13 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     hipLaunchKernelGGL(k_w_latent_bwd, dim3(B), dim3(256), 0, e->stream, lb);
     WCHK(heads_bwd(e, B, h, "representation_mean", "representation_logvariance"));
     WCHK(enc_backward(e, B, w->G));
-    const int64_t nBD = (int64_t)B * D;
-    WCHK(colsum(e, B, D, w->G, D, w->gvec + 2 * D));
-    hipLaunchKernelGGL(k_w_mul, dim3(grid_for(nBD)), dim3(256), 0, e->stream, nBD, (const float*)w->Xn, w->G);
-    WCHK(colsum(e, B, D, w->G, D, w->gvec + 3 * D));
+    {
+        const GemmX gx = enc_x(e);
+        ColOut o;
+        o.o0 = w->gvec + 2 * D;
+        o.o1 = w->gvec + 3 * D;
+        WCHK(colred(e, B, D, w->G, D, true, nullptr, nullptr, 0, 1, o, w->X, &gx));
+    }
     hipLaunchKernelGGL(k_w_xgrad, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)(w->gvec + 2 * D),
                        (const float*)w->gvec, e->greg("x_mean"), e->greg("ln_x_sd"));
     return hipGetLastError();
@@ -1140,14 +2093,8 @@ hipError_t wide_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar) {
     const float epsD = (float)(1e-2 / (double)(float)D);
     hipLaunchKernelGGL(k_w_gene, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)e->preg("ln_x_sd"),
                        vmf ? epsD : 1e-4f, w->gvec);
-    if (vmf)
-        hipLaunchKernelGGL(k_w_xn_vmf, dim3((unsigned)B), dim3(256), 0, e->stream, D, epsD, w->X,
-                           (const float*)e->preg("x_mean"), (const float*)w->gvec, w->Xn);
-    else
-        hipLaunchKernelGGL(k_w_xn_nb, dim3(grid_for(B * D)), dim3(256), 0, e->stream, (int64_t)B * D, D,
-                           (const float*)w->X, (const float*)e->preg("x_mean"), (const float*)w->gvec, w->Xn);
     hipError_t er = hipSuccess;
-    const float* h = enc_forward(e, (int)B, w->Xn, er);
+    const float* h = enc_forward(e, (int)B, er);
     WCHK(er);
     if (vmf) WCHK(heads_fwd(e, (int)B, h, "representation_mean", "representation_logvariance", false));
     else WCHK(heads_fwd(e, (int)B, h, "mu_representation_mean", "mu_representation_logvariance", false));
