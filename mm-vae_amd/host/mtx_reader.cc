@@ -23,6 +23,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -389,6 +390,8 @@ int read_triplets(const char* path, int threads, int64_t& D, int64_t& N, std::ve
 
 static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, std::vector<int32_t>& col,
                       std::vector<float>& val, mmvae_csr* out);
+template <class T> struct RawBuf;
+static int finish_rows(int threads, int64_t N, std::vector<int64_t>& rp, int32_t* col, float* val, int64_t& nnz);
 static int stream_sorted_csr(const char* path, int threads, mmvae_csr* out);
 
 }  // namespace mmvae_host
@@ -472,11 +475,9 @@ int mmvae_mtx_read(const char* path, int threads, mmvae_csr* out) {
 }  // extern "C"
 
 namespace mmvae_host {
-// rows strictly increasing in gene (stable sort + keep-last dedupe where needed), then copied out
-static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, std::vector<int32_t>& col,
-                      std::vector<float>& val, mmvae_csr* out) {
-    const int64_t nnz_all = rp[(size_t)N];
-    // rows must be strictly increasing in gene: stable sort + keep-last dedupe where needed
+// rows strictly increasing in gene: a stable sort + keep-last dedupe of the rows that need it
+// (the reference's dense scatter overwrites, mmvae_io.hh:115-123), in place; rp / nnz updated
+static int finish_rows(int threads, int64_t N, std::vector<int64_t>& rp, int32_t* col, float* val, int64_t& nnz) {
     std::vector<int64_t> newlen((size_t)N);
     std::atomic<bool> compact{false};
     parallel_for(threads, N, [&](int, int64_t a, int64_t b) {
@@ -510,21 +511,28 @@ static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& r
             newlen[(size_t)r] = (int64_t)cg.size();
         }
     });
-    out->N = N;
-    out->D = D;
-    out->rowptr = static_cast<int64_t*>(std::malloc(sizeof(int64_t) * ((size_t)N + 1)));
-    int64_t nnz = nnz_all;
+    nnz = rp[(size_t)N];
     if (compact) {
         std::vector<int64_t> np((size_t)N + 1, 0);
         for (int64_t r = 0; r < N; ++r) np[(size_t)r + 1] = np[(size_t)r] + newlen[(size_t)r];
         nnz = np[(size_t)N];
         for (int64_t r = 0; r < N; ++r) {
-            std::memmove(col.data() + np[(size_t)r], col.data() + rp[(size_t)r], sizeof(int32_t) * (size_t)newlen[(size_t)r]);
-            std::memmove(val.data() + np[(size_t)r], val.data() + rp[(size_t)r], sizeof(float) * (size_t)newlen[(size_t)r]);
+            std::memmove(col + np[(size_t)r], col + rp[(size_t)r], sizeof(int32_t) * (size_t)newlen[(size_t)r]);
+            std::memmove(val + np[(size_t)r], val + rp[(size_t)r], sizeof(float) * (size_t)newlen[(size_t)r]);
         }
         rp.swap(np);
     }
+    return MMVAE_OK;
+}
+
+static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, std::vector<int32_t>& col,
+                      std::vector<float>& val, mmvae_csr* out) {
+    int64_t nnz = 0;
+    finish_rows(threads, N, rp, col.data(), val.data(), nnz);
+    out->N = N;
+    out->D = D;
     out->nnz = nnz;
+    out->rowptr = static_cast<int64_t*>(std::malloc(sizeof(int64_t) * ((size_t)N + 1)));
     out->col = static_cast<int32_t*>(std::malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1)));
     out->val = static_cast<float*>(std::malloc(sizeof(float) * (size_t)std::max<int64_t>(nnz, 1)));
     if (!out->rowptr || !out->col || !out->val) {
@@ -537,155 +545,384 @@ static int finish_csr(int threads, int64_t N, int64_t D, std::vector<int64_t>& r
     return MMVAE_OK;
 }
 
+// ---- streaming load of a column-sorted BGZF MatrixMarket file ------------------------------
+// (the mmutil convention: entries grouped by column = cell, as write_matrix_market_stream and
+// 10x-style matrix.mtx.gz files are).  File order is then CSR order, so the file streams straight
+// into the cell-major CSR: windows of whole BGZF blocks (64 MB compressed, MMVAE_MTX_WINDOW bytes
+// to override) are split into one contiguous block range per worker, and each worker inflates its
+// blocks one at a time into a block-sized buffer and parses the complete lines at once, while the
+// block is in cache (replaces visit_bgzf_block's inflate-then-scan, mmutil_bgzf_util.hh:53-151).
+// A worker's output is its genes and values in file order plus (cell, count) runs; the line cut
+// by each range boundary is stitched and parsed serially.  Neither the text (~12 B per entry) nor
+// a per-entry cell id is ever stored: peak memory ~ the CSR plus one compressed window.  Returns 1
+// (the caller takes the whole-file path) for input that is not BGZF or whose columns are not
+// sorted.
 
-// Streaming load of a column-sorted BGZF MatrixMarket file (the mmutil convention: entries grouped
-// by column = cell, as write_matrix_market_stream and 10x-style matrix.mtx.gz files are): windows
-// of whole BGZF blocks (64 MB compressed, MMVAE_MTX_WINDOW bytes to override) are inflated in
-// parallel and parsed straight into the cell-major CSR — file order is CSR order — so neither the
-// whole text (~12 B per entry) nor a triplet copy is ever held: peak memory ~ the CSR plus one
-// window.  Returns 1 (the caller takes the whole-file path) for input that is not BGZF or whose
-// columns are not sorted.
+// malloc-backed array with uninitialised growth (no zero fill of bytes about to be overwritten)
+template <class T>
+struct RawBuf {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    RawBuf() = default;
+    RawBuf(const RawBuf&) = delete;
+    RawBuf& operator=(const RawBuf&) = delete;
+    ~RawBuf() { std::free(p); }
+    bool reserve(size_t c) {
+        if (c <= cap) return true;
+        const size_t nc = std::max(c, cap + cap / 2 + 1024);
+        T* q = static_cast<T*>(std::realloc(p, nc * sizeof(T)));
+        if (!q) return false;
+        p = q;
+        cap = nc;
+        return true;
+    }
+    T* release() {
+        T* q = p;
+        p = nullptr;
+        n = cap = 0;
+        return q;
+    }
+};
+
+struct Run {
+    int32_t cell;
+    int64_t count;
+};
+
+struct StreamPart {
+    RawBuf<int32_t> gene;
+    RawBuf<float> val;
+    std::vector<Run> runs;
+    std::string head, tail;  // text before the range's first newline / after its last
+    bool any_nl = false;
+    bool ok = true;
+    std::string err;
+};
+
+// the complete lines of [p, e) into o (file order): '%' lines and lines with < 3 fields skipped,
+// as mmutil_bgzf_util.hh:102-127 does
+static bool stream_lines(const char* p, const char* e, int64_t D, int64_t N, StreamPart& o) {
+    // every entry line takes >= 6 bytes ("1 1 1\n")
+    if (!o.gene.reserve(o.gene.n + (size_t)(e - p) / 6 + 1) || !o.val.reserve(o.val.n + (size_t)(e - p) / 6 + 1)) {
+        o.err = "out of host memory";
+        return false;
+    }
+    int32_t* gp = o.gene.p;
+    float* vp = o.val.p;
+    size_t n = o.gene.n;
+    int32_t run_cell = o.runs.empty() ? -1 : o.runs.back().cell;
+    int64_t run_n = 0;  // entries of run_cell not yet added to its run
+    auto flush = [&] {
+        if (run_n) o.runs.back().count += run_n;
+        run_n = 0;
+    };
+    while (p < e) {
+        // fast path, the common line "gene cell count\n" (unsigned decimal integers, single
+        // blanks or tabs): anything else falls through to the general tokenizer below
+        {
+            const char* q = p;
+            uint64_t r = 0, c = 0, x = 0;
+            const char* d = q;
+            while ((unsigned)(*q - '0') < 10u) r = r * 10 + (uint64_t)(*q++ - '0');
+            if (q > d && q - d < 10 && (*q == ' ' || *q == '\t')) {
+                ++q;
+                d = q;
+                while ((unsigned)(*q - '0') < 10u) c = c * 10 + (uint64_t)(*q++ - '0');
+                if (q > d && q - d < 10 && (*q == ' ' || *q == '\t')) {
+                    ++q;
+                    d = q;
+                    while ((unsigned)(*q - '0') < 10u) x = x * 10 + (uint64_t)(*q++ - '0');
+                    if (q > d && q - d < 16 && *q == '\n' && r >= 1 && (int64_t)r <= D && c >= 1 && (int64_t)c <= N) {
+                        gp[n] = (int32_t)(r - 1);
+                        vp[n] = (float)x;
+                        ++n;
+                        if ((int32_t)(c - 1) == run_cell) {
+                            ++run_n;
+                        } else {
+                            flush();
+                            o.runs.push_back(Run{(int32_t)(c - 1), 1});
+                            run_cell = (int32_t)(c - 1);
+                        }
+                        p = q + 1;
+                        continue;
+                    }
+                }
+            }
+        }
+        flush();
+        const char* le = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+        if (!le) le = e;
+        if (*p != '%') {
+            const char* tb[3];
+            const char* te[3];
+            int nt = 0;
+            const char* q = p;
+            while (q < le && nt < 3) {
+                while (q < le && is_ws(*q)) ++q;
+                if (q >= le) break;
+                tb[nt] = q;
+                while (q < le && !is_ws(*q)) ++q;
+                te[nt++] = q;
+            }
+            if (nt == 3) {
+                const int64_t r = parse_int(tb[0], te[0]) - 1, c = parse_int(tb[1], te[1]) - 1;
+                if (r < 0 || r >= D || c < 0 || c >= N) {
+                    o.err = "entry (" + std::to_string(r + 1) + ", " + std::to_string(c + 1) + ") outside the " +
+                            std::to_string(D) + " x " + std::to_string(N) + " header";
+                    o.gene.n = n;
+                    o.val.n = n;
+                    return false;
+                }
+                gp[n] = (int32_t)r;
+                vp[n] = parse_float(tb[2], te[2]);
+                ++n;
+                if (!o.runs.empty() && o.runs.back().cell == (int32_t)c) ++o.runs.back().count;
+                else o.runs.push_back(Run{(int32_t)c, 1});
+                run_cell = (int32_t)c;
+            }
+        }
+        p = le + 1;
+    }
+    flush();
+    o.gene.n = n;
+    o.val.n = n;
+    return true;
+}
+
+// the streamed buffers handed to `out` as they are (no copy)
+static int finish_csr_raw(int threads, int64_t N, int64_t D, std::vector<int64_t>& rp, RawBuf<int32_t>& col,
+                          RawBuf<float>& val, mmvae_csr* out) {
+    if (!col.reserve(1) || !val.reserve(1)) return fail(MMVAE_E_ARG, "out of host memory");
+    int64_t nnz = 0;
+    finish_rows(threads, N, rp, col.p, val.p, nnz);
+    out->N = N;
+    out->D = D;
+    out->nnz = nnz;
+    out->rowptr = static_cast<int64_t*>(std::malloc(sizeof(int64_t) * ((size_t)N + 1)));
+    if (!out->rowptr) return fail(MMVAE_E_ARG, "out of host memory");
+    std::memcpy(out->rowptr, rp.data(), sizeof(int64_t) * ((size_t)N + 1));
+    out->col = col.release();
+    out->val = val.release();
+    return MMVAE_OK;
+}
+
 static int stream_sorted_csr(const char* path, int threads, mmvae_csr* out) {
+    // MMVAE_MTX_PROFILE=1: phase times (read, parallel inflate + parse, stitch + append, rows)
+    const bool prof = std::getenv("MMVAE_MTX_PROFILE") != nullptr;
+    double tp[4] = {0, 0, 0, 0};
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto since = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return fail(MMVAE_E_ARG, std::string("cannot open ") + path + ": " + std::strerror(errno));
     size_t WIN = (size_t)64 << 20;
     if (const char* ev = std::getenv("MMVAE_MTX_WINDOW")) WIN = std::max<size_t>((size_t)std::atoll(ev), 4096);
-    std::vector<unsigned char> cbuf;
-    size_t have = 0;
-    std::string carry;  // a partial last line
+    // two window buffers: the next window is read by a helper thread while this one is processed;
+    // the partial BGZF block left at a window's end (< 64 KB) moves to just before the next one's
+    // bytes (PAD of room), so a window is always one contiguous range
+    constexpr size_t PAD = (size_t)128 << 10;
+    RawBuf<unsigned char> wbuf[2];
+    if (!wbuf[0].reserve(PAD + WIN) || !wbuf[1].reserve(PAD + WIN)) {
+        std::fclose(fp);
+        return fail(MMVAE_E_ARG, "out of host memory");
+    }
+    int cb = 0;
+    size_t lead = 0;                                       // leftover bytes before wbuf[cb] + PAD
+    size_t got = std::fread(wbuf[0].p + PAD, 1, WIN, fp);  // this window's new bytes
     bool header = false, first = true;
     int64_t D = 0, N = 0, nnz_hdr = 0, last_cell = -1;
     std::vector<int64_t> rp;
-    std::vector<int32_t> col;
-    std::vector<float> val;
+    RawBuf<int32_t> col;
+    RawBuf<float> val;
     std::vector<BgzfBlock> blocks;
-    std::vector<char> text;
+    std::string carry;  // the partial line at the end of the previous window
     int rc = MMVAE_OK;
-    // complete lines [p, e): the header first, then the entries appended in file order
-    auto lines = [&](const char* p, const char* e) -> int {
-        while (!header && p < e) {
-            const char* le = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
-            if (!le) le = e;
-            if (*p != '%' && le > p) {
-                std::vector<char> h(p, le);
-                h.push_back('\n');
-                size_t pos;
-                if (!parse_header(h, pos, D, N, nnz_hdr)) return fail(MMVAE_E_ARG, std::string("no MatrixMarket size line in ") + path);
-                if (N >= INT32_MAX || D >= INT32_MAX) return fail(MMVAE_E_ARG, "matrix dimensions exceed int32");
-                header = true;
-                rp.assign((size_t)N + 1, 0);
-                col.reserve((size_t)std::max<int64_t>(nnz_hdr, 0));
-                val.reserve((size_t)std::max<int64_t>(nnz_hdr, 0));
+    // one line of text outside every worker's range (a stitched boundary line or the file's last)
+    auto single = [&](const std::string& line, StreamPart& sp) -> bool {
+        if (line.empty()) return true;
+        std::string l = line;
+        l.push_back('\n');
+        return stream_lines(l.data(), l.data() + l.size(), D, N, sp);
+    };
+    // entries of the parts, in order, appended to the CSR; false: columns not sorted
+    auto append = [&](std::vector<StreamPart*>& parts) -> int {
+        size_t tot = col.n;
+        std::vector<size_t> off(parts.size() + 1, col.n);
+        for (size_t k = 0; k < parts.size(); ++k) {
+            if (!parts[k]->err.empty()) return fail(MMVAE_E_ARG, std::string(path) + ": " + parts[k]->err);
+            for (const Run& r : parts[k]->runs) {
+                if (r.cell < last_cell) return 1;  // not column-sorted: the whole-file path
+                last_cell = r.cell;
+                rp[(size_t)r.cell + 1] += r.count;
             }
-            p = le + 1;
+            tot += parts[k]->gene.n;
+            off[k + 1] = tot;
         }
-        if (p >= e) return MMVAE_OK;
-        const size_t body = (size_t)(e - p);
-        const int nch = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * 2, body / (1 << 16) + 1));
-        std::vector<const char*> cut(nch + 1);
-        cut[0] = p;
-        cut[nch] = e;
-        for (int k = 1; k < nch; ++k) {
-            const char* c = std::max(p + body * k / nch, cut[k - 1]);
-            while (c < e && c[-1] != '\n') ++c;
-            cut[k] = c;
-        }
-        std::vector<Chunk> ch(nch);
-        parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
-            for (int64_t k = a; k < b; ++k) parse_chunk(cut[k], cut[k + 1], D, N, ch[(size_t)k]);
-        });
-        // chunks in file order: sortedness across chunk boundaries and the output offsets (serial,
-        // per chunk); within a chunk the check, the copy and the row counts run in parallel.  A
-        // chunk counts every entry but those of its first cell, which may continue the previous
-        // chunk's last cell: that head count is added here, so no two chunks write one counter.
-        std::vector<size_t> off(nch + 1, col.size());
-        for (int k = 0; k < nch; ++k) {
-            const Chunk& c = ch[(size_t)k];
-            if (!c.err.empty()) return fail(MMVAE_E_ARG, std::string(path) + ": " + c.err);
-            if (!c.cell.empty()) {
-                if (c.cell.front() < last_cell) return 1;  // not column-sorted: the whole-file path
-                last_cell = c.cell.back();
-            }
-            off[(size_t)k + 1] = off[(size_t)k] + c.cell.size();
-        }
-        col.resize(off[(size_t)nch]);
-        val.resize(off[(size_t)nch]);
-        std::vector<int64_t> head(nch, 0);
-        std::atomic<bool> sorted{true};
-        parallel_for(threads, nch, [&](int, int64_t a, int64_t b) {
+        if (!col.reserve(tot) || !val.reserve(tot)) return fail(MMVAE_E_ARG, "out of host memory");
+        parallel_for(threads, (int64_t)parts.size(), [&](int, int64_t a, int64_t b) {
             for (int64_t k = a; k < b; ++k) {
-                const Chunk& c = ch[(size_t)k];
-                const size_t n = c.cell.size();
-                if (!n) continue;
-                std::memcpy(col.data() + off[(size_t)k], c.gene.data(), n * sizeof(int32_t));
-                std::memcpy(val.data() + off[(size_t)k], c.val.data(), n * sizeof(float));
-                const int64_t c0 = c.cell[0];
-                int64_t h = 0;
-                for (size_t i = 0; i < n; ++i) {
-                    if (i && c.cell[i] < c.cell[i - 1]) {
-                        sorted = false;
-                        break;
-                    }
-                    if (c.cell[i] == c0) ++h;
-                    else rp[(size_t)c.cell[i] + 1]++;
-                }
-                head[(size_t)k] = h;
+                const StreamPart& sp = *parts[(size_t)k];
+                if (!sp.gene.n) continue;
+                std::memcpy(col.p + off[(size_t)k], sp.gene.p, sp.gene.n * sizeof(int32_t));
+                std::memcpy(val.p + off[(size_t)k], sp.val.p, sp.val.n * sizeof(float));
             }
         });
-        if (!sorted) return 1;
-        for (int k = 0; k < nch; ++k)
-            if (!ch[(size_t)k].cell.empty()) rp[(size_t)ch[(size_t)k].cell[0] + 1] += head[(size_t)k];
+        col.n = val.n = tot;
         return MMVAE_OK;
     };
     for (bool eof = false; !eof && rc == MMVAE_OK;) {
-        cbuf.resize(have + WIN);
-        const size_t r = std::fread(cbuf.data() + have, 1, WIN, fp);
-        have += r;
-        eof = r == 0;
+        auto t0 = now();
+        unsigned char* const cbuf = wbuf[cb].p + PAD - lead;
+        const size_t have = lead + got;
+        eof = got == 0;
+        size_t got_next = 0;
+        std::thread reader;
+        if (!eof) reader = std::thread([&] { got_next = std::fread(wbuf[cb ^ 1].p + PAD, 1, WIN, fp); });
+        struct Join {
+            std::thread& t;
+            ~Join() {
+                if (t.joinable()) t.join();
+            }
+        } join_reader{reader};
         size_t used = 0;
-        if (!scan_bgzf_window(cbuf.data(), have, blocks, used)) {
+        if (!scan_bgzf_window(cbuf, have, blocks, used)) {
             rc = first ? 1 : fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + path);
             break;
         }
-        first = false;
         if (eof && used != have) {
             rc = fail(MMVAE_E_ARG, std::string("truncated BGZF block at the end of ") + path);
             break;
         }
-        if (blocks.empty()) continue;
-        const size_t total = blocks.back().out_off + blocks.back().out_len;
-        text.resize(carry.size() + total);
-        std::memcpy(text.data(), carry.data(), carry.size());
-        std::atomic<bool> ok{true};
-        parallel_for(threads, (int64_t)blocks.size(), [&](int, int64_t a, int64_t b) {
-            for (int64_t i = a; i < b; ++i) {
-                const BgzfBlock& k = blocks[(size_t)i];
-                if (!inflate_raw(cbuf.data() + k.in_off, k.in_len, text.data() + carry.size() + k.out_off, k.out_len))
-                    ok = false;
+        auto next_window = [&] {
+            if (reader.joinable()) reader.join();
+            const size_t left = have - used;
+            std::memcpy(wbuf[cb ^ 1].p + PAD - left, cbuf + used, left);
+            lead = left;
+            got = got_next;
+            cb ^= 1;
+        };
+        if (blocks.empty()) {
+            next_window();
+            continue;
+        }
+        size_t skip = 0;  // bytes of the first block taken by the header lines
+        if (first) {
+            first = false;
+            std::vector<char> b0(blocks[0].out_len);
+            if (!inflate_raw(cbuf + blocks[0].in_off, blocks[0].in_len, b0.data(), b0.size())) {
+                rc = fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + path);
+                break;
+            }
+            size_t pos = 0;
+            if (!parse_header(b0, pos, D, N, nnz_hdr) || pos > b0.size()) {
+                rc = 1;  // no size line in the first block: the whole-file path reports it
+                break;
+            }
+            if (N >= INT32_MAX || D >= INT32_MAX) {
+                rc = fail(MMVAE_E_ARG, "matrix dimensions exceed int32");
+                break;
+            }
+            header = true;
+            skip = pos;
+            rp.assign((size_t)N + 1, 0);
+            if (!col.reserve((size_t)std::max<int64_t>(nnz_hdr, 0)) || !val.reserve((size_t)std::max<int64_t>(nnz_hdr, 0))) {
+                rc = fail(MMVAE_E_ARG, "out of host memory");
+                break;
+            }
+        }
+        tp[0] += since(t0);
+        t0 = now();
+        const int nw = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, blocks.size()));
+        std::vector<StreamPart> part((size_t)nw);
+        parallel_for(nw, nw, [&](int, int64_t w0, int64_t w1) {
+            std::vector<char> buf;
+            for (int64_t w = w0; w < w1; ++w) {
+                StreamPart& sp = part[(size_t)w];
+                const size_t b0 = blocks.size() * (size_t)w / (size_t)nw, b1 = blocks.size() * (size_t)(w + 1) / (size_t)nw;
+                std::string pend;  // a line continued from the previous block of this range
+                for (size_t i = b0; i < b1 && sp.ok; ++i) {
+                    const BgzfBlock& k = blocks[i];
+                    buf.resize(k.out_len);
+                    if (!inflate_raw(cbuf + k.in_off, k.in_len, buf.data(), k.out_len)) {
+                        sp.ok = false;
+                        sp.err = std::string("corrupt BGZF block");
+                        break;
+                    }
+                    const char* t = buf.data();
+                    const char* te = t + k.out_len;
+                    if (i == 0 && skip) {  // the header (whole lines) is consumed
+                        t += skip;
+                        sp.any_nl = true;
+                    }
+                    if (!sp.any_nl) {
+                        const char* nl = static_cast<const char*>(std::memchr(t, '\n', (size_t)(te - t)));
+                        if (!nl) {
+                            sp.head.append(t, (size_t)(te - t));
+                            continue;
+                        }
+                        sp.head.append(t, (size_t)(nl - t));
+                        sp.any_nl = true;
+                        t = nl + 1;
+                    }
+                    const char* last = te;
+                    while (last > t && last[-1] != '\n') --last;  // complete lines end at last
+                    if (last == t) {
+                        pend.append(t, (size_t)(te - t));
+                        continue;
+                    }
+                    if (!pend.empty()) {
+                        const char* nl = static_cast<const char*>(std::memchr(t, '\n', (size_t)(te - t)));
+                        pend.append(t, (size_t)(nl - t + 1));
+                        if (!stream_lines(pend.data(), pend.data() + pend.size(), D, N, sp)) sp.ok = false;
+                        pend.clear();
+                        t = nl + 1;
+                    }
+                    if (t < last && !stream_lines(t, last, D, N, sp)) sp.ok = false;
+                    pend.assign(last, (size_t)(te - last));
+                }
+                sp.tail = pend;
             }
         });
-        if (!ok) {
-            rc = fail(MMVAE_E_ARG, std::string("corrupt BGZF block in ") + path);
-            break;
+        tp[1] += since(t0);
+        t0 = now();
+        // stitch: carry + the first range's head, each range's tail + the next range's head
+        std::vector<StreamPart> glue((size_t)nw);
+        std::vector<StreamPart*> order;
+        for (int w = 0; w < nw; ++w) {
+            StreamPart& sp = part[(size_t)w];
+            if (!sp.ok && sp.err.empty()) sp.err = "parse error";
+            if (!sp.any_nl) {  // the range holds no line end: all of it continues the carry
+                carry += sp.head;
+                continue;
+            }
+            carry += sp.head;
+            if (!single(carry, glue[(size_t)w])) glue[(size_t)w].ok = false;
+            carry = sp.tail;
+            order.push_back(&glue[(size_t)w]);
+            order.push_back(&sp);
         }
-        size_t nl = text.size();
-        while (nl > 0 && text[nl - 1] != '\n') --nl;  // the last complete line ends at nl
-        carry.assign(text.data() + nl, text.size() - nl);
-        rc = lines(text.data(), text.data() + nl);
-        std::memmove(cbuf.data(), cbuf.data() + used, have - used);
-        have -= used;
+        rc = append(order);
+        next_window();
+        tp[2] += since(t0);
     }
     std::fclose(fp);
     if (rc == MMVAE_OK && !carry.empty()) {
-        carry.push_back('\n');
-        rc = lines(carry.data(), carry.data() + carry.size());
+        StreamPart last;
+        if (!single(carry, last)) rc = fail(MMVAE_E_ARG, std::string(path) + ": " + last.err);
+        std::vector<StreamPart*> o{&last};
+        if (rc == MMVAE_OK) rc = append(o);
     }
     if (rc != MMVAE_OK) return rc;
     if (!header) return 1;
     for (int64_t i = 0; i < N; ++i) rp[(size_t)i + 1] += rp[(size_t)i];
-    std::vector<char>().swap(text);
-    std::vector<unsigned char>().swap(cbuf);
-    return finish_csr(threads, N, D, rp, col, val, out);
+    const auto t0 = now();
+    rc = finish_csr_raw(threads, N, D, rp, col, val, out);
+    tp[3] = since(t0);
+    if (prof)
+        std::fprintf(stderr, "mtx stream: read %.3f  inflate+parse %.3f  stitch+append %.3f  rows %.3f s\n", tp[0], tp[1],
+                     tp[2], tp[3]);
+    return rc;
 }
 }  // namespace mmvae_host
 

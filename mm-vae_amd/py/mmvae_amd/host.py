@@ -6,6 +6,7 @@ the counter-based bootstrap index generator and the train_vae_model driver
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -72,14 +73,19 @@ def _err(what, rc):
     raise MMVAEError(f"{what} failed ({rc}): {hlib().mmvae_host_last_error().decode()}")
 
 
+def _owned(ptr, n):
+    """numpy view of a malloc'd C array of n elements that frees it (mmvae_free) when the last
+    view is gone: the loader's buffers are handed over without a copy."""
+    a = np.ctypeslib.as_array(ptr, shape=(max(n, 1),))
+    weakref.finalize(a, hlib().mmvae_free, ctypes.cast(ptr, ctypes.c_void_p))
+    return a[:n]
+
+
 def _take(c):
-    n, nnz = c.N, c.nnz
-    rp = np.ctypeslib.as_array(c.rowptr, shape=(n + 1,)).copy()
-    col = np.ctypeslib.as_array(c.col, shape=(max(nnz, 1),))[:nnz].copy()
-    val = np.ctypeslib.as_array(c.val, shape=(max(nnz, 1),))[:nnz].copy()
-    D = c.D
-    hlib().mmvae_csr_free(ctypes.byref(c))
-    return rp, col, val, D
+    rp = _owned(c.rowptr, c.N + 1)
+    col = _owned(c.col, c.nnz)
+    val = _owned(c.val, c.nnz)
+    return rp, col, val, c.D
 
 
 def mtx_read(path, threads=0):

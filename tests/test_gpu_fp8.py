@@ -37,10 +37,12 @@ def test_fp8_against_oracle_fixtures(path):
         row[dtype] = {"loss_rel": abs(loss - want) / abs(want), "grad_rel": _grad_err(eng.grads(), params_of(z, "s0/grad/"))}
     TABLE[os.path.basename(path)] = row
     assert row["fp8"]["loss_rel"] <= 1e-2, row  # fp8 ELBO within 1e-2 rel
-    # gradients: documented, not parity.  With the encoder GEMM on e4m3 a tiny model's encoder
-    # output (a few genes' 3-mantissa-bit products, e.g. nb_k1: D = 30, K = 1) can lose most of
-    # its digits; the bound here only catches a broken scale (overflow / NaN, wrong unscale)
-    assert np.isfinite(row["fp8"]["grad_rel"]) and row["fp8"]["grad_rel"] <= 1.0, row
+    # gradients (documented, not parity): within 10 % norm-relative of the oracle on every
+    # fixture (measured 3-5 %, profiles/r3_fp8_accuracy.json), except nb_k1 (D = 30, K = 1): its
+    # single encoder output is a sum of a few 3-mantissa-bit products and loses most of its
+    # digits (measured 58 %), so it is held to 80 %
+    lim = 0.8 if os.path.basename(path) == "nb_k1.npz" else 0.1
+    assert np.isfinite(row["fp8"]["grad_rel"]) and row["fp8"]["grad_rel"] <= lim, row
 
 
 def test_fp8_configs4_shape_against_x3():
