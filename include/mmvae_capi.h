@@ -103,6 +103,16 @@ const char* mmvae_last_error(mmvae_h h);
  * covar: [N, C] row-major (NULL -> all ones, the reference's auto covariate). */
 int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
                      int64_t N, int64_t D, const float* covar);
+/* Host-resident dataset for data beyond HBM (the reference streams each batch from its BGZF
+ * file, mtx_data_block_t::read, mmvae_io.hh:208-245): the caller's cell-major CSR (and covariates,
+ * or NULL for ones) stays in host memory, registered here as mapped pinned memory; the caller keeps
+ * the arrays alive and unchanged until mmvae_destroy or the next upload / synth / stream.  Every
+ * step's device work then opens with a gather kernel that pulls the batch's rows over PCIe into a
+ * per-step batch CSR in HBM (two slots, alternating with the staging slots) and indexes it; the
+ * kernels after it are the resident path's, on the batch's rows.  Results are bit-identical to
+ * mmvae_upload_csr of the same data.  HBM holds O(B nnz_b) of the dataset instead of O(N nnz). */
+int mmvae_stream_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
+                     int64_t N, int64_t D, const float* covar);
 /* Dataset size after upload/synth (mtx_data_block_t::ntot / nfeature, mmvae_io.hh:73-74). */
 int mmvae_dataset_size(mmvae_h h, int64_t* N, int64_t* D);
 /* Device-side synthetic dataset (bench / smoke): SURVEY §8(d) count distribution. */

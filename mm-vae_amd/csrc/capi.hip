@@ -218,7 +218,9 @@ static void use_slot(Engine* e, int s) {
     e->h_seg_pin = sl.block + Bp;
     e->h_perm_pin = reinterpret_cast<int32_t*>(e->h_seg_pin + Bp / 16 + 1);
     e->h_ss = reinterpret_cast<StepScalars*>(e->h_perm_pin + Bp);
+    e->h_brp_pin = reinterpret_cast<int64_t*>(e->h_ss + 1);
     e->h_eps_pin = sl.eps;
+    stream_bind(e, s);
     e->ev_staged = sl.ev;
 }
 
@@ -407,14 +409,18 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // list segments int64 [Bp/16 + 1] | balancing permutation int32 [Bp]
     e->stage_bytes = sizeof(int64_t) * (size_t)(Bp + Bp / 16 + 1) + sizeof(int32_t) * (size_t)Bp + sizeof(StepScalars);
     e->stage_bytes = (e->stage_bytes + 15) / 16 * 16;  // copied in 16-byte chunks (StageCopy)
-    HIPCHK(e, hipMalloc((void**)&e->d_cells, e->stage_bytes));
+    e->stage_bytes_res = e->stage_bytes;
+    // (+ the batch rowptr [Bp + 1] of a streamed dataset, staged only in that mode)
+    const size_t stage_cap = (e->stage_bytes + sizeof(int64_t) * (size_t)(Bp + 1) + 15) / 16 * 16;
+    HIPCHK(e, hipMalloc((void**)&e->d_cells, stage_cap));
     e->d_seg = e->d_cells + Bp;
     e->d_perm = reinterpret_cast<int32_t*>(e->d_seg + Bp / 16 + 1);
     e->d_ss = reinterpret_cast<const StepScalars*>(e->d_perm + Bp);  // 8-aligned: Bp % 128 == 0
+    e->d_brp = reinterpret_cast<const int64_t*>(e->d_ss + 1);
     for (auto& sl : e->slots2) {
         // device-accessible, coherent: the step's prep kernel reads it directly (StageCopy)
-        HIPCHK(e, hipHostMalloc((void**)&sl.block, e->stage_bytes, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(sl.block, 0, e->stage_bytes);
+        HIPCHK(e, hipHostMalloc((void**)&sl.block, stage_cap, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(sl.block, 0, stage_cap);
         HIPCHK(e, hipHostMalloc((void**)&sl.eps, sizeof(float) * Bp * (e->K + e->R)));
         HIPCHK(e, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     }
@@ -483,6 +489,7 @@ int mmvae_destroy(mmvae_h e) {
         if (sl.ev) hipEventDestroy(sl.ev);
     }
     if (e->comm) ncclCommDestroy(e->comm);
+    stream_release(e);
     wide_destroy(e);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
@@ -544,13 +551,13 @@ static hipError_t upload_chunked(Engine* e, void* dst, const void* src, size_t b
 
 extern "C" {
 
-int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
-                     int64_t D, const float* covar) {
-    if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
-    ++e->graph_gen;  // dataset buffers are replaced: step graphs are re-captured
-    if (D != e->D) FAIL(e, MMVAE_E_ARG, "upload_csr: D does not match the model's data_dim");
-    if (rowptr[0] != 0) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr[0] must be 0");
-    // row validation on host threads (the first bad row of each thread's range is reported)
+}  // extern "C"
+
+// a caller's cell-major CSR: rowptr monotone from 0, genes in range and strictly increasing per
+// row (row validation on host threads; the first bad row of each thread's range is reported)
+static int validate_csr(Engine* e, const char* what, const int64_t* rowptr, const int32_t* col, int64_t N, int64_t D) {
+    if (D != e->D) FAIL(e, MMVAE_E_ARG, std::string(what) + ": D does not match the model's data_dim");
+    if (rowptr[0] != 0) FAIL(e, MMVAE_E_ARG, std::string(what) + ": rowptr[0] must be 0");
     {
         const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(16, N / 4096));
         std::vector<int> bad((size_t)nth, 0);  // 1 monotone, 2 range, 3 order
@@ -567,11 +574,28 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
             });
         for (auto& x : th) x.join();
         for (int b : bad) {
-            if (b == 1) FAIL(e, MMVAE_E_ARG, "upload_csr: rowptr not monotone");
-            if (b == 2) FAIL(e, MMVAE_E_ARG, "upload_csr: gene index out of range");
-            if (b == 3) FAIL(e, MMVAE_E_ARG, "upload_csr: gene indices must be strictly increasing within a row");
+            if (b == 1) FAIL(e, MMVAE_E_ARG, std::string(what) + ": rowptr not monotone");
+            if (b == 2) FAIL(e, MMVAE_E_ARG, std::string(what) + ": gene index out of range");
+            if (b == 3) FAIL(e, MMVAE_E_ARG, std::string(what) + ": gene indices must be strictly increasing within a row");
         }
     }
+    return MMVAE_OK;
+}
+
+extern "C" {
+
+int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                     int64_t D, const float* covar) {
+    if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
+    ++e->graph_gen;  // dataset buffers are replaced: step graphs are re-captured
+    {
+        const int rc = validate_csr(e, "upload_csr", rowptr, col, N, D);
+        if (rc) return rc;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    stream_release(e);
+    e->stage_bytes = e->stage_bytes_res;
     const int64_t nnz = rowptr[N];
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -603,6 +627,7 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
         HIPCHK(e, hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice));
     }
     e->N = N;
+    e->N_host = N;
     e->nnz = nnz;
     e->cell_nnz.resize((size_t)N);
     for (int64_t i = 0; i < N; ++i) e->cell_nnz[(size_t)i] = (int32_t)(rowptr[i + 1] - rowptr[i]);
@@ -610,9 +635,106 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     return MMVAE_OK;
 }
 
+}  // extern "C"
+
+// allocate slot s's batch set for `cap` entries (rowptr / covariates / index sized by Bpad)
+static hipError_t batch_set_alloc(Engine* e, int s, int64_t cap) {
+    Engine::BatchSet& q = e->bset[s];
+    hipFree(q.col);
+    hipFree(q.val);
+    q.col = nullptr;
+    q.val = nullptr;
+    hipError_t er;
+    if ((er = dalloc(&q.col, cap)) != hipSuccess) return er;
+    if ((er = dalloc(&q.val, cap)) != hipSuccess) return er;
+    q.cap = cap;
+    const int64_t Bp = e->Bpad;
+    if (!q.rowptr) {
+        if ((er = dalloc(&q.rowptr, Bp + 2)) != hipSuccess) return er;
+        if ((er = dalloc(&q.covar, (Bp + 1) * e->C)) != hipSuccess) return er;
+        if (!e->wide) {
+            if ((er = hipMalloc(&q.rtp, sizeof(int32_t) * (size_t)(Bp + 1) * (size_t)(e->NT + 1))) != hipSuccess) return er;
+            if ((er = hipMalloc(&q.cellnorm, sizeof(float2) * (size_t)(Bp + 1))) != hipSuccess) return er;
+        }
+    }
+    return hipSuccess;
+}
+
+extern "C" {
+
+int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N, int64_t D,
+                     const float* covar) {
+    if (!e || !rowptr || !col || !val || N < 1) FAIL(e, MMVAE_E_ARG, "stream_csr: bad arguments");
+    ++e->graph_gen;
+    {
+        const int rc = validate_csr(e, "stream_csr", rowptr, col, N, D);
+        if (rc) return rc;
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    stream_release(e);
+    // the resident dataset (if any) is dropped
+    for (void* b : {(void*)e->d_rowptr, (void*)e->d_col, (void*)e->d_val, (void*)e->d_covar, (void*)e->d_rtp,
+                    (void*)e->d_cellnorm})
+        if (b) hipFree(b);
+    e->d_rowptr = nullptr;
+    e->d_col = nullptr;
+    e->d_val = nullptr;
+    e->d_covar = nullptr;
+    e->d_rtp = nullptr;
+    e->d_cellnorm = nullptr;
+    const int64_t nnz = rowptr[N];
+    // the caller's arrays as mapped pinned memory: the gather kernel reads them over PCIe
+    auto reg = [&](const void* p, size_t bytes, const void** dev) -> hipError_t {
+        if (!bytes) {
+            *dev = p;
+            return hipSuccess;
+        }
+        void* h = const_cast<void*>(p);
+        hipError_t er = hipHostRegister(h, bytes, hipHostRegisterMapped);
+        if (er != hipSuccess) return er;
+        e->hs_registered.push_back(h);
+        void* d = nullptr;
+        er = hipHostGetDevicePointer(&d, h, 0);
+        *dev = d;
+        return er;
+    };
+    const void* d;
+    HIPCHK(e, reg(rowptr, sizeof(int64_t) * (size_t)(N + 1), &d));
+    e->hs_rowptr = static_cast<const int64_t*>(d);
+    HIPCHK(e, reg(col, sizeof(int32_t) * (size_t)nnz, &d));
+    e->hs_col = static_cast<const int32_t*>(d);
+    HIPCHK(e, reg(val, sizeof(float) * (size_t)nnz, &d));
+    e->hs_val = static_cast<const float*>(d);
+    e->hs_covar = nullptr;
+    if (covar) {
+        HIPCHK(e, reg(covar, sizeof(float) * (size_t)(N * e->C), &d));
+        e->hs_covar = static_cast<const float*>(d);
+    }
+    e->hh_rowptr = rowptr;
+    e->hh_col = col;
+    e->hh_val = val;
+    e->streamed = true;
+    e->N_host = N;
+    e->N = e->Bpad;  // the device dataset: the batch's rows, row Bpad empty
+    e->nnz = nnz;
+    e->cell_nnz.resize((size_t)N);
+    int64_t mx = 0;
+    for (int64_t i = 0; i < N; ++i) {
+        e->cell_nnz[(size_t)i] = (int32_t)(rowptr[i + 1] - rowptr[i]);
+        mx = std::max<int64_t>(mx, e->cell_nnz[(size_t)i]);
+    }
+    // initial batch capacity: twice the mean row's share of a full batch (grown on demand)
+    const int64_t cap = std::max<int64_t>(1024, 2 * (nnz / N + 1) * e->Bmax);
+    for (int s2 = 0; s2 < 2; ++s2) HIPCHK(e, batch_set_alloc(e, s2, cap));
+    e->stage_bytes = (e->stage_bytes_res + sizeof(int64_t) * (size_t)(e->Bpad + 1) + 15) / 16 * 16;
+    stream_bind(e, e->cur_slot);
+    return MMVAE_OK;
+}
+
 int mmvae_dataset_size(mmvae_h e, int64_t* N, int64_t* D) {
     if (!e) FAIL(e, MMVAE_E_ARG, "dataset_size: null");
-    if (N) *N = e->N;
+    if (N) *N = e->N_host;
     if (D) *D = e->D;
     return MMVAE_OK;
 }
@@ -621,7 +743,11 @@ int mmvae_synth_csr(mmvae_h e, int64_t N, double lib_size, uint64_t seed, int64_
     if (!e || N < 1 || lib_size <= 0) FAIL(e, MMVAE_E_ARG, "synth_csr: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
     ++e->graph_gen;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    stream_release(e);
+    e->stage_bytes = e->stage_bytes_res;
     HIPCHK(e, synth_dataset(e, N, lib_size, seed, nnz_out));
+    e->N_host = e->N;
     return MMVAE_OK;
 }
 
@@ -631,6 +757,23 @@ int mmvae_get_rows(mmvae_h e, const int64_t* rows, int64_t nrows, int64_t* rowpt
     if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "get_rows: no dataset");
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->streamed) {  // the caller's own host arrays
+        int64_t need = 0;
+        rowptr_out[0] = 0;
+        for (int64_t i = 0; i < nrows; ++i) {
+            if (rows[i] < 0 || rows[i] >= e->N_host) FAIL(e, MMVAE_E_ARG, "get_rows: row out of range");
+            need += e->hh_rowptr[rows[i] + 1] - e->hh_rowptr[rows[i]];
+            rowptr_out[i + 1] = need;
+        }
+        if (need <= *nnz_io && col_out && val_out)
+            for (int64_t i = 0; i < nrows; ++i) {
+                const int64_t a = e->hh_rowptr[rows[i]], n = e->hh_rowptr[rows[i] + 1] - a;
+                std::memcpy(col_out + rowptr_out[i], e->hh_col + a, sizeof(int32_t) * (size_t)n);
+                std::memcpy(val_out + rowptr_out[i], e->hh_val + a, sizeof(float) * (size_t)n);
+            }
+        *nnz_io = need;
+        return MMVAE_OK;
+    }
     std::vector<int64_t> rp(e->N + 1);
     HIPCHK(e, hipMemcpy(rp.data(), e->d_rowptr, sizeof(int64_t) * (e->N + 1), hipMemcpyDeviceToHost));
     int64_t need = 0;
@@ -847,10 +990,11 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
             if (r < 0 || r >= B) FAIL(e, MMVAE_E_ARG, "ridx out of range [0, B)");
         }
         const int64_t c = cell_ids[r];
-        if (c < 0 || c >= e->N) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
+        if (c < 0 || c >= e->N_host) FAIL(e, MMVAE_E_ARG, "cell id out of range [0, N)");
         e->h_cells_pin[j] = c;
     }
-    e->perm_active = balance && !e->wide && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == e->N &&
+    const int64_t Nv = e->N_host;  // the caller's cells (the padding marker: Nv)
+    e->perm_active = balance && !e->wide && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == Nv &&
                      !std::getenv("MMVAE_NO_BALANCE");
     if (e->perm_active) {
         balance_rows(e, B);
@@ -859,7 +1003,7 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
     // at row N: the empty row of the dataset index, a zero covariate row and rowptr[N] — so
     // every per-row load in the kernels is unconditional
     const int64_t Bp = e->Bpad;
-    for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = e->N;
+    for (int64_t j = B; j < Bp; ++j) e->h_cells_pin[j] = Nv;
     // entry-list segments of the batch's 16-row wave blocks (batch.hip): host prefix of the
     // rows' nonzero counts; the list buffer grows (outside any step) when a batch needs more
     const int64_t Bq = pad_rows(B), WB = Bq / 16;
@@ -868,10 +1012,27 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         e->h_seg_pin[wb] = tot;
         for (int r = 0; r < 16; ++r) {
             const int64_t c = e->h_cells_pin[wb * 16 + r];
-            tot += (c < e->N) ? e->cell_nnz[(size_t)c] : 0;
+            tot += (c < Nv) ? e->cell_nnz[(size_t)c] : 0;
         }
     }
     e->h_seg_pin[WB] = tot;
+    if (e->streamed) {
+        // the batch CSR's row offsets (every padded row; padding rows empty), staged for the
+        // gather kernel; the slot's batch set grows (outside any step) when the batch needs more
+        int64_t o = 0;
+        for (int64_t b = 0; b < Bp; ++b) {
+            e->h_brp_pin[b] = o;
+            const int64_t c = e->h_cells_pin[b];
+            o += (c < Nv) ? e->cell_nnz[(size_t)c] : 0;
+        }
+        e->h_brp_pin[Bp] = o;
+        if (o > e->bset[e->cur_slot].cap) {
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            HIPCHK(e, batch_set_alloc(e, e->cur_slot, o + o / 4 + 1024));
+            ++e->graph_gen;  // the slot's graphs point at the old buffers
+        }
+        stream_bind(e, e->cur_slot);
+    }
     if (!e->wide && tot + 64 > e->ent_cap) {  // (the wide path reads the CSR rows directly)
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (e->d_ents) hipFree(e->d_ents);
@@ -910,6 +1071,7 @@ static int enqueue_run(Engine* e, const mmvae_step_args* a, int64_t n_total) {
         HIPCHK(e, wide_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));  // + staged copy
     } else {
     HIPCHK(e, vmf ? vmf_prep(e, a->B, n_total, a->beta) : nb_prep(e, a->B, n_total, a->beta));  // + staged copy
+    HIPCHK(e, stream_gather(e));  // (streamed dataset: the batch's rows from host memory)
     HIPCHK(e, build_lists(e, a->B));
     if (vmf) HIPCHK(e, vmf_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
     else HIPCHK(e, nb_forward_backward(e, a->B, n_total, a->beta, a->update != 0, a->eps != nullptr));
@@ -1080,6 +1242,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     } else {
     if (e->cfg.model != MMVAE_MODEL_VMF) HIPCHK(e, nb_prep(e, B, B, 1.f));  // + the staged copy
     else HIPCHK(e, vmf_prep(e, B, B, 1.f));
+    HIPCHK(e, stream_gather(e));
     HIPCHK(e, release_slot(e, true));
     HIPCHK(e, build_lists(e, B));
     if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
@@ -1382,6 +1545,18 @@ int mmvae_debug_poison(mmvae_h e, int32_t byte) {
     };
     for (const auto& b : bufs)
         if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));
+    if (e->streamed)  // the batch CSR sets are rewritten by every step's gather and index
+        for (const auto& q : e->bset) {
+            const size_t rows = (size_t)(Bp + 1);
+            const struct {
+                void* p;
+                size_t bytes;
+            } sb[] = {{q.rowptr, sizeof(int64_t) * (rows + 1)}, {q.col, sizeof(int32_t) * (size_t)q.cap},
+                      {q.val, sizeof(float) * (size_t)q.cap}, {q.covar, sizeof(float) * rows * (size_t)e->C},
+                      {q.rtp, sizeof(int32_t) * rows * (size_t)(e->NT + 1)}, {q.cellnorm, sizeof(float) * 2 * rows}};
+            for (const auto& b : sb)
+                if (b.p && b.bytes) HIPCHK(e, hipMemsetAsync(b.p, byte & 0xff, b.bytes, e->stream));
+        }
     for (const auto& b : wide_poison_bufs(e))
         if (b.first && b.second) HIPCHK(e, hipMemsetAsync(b.first, byte & 0xff, b.second, e->stream));
     // and the LDS of every CU: a kernel reading LDS it did not write this launch (a tile row or

@@ -281,8 +281,31 @@ MMVAE_DEV float clamp_nu(float sp) { return __builtin_amdgcn_fmed3f(sp, 1e-4f, 1
 // Packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): one issue covers two
 // elements, which halves the issue cost of a VALU-issue-bound loop run by one wave per SIMD.
 // ---------------------------------------------------------------------------------------
+#ifndef MMVAE_F2_SCALAR
 typedef float f2 __attribute__((ext_vector_type(2)));
 MMVAE_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+#else
+// the same row-pair code as two scalar f32 streams (v_fma_f32 / v_mul_f32 / v_add_f32)
+struct f2 {
+    float x, y;
+    MMVAE_DEV float& operator[](int i) { return i ? y : x; }
+    MMVAE_DEV float operator[](int i) const { return i ? y : x; }
+    MMVAE_DEV f2& operator+=(f2 o) { x += o.x; y += o.y; return *this; }
+    MMVAE_DEV f2& operator-=(f2 o) { x -= o.x; y -= o.y; return *this; }
+    MMVAE_DEV f2& operator*=(f2 o) { x *= o.x; y *= o.y; return *this; }
+};
+MMVAE_DEV f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
+MMVAE_DEV f2 operator-(f2 a, f2 b) { return f2{a.x - b.x, a.y - b.y}; }
+MMVAE_DEV f2 operator*(f2 a, f2 b) { return f2{a.x * b.x, a.y * b.y}; }
+MMVAE_DEV f2 operator+(f2 a, float b) { return f2{a.x + b, a.y + b}; }
+MMVAE_DEV f2 operator-(f2 a, float b) { return f2{a.x - b, a.y - b}; }
+MMVAE_DEV f2 operator*(f2 a, float b) { return f2{a.x * b, a.y * b}; }
+MMVAE_DEV f2 operator+(float a, f2 b) { return f2{a + b.x, a + b.y}; }
+MMVAE_DEV f2 operator-(float a, f2 b) { return f2{a - b.x, a - b.y}; }
+MMVAE_DEV f2 operator*(float a, f2 b) { return f2{a * b.x, a * b.y}; }
+MMVAE_DEV f2 operator-(f2 a) { return f2{-a.x, -a.y}; }
+MMVAE_DEV f2 fma2(f2 a, f2 b, f2 c) { return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+#endif
 MMVAE_DEV f2 splat2(float v) { return f2{v, v}; }
 
 // Dense NB terms of two (cell, gene) elements at x = 0 (nb.hh:456-459, 518-528):

@@ -87,11 +87,38 @@ struct Engine {
     int64_t nrb_max = 0;            // row blocks of 64 at Bmax
 
     // ---- dataset ----
-    int64_t N = 0, nnz = 0;
+    // N = rows of the device dataset the kernels index (resident: every cell; streamed: the
+    // batch's Bpad rows, row Bpad empty); N_host = the caller's cells (cell ids are validated
+    // against it)
+    int64_t N = 0, nnz = 0, N_host = 0;
     int64_t* d_rowptr = nullptr;
     int32_t* d_col = nullptr;
     float* d_val = nullptr;
     float* d_covar = nullptr;  // [N+1][C], row N = zeros (padding rows)
+    // streamed dataset (mmvae_stream_csr): the caller's CSR as mapped pinned host memory (device
+    // pointers), and per staging slot the batch CSR the step gathers into; d_rowptr / d_col /
+    // d_val / d_covar / d_rtp / d_cellnorm then view the current slot's set
+    bool streamed = false;
+    const int64_t* hs_rowptr = nullptr;
+    const int32_t* hs_col = nullptr;
+    const float* hs_val = nullptr;
+    const float* hs_covar = nullptr;
+    std::vector<void*> hs_registered;  // host ranges to hipHostUnregister
+    const int64_t* hh_rowptr = nullptr;  // the same arrays' host addresses (mmvae_get_rows)
+    const int32_t* hh_col = nullptr;
+    const float* hh_val = nullptr;
+    struct BatchSet {
+        int64_t* rowptr = nullptr;  // [Bpad + 2]
+        int32_t* col = nullptr;     // [cap]
+        float* val = nullptr;
+        float* covar = nullptr;     // [Bpad + 1][C]
+        int32_t* rtp = nullptr;     // [Bpad + 1][NT + 1]
+        float* cellnorm = nullptr;  // [Bpad + 1] float2
+        int64_t cap = 0;
+    } bset[2];
+    int64_t* h_brp_pin = nullptr;   // pinned: the staged batch rowptr [Bpad + 1] (streamed)
+    const int64_t* d_brp = nullptr;
+    size_t stage_bytes_res = 0;     // the resident path's staged block (streamed adds the rowptr)
 
     // ---- parameters ----
     std::vector<ParamSlot> slots;
@@ -341,6 +368,13 @@ hipError_t lds_poison(Engine* e, int byte);
 void adam_scalars(const Engine* e, int64_t t, StepScalars* ss);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
 hipError_t build_dataset_index(Engine* e);
+hipError_t index_rows(Engine* e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N, int32_t* rtp,
+                      float* cellnorm);
+// streamed dataset: point the dataset views at staging slot s's batch set, and the step's gather
+// (after the staged block's copy) + batch index (stream.hip)
+void stream_bind(Engine* e, int s);
+hipError_t stream_gather(Engine* e);
+void stream_release(Engine* e);
 
 }  // namespace mmvae
 

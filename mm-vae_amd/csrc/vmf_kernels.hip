@@ -646,7 +646,10 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 }
 
 template <class P, int KP, int CM>
-__global__ __launch_bounds__(256, 2) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 0, CM>(Q, d, epsD); }
+#ifndef MMVAE_VDEC_FWD_OCC
+#define MMVAE_VDEC_FWD_OCC 2
+#endif
+__global__ __launch_bounds__(256, MMVAE_VDEC_FWD_OCC) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 0, CM>(Q, d, epsD); }
 template <class P, int KP, int CM>
 __global__ __launch_bounds__(256, 2) void k_vdec_bwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 1, CM>(Q, d, epsD); }
 

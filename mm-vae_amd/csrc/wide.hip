@@ -1626,6 +1626,10 @@ static hipError_t wide_input(Engine* e, int64_t B) {
     WideState* w = e->wide_st;
     const StageCopy sc = stage_copy_args(e);
     hipLaunchKernelGGL(k_w_stage, dim3((sc.n16 + 255) / 256), dim3(256), 0, e->stream, sc.src, sc.dst, sc.n16);
+    {
+        const hipError_t er = stream_gather(e);  // (streamed dataset: the batch's rows from host memory)
+        if (er != hipSuccess) return er;
+    }
     WDens a;
     std::memset(&a, 0, sizeof(a));
     a.D = (int)e->D;

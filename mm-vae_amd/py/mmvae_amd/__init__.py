@@ -68,6 +68,7 @@ def lib():
         "mmvae_last_error": (ctypes.c_char_p, [h]),
         "mmvae_upload_csr": (ctypes.c_int, [h, i64p, ctypes.POINTER(ctypes.c_int32), f32p, i64, i64, f32p]),
         "mmvae_synth_csr": (ctypes.c_int, [h, i64, ctypes.c_double, ctypes.c_uint64, i64p]),
+        "mmvae_stream_csr": (ctypes.c_int, [h, i64p, ctypes.POINTER(ctypes.c_int32), f32p, i64, i64, f32p]),
         "mmvae_dataset_size": (ctypes.c_int, [h, i64p, i64p]),
         "mmvae_param_shape": (ctypes.c_int, [h, i32, ctypes.POINTER(i32), i64p]),
         "mmvae_comm_allreduce": (ctypes.c_int, [h, f32p, i64]),
@@ -159,6 +160,7 @@ class Engine:
         if self._h:
             lib().mmvae_destroy(self._h)
             self._h = ctypes.c_void_p()
+        self._stream_keep = None  # (after destroy: the engine no longer reads them)
 
     def __del__(self):
         try:
@@ -176,6 +178,20 @@ class Engine:
         self._chk(lib().mmvae_upload_csr(self._h, _ptr(rowptr, ctypes.c_int64), _ptr(col, ctypes.c_int32),
                                          _ptr(val, ctypes.c_float), N, self.D,
                                          _ptr(cv, ctypes.c_float) if cv is not None else None), "upload_csr")
+        self.N = N
+
+    def stream_csr(self, rowptr, col, val, covar=None):
+        """A host-resident dataset (mmvae_stream_csr): the arrays stay in host memory and every
+        step gathers its batch's rows over PCIe; they are kept alive by the engine."""
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        val = _f32(val)
+        cv = _f32(covar) if covar is not None else None
+        N = rowptr.size - 1
+        self._chk(lib().mmvae_stream_csr(self._h, _ptr(rowptr, ctypes.c_int64), _ptr(col, ctypes.c_int32),
+                                         _ptr(val, ctypes.c_float), N, self.D,
+                                         _ptr(cv, ctypes.c_float) if cv is not None else None), "stream_csr")
+        self._stream_keep = (rowptr, col, val, cv)
         self.N = N
 
     def synth_csr(self, N, lib_size=2000.0, seed=0):

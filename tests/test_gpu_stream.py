@@ -1,0 +1,107 @@
+"""The streamed dataset (mmvae_stream_csr, -m gpu): the CSR stays in host memory and every step
+gathers its batch's rows over PCIe into a batch CSR in HBM (csrc/stream.hip) — the reference's
+per-batch read of a dataset it never holds whole (mtx_data_block_t::read, mmvae_io.hh:208-245).
+The batch's row b is then dataset row b for every kernel after the gather, so a streamed handle
+must give bit-identical losses, clip norms, gradients, parameters and encodings to a resident
+one (mmvae_upload_csr) on the same data — over ragged batches, bootstrap resampling (duplicate
+rows), eval forwards, step graphs, both staging slots, a batch-capacity growth and workspace
+poisoning — on the fused NB / vMF kernels and on the wide path.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(N, D, seed, C=1):
+    from oracle import synth
+    rp, col, val = synth.synth_csr(N, D, lib_size=1500.0, seed=seed)
+    cov = np.random.default_rng(seed).standard_normal((N, C)).astype(np.float32) if C > 1 else None
+    return rp, col, val, cov
+
+
+def _pair(model, dtype, D, K, B, data, C=1, **kw):
+    from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
+    rp, col, val, cov = data
+    out = []
+    for streamed in (False, True):
+        eng = Engine(D=D, K=K, C=C, max_batch=B, dtype=dtype, seed=11,
+                     model=MODEL_VMF if model == "vmf" else MODEL_NB, **kw)
+        if streamed:
+            eng.stream_csr(rp, col, val, covar=cov)
+        else:
+            eng.upload_csr(rp, col, val, covar=cov)
+        eng.init_params(seed=5)
+        out.append(eng)
+    return out
+
+
+def _drive(eng, N, B, graph, poison):
+    eng.graph(graph)
+    rng = np.random.default_rng(3)
+    res = []
+    for s in range(7):
+        b = B if s % 3 else B - 37  # ragged every third step
+        cells = rng.integers(0, N, b)
+        if poison:
+            eng.poison(0xFF)
+        if s == 2:
+            res.append((eng.eval_loss(cells, 0.8, step_id=s), 0.0))
+            continue
+        ridx = rng.integers(0, b, b) if s == 4 else None  # bootstrap resample: duplicate rows
+        res.append(eng.step(cells, 0.8, ridx=ridx, step_id=s))
+    m, lv = eng.encode(rng.integers(0, N, B // 2))
+    return res, eng.params(registered_only=True), eng.grads(), m, lv
+
+
+@pytest.mark.parametrize("model,dtype,K", [("nb", "bf16x3", 32), ("nb", "f32", 16), ("nb", "bf16", 64),
+                                           ("vmf", "bf16x3", 32), ("nb", "bf16x3", 96), ("vmf", "f32", 80)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_streamed_equals_resident(model, dtype, K, graph):
+    N, D, B = 2500, 3000, 256
+    data = _data(N, D, seed=7)
+    res, st = _pair(model, dtype, D, K, B, data)
+    a = _drive(res, N, B, graph, poison=False)
+    b = _drive(st, N, B, graph, poison=graph)  # (poisoned workspace and batch CSR sets)
+    assert a[0] == b[0], (a[0], b[0])
+    for x, y in ((a[1], b[1]), (a[2], b[2])):
+        for k in x:
+            assert np.array_equal(x[k], y[k]), k
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+    if K > 64 or (model == "vmf" and K > 64):
+        assert st.path() == "wide"
+
+
+def test_streamed_covariates_and_rows():
+    """Covariates (C = 3) stream with the rows; get_rows reads the caller's arrays."""
+    N, D, B = 1200, 2000, 128
+    data = _data(N, D, seed=9, C=3)
+    res, st = _pair("nb", "bf16x3", D, 16, B, data, C=3)
+    rng = np.random.default_rng(1)
+    for s in range(3):
+        cells = rng.integers(0, N, B)
+        assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s)
+    rows = np.array([0, 7, N - 1, 7], np.int64)
+    for x, y in zip(res.get_rows(rows), st.get_rows(rows)):
+        assert np.array_equal(x, y)
+
+
+def test_streamed_batch_growth():
+    """A batch heavier than the initial capacity (twice the mean row's share) grows the batch set
+    outside the step and re-captures the step graphs; results stay those of the resident handle."""
+    from oracle import synth
+    N, D, B = 600, 4000, 128
+    rp, col, val = synth.synth_csr(N, D, lib_size=800.0, seed=2)
+    # 40 heavy cells (lib size 20x), the rest light
+    rp2, col2, val2 = synth.synth_csr(40, D, lib_size=16000.0, seed=3)
+    rpx = np.concatenate([rp2, rp2[-1] + rp[1:]])
+    colx = np.concatenate([col2, col])
+    valx = np.concatenate([val2, val])
+    res, st = _pair("nb", "bf16x3", D, 32, B, (rpx, colx, valx, None))
+    for eng in (res, st):
+        eng.graph(True)
+    light = np.arange(40, 40 + B, dtype=np.int64)
+    heavy = np.arange(0, B, dtype=np.int64) % 40
+    for s, cells in enumerate([light, light, heavy, heavy, light]):
+        assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
+    assert st.graph_stats()["captures"] >= 3

@@ -4,7 +4,7 @@
 NAME=$1; FLAGS=$2
 cd "$(dirname "$0")/../mm-vae_amd"
 mkdir -p build_$NAME lib_$NAME
-for f in capi nb_kernels vmf_kernels opt_kernels synth batch wide; do
+for f in $(sed -n "s/^SRCS *:= *//p" Makefile | tr " " "\n" | sed -n "s|csrc/\(.*\)\.hip|\1|p"); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics -I/opt/rocm/include $FLAGS \
     -c csrc/$f.hip -o build_$NAME/$f.o &
 done
