@@ -688,11 +688,10 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                     mrun[j][2 * h] = mn.x;
                     mrun[j][2 * h + 1] = mn.y;
                 }
-        } else
-#pragma unroll
-        for (int gb = 0; gb < 4; ++gb) {
+        } else {
+        // pass C: gene block gb + 1's logit MFMAs are issued ahead of block gb's element math
+        auto logits = [&](int gb, f32x4 (&acc)[J]) {
             const int gl = 16 * gb + (lane & 15);
-            f32x4 acc[J];
 #pragma unroll
             for (int j = 0; j < J; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -702,6 +701,16 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 #pragma unroll
                 for (int j = 0; j < J; ++j) acc[j] = M::mma(zfr[j][s], bw, acc[j]);
             }
+        };
+        f32x4 accn[J];
+        logits(0, accn);
+#pragma unroll
+        for (int gb = 0; gb < 4; ++gb) {
+            const int gl = 16 * gb + (lane & 15);
+            f32x4 acc[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) acc[j] = accn[j];
+            if (gb + 1 < 4) logits(gb + 1, accn);
             const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -741,6 +750,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                         }
                 }
             }
+        }
         }
         lap(0);
         if (t + 1 < t1) st(hold, ghold, buf ^ 1);

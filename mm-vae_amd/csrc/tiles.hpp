@@ -113,8 +113,8 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
 struct ListEntries {
     int n;
     int64_t base;
-    int pos[2];
-    float x[2];
+    uint2 raw[2];  // the loaded words as they are: nothing reads them before visit (a select on
+                   // them at fetch time would make the compiler wait for the loads right there)
     MMVAE_DEV void fetch(const uint2* __restrict__ ents, int64_t seg, const int32_t* toffl, int tl, int lane) {
         const int a = toffl[tl];
         n = toffl[tl + 1] - a;
@@ -122,17 +122,17 @@ struct ListEntries {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // unconditional loads (the list buffer has 64 spare entries)
             const int e = lane + 64 * k;
-            const uint2 r = ents[base + (e < n ? e : 0)];
-            pos[k] = (e < n) ? (int)r.x : -1;
-            x[k] = __uint_as_float(r.y);
+            raw[k] = ents[base + (e < n ? e : 0)];
         }
     }
+    // packed position (row-in-block << 6 | gene-in-tile) of register entry k, -1 past the list
+    MMVAE_DEV int pos(int k, int lane) const { return (lane + 64 * k < n) ? (int)raw[k].x : -1; }
     // f(row-in-block, gene-in-tile, x) for every entry of the tile
     template <class F>
     MMVAE_DEV void visit(const uint2* __restrict__ ents, int lane, F&& f) const {
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (pos[k] >= 0) f(pos[k] >> 6, pos[k] & 63, x[k]);
+            if (lane + 64 * k < n) f((int)(raw[k].x >> 6), (int)(raw[k].x & 63), __uint_as_float(raw[k].y));
         for (int e = 128 + lane; e < n; e += 64) {
             const uint2 r = ents[base + e];
             f((int)(r.x >> 6), (int)(r.x & 63), __uint_as_float(r.y));

@@ -504,29 +504,82 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const int64_t segw = Q.seg[wbk];
     wave_sync();
 
-    ListEntries pend;
+    // the tile's entries are fetched two tiles ahead (two register sets, the tile loop unrolled
+    // by two): a global load's latency under load is about a tile of this kernel's work
+    ListEntries pendA, pendB;
+    // lt starts zeroed; afterwards each tile clears only the positions it wrote
+    for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
     if (t0 < t1) {
-        pend.fetch(Q.ents, segw, toffl, 0, lane);
+        pendA.fetch(Q.ents, segw, toffl, 0, lane);
+        pendB.fetch(Q.ents, segw, toffl, min(1, t1 - t0 - 1), lane);
         stage_store();
     }
-    lds_barrier();  // the first tile's entry loads stay in flight
+    lds_barrier();  // the first tiles' entry loads stay in flight
+    // diagnostic (MMVAE_DBG & 256, -DMMVAE_DIAG builds): per-wave phase cycles into dzp
+    // (outputs invalid): densify, gene blocks, tile barrier, slab store, stage store + barrier
+    const bool stamps = dbg_bit(d.dbg, 256);
+    uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp_ = stamps ? stamp_now() : 0;
+    auto lap = [&](int i_) {
+        if (stamps) {
+            const uint64_t tn = stamp_now();
+            st_[i_] += tn - tp_;
+            tp_ = tn;
+        }
+    };
 
-    for (int t = t0; t < t1; ++t) {
+    auto tile = [&](int t, ListEntries& pend) {
         const int tl = t - t0;
-        stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
-        // ---- densify this wave's 16 x 64 log1p(relu x) tile ----
-        for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
-        wave_sync();
+        if (!dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits
+        lap(5);
+        // ---- densify this wave's 16 x 64 log1p(relu x) tile (zero outside the entries) ----
         pend.visit(Q.ents, lane, [&](int r, int gl, float x) { VTabT::put(ltab, lt, r * LS + gl, 0, fmaxf(x, 0.f)); });
         wave_sync();
-        pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
-#pragma unroll
-        for (int gb = 0; gb < 4; ++gb) {
+        lap(7);
+        int zpos0 = pend.pos(0, lane), zpos1 = pend.pos(1, lane);
+        // materialised here: pend's registers are free for the next fetch (no loop-carried copy)
+        asm volatile("" : "+v"(zpos0), "+v"(zpos1));
+        const bool zall = pend.n > 128;  // entries past the register pair: clear the whole tile
+        pend.fetch(Q.ents, segw, toffl, min(tl + 2, t1 - t0 - 1), lane);
+        lap(0);
+        // the logits of gene block gb (16 genes x this wave's 16 rows); block gb + 1's MFMAs are
+        // issued ahead of block gb's element math, so the two overlap inside the wave
+        auto logit = [&](int gb) {
             const int gl = 16 * gb + (lane & 15);
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; ++s)
                 acc = M::mma(zfr[s], M::load(reinterpret_cast<const T*>(wst + swz_off<RBW>(gl, (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))), WIMG / (int)sizeof(T)), acc);
+            return acc;
+        };
+        // dz[cell][latent] += sum_g da[cell][g] W_d[g][latent] over the k step s's genes — run as
+        // soon as the gene blocks it covers have written their da (this wave's own q1 rows)
+        auto dz_step = [&](int s) {
+            Fr a1;
+            if constexpr (X) {
+                const char* qb = reinterpret_cast<const char*>(q1);
+                a1 = Fr{pqt_frag<512>(qb, s * M::KSTEP), pqt_frag<512>(qb + 2048, s * M::KSTEP)};
+            } else if constexpr (BF) {
+                a1 = pqt_frag<512>(reinterpret_cast<const char*>(q1), s * M::KSTEP);
+            } else {
+                a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
+            }
+#pragma unroll
+            for (int lb = 0; lb < KP / 16; ++lb) {
+                Fr bw;
+                if constexpr (TRW) bw = TrFrag<P, RBW>::load(wst, s * M::KSTEP, 16 * lb, WIMG);
+                else
+                    bw = M::load(reinterpret_cast<const T*>(
+                        tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                        WIMG / (int)sizeof(T));
+                dz[lb] = M::mma(a1, bw, dz[lb]);
+            }
+        };
+        f32x4 accn = logit(0);
+#pragma unroll
+        for (int gb = 0; gb < 4; ++gb) {
+            const int gl = 16 * gb + (lane & 15);
+            const f32x4 acc = accn;
+            if (gb + 1 < 4) accn = logit(gb + 1);
             const float4 g4 = gst[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -580,35 +633,27 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                             if (lane < 16) pw[c * 64] = s;
                         }
                 }
-            }
-        }
-        if (PASS) {
-            wave_sync();
-            // dz[cell][latent] += sum_g da[cell][g] W_d[g][latent]
+                // the k steps whose last gene is in this block (x3 / bf16: one step per two
+                // blocks; f32: four per block)
+                constexpr int GPS = M::KSTEP;
+                if ((16 * (gb + 1)) % GPS == 0) {
+                    wave_sync();
 #pragma unroll
-            for (int s = 0; s < GK; ++s) {
-                Fr a1;
-                if constexpr (X) {
-                    const char* qb = reinterpret_cast<const char*>(q1);
-                    a1 = Fr{pqt_frag<512>(qb, s * M::KSTEP), pqt_frag<512>(qb + 2048, s * M::KSTEP)};
-                } else if constexpr (BF) {
-                    a1 = pqt_frag<512>(reinterpret_cast<const char*>(q1), s * M::KSTEP);
-                } else {
-                    a1 = M::load(&q1[(lane & 15) * QS + s * M::KSTEP + (lane >> 4) * M::EPL], QPL);
-                }
-#pragma unroll
-                for (int lb = 0; lb < KP / 16; ++lb) {
-                    Fr bw;
-                    if constexpr (TRW) bw = TrFrag<P, RBW>::load(wst, s * M::KSTEP, 16 * lb, WIMG);
-                    else
-                        bw = M::load(reinterpret_cast<const T*>(
-                            tst + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
-                            WIMG / (int)sizeof(T));
-                    dz[lb] = M::mma(a1, bw, dz[lb]);
+                    for (int s = 0; s < GK; ++s)
+                        if ((s + 1) * GPS > 16 * gb && (s + 1) * GPS <= 16 * (gb + 1)) dz_step(s);
                 }
             }
         }
+        // clear what this tile wrote into lt (the gene blocks above were its last readers)
+        if (zall) {
+            for (int i = lane; i < 16 * LS / 4; i += 64) reinterpret_cast<float4*>(lt)[i] = float4{0.f, 0.f, 0.f, 0.f};
+        } else {
+            if (zpos0 >= 0) lt[(zpos0 >> 6) * LS + (zpos0 & 63)] = 0.f;
+            if (zpos1 >= 0) lt[(zpos1 >> 6) * LS + (zpos1 & 63)] = 0.f;
+        }
+        lap(1);
         lds_barrier();
+        lap(2);
         if (PASS) {
             for (int i = threadIdx.x; i < nq * 64; i += 256) {
                 const int q = i >> 6, g = i & 63;
@@ -617,8 +662,23 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                     part[(3 * nq + q) * 64 + g];
             }
         }
+        lap(3);
         if (t + 1 < t1) stage_store();
         lds_barrier();
+        lap(4);
+    };
+    for (int t = t0; t < t1; t += 2) {
+        tile(t, pendA);
+        if (t + 1 < t1) tile(t + 1, pendB);
+    }
+    if (stamps) {
+        if (lane == 0) {
+            float* o = Q.dzp + ((int64_t)blockIdx.x * 4 + w) * 12;
+            for (int i = 0; i < 8; ++i) o[i] = (float)st_[i];
+            o[8] = (float)(t1 - t0);
+            o[9] = (float)wave_place();
+        }
+        return;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1110,7 +1170,11 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.rowx_stride = 2 + (int)e->H;
     d.Ncells = (int)e->N;
     d.nmv = (int)((e->DP + 255) / 256);
+#ifdef MMVAE_DIAG
+    { const char* ev = getenv("MMVAE_DBG"); d.dbg = ev ? atoi(ev) : 0; }
+#else
     d.dbg = 0;
+#endif
     d.relu = e->cfg.relu != 0;
     d.inv_wscale = 1.f;
     dims_hidden(e, d);
