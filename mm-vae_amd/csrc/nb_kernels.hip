@@ -536,6 +536,9 @@ struct DecPtrs {
 // LDS (register-staged, double-buffered, swizzled image) and shared by the four waves; a wave
 // owns 32 rows (two 16-row MFMA blocks), so every W fragment read from LDS feeds two MFMAs.
 // Workgroup = 128 rows x one gene split.
+#ifndef MMVAE_PASSC_PIPE
+#define MMVAE_PASSC_PIPE 0  // 1: block gb + 1's logits issued ahead of block gb's element math (A/B: no gain)
+#endif
 static constexpr int AC_RPW = 2;  // 16-row MFMA blocks per wave
 template <class P, int KP, int PASS, int CM>
 MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
@@ -703,14 +706,15 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             }
         };
         f32x4 accn[J];
-        logits(0, accn);
+        if (MMVAE_PASSC_PIPE) logits(0, accn);
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
             f32x4 acc[J];
 #pragma unroll
             for (int j = 0; j < J; ++j) acc[j] = accn[j];
-            if (gb + 1 < 4) logits(gb + 1, accn);
+            if (MMVAE_PASSC_PIPE && gb + 1 < 4) logits(gb + 1, accn);
+            if (!MMVAE_PASSC_PIPE) logits(gb, acc);
             const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
             float wcd[CM];
             wcd[0] = g4.z;

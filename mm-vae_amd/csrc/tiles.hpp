@@ -174,6 +174,19 @@ template <class P, int N = LTAB> struct Log1pTab {
                 }
             }
     }
+    // log1p(x) as the f32 the image of a float / bf16 table holds (P = float or __bf16)
+    MMVAE_DEV static float value(const uint32_t* tab, float x) {
+        static_assert(!IsX3<P>::value && !IsF8<P>::value, "f32 values only");
+        if constexpr (!ON) {
+            return flog(1.f + x);
+        } else {
+            const int xi = (int)x;
+            float v;
+            if (x == (float)xi && (unsigned)xi < (unsigned)N) v = __uint_as_float(tab[xi]);
+            else v = log1pf(x);
+            return v;
+        }
+    }
     // operand image of log1p(x) into tile t at idx (x3: lo plane `plane` elements after)
     template <class T>
     MMVAE_DEV static void put(const uint32_t* tab, T* t, int idx, int plane, float x) {

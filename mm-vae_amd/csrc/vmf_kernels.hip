@@ -385,6 +385,12 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 
 // trw (16-bit operands): pass 1 reads the dz GEMM's B operand transposed from the W image, so
 // no WdT image is staged (x3 at K <= 32: 3 workgroups per CU instead of 2)
+#ifndef MMVAE_VDEC_LPIPE
+#define MMVAE_VDEC_LPIPE 1  // 0: each gene block's logits right before its element math (A/B)
+#endif
+#ifndef MMVAE_VDEC_DZ_LATE
+#define MMVAE_VDEC_DZ_LATE 1  // 0: dz k-steps interleaved with the gene blocks (A/B: 90.6 vs 88.9 us x3)
+#endif
 static constexpr int VTAB = 512;  // log1p table entries of the fp32-accurate modes (x3, f32)
 struct VDecLds {
     int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, o_tab, bytes;
@@ -515,6 +521,17 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         stage_store();
     }
     lds_barrier();  // the first tiles' entry loads stay in flight
+    // bf16 mode: log1p of a set's two register entries (one v_log each) computed a tile before
+    // their visit, off the densify's critical path (bf16 16.62M -> 16.93M cells/s).  The table
+    // modes (x3, f32) read their LDS table in the visit: looked up early, the reads cost more in
+    // the gene blocks than they saved (x3 13.34M -> 13.22M).
+    constexpr bool PRE = !VTabT::ON;
+    float lvA[2] = {0.f, 0.f}, lvB[2] = {0.f, 0.f};
+    auto lookup = [&](const ListEntries& p, float (&lv)[2]) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) lv[k] = VTabT::value(ltab, fmaxf(__uint_as_float(p.raw[k].y), 0.f));
+    };
+    if (PRE && t0 < t1) lookup(pendA, lvA);
     // diagnostic (MMVAE_DBG & 256, -DMMVAE_DIAG builds): per-wave phase cycles into dzp
     // (outputs invalid): densify, gene blocks, tile barrier, slab store, stage store + barrier
     const bool stamps = dbg_bit(d.dbg, 256);
@@ -527,12 +544,22 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         }
     };
 
-    auto tile = [&](int t, ListEntries& pend) {
+    auto tile = [&](int t, ListEntries& pend, const float (&lv)[2], const ListEntries& pnext, float (&lvnext)[2]) {
         const int tl = t - t0;
         if (!dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits
         lap(5);
         // ---- densify this wave's 16 x 64 log1p(relu x) tile (zero outside the entries) ----
-        pend.visit(Q.ents, lane, [&](int r, int gl, float x) { VTabT::put(ltab, lt, r * LS + gl, 0, fmaxf(x, 0.f)); });
+        if constexpr (PRE) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (lane + 64 * k < pend.n) lt[(int)(pend.raw[k].x >> 6) * LS + (int)(pend.raw[k].x & 63)] = lv[k];
+            for (int e = 128 + lane; e < pend.n; e += 64) {  // past the register pair: read here
+                const uint2 r = Q.ents[pend.base + e];
+                VTabT::put(ltab, lt, (int)(r.x >> 6) * LS + (int)(r.x & 63), 0, fmaxf(__uint_as_float(r.y), 0.f));
+            }
+        } else {
+            pend.visit(Q.ents, lane, [&](int r, int gl, float x) { VTabT::put(ltab, lt, r * LS + gl, 0, fmaxf(x, 0.f)); });
+        }
         wave_sync();
         lap(7);
         int zpos0 = pend.pos(0, lane), zpos1 = pend.pos(1, lane);
@@ -574,12 +601,14 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                 dz[lb] = M::mma(a1, bw, dz[lb]);
             }
         };
-        f32x4 accn = logit(0);
+        // (bf16 operand modes: x3 89.1 -> 87.6 us; the f32 mode is faster without, 158 vs 163 us)
+        constexpr bool LP = MMVAE_VDEC_LPIPE && BF;
+        f32x4 accn = LP ? logit(0) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int gb = 0; gb < 4; ++gb) {
             const int gl = 16 * gb + (lane & 15);
-            const f32x4 acc = accn;
-            if (gb + 1 < 4) accn = logit(gb + 1);
+            const f32x4 acc = LP ? accn : logit(gb);
+            if (LP && gb + 1 < 4) accn = logit(gb + 1);
             const float4 g4 = gst[gl];
             float wcd[CM];
             wcd[0] = g4.z;
@@ -636,13 +665,18 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                 // the k steps whose last gene is in this block (x3 / bf16: one step per two
                 // blocks; f32: four per block)
                 constexpr int GPS = M::KSTEP;
-                if ((16 * (gb + 1)) % GPS == 0) {
+                if (!MMVAE_VDEC_DZ_LATE && (16 * (gb + 1)) % GPS == 0) {
                     wave_sync();
 #pragma unroll
                     for (int s = 0; s < GK; ++s)
                         if ((s + 1) * GPS > 16 * gb && (s + 1) * GPS <= 16 * (gb + 1)) dz_step(s);
                 }
             }
+        }
+        if (PASS && MMVAE_VDEC_DZ_LATE) {
+            wave_sync();
+#pragma unroll
+            for (int s = 0; s < GK; ++s) dz_step(s);
         }
         // clear what this tile wrote into lt (the gene blocks above were its last readers)
         if (zall) {
@@ -651,6 +685,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             if (zpos0 >= 0) lt[(zpos0 >> 6) * LS + (zpos0 & 63)] = 0.f;
             if (zpos1 >= 0) lt[(zpos1 >> 6) * LS + (zpos1 & 63)] = 0.f;
         }
+        if (PRE && t + 1 < t1) lookup(pnext, lvnext);
         lap(1);
         lds_barrier();
         lap(2);
@@ -668,8 +703,8 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         lap(4);
     };
     for (int t = t0; t < t1; t += 2) {
-        tile(t, pendA);
-        if (t + 1 < t1) tile(t + 1, pendB);
+        tile(t, pendA, lvA, pendB, lvB);
+        if (t + 1 < t1) tile(t + 1, pendB, lvB, pendA, lvA);
     }
     if (stamps) {
         if (lane == 0) {
