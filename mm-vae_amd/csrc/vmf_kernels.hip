@@ -102,7 +102,8 @@ __global__ void k_vpack_dec(const float* Wd, int D, int DP, int KD, int KP, floa
 // k_vprep — per-gene constants of the step:
 //   inv_g = 1 / (softplus(ln_x_sd_g) + eps)       (vmf.hh:255-256)
 //   xmi_g = x_mean_g inv_g                         (dense part of the encoder input)
-//   grec_g = (b_dec_g, b_cd_g, W_cd[g][0], valid)  (vmf.hh:285-287)
+//   grec_g = (b_dec_g log2(e), b_cd_g, W_cd[g][0], epsD)  (vmf.hh:285-287); a padded gene holds
+//            (-inf, 0, 0, 0), so its u = exp2(-inf), hc and dv are exact zeros with no mask
 //   WeS[k][g] = inv_g W~[k][g]                     (encoder B operand, bf16 or f32)
 // =======================================================================================
 MMVAE_DEV void vkappa_body(const VPtrs& P, const VScal& s, float* __restrict__ vk);
@@ -126,7 +127,8 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
         gene[g] = inv;
         gene[3 * d.DP + g] = v ? P.xm[g] * inv : 0.f;
         reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
-            float4{v ? P.bd[g] : 0.f, v ? P.bcd[g] : 0.f, v ? P.Wcd[(int64_t)g * d.C] : 0.f, v ? 1.f : 0.f};
+            float4{v ? P.bd[g] * 1.4426950408889634f : -INFINITY, v ? P.bcd[g] : 0.f, v ? P.Wcd[(int64_t)g * d.C] : 0.f,
+                   v ? epsD : 0.f};
     }
     const float xmv = v ? P.xm[g] : 0.f;
     float mp[8];
@@ -621,19 +623,19 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
                 const int rl = 4 * (lane >> 4) + 2 * h;
-                const f2 ex = (f2{acc[2 * h], acc[2 * h + 1]} + g4.x) * L2E;
+                const f2 ex = fma2(f2{acc[2 * h], acc[2 * h + 1]}, splat2(L2E), splat2(g4.x));
                 const f2 u = f2{fexp2(ex.x), fexp2(ex.y)};      // exp(z_dec(z))   vmf.hh:285
                 f2 hc = splat2(g4.y);                           // covar_dec(c)    vmf.hh:286
 #pragma unroll
                 for (int c = 0; c < CM; ++c) hc = fma2(crow2[h][c], splat2(wcd[c]), hc);
-                const f2 v = (u + hc) * g4.w;                   // padded genes: 0
+                const f2 v = u + hc;                            // padded genes: 0 + 0
                 const f2 l = f2{lt[rl * LS + gl], lt[(rl + 1) * LS + gl]};
                 if (PASS == 0) {
                     svv2[h] = fma2(v, v, svv2[h]);
                     sv2[h] += v;
                     slv2[h] = fma2(l, v, slv2[h]);
                 } else {
-                    const f2 dv = fma2(ra2[h], (l + epsD) * g4.w, rbt2[h] * v);
+                    const f2 dv = fma2(ra2[h], l + g4.w, rbt2[h] * v);  // g4.w = epsD (padded: 0)
                     csp[0] += dv;
 #pragma unroll
                     for (int c = 0; c < CM; ++c) csp[1 + c] = fma2(dv, crow2[h][c], csp[1 + c]);
