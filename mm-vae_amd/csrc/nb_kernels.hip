@@ -204,16 +204,45 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
 #pragma unroll
     for (int lb = 0; lb < KP / 16; ++lb) acc[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nt = t1 - t0;
-    // entry ring: q[0] = next tile to scatter; loads issued EDEPTH tiles ahead of their use
-    constexpr int EDEPTH = 2;
-    ListEntries q[EDEPTH];
+    // tile t + 1's entries come from one of two register sets, fetched two tiles ahead; the loop
+    // is unrolled by two so neither set is ever copied (a loop-carried copy of a register with a
+    // load in flight makes the compiler wait for that load at the loop latch)
+    ListEntries qA, qB;
+    // each x tile buffer is cleared only where its last scatter wrote (whole tile past 128 entries)
+    int zp[NB][2];
+    bool zall[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        zp[b][0] = zp[b][1] = -1;
+        zall[b] = true;
+    }
+    auto keep = [&](const ListEntries& le, int b) {
+        zp[b][0] = le.pos(0, lane);
+        zp[b][1] = le.pos(1, lane);
+        asm volatile("" : "+v"(zp[b][0]), "+v"(zp[b][1]));  // taken now: le is refetched next
+        zall[b] = le.n > 128;
+    };
+    auto clear = [&](T* x0, int b) {
+        if (zall[b]) {
+            zero_tile(x0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (zp[b][k] >= 0) {
+                    const int idx = (zp[b][k] >> 6) * XS + (zp[b][k] & 63);
+                    x0[idx] = T{};
+                    if constexpr (NPL == 2) x0[idx + XPL] = T{};
+                }
+        }
+    };
     if (t0 < t1) {
         ListEntries first;  // every prologue load is issued before the first wait
         first.fetch(ents, segw, toffl, 0, lane);
-#pragma unroll
-        for (int i = 0; i < EDEPTH; ++i) q[i].fetch(ents, segw, toffl, min(1 + i, nt - 1), lane);
+        qA.fetch(ents, segw, toffl, min(1, nt - 1), lane);
+        qB.fetch(ents, segw, toffl, min(2, nt - 1), lane);
         wreg.store(wst, NB * STB);
         scatter(first, xt);
+        keep(first, 0);
     }
     lds_barrier();
     const bool stamps = dbg_bit(d.dbg, 32);
@@ -225,8 +254,9 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
             tp = tn;
         }
     };
-    for (int t = t0; t < t1; ++t) {
-        const int tl = t - t0, buf = SB ? 0 : (tl & 1);
+    // q: tile t + 1's entries; buf: the x tile buffer holding tile t
+    auto tile = [&](int t, ListEntries& q, int buf) {
+        const int tl = t - t0;
         // unconditional (clamped) prefetch of the next weight tile: counted vmcnt waits
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
         const T* xb = xt + buf * XT;
@@ -242,17 +272,16 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
             }
         }
         lap(sa);
-        T* xn = xt + (SB ? 0 : (buf ^ 1)) * XT;
+        const int nb = SB ? 0 : (buf ^ 1);
+        T* xn = xt + nb * XT;
         if (t + 1 < t1) {
-            zero_tile(xn);
+            clear(xn, nb);  // SB: after this wave's own operand reads of it (LDS is in order)
             wave_sync();
-            scatter(q[0], xn);
+            scatter(q, xn);
+            keep(q, nb);
         }
         lap(sb);
-        // rotate the ring; the new tail's entry loads stay in flight across the barriers
-#pragma unroll
-        for (int i = 0; i + 1 < EDEPTH; ++i) q[i] = q[i + 1];
-        q[EDEPTH - 1].fetch(ents, segw, toffl, min(tl + 1 + EDEPTH, nt - 1), lane);
+        q.fetch(ents, segw, toffl, min(tl + 3, nt - 1), lane);  // the loads stay in flight across the barriers
         if constexpr (SB) {
             lds_barrier();  // every wave's reads of this W stage done
             if (t + 1 < t1) wreg.store(wst, STB);
@@ -262,6 +291,10 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
         lap(sc);
         lds_barrier();
         lap(sd);
+    };
+    for (int t = t0; t < t1; t += 2) {
+        tile(t, qA, 0);
+        if (t + 1 < t1) tile(t + 1, qB, SB ? 0 : 1);
     }
     if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
         const uint64_t t_loop_end = stamp_now();
