@@ -135,21 +135,53 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 
     wave_sync();  // toffl written above by this wave
     const int nt = t1 - t0;
-    ListEntries nxt;
+    // tile t + 1's entries come from one of two register sets, fetched two tiles ahead, and the
+    // loop is unrolled by two: no register set (nor the WREG W tile) is copied at the latch, where
+    // a copy of a register with a load in flight would wait for that load
+    ListEntries qA, qB;
+    // this wave's cells in the shared tiles are cleared only where its last scatter wrote
+    int zp0 = -1, zp1 = -1;
+    bool zall = true;
+    auto keep = [&](const ListEntries& le) {
+        zp0 = le.pos(0, lane);
+        zp1 = le.pos(1, lane);
+        asm volatile("" : "+v"(zp0), "+v"(zp1));  // taken now: le is refetched next
+        zall = le.n > 128;
+    };
+    auto clear = [&]() {
+        if (zall) {
+            zero_cols();
+            wave_sync();
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int zp = k ? zp1 : zp0;
+                if (zp >= 0) {
+                    const int gl = zp & 63, r = zp >> 6;
+                    lt[gl * LS + 16 * w + r] = T{};
+                    if constexpr (X) lt[LT + gl * LS + 16 * w + r] = T{};
+                    if (RAW) raw[gl * 68 + 16 * w + r] = 0.f;
+                }
+            }
+        }
+    };
     if (t0 < t1) {
         ListEntries first;
         first.fetch(ents, segw, toffl, 0, lane);
-        nxt.fetch(ents, segw, toffl, min(1, nt - 1), lane);
+        qA.fetch(ents, segw, toffl, min(1, nt - 1), lane);
+        qB.fetch(ents, segw, toffl, min(2, nt - 1), lane);
         if constexpr (!WREG) wreg.store(wst);
         zero_cols();
         if constexpr (Log1pTab<P>::ON) __syncthreads();  // the table
         else wave_sync();
         scatter(first);
+        keep(first);
     }
     lds_barrier();
-    for (int t = t0; t < t1; ++t) {
+    // q: tile t + 1's entries; wc / wx: this / the next tile's W registers (WREG)
+    auto tile = [&](int t, ListEntries& q, float (&wc)[4][4], float (&wx)[4][4]) {
         const int tl = t - t0;
-        if constexpr (WREG) wload(wn, min(t + 1, t1 - 1));
+        if constexpr (WREG) wload(wx, min(t + 1, t1 - 1));
         else wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(WT));
         // ---- raw-count column sums of gene block w: lane = (gene 16w + (l&15), cell quarter l>>4) ----
         if (RAW) {
@@ -191,7 +223,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int k = 16 * lb + 4 * (lane >> 4) + r;
-                    const float wv = WREG ? wr[i][r]
+                    const float wv = WREG ? wc[i][r]
                                           : static_cast<float>(*reinterpret_cast<const WT*>(wst + swz_off<RB>(k, gl * (int)sizeof(WT))));
                     v = fmaf(wv, acc[r], v);
                 }
@@ -208,18 +240,17 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
             slabE[((int64_t)rb * nq) * d.DP + 64 * t + g] = part[g] + part[64 + g] + part[128 + g] + part[192 + g];
         }
         if (t + 1 < t1) {
-            zero_cols();
-            wave_sync();
-            scatter(nxt);
+            clear();
+            scatter(q);
+            keep(q);
             if constexpr (!WREG) wreg.store(wst);
         }
-        if constexpr (WREG)
-#pragma unroll
-            for (int i = 0; i < NGB; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) wr[i][r] = wn[i][r];
-        nxt.fetch(ents, segw, toffl, min(tl + 2, nt - 1), lane);
+        q.fetch(ents, segw, toffl, min(tl + 3, nt - 1), lane);
         lds_barrier();
+    };
+    for (int t = t0; t < t1; t += 2) {
+        tile(t, qA, wr, wn);
+        if (t + 1 < t1) tile(t + 1, qB, wn, wr);
     }
 }
 
