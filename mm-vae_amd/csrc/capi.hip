@@ -584,6 +584,14 @@ static int validate_csr(Engine* e, const char* what, const int64_t* rowptr, cons
 
 extern "C" {
 
+// C == 1 covariates that are all exactly 1 (nullptr: the default ones) — Engine::unit_covar
+static bool all_ones(const float* covar, int64_t N) {
+    if (!covar) return true;
+    for (int64_t i = 0; i < N; ++i)
+        if (covar[i] != 1.f) return false;
+    return true;
+}
+
 int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
                      int64_t D, const float* covar) {
     if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
@@ -620,6 +628,7 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
         HIPCHK(e, upload_chunked(e, e->d_col, col, sizeof(int32_t) * nnz));
         HIPCHK(e, upload_chunked(e, e->d_val, val, sizeof(float) * nnz));
     }
+    e->unit_covar = e->C == 1 && all_ones(covar, N);
     if (covar) {
         HIPCHK(e, hipMemcpy(e->d_covar, covar, sizeof(float) * N * e->C, hipMemcpyHostToDevice));
     } else {
@@ -707,6 +716,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     HIPCHK(e, reg(val, sizeof(float) * (size_t)nnz, &d));
     e->hs_val = static_cast<const float*>(d);
     e->hs_covar = nullptr;
+    e->unit_covar = e->C == 1 && all_ones(covar, N);
     if (covar) {
         HIPCHK(e, reg(covar, sizeof(float) * (size_t)(N * e->C), &d));
         e->hs_covar = static_cast<const float*>(d);

@@ -99,6 +99,9 @@ struct Engine {
     // pointers), and per staging slot the batch CSR the step gathers into; d_rowptr / d_col /
     // d_val / d_covar / d_rtp / d_cellnorm then view the current slot's set
     bool streamed = false;
+    // C == 1 and every dataset row's covariate is 1 (no covariate file: the reference's default):
+    // the decoder kernels fold the covariate Linear into per-gene constants (instances CM = 0)
+    bool unit_covar = false;
     const int64_t* hs_rowptr = nullptr;
     const int32_t* hs_col = nullptr;
     const float* hs_val = nullptr;

@@ -595,7 +595,10 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     const int sp = blockIdx.x % d.nsA, rbw = blockIdx.x / d.nsA;
     const int row0 = rbw * 4 * WR + WR * w;
     const int t0 = sp * d.tpsA, t1 = min(d.NT, t0 + d.tpsA);
-    const int C = (CM == 1) ? 1 : d.C;
+    // CM = 0: unit covariate (Engine::unit_covar, C = 1): the covariate Linear folds into the
+    // gene's bias, and its weight gradient's column sums are the bias gradient's
+    constexpr int CA = CM > 0 ? CM : 1;  // covariate array extent
+    const int C = (CM <= 1) ? 1 : d.C;
     const int nq = 1 + C;
     char* stg = smem;
     float* part = reinterpret_cast<float*>(smem + 2 * STB);  // C: [2][4][nq][64]; prologue: [4 WR]
@@ -625,7 +628,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             else zfr[j][s] = M::load(&Z[zo], Q.zplane);
         }
     const float ainv = F8M ? d.inv_wscale : 1.f;  // logit accumulator unscale (fp8 W_dec)
-    float lse2[J][4], wE[J][4], crow[J][4][CM], mrun[J][4], srun[J][4];
+    float lse2[J][4], wE[J][4], crow[J][4][CA], mrun[J][4], srun[J][4];
 #pragma unroll
     for (int j = 0; j < J; ++j)
 #pragma unroll
@@ -656,7 +659,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
     };
     // diagnostic (MMVAE_DBG & 256): per-wave phase cycles into slabC (outputs invalid)
     const bool stamps = dbg_bit(d.dbg, 256);
-    uint64_t st_[3] = {0, 0, 0}, tp_ = 0;
+    uint64_t st_[4] = {0, 0, 0, 0}, tp_ = 0;
     auto lap = [&](int i_) {
         if (stamps) {
             const uint64_t tn = stamp_now();
@@ -685,12 +688,13 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
                     for (int j = 0; j < J; ++j) acc[gb][j] = M::mma(zfr[j][s], bw, acc[gb][j]);
                 }
             }
-            float b2[4], w2[4][CM];
+            lap(3);
+            float b2[4], w2[4][CA];
 #pragma unroll
             for (int gb = 0; gb < 4; ++gb) {
                 const int gl = 16 * gb + (lane & 15);
                 const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
-                b2[gb] = g4.x * L2E;  // padded genes: -inf
+                b2[gb] = (CM == 0 ? g4.x + g4.z : g4.x) * L2E;  // padded genes: -inf
                 w2[gb][0] = g4.z * L2E;
 #pragma unroll
                 for (int c = 1; c < CM; ++c)
@@ -749,19 +753,20 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             if (MMVAE_PASSC_PIPE && gb + 1 < 4) logits(gb + 1, accn);
             if (!MMVAE_PASSC_PIPE) logits(gb, acc);
             const float4 g4 = reinterpret_cast<const float4*>(sb + NPL * WIMG)[gl];
-            float wcd[CM];
+            const float gx = CM == 0 ? g4.x + g4.z : g4.x;  // unit covariate: folded into the bias
+            float wcd[CA];
             wcd[0] = g4.z;
 #pragma unroll
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
             {  // pass C: rows 2h, 2h + 1 as one packed-f32 pair
-                f2 csp[1 + CM];
+                f2 csp[1 + CA];
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) csp[c] = splat2(0.f);
+                for (int c = 0; c < 1 + CA; ++c) csp[c] = splat2(0.f);
 #pragma unroll
                 for (int j = 0; j < J; ++j)
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        f2 lg = fma2(f2{acc[j][2 * h], acc[j][2 * h + 1]}, splat2(ainv), splat2(g4.x));
+                        f2 lg = fma2(f2{acc[j][2 * h], acc[j][2 * h + 1]}, splat2(ainv), splat2(gx));
 #pragma unroll
                         for (int c = 0; c < CM; ++c) lg = fma2(f2{crow[j][2 * h][c], crow[j][2 * h + 1][c]}, splat2(wcd[c]), lg);
                         const f2 ex = fma2(lg, splat2(L2E), -f2{lse2[j][2 * h], lse2[j][2 * h + 1]});
@@ -770,12 +775,13 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
 #pragma unroll
                         for (int c = 0; c < CM; ++c) csp[1 + c] = fma2(wp, f2{crow[j][2 * h][c], crow[j][2 * h + 1][c]}, csp[1 + c]);
                     }
-                float cs[1 + CM];
+                float cs[1 + CA];
 #pragma unroll
-                for (int c = 0; c < 1 + CM; ++c) cs[c] = csp[c].x + csp[c].y;
+                for (int c = 0; c < 1 + CA; ++c) cs[c] = csp[c].x + csp[c].y;
+                if (CM == 0) cs[1] = cs[0];  // sum_b w_b E_b p c_b with c_b = 1
                 // per-wave partial of this tile (fixed-order combine after the tile barrier)
                 float* pw = part + ((buf * 4 + w) * nq) * 64 + gl;
-                if (CM == 1) {  // nq = 2
+                if (CM <= 1) {  // nq = 2
                     const float v = sum_rowgroups2(cs[0], cs[1]);
                     if (!(lane & 16)) pw[(lane >> 5) * 64] = v;
                 } else {
@@ -826,6 +832,7 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
             o[4] = (float)(rt_loop & 0xffffffu);
             o[5] = (float)(realtime_now() & 0xffffffu);
             o[6] = (float)wave_place();
+            o[7] = (float)st_[3];
         }
         return;
     }
@@ -974,7 +981,10 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     // (16-byte row quads XOR-swizzled by gene so the 16 genes of a lane group hit distinct banks)
     auto ccp = [](int r, int g) { return (g >> 4) * 2048 + (g & 15) * 64 + (((r >> 2) ^ ((g >> 2) & 3)) << 4) + (r & 3) * 4; };
     constexpr int PS = 68;
-    constexpr int NRS = 3 + RM + CM;    // row scalars: d, w, valid, znu[R], c[C]
+    // CM = 0: unit covariate (Engine::unit_covar, C = 1): the covariate Linear folds into the
+    // gene's bias, and its weight gradient's column sums are the bias gradient's
+    constexpr int CA = CM > 0 ? CM : 1;  // covariate array extent
+    constexpr int NRS = 3 + RM + CA;    // row scalars: d, w, valid, znu[R], c[C]
     constexpr int RBW = KP * (int)sizeof(TL);  // staged decoder row (one gene)
     constexpr int RBT = 64 * (int)sizeof(T);  // staged WdT row (one latent, 64 genes)
     constexpr float L2E = 1.4426950408889634f;
@@ -985,7 +995,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const int row0 = rbw * 16 * NW + 16 * w;
     const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
     const int S = d.tpsD + 1;
-    const int C = (CM == 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
+    const int C = (CM <= 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
     static_assert(!SG || (X && DB && NW == 8 && !LOSS), "the staggered pass B is the x3 training instance");
     const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG);
@@ -1065,8 +1075,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     }
     // rows 4(lane>>4) + 2h + j live in component j of the pair h (packed f32 epilogue)
     float lse2[4];
-    f2 rv2[2], dv2[2], wv2[2], crow2[2][CM], znu2[2][RM];
-    f2 Eacc2[2], dzn2[2][RM], wc2[2][CM];
+    f2 rv2[2], dv2[2], wv2[2], crow2[2][CA], znu2[2][RM];
+    f2 Eacc2[2], dzn2[2][RM], wc2[2][CA];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int h = r >> 1, j = r & 1;
@@ -1160,13 +1170,14 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             for (int s = 0; s < KSL; ++s)
                 acc = ML::mma(zfr[s], ML::load(reinterpret_cast<const TL*>(wsb + swz_off<RBW>(gl, (s * ML::KSTEP + (lane >> 4) * ML::EPL) * (int)sizeof(TL))), L.swp / (int)sizeof(TL)), acc);
             const float4 g4 = gsb[gl];
-            float wcd[CM];
+            const float gx = CM == 0 ? g4.x + g4.z : g4.x;  // unit covariate: folded into the bias
+            float wcd[CA];
             wcd[0] = g4.z;
 #pragma unroll
             for (int c2 = 1; c2 < CM; ++c2) wcd[c2] = (c2 < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c2] : 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float lg = fmaf(acc[r], ainv, g4.x);
+                float lg = fmaf(acc[r], ainv, gx);
 #pragma unroll
                 for (int c2 = 0; c2 < CM; ++c2) lg = fmaf(crow2[r >> 1][c2][r & 1], wcd[c2], lg);
                 q2[(4 * (lane >> 4) + r) * PS + gl] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
@@ -1226,7 +1237,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         auto epilogue = [&](auto mask_c) {
             constexpr bool MASK = decltype(mask_c)::value;
             constexpr float LN2 = 0.6931471805599453f;
-            constexpr int GBU = (CM == 1 && RM == 1) ? 4 : 1;  // the general variant stays rolled
+            constexpr int GBU = (CM <= 1 && RM == 1) ? 4 : 1;  // the general variant stays rolled
 #pragma unroll GBU
             for (int gb = 0; gb < 4; ++gb) {
                 const int gl = 16 * gb + (lane & 15);
@@ -1239,9 +1250,9 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
 #pragma unroll
                 for (int q = 1; q < RM; ++q) wnd[q] = (q < R && gv) ? Q.Wnd[(int64_t)gene * R + q] : 0.f;
                 const float gvf = gv ? 1.f : 0.f;
-                f2 cs1[1 + CM], csdu = splat2(0.f), csduz[RM];
+                f2 cs1[1 + CA], csdu = splat2(0.f), csduz[RM];
 #pragma unroll
-                for (int c2 = 0; c2 < 1 + CM; ++c2) cs1[c2] = splat2(0.f);
+                for (int c2 = 0; c2 < 1 + CA; ++c2) cs1[c2] = splat2(0.f);
 #pragma unroll
                 for (int q = 0; q < RM; ++q) csduz[q] = splat2(0.f);
                 // the block's corrections first (x3: this block's pq overwrites them below)
@@ -1313,14 +1324,17 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 }
                 if constexpr (LOSS) continue;
                 float* pw = pb + w * nq * 64 + gl;
-                if (CM == 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
-                    pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1[1].x + cs1[1].y, csdu.x + csdu.y,
+                // (CM = 0: the covariate column sums sum_b w_b c_b pq with c_b = 1 are cs1[0])
+                const f2 cs1c = (CM == 0) ? cs1[0] : cs1[1];
+                if (CM <= 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
+                    pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1c.x + cs1c.y, csdu.x + csdu.y,
                                                           csduz[0].x + csduz[0].y);
                 } else {
 #pragma unroll
-                    for (int c2 = 0; c2 < 1 + CM; ++c2)
+                    for (int c2 = 0; c2 < 1 + CA; ++c2)
                         if (c2 <= C) {
-                            const float v = sum_rowgroups(cs1[c2].x + cs1[c2].y);
+                            const f2 cv = (c2 == 1) ? cs1c : cs1[c2];
+                            const float v = sum_rowgroups(cv.x + cv.y);
                             if (lane < 16) pw[c2 * 64] = v;
                         }
                     {
@@ -2332,6 +2346,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     const DecPtrs Q = dec_ptrs(e, d, P, bf);
     const bool small_cr = (d.C == 1 && d.R == 1);
+    // unit covariate (no covariate file): the CM = 0 instances fold it into per-gene constants
+    const bool ucov = d.C == 1 && e->unit_covar;
     // pass B: 16 NW rows per workgroup.  bf16: NW = 8 with double-buffered stages (one barrier
     // per tile); x3: NW = 8 single-buffered (the hi + lo images of double buffers exceed the
     // 160 KB LDS); f32 or MMVAE_DEC_NW=4: NW = 4 (64 rows, two workgroups per CU)
@@ -2345,7 +2361,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const size_t ldsA = dec_lds(d, 0, (int)sizeof(TL), NPL), ldsC = dec_lds(d, 2, (int)sizeof(TL), NPL);
     {
         ScopedTimer tm(e, "k_dec_lse");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
+        if (ucov) hipLaunchKernelGGL((k_dec_lse<PM, KP, 0>), gdecA, dim3(256), ldsA, st, Q, d);
+        else if (d.C == 1) hipLaunchKernelGGL((k_dec_lse<PM, KP, 1>), gdecA, dim3(256), ldsA, st, Q, d);
         else hipLaunchKernelGGL((k_dec_lse<PM, KP, CMAX>), gdecA, dim3(256), ldsA, st, Q, d);
     }
     // x3 training, MMVAE_DEC_SG=1: the staggered instance (waves 4-7 half a tile behind).
@@ -2365,11 +2382,15 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
                     return;
                 }
             }
-            if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM, LS>), gdecB, dim3(512), lds, st, Q, d);
-        } else if (small_cr)
-            hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM, LS>), gdecB, dim3(256),
-                               (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL), LS).bytes, st, Q, d);
-        else
+            if constexpr (sizeof(T) == 2) {
+                if (ucov) hipLaunchKernelGGL((k_dec_nb<PB, KP, 0, 1, 8, !X, PM, LS>), gdecB, dim3(512), lds, st, Q, d);
+                else hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, !X, PM, LS>), gdecB, dim3(512), lds, st, Q, d);
+            }
+        } else if (small_cr) {
+            const size_t lds4 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL), LS).bytes;
+            if (ucov) hipLaunchKernelGGL((k_dec_nb<PB, KP, 0, 1, 4, false, PM, LS>), gdecB, dim3(256), lds4, st, Q, d);
+            else hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM, LS>), gdecB, dim3(256), lds4, st, Q, d);
+        } else
             hipLaunchKernelGGL((k_dec_nb<PB, KP, CMAX, RMAX, 4, false, PM, LS>), gdecB, dim3(256),
                                (size_t)DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + RMAX + CMAX, csz, 4, 1, NPL, (int)sizeof(TL), LS).bytes, st, Q, d);
     };
@@ -2389,7 +2410,8 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_dec_tail");
-        if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<PM, KP, 1>), gdecA, dim3(256), ldsC, st, Q, d);
+        if (ucov) hipLaunchKernelGGL((k_dec_tail<PM, KP, 0>), gdecA, dim3(256), ldsC, st, Q, d);
+        else if (d.C == 1) hipLaunchKernelGGL((k_dec_tail<PM, KP, 1>), gdecA, dim3(256), ldsC, st, Q, d);
         else hipLaunchKernelGGL((k_dec_tail<PM, KP, CMAX>), gdecA, dim3(256), ldsC, st, Q, d);
     }
     const bool split = split_grads(e);

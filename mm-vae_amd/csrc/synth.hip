@@ -121,6 +121,7 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 2), hipMemcpyHostToDevice);
     std::vector<float> ones((size_t)N * e->C, 1.f);
     hipMemcpy(e->d_covar, ones.data(), sizeof(float) * N * e->C, hipMemcpyHostToDevice);
+    e->unit_covar = e->C == 1;
     hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)N), dim3(256), 0, e->stream, seed, N, D, loglib, d_pg,
                        e->d_rowptr, e->d_col, e->d_val);
     if ((er = hipStreamSynchronize(e->stream)) != hipSuccess) return er;

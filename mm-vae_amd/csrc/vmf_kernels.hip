@@ -432,7 +432,10 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
     const int S = d.tpsD + 1;
-    const int C = (CM == 1) ? 1 : d.C;
+    // CM = 0: unit covariate (Engine::unit_covar, C = 1): covar_dec folds into a per-gene
+    // constant, and the covariate gradient's column sums are the bias gradient's
+    constexpr int CA = CM > 0 ? CM : 1;  // covariate array extent
+    const int C = (CM <= 1) ? 1 : d.C;
     const int nq = 1 + C;
     const VDecLds L(KP, (int)sizeof(T), S, nq, PASS, NPL);
     constexpr int WIMG = 64 * KP * (int)sizeof(T);  // one plane of the W / WdT images
@@ -487,7 +490,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     for (int s = 0; s < KS; ++s)
         zfr[s] = M::load(&Z[(int64_t)(row0 + (lane & 15)) * KP + s * M::KSTEP + (lane >> 4) * M::EPL], Q.zplane);
     // rows 4 (lane >> 4) + 2h + j live in component j of the pair h (packed-f32 element math)
-    f2 crow2[2][CM], ra2[2], rbt2[2], svv2[2], sv2[2], slv2[2];
+    f2 crow2[2][CA], ra2[2], rbt2[2], svv2[2], sv2[2], slv2[2];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int h = r >> 1, j = r & 1;
@@ -612,20 +615,20 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             const f32x4 acc = LP ? accn : logit(gb);
             if (LP && gb + 1 < 4) accn = logit(gb + 1);
             const float4 g4 = gst[gl];
-            float wcd[CM];
+            float wcd[CA];
             wcd[0] = g4.z;
 #pragma unroll
             for (int c = 1; c < CM; ++c) wcd[c] = (c < C && 64 * t + gl < d.D) ? Q.Wcd[(int64_t)(64 * t + gl) * C + c] : 0.f;
-            f2 csp[1 + CM];
+            f2 csp[1 + CA];
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c) csp[c] = splat2(0.f);
+            for (int c = 0; c < 1 + CA; ++c) csp[c] = splat2(0.f);
             constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
                 const int rl = 4 * (lane >> 4) + 2 * h;
                 const f2 ex = fma2(f2{acc[2 * h], acc[2 * h + 1]}, splat2(L2E), splat2(g4.x));
                 const f2 u = f2{fexp2(ex.x), fexp2(ex.y)};      // exp(z_dec(z))   vmf.hh:285
-                f2 hc = splat2(g4.y);                           // covar_dec(c)    vmf.hh:286
+                f2 hc = splat2(CM == 0 ? g4.y + g4.z : g4.y);  // covar_dec(c)    vmf.hh:286
 #pragma unroll
                 for (int c = 0; c < CM; ++c) hc = fma2(crow2[h][c], splat2(wcd[c]), hc);
                 const f2 v = u + hc;                            // padded genes: 0 + 0
@@ -648,12 +651,13 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
                     }
                 }
             }
-            float cs[1 + CM];
+            float cs[1 + CA];
 #pragma unroll
-            for (int c = 0; c < 1 + CM; ++c) cs[c] = csp[c].x + csp[c].y;
+            for (int c = 0; c < 1 + CA; ++c) cs[c] = csp[c].x + csp[c].y;
+            if (CM == 0) cs[1] = cs[0];  // sum_b dv c_b with c_b = 1
             if (PASS) {
                 float* pw = part + w * nq * 64 + gl;
-                if (CM == 1) {  // nq = 2
+                if (CM <= 1) {  // nq = 2
                     const float s = sum_rowgroups2(cs[0], cs[1]);
                     if (!(lane & 16)) pw[(lane >> 5) * 64] = s;
                 } else {
@@ -1264,12 +1268,14 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.zplane = (int64_t)d.Bpad * d.KP;
     Q.wplane = (int64_t)e->KP * e->DP;
     const dim3 gdec(nrb * d.nsD);
+    const bool ucov = d.C == 1 && e->unit_covar;  // the CM = 0 decoder instances
     const int nq = 1 + d.C;
     const int S = d.tpsD + 1;
     {
         ScopedTimer tm(e, "k_vdec_fwd");
         const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0, NPL).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        if (ucov) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 0>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
         else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     VGrads G = vmf_grads(e);
@@ -1288,7 +1294,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vdec_bwd");
         const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 1, NPL).bytes;
-        if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        if (ucov) hipLaunchKernelGGL((k_vdec_bwd<PM, KP, 0>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        else if (d.C == 1) hipLaunchKernelGGL((k_vdec_bwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
         else hipLaunchKernelGGL((k_vdec_bwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
     }
     const bool split = split_grads(e);
