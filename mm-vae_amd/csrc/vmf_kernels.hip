@@ -387,6 +387,9 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 
 // trw (16-bit operands): pass 1 reads the dz GEMM's B operand transposed from the W image, so
 // no WdT image is staged (x3 at K <= 32: 3 workgroups per CU instead of 2)
+#ifndef MMVAE_VDEC_SLOAD_LATE
+#define MMVAE_VDEC_SLOAD_LATE 0
+#endif
 #ifndef MMVAE_VDEC_LPIPE
 #define MMVAE_VDEC_LPIPE 1  // 0: each gene block's logits right before its element math (A/B)
 #endif
@@ -551,7 +554,9 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 
     auto tile = [&](int t, ListEntries& pend, const float (&lv)[2], const ListEntries& pnext, float (&lvnext)[2]) {
         const int tl = t - t0;
-        if (!dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits
+        // unconditional (clamped) next-stage loads: counted waits (MMVAE_VDEC_SLOAD_LATE: issued
+        // after the densify instead, off the post-barrier burst of every wave's loads)
+        if (!MMVAE_VDEC_SLOAD_LATE && !dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));
         lap(5);
         // ---- densify this wave's 16 x 64 log1p(relu x) tile (zero outside the entries) ----
         if constexpr (PRE) {
@@ -572,6 +577,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         asm volatile("" : "+v"(zpos0), "+v"(zpos1));
         const bool zall = pend.n > 128;  // entries past the register pair: clear the whole tile
         pend.fetch(Q.ents, segw, toffl, min(tl + 2, t1 - t0 - 1), lane);
+        if (MMVAE_VDEC_SLOAD_LATE && !dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));
         lap(0);
         // the logits of gene block gb (16 genes x this wave's 16 rows); block gb + 1's MFMAs are
         // issued ahead of block gb's element math, so the two overlap inside the wave
