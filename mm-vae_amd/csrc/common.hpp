@@ -203,7 +203,12 @@ template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0) {
 // all ones.
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 MMVAE_DEV uint32_t pk_bf16(float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)a, (__bf16)b}); }
-template <int BS = 2048> MMVAE_DEV int pqt_off(int g, int r) { return (g >> 4) * BS + (g & 15) * 32 + r * 2; }  // bytes
+// (bytes; a gene's 8-byte row quads XOR-swizzled by (g >> 2) & 3: the epilogue's row-pair stores
+// go from 4-way to 2-way bank conflicts (free for ds_write_b32) and the transposed reads of genes
+// g and g + 8 from 2-way to none — MI355X_MICROARCH.md LDS bank table)
+template <int BS = 2048> MMVAE_DEV int pqt_off(int g, int r) {
+    return (g >> 4) * BS + (g & 15) * 32 + (((r >> 2) ^ ((g >> 2) & 3)) << 3) + (r & 3) * 2;
+}
 template <int BS = 2048> MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0) {
     const int lane = threadIdx.x & 63;
     const int k = k0 + 8 * (lane >> 4) + ((lane >> 2) & 3), r = 4 * (lane & 3);
