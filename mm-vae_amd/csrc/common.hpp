@@ -176,7 +176,11 @@ MMVAE_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); 
 MMVAE_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
     constexpr int NCH = RB / 16;
-    return row * RB + ((((byte >> 4) ^ ((row >> 1) & (NCH - 1)))) << 4) + (byte & 15);
+    // 64-byte rows (4 chunks): rows r and r + 8 of a transposed read (tr_frag) share their 256-byte
+    // bank window, so bit 3 of the row selects the other chunk pair; the 16-lane ds_read_b128 row
+    // reads stay conflict-free with it
+    const int x = NCH == 4 ? (((row >> 1) & 1) | ((row >> 2) & 2)) : ((row >> 1) & (NCH - 1));
+    return row * RB + (((byte >> 4) ^ x) << 4) + (byte & 15);
 }
 
 // MFMA 16x16x32 B fragment of a k-by-column block read TRANSPOSED from a swizzled row-major
