@@ -337,6 +337,9 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     const int dec_cu = vmf_model ? (bf_ops ? 4 : (cfg->dtype == MMVAE_DTYPE_BF16X3 && e->KP == 32 ? 3 : 2))
                                  : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
     e->nsplit_d = pick_split(dec_cu);
+    // vMF forward decoder pass: ~29 KB of LDS and <= 128 VGPRs in the 16-bit operand modes at
+    // K <= 32 with one covariate (VFwdOcc, vmf_kernels.hip): 4 per CU instead of the backward's 3
+    e->nsplit_f = (vmf_model && e->KP == 32 && e->C == 1 && cfg->dtype != MMVAE_DTYPE_F32) ? pick_split(4) : e->nsplit_d;
     // passes A / C are light: a finer gene split gives 4x the waves for latency hiding
     e->nsplit_a = (int)std::min<int64_t>(e->NT, std::max<int64_t>(e->nsplit_d, (2048 + e->nrb_max - 1) / e->nrb_max));
     // encoder forward: bf16 ~37 KB (double-buffered), x3 ~39 KB single-buffered: 4 per CU; f32 2
@@ -354,6 +357,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     if (std::getenv("MMVAE_NSPLIT_E")) e->nsplit_b = e->nsplit_e;  // a forced encoder split covers both
     env_split("MMVAE_NSPLIT_B", e->nsplit_b);
     env_split("MMVAE_NSPLIT_D", e->nsplit_d);
+    env_split("MMVAE_NSPLIT_F", e->nsplit_f);
     env_split("MMVAE_NSPLIT_A", e->nsplit_a);
     e->n_lat_wg = (int)(e->Bpad / LAT_CELLS);  // latent kernels: 16 cells per workgroup
     e->klp_off = e->nrb_max * e->nsplit_d;
@@ -437,7 +441,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     HIPCHK(e, dalloc(&e->d_zf, Bp * KP));
     HIPCHK(e, dalloc(&e->d_zb, 2 * Bp * KP));  // hi + lo planes (x3 mode)
     HIPCHK(e, dalloc(&e->d_lsep, (int64_t)e->nsplit_a * Bp * 2));
-    HIPCHK(e, dalloc(&e->d_rowB, (int64_t)e->nsplit_d * Bp * (2 + e->R)));
+    HIPCHK(e, dalloc(&e->d_rowB, (int64_t)std::max(e->nsplit_d, e->nsplit_f) * Bp * (2 + e->R)));
     HIPCHK(e, dalloc(&e->d_rowfin, Bp * 2));
     HIPCHK(e, dalloc(&e->d_dzp, (int64_t)e->nsplit_d * Bp * 2 * KP));
     HIPCHK(e, dalloc(&e->d_dh, Bp * KP));
@@ -1533,7 +1537,7 @@ int mmvae_debug_poison(mmvae_h e, int32_t byte) {
         {e->d_zf, sizeof(float) * (size_t)(Bp * KP)},
         {e->d_zb, sizeof(__bf16) * (size_t)(2 * Bp * KP)},
         {e->d_lsep, sizeof(float) * (size_t)(e->nsplit_a * Bp * 2)},
-        {e->d_rowB, sizeof(float) * (size_t)(e->nsplit_d * Bp * (2 + e->R))},
+        {e->d_rowB, sizeof(float) * (size_t)(std::max(e->nsplit_d, e->nsplit_f) * Bp * (2 + e->R))},
         {e->d_rowfin, sizeof(float) * (size_t)(Bp * 2)},
         {e->d_dzp, sizeof(float) * (size_t)(e->nsplit_d * Bp * 2 * KP)},
         {e->d_dh, sizeof(float) * (size_t)(Bp * KP)},

@@ -2089,6 +2089,7 @@ static Dims nb_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.nsB = e->nsplit_b;
     d.tpsB = (int)((e->NT + d.nsB - 1) / d.nsB);
     d.nsD = e->nsplit_d;
+    d.nsF = d.nsD;
     d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
     d.nsA = e->nsplit_a;
     d.tpsA = (int)((e->NT + d.nsA - 1) / d.nsA);

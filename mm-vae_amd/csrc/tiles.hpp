@@ -18,6 +18,7 @@ struct Dims {
     int nsE, tpsE;  // encoder (forward) splits, tiles per split
     int nsB, tpsB;  // encoder backward splits
     int nsD, tpsD;  // decoder pass-B splits
+    int nsF, tpsF;  // vMF decoder forward pass splits (its own occupancy; = nsD otherwise)
     int nsA, tpsA;  // decoder passes A / C splits
     float inv_n, beta;
     int lat_stride, LAT_H, LAT_MEAN, LAT_A, LAT_EPS, LAT_NMEAN, LAT_AN, LAT_EPSN, LAT_ZNU, LAT_D,

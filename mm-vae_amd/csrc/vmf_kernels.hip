@@ -337,7 +337,7 @@ struct VDecPtrs {
     const void* WdP;       // [DP][KP] T
     const void* WdT;       // [KP][DP] T
     const float* rowfin;   // [Bpad][2]: alpha, beta (eval path: k_vrowfin)
-    float* rowB;           // [nsD][Bpad][3]: |v|^2, sum v, sum l v
+    float* rowB;           // [nsF][Bpad][3]: |v|^2, sum v, sum l v (forward pass splits)
     const float* rowx;     // [Bpad][..]: [1] = sum (l^2 + 2 eps l)
     const float* vk;       // kappa scalars (vkappa_body in k_vprep)
     float* rowcos;         // [Bpad] cos_b (written by split 0 of the backward pass)
@@ -355,7 +355,7 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
                            const float* __restrict__ rowB, const float* __restrict__ vk, int b, int p0, int np,
                            float& al, float& be, float& cosb) {
     float Svv = 0.f, Sv = 0.f, Slv = 0.f;
-    for (int s = p0; s < d.nsD; s += np) {
+    for (int s = p0; s < d.nsF; s += np) {  // the forward pass's splits
         const float* rp = rowB + ((int64_t)s * d.Bpad + b) * 3;
         Svv += rp[0];
         Sv += rp[1];
@@ -431,10 +431,11 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     constexpr bool TRW = BF;  // dz B operand read transposed from the W image (VDecLds)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = blockIdx.x % d.nsD, rb = blockIdx.x / d.nsD;
+    const int nsp = PASS ? d.nsD : d.nsF, tps = PASS ? d.tpsD : d.tpsF;  // the forward pass: own split
+    const int sp = blockIdx.x % nsp, rb = blockIdx.x / nsp;
     const int row0 = rb * 64 + 16 * w;
-    const int t0 = sp * d.tpsD, t1 = min(d.NT, t0 + d.tpsD);
-    const int S = d.tpsD + 1;
+    const int t0 = sp * tps, t1 = min(d.NT, t0 + tps);
+    const int S = tps + 1;
     // CM = 0: unit covariate (Engine::unit_covar, C = 1): covar_dec folds into a per-gene
     // constant, and the covariate gradient's column sums are the bias gradient's
     constexpr int CA = CM > 0 ? CM : 1;  // covariate array extent
@@ -556,7 +557,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         const int tl = t - t0;
         // unconditional (clamped) next-stage loads: counted waits (MMVAE_VDEC_SLOAD_LATE: issued
         // after the densify instead, off the post-barrier burst of every wave's loads)
-        if (!MMVAE_VDEC_SLOAD_LATE && !dbg_bit(d.dbg, 512)) stage_load(min(t + 1, t1 - 1));
+        if (!MMVAE_VDEC_SLOAD_LATE && !dbg_bit(d.dbg, 512)) stage_load(dbg_bit(d.dbg, 1024) ? t0 : min(t + 1, t1 - 1));
         lap(5);
         // ---- densify this wave's 16 x 64 log1p(relu x) tile (zero outside the entries) ----
         if constexpr (PRE) {
@@ -752,11 +753,14 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     }
 }
 
+// forward pass occupancy: 4 waves per SIMD (<= 128 VGPRs, no spills) for the 16-bit operand
+// modes at K <= 32 with one covariate — the pass is latency-bound (phase stamps: one wave per SIMD
+// takes ~3.1k cycles per tile, three take ~3.5k), so a fourth workgroup per CU adds throughput
+template <class P, int KP, int CM> struct VFwdOcc {
+    static constexpr int value = (sizeof(typename Elem<P>::type) == 2 && KP <= 32 && CM <= 1) ? 4 : 2;
+};
 template <class P, int KP, int CM>
-#ifndef MMVAE_VDEC_FWD_OCC
-#define MMVAE_VDEC_FWD_OCC 2
-#endif
-__global__ __launch_bounds__(256, MMVAE_VDEC_FWD_OCC) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 0, CM>(Q, d, epsD); }
+__global__ __launch_bounds__(256, (VFwdOcc<P, KP, CM>::value)) void k_vdec_fwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 0, CM>(Q, d, epsD); }
 template <class P, int KP, int CM>
 __global__ __launch_bounds__(256, 2) void k_vdec_bwd(VDecPtrs Q, Dims d, float epsD) { vdec_body<P, KP, 1, CM>(Q, d, epsD); }
 
@@ -1203,6 +1207,8 @@ static Dims vmf_dims(Engine* e, int64_t B, int64_t n_total, float beta) {
     d.tpsB = (int)((e->NT + d.nsB - 1) / d.nsB);
     d.nsD = e->nsplit_d;
     d.tpsD = (int)((e->NT + d.nsD - 1) / d.nsD);
+    d.nsF = e->nsplit_f;
+    d.tpsF = (int)((e->NT + d.nsF - 1) / d.nsF);
     d.nsA = e->nsplit_a;
     d.tpsA = (int)((e->NT + d.nsA - 1) / d.nsA);
     d.inv_n = 1.f / (float)n_total;
@@ -1279,10 +1285,11 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     const int S = d.tpsD + 1;
     {
         ScopedTimer tm(e, "k_vdec_fwd");
-        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), S, nq, 0, NPL).bytes;
-        if (ucov) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 0>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
-        else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gdec, dim3(256), lds, st, Q, d, sc.epsD);
+        const dim3 gfwd(nrb * d.nsF);  // the forward pass's own split (VFwdOcc)
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), d.tpsF + 1, nq, 0, NPL).bytes;
+        if (ucov) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 0>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
+        else if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
+        else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
     }
     VGrads G = vmf_grads(e);
     const int SMALL = small_len(d.K, d.E, d.KE, d.C, 0);

@@ -11,12 +11,13 @@ eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dt, seed=1, model=mmvae_amd.
 eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 nsd = int(os.environ.get("MMVAE_NSPLIT_D", "12"))
-nwg = (B // 64) * nsd
+nsf = int(os.environ.get("MMVAE_NSPLIT_F", "16"))  # the forward pass's own split
 names = ["entry fetch", "gene blocks", "barrier 1", "slab store", "stage+barrier 2", "stage load", "zero", "visit"]
 for label, run in (("fwd", lambda i: eng.eval_loss(np.arange(B), 1.0, step_id=i)),
                    ("bwd", lambda i: eng.step(np.arange(B), 1.0, step_id=i))):
     for i in range(3):
         run(i)
+    nwg = (B // 64) * (nsf if label == "fwd" else nsd)
     buf = np.zeros(nwg * 4 * 12, np.float32)
     rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
     assert rc == 0
