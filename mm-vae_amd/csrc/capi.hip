@@ -345,7 +345,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     // encoder forward: bf16 ~37 KB (double-buffered), x3 ~39 KB single-buffered: 4 per CU; f32 2
     e->nsplit_e = pick_split(cfg->dtype == MMVAE_DTYPE_F32 ? 2 : 4);
     // encoder backward: bf16 ~37 KB LDS (4 per CU); x3 / f32 keep W in registers, ~43 KB (3 per CU)
-    e->nsplit_b = pick_split(bf_ops ? 4 : 3);
+    e->nsplit_b = pick_split((bf_ops || vmf_model) ? 4 : 3);  // vMF: no raw-count tile (enc_bwd.hpp)
     // tuning overrides (diagnostics): MMVAE_NSPLIT_E / _D / _A
     auto env_split = [&](const char* name, int& v) {
         if (const char* ev = std::getenv(name)) {

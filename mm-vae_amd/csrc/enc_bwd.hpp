@@ -22,10 +22,12 @@ struct EncBwdLds {
     // wsz: element size of the staged W image (f32 in the x3 mode: W only feeds a VALU dot);
     // planes: operand planes of the log1p tile (x3: hi + lo)
     // wsz 4 (f32 / x3): W stays in registers, no LDS image
-    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes, int tab_bytes) {
+    // raw: the raw-count tile (NB only; the vMF backward has no raw-count term, and without the
+    // 17 KB tile its x3 workgroup fits 4 per CU instead of 3)
+    MMVAE_HOSTDEV EncBwdLds(int KP, int esz, int S, int LS, int nsc, int wsz, int planes, int tab_bytes, bool raw) {
         o_lt = wsz == 4 ? 0 : KP * 64 * wsz;
         o_raw = o_lt + planes * 64 * LS * esz;
-        o_part = o_raw + 64 * 68 * 4;
+        o_part = o_raw + (raw ? 64 * 68 * 4 : 0);
         o_scal = o_part + 4 * 64 * 4;
         o_wave = o_scal + nsc * 64 * 4;
         wave_bytes = ((S * 4 + 15) / 16) * 16;  // the wave block's tile offsets
@@ -64,7 +66,7 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     const int S = d.tpsB + 1;
     const int H = H1 ? 1 : d.H;
     const int nq = RAW ? 2 + H : 1;  // vMF (RAW = false): only the log1p term
-    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1, Log1pTab<P>::BYTES);
+    const EncBwdLds L(KP, (int)sizeof(T), S, LS, 1 + HN, (int)sizeof(WT), X ? 2 : 1, Log1pTab<P>::BYTES, RAW);
     uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
     Log1pTab<P>::fill(ltab);
     char* wst = smem;
@@ -254,12 +256,12 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     }
 }
 
-template <class P, int KP>
+template <class P, int KP, bool RAW = true>
 inline size_t enc_bwd_lds(const Dims& d) {
     using T = typename Elem<P>::type;
     constexpr int LS = sizeof(T) == 2 ? 80 : 68;
     return (size_t)EncBwdLds(KP, (int)sizeof(T), d.tpsB + 1, LS, 1 + (d.H == 1 ? 1 : HMAX),
-                             (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1, Log1pTab<P>::BYTES).bytes;
+                             (int)sizeof(typename WEnc<P>::type), IsX3<P>::value ? 2 : 1, Log1pTab<P>::BYTES, RAW).bytes;
 }
 
 }  // namespace mmvae

@@ -1336,7 +1336,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         const T* dhT = reinterpret_cast<const T*>(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f);
         const auto* WeT = reinterpret_cast<const typename WEnc<PM>::type*>(
             std::is_same<typename WEnc<PM>::type, __bf16>::value ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f);
-        hipLaunchKernelGGL((k_enc_bwd_vsmall<PM, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP>(d)), st, e->d_ents,
+        hipLaunchKernelGGL((k_enc_bwd_vsmall<PM, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP, false>(d)), st, e->d_ents,
                            e->d_seg, e->d_toff, e->d_lat, dhT, (int64_t)KP * d.Bpad, WeT, d, e->d_slabE, nenc, sc,
                            e->d_small, e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk,
                            e->d_out, sqS);
