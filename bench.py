@@ -377,6 +377,26 @@ def secondary(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=50, warmup=5, 
     return out
 
 
+def streamed(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=30, warmup=5, label=""):
+    """The out-of-core mode (mmvae_stream_csr): the dataset in host memory, each step's rows gathered
+    over PCIe into a batch CSR in HBM — the same synthetic dataset, copied to the host."""
+    src, nnz = make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, 0)
+    rp, col, val = src.get_rows(np.arange(cells, dtype=np.int64))
+    src.close()
+    eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dtype, device=0, seed=1234,
+                           model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
+    eng.init_params(seed=7)
+    eng.graph(True)
+    eng.stream_csr(rp, col, val)
+    batches = [(s * B + np.arange(B)) % cells for s in range(warmup + steps)]
+    dt = time_steps(eng, batches, 1.0, B, 0, steps, warmup)
+    out = {"label": label, "value": round(B * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
+           "dtype": dtype, "workload": f"{model.upper()} {cells} x {D}, latent {K}, batch {B}", "path": eng.path(),
+           "pcie_bytes_per_step": round(8 * nnz / cells * B), "host_dataset_gb": round((8 * nnz + 8 * cells) / 2 ** 30, 2)}
+    eng.close()
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -495,6 +515,9 @@ def main():
             for dt_ in ("bf16x3", "f32"):
                 lines.append(secondary(mmvae_amd, "nb", 20000, 128, 4096, dt_, 100000, args.lib_size, steps=20,
                                        label=f"wide path: NB 100k x 20k, --mean_latent 128 (dense batch), {dt_}"))
+            # the out-of-core mode: CSR in host memory, batch rows gathered over PCIe every step
+            lines.append(streamed(mmvae_amd, "nb", 20000, 64, 4096, "bf16x3", 100000, args.lib_size,
+                                  label="streamed dataset (mmvae_stream_csr): NB 100k x 20k in host memory, bf16x3"))
             out["lines"] = lines
     print(json.dumps(out), flush=True)
     if world > 1:

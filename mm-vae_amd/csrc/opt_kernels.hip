@@ -30,6 +30,20 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
     const float lr_bc1 = ss->lr_bc1, inv_sqrt_bc2 = ss->inv_sqrt_bc2;  // this step's (staged with the batch)
     __shared__ float s_coef;
     __shared__ double sb[4];
+    // the first EPT elements of this thread's grid-stride range are loaded before the clip norm's
+    // partials are reduced: the update's loads do not wait for the norm
+    constexpr int EPT = 4;
+    const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+    float gv[EPT], pv[EPT], mv[EPT], vv[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        const int64_t i = i0 + e * stride;
+        const bool in = i < n;
+        gv[e] = in ? g[i] : 0.f;
+        pv[e] = in ? p[i] : 0.f;
+        mv[e] = in ? m[i] : 0.f;
+        vv[e] = in ? v[i] : 0.f;
+    }
     double tp = 0.0;
     for (int i = threadIdx.x; i < nparts; i += 256) tp += part[i];  // fixed order per block
     tp = wave_sum_d(tp);
@@ -45,17 +59,22 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
     }
     __syncthreads();
     const float coef = s_coef;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        float gi = g[i] * coef;                         // grad.mul_(clip_coef_clamped)
-        const float pi = p[i];
+    auto update = [&](int64_t i, float gi, float pi, float m0, float v0) {
+        gi = gi * coef;                                 // grad.mul_(clip_coef_clamped)
         gi = gi + wd * pi;                              // grad.add(p, weight_decay)
-        const float mi = m[i] * b1 + gi * (1.f - b1);   // exp_avg.mul_(b1).add_(grad, 1-b1)
-        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+        const float mi = m0 * b1 + gi * (1.f - b1);     // exp_avg.mul_(b1).add_(grad, 1-b1)
+        const float vi = v0 * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
         const float denom = sqrtf(vi) * inv_sqrt_bc2 + eps;
         m[i] = mi;
         v[i] = vi;
         p[i] = pi - lr_bc1 * (mi / denom);              // p.addcdiv_(exp_avg, denom, -lr/bc1)
+    };
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        const int64_t i = i0 + e * stride;
+        if (i < n) update(i, gv[e], pv[e], mv[e], vv[e]);
     }
+    for (int64_t i = i0 + EPT * stride; i < n; i += stride) update(i, g[i], p[i], m[i], v[i]);
 }
 
 // Adam's bias-corrected rates of optimiser step t (optim/adam.cpp), into the staged scalars
