@@ -14,3 +14,5 @@ cat gpurun_out/$TAG.bench_vmf.json
 export TMPDIR=/tmp; cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_trace -o run --output-format csv -- python3 $R/bench.py --no-cpu --steps 30 --warmup 5 > $R/gpurun_out/${TAG}_trace.json 2>$R/gpurun_out/${TAG}_trace.err || exit 4
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_vtrace -o run --output-format csv -- python3 $R/bench.py --model vmf --no-cpu --steps 30 --warmup 5 > $R/gpurun_out/${TAG}_vtrace.json 2>$R/gpurun_out/${TAG}_vtrace.err || exit 5
+# keep the merged-back output small (gpurun copies at most 64 MiB): the per-dispatch traces go
+rm -f $R/gpurun_out/${TAG}_trace/run_kernel_trace.csv $R/gpurun_out/${TAG}_vtrace/run_kernel_trace.csv
