@@ -743,6 +743,18 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     for (int s2 = 0; s2 < 2; ++s2) HIPCHK(e, batch_set_alloc(e, s2, cap));
     e->stage_bytes = (e->stage_bytes_res + sizeof(int64_t) * (size_t)(e->Bpad + 1) + 15) / 16 * 16;
     stream_bind(e, e->cur_slot);
+    // the prefetched gather (stream.hip stream_prefetch); MMVAE_STREAM_SYNC=1 keeps it in the step
+    e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");
+    if (e->stream_prefetch) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+        for (int s2 = 0; s2 < 2; ++s2) {
+            HIPCHK(e, hipEventCreateWithFlags(&e->ev_gathered[s2], hipEventDisableTiming));
+            HIPCHK(e, hipEventCreateWithFlags(&e->ev_setfree[s2], hipEventDisableTiming));
+            HIPCHK(e, hipEventRecord(e->ev_setfree[s2], e->stream));  // no step on either set yet
+            HIPCHK(e, hipHostMalloc((void**)&e->h_gcells[s2], sizeof(int64_t) * (size_t)(e->Bpad + 1),
+                                    hipHostMallocMapped | hipHostMallocCoherent));
+        }
+    }
     return MMVAE_OK;
 }
 
@@ -1040,8 +1052,18 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
             o += (c < Nv) ? e->cell_nnz[(size_t)c] : 0;
         }
         e->h_brp_pin[Bp] = o;
+        if (e->stream_prefetch) {
+            // the gather reads the slot's row ids; the staged cells become the identity (the
+            // batch's row b is batch-CSR row b), as the in-step gather leaves them
+            int64_t* gc = e->h_gcells[e->cur_slot];
+            for (int64_t b = 0; b < Bp; ++b) {
+                gc[b] = e->h_cells_pin[b];
+                e->h_cells_pin[b] = b;
+            }
+        }
         if (o > e->bset[e->cur_slot].cap) {
             HIPCHK(e, hipStreamSynchronize(e->stream));
+            if (e->gstream) HIPCHK(e, hipStreamSynchronize(e->gstream));
             HIPCHK(e, batch_set_alloc(e, e->cur_slot, o + o / 4 + 1024));
             ++e->graph_gen;  // the slot's graphs point at the old buffers
         }
@@ -1117,6 +1139,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, a->cell_ids, a->ridx, a->B, /*balance=*/true);
     if (rc) return rc;
+    HIPCHK(e, stream_prefetch(e));  // (streamed dataset: the rows' gather on its own stream)
     const bool vmf = e->cfg.model == MMVAE_MODEL_VMF;
     if (a->eps) std::memcpy(e->h_eps_pin, a->eps, sizeof(float) * a->B * (e->K + (vmf ? 0 : e->R)));
     // the step's scalars travel in the staged block (the kernels read them from there)
@@ -1203,6 +1226,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
         if (rc) return rc;
     }
     HIPCHK(e, release_slot(e, !e->wide));  // this slot's block is free after this step's copy
+    HIPCHK(e, stream_step_done(e));
     if (a->update) {
         e->adam_step += 1;
         e->have_grads = true;
@@ -1248,6 +1272,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     HIPCHK(e, hipSetDevice(e->device));
     int rc = stage_rows(e, cell_ids, nullptr, B);
     if (rc) return rc;
+    HIPCHK(e, stream_prefetch(e));
     if (e->wide) {
         if (e->frozen_dirty) HIPCHK(e, wide_prepare_frozen(e));
         if (!e->d_tmp) HIPCHK(e, dalloc(&e->d_tmp, 2 * e->Bpad * e->K));
@@ -1266,6 +1291,7 @@ int mmvae_encode(mmvae_h e, const int64_t* cell_ids, int64_t B, float* mean, flo
     HIPCHK(e, hipMemcpyAsync(mean, e->d_tmp, sizeof(float) * B * e->K, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(lnvar, e->d_tmp + e->Bpad * e->K, sizeof(float) * B * e->K, hipMemcpyDeviceToHost,
                              e->stream));
+    HIPCHK(e, stream_step_done(e));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MMVAE_OK;
 }
@@ -1518,6 +1544,7 @@ int mmvae_tiling_info(mmvae_h e, int32_t* out) {
 int mmvae_debug_poison(mmvae_h e, int32_t byte) {
     if (!e) FAIL(e, MMVAE_E_ARG, "debug_poison: null");
     HIPCHK(e, hipSetDevice(e->device));
+    if (e->gstream) HIPCHK(e, hipStreamSynchronize(e->gstream));  // no gather in flight into a set
     const int64_t Bp = e->Bpad, DP = e->DP, KP = e->KP, nrb = e->nrb_max;
     const int64_t SMALL = small_len((int)e->K, (int)e->E, (int)e->KE, (int)e->C,
                                     e->cfg.model == MMVAE_MODEL_VMF ? 0 : (int)(2 * e->R * e->H + 2 * e->R + e->H + 1));

@@ -120,6 +120,15 @@ struct Engine {
         int64_t cap = 0;
     } bset[2];
     int64_t* h_brp_pin = nullptr;   // pinned: the staged batch rowptr [Bpad + 1] (streamed)
+    // prefetched gather (streamed, default; MMVAE_STREAM_SYNC=1: in the step's stream): the
+    // step's rows are gathered on gstream as soon as the step is staged, under the previous
+    // step's kernels.  h_gcells[s]: slot s's dataset row ids (mapped, read by the gather; the
+    // staged block then carries the identity), ev_gathered[s]: the gather done, the step waits;
+    // ev_setfree[s]: the last step on batch set s done, the next gather into it waits
+    bool stream_prefetch = false;
+    hipStream_t gstream = nullptr;
+    hipEvent_t ev_gathered[2] = {nullptr, nullptr}, ev_setfree[2] = {nullptr, nullptr};
+    int64_t* h_gcells[2] = {nullptr, nullptr};
     const int64_t* d_brp = nullptr;
     size_t stage_bytes_res = 0;     // the resident path's staged block (streamed adds the rowptr)
 
@@ -373,11 +382,13 @@ void adam_scalars(const Engine* e, int64_t t, StepScalars* ss);
 hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_t* nnz_out);
 hipError_t build_dataset_index(Engine* e);
 hipError_t index_rows(Engine* e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N, int32_t* rtp,
-                      float* cellnorm);
+                      float* cellnorm, hipStream_t st = nullptr);  // st: e->stream when null
 // streamed dataset: point the dataset views at staging slot s's batch set, and the step's gather
 // (after the staged block's copy) + batch index (stream.hip)
 void stream_bind(Engine* e, int s);
 hipError_t stream_gather(Engine* e);
+hipError_t stream_prefetch(Engine* e);
+hipError_t stream_step_done(Engine* e);
 void stream_release(Engine* e);
 
 }  // namespace mmvae

@@ -7,6 +7,9 @@
 // the rows' nonzero counts) and the batch rows' tile index (k_dataset_index), and every kernel
 // after it runs on the batch CSR as the resident path runs on the whole dataset — the batch's row
 // b is dataset row b, so the step's results are bit-identical to the resident path's.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "engine.hpp"
 #include "tiles.hpp"
@@ -15,35 +18,65 @@ namespace mmvae {
 
 // rows 0 .. Bp - 1 of the batch (cells[b] = the caller's cell, >= Nh for padding rows), plus
 // the batch's empty row Bp; afterwards cells[b] = b
+// gcells (prefetched gather): the batch's dataset rows from the slot's mapped row-id array, the
+// staged cells already the identity (cells is then not written).
+// A few workgroups (gather_wgs) walk the rows, each thread keeping 8 loads per array in flight:
+// PCIe latency wants many bytes in flight, not many waves — a grid of one workgroup per row held
+// every CU's wave slots while it waited on PCIe and slowed the step it overlapped.
+static constexpr int GU = 8;
 __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict__ hrp, const int32_t* __restrict__ hcol,
                                                        const float* __restrict__ hval, const float* __restrict__ hcov,
                                                        int64_t Nh, int C, int64_t* __restrict__ cells,
+                                                       const int64_t* __restrict__ gcells,
                                                        const int64_t* __restrict__ brp, int64_t Bp,
                                                        int64_t* __restrict__ rowptr, int32_t* __restrict__ col,
                                                        float* __restrict__ val, float* __restrict__ cov) {
-    const int64_t b = blockIdx.x;
-    if (b == Bp) {  // the empty row (and rowptr[N + 1] for readers of rowptr[c + 1])
-        if (threadIdx.x == 0) {
-            rowptr[Bp] = brp[Bp];
-            rowptr[Bp + 1] = brp[Bp];
+    for (int64_t b = blockIdx.x; b <= Bp; b += gridDim.x) {
+        if (b == Bp) {  // the empty row (and rowptr[N + 1] for readers of rowptr[c + 1])
+            if (threadIdx.x == 0) {
+                rowptr[Bp] = brp[Bp];
+                rowptr[Bp + 1] = brp[Bp];
+            }
+            for (int c = threadIdx.x; c < C; c += 256) cov[Bp * C + c] = 0.f;
+            continue;
         }
-        for (int c = threadIdx.x; c < C; c += 256) cov[Bp * C + c] = 0.f;
-        return;
+        const int64_t g = gcells ? gcells[b] : cells[b];
+        const bool real = g < Nh;
+        const int64_t s = brp[b], n = brp[b + 1] - s;
+        const int64_t src = real ? hrp[g] : 0;
+        for (int64_t i0 = 0; i0 < n; i0 += 256 * GU) {
+            int32_t cv[GU];
+            float vv[GU];
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {  // every load of the group in flight before the stores
+                const int64_t i = i0 + u * 256 + threadIdx.x;
+                if (i < n) {
+                    cv[u] = hcol[src + i];
+                    vv[u] = hval[src + i];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+                const int64_t i = i0 + u * 256 + threadIdx.x;
+                if (i < n) {
+                    col[s + i] = cv[u];
+                    val[s + i] = vv[u];
+                }
+            }
+        }
+        for (int c = threadIdx.x; c < C; c += 256) cov[b * C + c] = (real && hcov) ? hcov[g * C + c] : (hcov ? 0.f : (real ? 1.f : 0.f));
+        if (!gcells) __syncthreads();  // every thread has read cells[b]
+        if (threadIdx.x == 0) {
+            rowptr[b] = s;
+            if (!gcells) cells[b] = b;
+        }
     }
-    const int64_t g = cells[b];
-    const bool real = g < Nh;
-    const int64_t s = brp[b], n = brp[b + 1] - s;
-    const int64_t src = real ? hrp[g] : 0;
-    for (int64_t i = threadIdx.x; i < n; i += 256) {
-        col[s + i] = hcol[src + i];
-        val[s + i] = hval[src + i];
-    }
-    for (int c = threadIdx.x; c < C; c += 256) cov[b * C + c] = (real && hcov) ? hcov[g * C + c] : (hcov ? 0.f : (real ? 1.f : 0.f));
-    __syncthreads();  // every thread has read cells[b]
-    if (threadIdx.x == 0) {
-        rowptr[b] = s;
-        cells[b] = b;
-    }
+}
+
+static unsigned gather_wgs(const Engine* e) {
+    static const int env = [] { const char* v = std::getenv("MMVAE_GATHER_WGS"); return v ? std::atoi(v) : 0; }();
+    const int64_t rows = e->Bpad + 1;
+    return (unsigned)std::min<int64_t>(rows, env > 0 ? env : 64);
 }
 
 void stream_bind(Engine* e, int s) {
@@ -57,20 +90,59 @@ void stream_bind(Engine* e, int s) {
     e->d_cellnorm = q.cellnorm;
 }
 
+// in the step's stream (MMVAE_STREAM_SYNC=1, or a step graph's capture of it): nothing to do when
+// stream_prefetch already enqueued the gather on gstream
 hipError_t stream_gather(Engine* e) {
-    if (!e->streamed) return hipSuccess;
+    if (!e->streamed || e->stream_prefetch) return hipSuccess;
     ScopedTimer tm(e, "k_stream_gather");
     const int64_t Bp = e->Bpad;
-    hipLaunchKernelGGL(k_stream_gather, dim3((unsigned)(Bp + 1)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, e->hs_covar, e->N_host, (int)e->C, e->d_cells, e->d_brp, Bp, e->d_rowptr, e->d_col,
-                       e->d_val, e->d_covar);
+    hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
+                       e->hs_val, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
+                       e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
     if (e->wide) return hipSuccess;  // the wide path densifies from the CSR rows directly
     return index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm);
 }
 
+// the staged step's gather on gstream, right after staging (host side, before the step's launch
+// or graph): it starts once the last step on the slot's batch set is done and runs under the
+// previous step's kernels; the step's stream waits for it.  The row ids and row offsets are read
+// from the slot's mapped pinned memory, so nothing of the step's own staged copy is needed.
+hipError_t stream_prefetch(Engine* e) {
+    if (!e->streamed || !e->stream_prefetch) return hipSuccess;
+    const int s = e->cur_slot;
+    const int64_t Bp = e->Bpad;
+    hipError_t er = hipStreamWaitEvent(e->gstream, e->ev_setfree[s], 0);
+    if (er != hipSuccess) return er;
+    hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
+                       e->hs_val, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
+                       (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
+    if ((er = hipGetLastError()) != hipSuccess) return er;
+    if (!e->wide && (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
+        return er;
+    if ((er = hipEventRecord(e->ev_gathered[s], e->gstream)) != hipSuccess) return er;
+    return hipStreamWaitEvent(e->stream, e->ev_gathered[s], 0);
+}
+
+// after the step's launches: its batch set is free once the step is done
+hipError_t stream_step_done(Engine* e) {
+    if (!e->streamed || !e->stream_prefetch) return hipSuccess;
+    return hipEventRecord(e->ev_setfree[e->cur_slot], e->stream);
+}
+
 void stream_release(Engine* e) {
+    if (e->gstream) hipStreamSynchronize(e->gstream);
+    for (int s = 0; s < 2; ++s) {
+        if (e->ev_gathered[s]) hipEventDestroy(e->ev_gathered[s]);
+        if (e->ev_setfree[s]) hipEventDestroy(e->ev_setfree[s]);
+        if (e->h_gcells[s]) hipHostFree(e->h_gcells[s]);
+        e->ev_gathered[s] = e->ev_setfree[s] = nullptr;
+        e->h_gcells[s] = nullptr;
+    }
+    if (e->gstream) hipStreamDestroy(e->gstream);
+    e->gstream = nullptr;
+    e->stream_prefetch = false;
     for (auto& q : e->bset) {
         for (void* p : {(void*)q.rowptr, (void*)q.col, (void*)q.val, (void*)q.covar, (void*)q.rtp, (void*)q.cellnorm})
             if (p) hipFree(p);

@@ -179,9 +179,9 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
 
 // the index of rows [0, N] of a CSR (row N: the empty row) on the handle's stream, no sync
 hipError_t index_rows(Engine* e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N, int32_t* rtp,
-                      float* cellnorm) {
+                      float* cellnorm, hipStream_t st) {
     const float epsD = (float)(1e-2 / (double)(float)e->D);
-    hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((N + 1 + 3) / 4)), dim3(256), 0, e->stream, rowptr, col, val, N,
+    hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((N + 1 + 3) / 4)), dim3(256), 0, st ? st : e->stream, rowptr, col, val, N,
                        (int)e->NT, epsD, rtp, (float2*)cellnorm);
     return hipGetLastError();
 }
