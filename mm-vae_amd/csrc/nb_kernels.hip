@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         const float sig = expf(lnvar / 2.f);
         float eps = 0.f;
         if (k < K && b < d.B)
-            eps = eps_in ? epv[c] : philox_normal(seed, step, row_offset + pb, k);
+            eps = eps_in ? epv[c] : (dbg_bit(d.dbg, 4096) ? 0.f : philox_normal(seed, step, row_offset + pb, k));  // 4096: diagnostic
         const float z = mn + eps * sig;
         if (k < KE) L[d.LAT_H + k] = sH[(4 * w + c) * 68 + k];
         if (k < K) {
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
             if (b < d.B)
-                en = eps_in ? enp[c] : philox_normal(seed, step, row_offset + pb, NU_LANE + k);
+                en = eps_in ? enp[c] : (dbg_bit(d.dbg, 4096) ? 0.f : philox_normal(seed, step, row_offset + pb, NU_LANE + k));
             const float zn = nm + en * expf(nlv / 2.f);
             L[d.LAT_NMEAN + k] = nm;
             L[d.LAT_AN + k] = an;

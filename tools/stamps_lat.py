@@ -3,7 +3,7 @@ import ctypes, os, sys
 import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "mm-vae_amd", "py"))
 KER = os.environ.get("KER", "bwd")
-os.environ["MMVAE_DBG"] = "1024" if KER == "bwd" else "2048"
+os.environ["MMVAE_DBG"] = str((1024 if KER == "bwd" else 2048) | int(os.environ.get("EXTRA", "0")))
 import mmvae_amd
 B, D, K = 4096, 20000, 64
 eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
