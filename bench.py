@@ -392,7 +392,8 @@ def streamed(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=30, warmup=5, l
     dt = time_steps(eng, batches, 1.0, B, 0, steps, warmup)
     out = {"label": label, "value": round(B * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
            "dtype": dtype, "workload": f"{model.upper()} {cells} x {D}, latent {K}, batch {B}", "path": eng.path(),
-           "pcie_bytes_per_step": round(8 * nnz / cells * B), "host_dataset_gb": round((8 * nnz + 8 * cells) / 2 ** 30, 2)}
+           "pcie_bytes_per_step": round(4 * nnz / cells * B),  # packed entries (integer counts, D <= 65536)
+           "host_dataset_gb": round((8 * nnz + 8 * cells) / 2 ** 30, 2)}
     eng.close()
     return out
 

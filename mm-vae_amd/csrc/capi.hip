@@ -715,10 +715,40 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     const void* d;
     HIPCHK(e, reg(rowptr, sizeof(int64_t) * (size_t)(N + 1), &d));
     e->hs_rowptr = static_cast<const int64_t*>(d);
-    HIPCHK(e, reg(col, sizeof(int32_t) * (size_t)nnz, &d));
-    e->hs_col = static_cast<const int32_t*>(d);
-    HIPCHK(e, reg(val, sizeof(float) * (size_t)nnz, &d));
-    e->hs_val = static_cast<const float*>(d);
+    // integer counts below 2^16 over at most 2^16 genes: the packed copy (bit-exact values)
+    if (D <= 65536 && nnz > 0 && !getenv_is("MMVAE_STREAM_PACK", "0")) {
+        HIPCHK(e, hipHostMalloc((void**)&e->hs_packed, sizeof(uint32_t) * (size_t)nnz, hipHostMallocMapped));
+        const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        std::vector<char> ok(nth, 1);
+        for (unsigned t = 0; t < nth; ++t)
+            th.emplace_back([&, t] {
+                const int64_t a = nnz * t / nth, b = nnz * (t + 1) / nth;
+                for (int64_t i = a; i < b; ++i) {
+                    const float v = val[i];
+                    const uint32_t c = (uint32_t)(v >= 0.f && v < 65536.f ? (int)v : 0);
+                    const float back = (float)c;
+                    if (std::memcmp(&back, &v, 4) != 0) {  // non-integer, negative, -0, too large
+                        ok[t] = 0;
+                        return;
+                    }
+                    e->hs_packed[i] = ((uint32_t)col[i] << 16) | c;
+                }
+            });
+        for (auto& x : th) x.join();
+        if (std::find(ok.begin(), ok.end(), 0) != ok.end()) {
+            hipHostFree(e->hs_packed);
+            e->hs_packed = nullptr;
+        }
+    }
+    e->hs_col = nullptr;
+    e->hs_val = nullptr;
+    if (!e->hs_packed) {
+        HIPCHK(e, reg(col, sizeof(int32_t) * (size_t)nnz, &d));
+        e->hs_col = static_cast<const int32_t*>(d);
+        HIPCHK(e, reg(val, sizeof(float) * (size_t)nnz, &d));
+        e->hs_val = static_cast<const float*>(d);
+    }
     e->hs_covar = nullptr;
     e->unit_covar = e->C == 1 && all_ones(covar, N);
     if (covar) {

@@ -24,8 +24,10 @@ namespace mmvae {
 // PCIe latency wants many bytes in flight, not many waves — a grid of one workgroup per row held
 // every CU's wave slots while it waited on PCIe and slowed the step it overlapped.
 static constexpr int GU = 8;
+// hpk (packed dataset): gene << 16 | count per entry instead of hcol / hval
 __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict__ hrp, const int32_t* __restrict__ hcol,
-                                                       const float* __restrict__ hval, const float* __restrict__ hcov,
+                                                       const float* __restrict__ hval, const uint32_t* __restrict__ hpk,
+                                                       const float* __restrict__ hcov,
                                                        int64_t Nh, int C, int64_t* __restrict__ cells,
                                                        const int64_t* __restrict__ gcells,
                                                        const int64_t* __restrict__ brp, int64_t Bp,
@@ -44,23 +46,63 @@ __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict
         const bool real = g < Nh;
         const int64_t s = brp[b], n = brp[b + 1] - s;
         const int64_t src = real ? hrp[g] : 0;
-        for (int64_t i0 = 0; i0 < n; i0 += 256 * GU) {
-            int32_t cv[GU];
-            float vv[GU];
+        if (hpk) {
+            // packed words: 16-byte loads from the row's first 16-byte boundary (4 entries per
+            // lane, two loads in flight per lane), the unaligned head word by word
+            const int64_t head = std::min<int64_t>(n, (4 - (src & 3)) & 3);
+            if (threadIdx.x < head) {
+                const uint32_t w = hpk[src + threadIdx.x];
+                col[s + threadIdx.x] = (int32_t)(w >> 16);
+                val[s + threadIdx.x] = (float)(w & 0xffffu);
+            }
+            const uint4* p4 = reinterpret_cast<const uint4*>(hpk + src + head);
+            const int64_t n4 = (n - head) >> 2;
+            for (int64_t q0 = 0; q0 < n4; q0 += 512) {
+                uint4 w[2];
 #pragma unroll
-            for (int u = 0; u < GU; ++u) {  // every load of the group in flight before the stores
-                const int64_t i = i0 + u * 256 + threadIdx.x;
-                if (i < n) {
-                    cv[u] = hcol[src + i];
-                    vv[u] = hval[src + i];
+                for (int u = 0; u < 2; ++u) {
+                    const int64_t q = q0 + u * 256 + threadIdx.x;
+                    if (q < n4) w[u] = p4[q];
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int64_t q = q0 + u * 256 + threadIdx.x;
+                    if (q < n4) {
+                        const int64_t o = s + head + 4 * q;
+                        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            col[o + j] = (int32_t)(ww[j] >> 16);
+                            val[o + j] = (float)(ww[j] & 0xffffu);
+                        }
+                    }
                 }
             }
+            const int64_t tail0 = head + 4 * n4;
+            if (tail0 + threadIdx.x < n) {
+                const uint32_t w = hpk[src + tail0 + threadIdx.x];
+                col[s + tail0 + threadIdx.x] = (int32_t)(w >> 16);
+                val[s + tail0 + threadIdx.x] = (float)(w & 0xffffu);
+            }
+        } else {
+            for (int64_t i0 = 0; i0 < n; i0 += 256 * GU) {
+                int32_t cv[GU];
+                float vv[GU];
 #pragma unroll
-            for (int u = 0; u < GU; ++u) {
-                const int64_t i = i0 + u * 256 + threadIdx.x;
-                if (i < n) {
-                    col[s + i] = cv[u];
-                    val[s + i] = vv[u];
+                for (int u = 0; u < GU; ++u) {  // every load of the group in flight before the stores
+                    const int64_t i = i0 + u * 256 + threadIdx.x;
+                    if (i < n) {
+                        cv[u] = hcol[src + i];
+                        vv[u] = hval[src + i];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < GU; ++u) {
+                    const int64_t i = i0 + u * 256 + threadIdx.x;
+                    if (i < n) {
+                        col[s + i] = cv[u];
+                        val[s + i] = vv[u];
+                    }
                 }
             }
         }
@@ -97,7 +139,7 @@ hipError_t stream_gather(Engine* e) {
     ScopedTimer tm(e, "k_stream_gather");
     const int64_t Bp = e->Bpad;
     hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
+                       e->hs_val, (const uint32_t*)e->hs_packed, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
                        e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
@@ -116,7 +158,7 @@ hipError_t stream_prefetch(Engine* e) {
     hipError_t er = hipStreamWaitEvent(e->gstream, e->ev_setfree[s], 0);
     if (er != hipSuccess) return er;
     hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
+                       e->hs_val, (const uint32_t*)e->hs_packed, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
                        (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     if ((er = hipGetLastError()) != hipSuccess) return er;
     if (!e->wide && (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
@@ -149,6 +191,8 @@ void stream_release(Engine* e) {
         q = Engine::BatchSet{};
     }
     for (void* p : e->hs_registered) hipHostUnregister(p);
+    if (e->hs_packed) hipHostFree(e->hs_packed);
+    e->hs_packed = nullptr;
     e->hs_registered.clear();
     e->hs_rowptr = nullptr;
     e->hs_col = nullptr;

@@ -105,3 +105,19 @@ def test_streamed_batch_growth():
     for s, cells in enumerate([light, light, heavy, heavy, light]):
         assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
     assert st.graph_stats()["captures"] >= 3
+
+
+@pytest.mark.parametrize("kind", ["fractional", "wide_gene_ids"])
+def test_streamed_unpacked_entries(kind):
+    """Values that are not 16-bit integer counts (or D > 65536) keep the caller's col / val arrays
+    (no packed copy); the steps stay bit-identical to the resident handle."""
+    N, B = 800, 128
+    D = 3000 if kind == "fractional" else 70000
+    rp, col, val, _ = _data(N, D, seed=12)
+    if kind == "fractional":
+        val = (val * 0.5 + 0.25).astype(np.float32)
+    res, st = _pair("nb", "bf16x3", D, 16, B, (rp, col, val, None))
+    rng = np.random.default_rng(4)
+    for s in range(3):
+        cells = rng.integers(0, N, B)
+        assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
