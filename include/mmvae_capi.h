@@ -107,10 +107,13 @@ int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const
  * file, mtx_data_block_t::read, mmvae_io.hh:208-245): the caller's cell-major CSR (and covariates,
  * or NULL for ones) stays in host memory, registered here as mapped pinned memory; the caller keeps
  * the arrays alive and unchanged until mmvae_destroy or the next upload / synth / stream.  Every
- * step's device work then opens with a gather kernel that pulls the batch's rows over PCIe into a
- * per-step batch CSR in HBM (two slots, alternating with the staging slots) and indexes it; the
- * kernels after it are the resident path's, on the batch's rows.  Results are bit-identical to
- * mmvae_upload_csr of the same data.  HBM holds O(B nnz_b) of the dataset instead of O(N nnz). */
+ * step's rows are gathered over PCIe into a per-step batch CSR in HBM (two slots, alternating with
+ * the staging slots) and indexed; the gather runs on its own stream as soon as the step is staged,
+ * under the previous step's kernels, and the step waits for it.  When D <= 65536 and every value
+ * is a 16-bit integer count, the engine keeps a packed pinned copy (4 bytes per entry) and gathers
+ * from it.  The kernels after the gather are the resident path's, on the batch's rows.  Results
+ * are bit-identical to mmvae_upload_csr of the same data.  HBM holds O(B nnz_b) of the dataset
+ * instead of O(N nnz). */
 int mmvae_stream_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
                      int64_t N, int64_t D, const float* covar);
 /* Dataset size after upload/synth (mtx_data_block_t::ntot / nfeature, mmvae_io.hh:73-74). */
