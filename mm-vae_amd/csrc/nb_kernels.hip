@@ -953,7 +953,10 @@ struct DecNBLds {
 // (the 8-wave loss instance fits two workgroups per CU: 128 VGPRs, ~60 KB of LDS in bf16)
 // SG: the staggered instance (x3, NW = 8, training): waves 4-7 run half a tile behind waves 0-3
 // (below), the W stage is double-buffered and serves the dz GEMM transposed (no WdT stage)
-template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false, bool SG = false>
+// TRW: no WdT stage, the dz GEMM reads W transposed (as SG does) — with DB, the x3 8-wave instance
+// then double-buffers its stage and meets one barrier per tile (the default x3 training instance)
+template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false, bool SG = false,
+          bool TRW = false>
 __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
@@ -998,7 +1001,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const int C = (CM <= 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
     static_assert(!SG || (X && DB && NW == 8 && !LOSS), "the staggered pass B is the x3 training instance");
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG);
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG || TRW);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
@@ -1041,12 +1044,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
         wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
-        if constexpr (!LOSS && !SG) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
+        if constexpr (!LOSS && !SG && !TRW) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (stid < 64) greg = grec[64 * t + stid];
     };
     auto stage_store = [&](int b_) {
         wreg.store(wst + b_ * L.sw, L.swp);
-        if constexpr (!LOSS && !SG) treg.store(tst + b_ * L.st, L.stp);
+        if constexpr (!LOSS && !SG && !TRW) treg.store(tst + b_ * L.st, L.stp);
         if (stid < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + stid] = greg;
     };
     if (stager) stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
@@ -1375,7 +1378,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
                     Fr bw;
-                    if constexpr (SG)  // transposed from the logit GEMM's W image (genes = k)
+                    if constexpr (SG || TRW)  // transposed from the logit GEMM's W image (genes = k)
                         bw = TrFrag<P, RBW>::load(c.wsb, s * M::KSTEP, 16 * lb, L.swp);
                     else
                         bw = M::load(reinterpret_cast<const T*>(
@@ -2372,6 +2375,11 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     static const bool sg_on = getenv_is("MMVAE_DEC_SG", "1");
     const size_t ldsSG = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, 2, NPL, (int)sizeof(TL), false, true).bytes;
     const bool use_sg = X && nwB == 8 && sg_on && ldsSG <= 160 * 1024;
+    // the x3 instance double-buffered without a WdT stage (SG's layout, lock-step waves): one
+    // barrier per tile instead of two (k_dec_nb 244.8 -> 241.2 us); MMVAE_DEC_TRWDB=0: the
+    // single-buffered instance with its WdT stage
+    static const bool trwdb_on = !getenv_is("MMVAE_DEC_TRWDB", "0");
+    const bool use_trwdb = X && nwB == 8 && trwdb_on && !use_sg && ldsSG <= 160 * 1024;
     auto launch_b = [&](auto loss_c) {
         constexpr bool LS = decltype(loss_c)::value;
         if (nwB == 8) {
@@ -2380,6 +2388,11 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
             if constexpr (X && !LS) {
                 if (use_sg) {
                     hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, true, PM, false, true>), gdecB, dim3(512), ldsSG, st, Q, d);
+                    return;
+                }
+                if (use_trwdb) {
+                    if (ucov) hipLaunchKernelGGL((k_dec_nb<PB, KP, 0, 1, 8, true, PM, false, false, true>), gdecB, dim3(512), ldsSG, st, Q, d);
+                    else hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 8, true, PM, false, false, true>), gdecB, dim3(512), ldsSG, st, Q, d);
                     return;
                 }
             }
