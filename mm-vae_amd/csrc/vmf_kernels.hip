@@ -399,10 +399,11 @@ MMVAE_DEV void vrow_coeffs(const Dims& d, float epsD, const float* __restrict__ 
 static constexpr int VTAB = 512;  // log1p table entries of the fp32-accurate modes (x3, f32)
 struct VDecLds {
     int o_g, o_t, o_part, o_wave, o_q1, o_toff, wave_bytes, o_tab, bytes;
-    MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass, int planes = 1) {
+    // nbuf: W stage buffers (the forward pass double-buffers: one barrier per tile)
+    MMVAE_HOSTDEV VDecLds(int KP, int esz, int S, int nq, int pass, int planes = 1, int nbuf = 1) {
         const bool trw = esz == 2;
-        o_g = planes * 64 * KP * esz;                         // W image (hi [+ lo])
-        o_t = o_g + 1024;
+        o_g = nbuf * planes * 64 * KP * esz;                  // W images (hi [+ lo]) per buffer
+        o_t = o_g + nbuf * 1024;                              // gene records per buffer
         o_part = o_t + (pass && !trw ? planes * KP * 64 * esz : 0);
         o_wave = o_part + (pass ? 4 * nq * 64 * 4 : 0);
         const int QS = 64 + (esz == 2 ? 8 : 4);
@@ -441,11 +442,14 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     constexpr int CA = CM > 0 ? CM : 1;  // covariate array extent
     const int C = (CM <= 1) ? 1 : d.C;
     const int nq = 1 + C;
-    const VDecLds L(KP, (int)sizeof(T), S, nq, PASS, NPL);
+    // the forward pass double-buffers its W stage (~9 KB more LDS, still 4 workgroups per CU)
+    // and meets one barrier per tile; the backward keeps one buffer (3 workgroups per CU)
+    constexpr int NBF = PASS ? 1 : 2;
+    const VDecLds L(KP, (int)sizeof(T), S, nq, PASS, NPL, NBF);
     constexpr int WIMG = 64 * KP * (int)sizeof(T);  // one plane of the W / WdT images
     constexpr int QPL = 16 * QS;                     // the pq tile's lo plane (x3)
-    char* wst = smem;
-    const float4* gst = reinterpret_cast<const float4*>(smem + L.o_g);
+    auto wbuf = [&](int b) { return smem + b * NPL * WIMG; };
+    auto gbuf = [&](int b) { return reinterpret_cast<float4*>(smem + L.o_g + b * 1024); };
     char* tst = smem + L.o_t;
     float* part = reinterpret_cast<float*>(smem + L.o_part);
     char* wp = smem + L.o_wave + w * L.wave_bytes;
@@ -471,10 +475,10 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         if (PASS && !TRW) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (threadIdx.x < 64) greg = grec[64 * t + threadIdx.x];
     };
-    auto stage_store = [&]() {
-        wreg.store(wst, WIMG);
+    auto stage_store = [&](int b) {
+        wreg.store(wbuf(b), WIMG);
         if (PASS && !TRW) treg.store(tst, WIMG);
-        if (threadIdx.x < 64) reinterpret_cast<float4*>(smem + L.o_g)[threadIdx.x] = greg;
+        if (threadIdx.x < 64) gbuf(b)[threadIdx.x] = greg;
     };
     stage_load(min(t0, d.NT - 1));  // independent of everything below: issued first
     if (PASS) {  // the per-row backward coefficients from pass 0's split sums (k_vrowfin), 4 threads per row
@@ -527,7 +531,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     if (t0 < t1) {
         pendA.fetch(Q.ents, segw, toffl, 0, lane);
         pendB.fetch(Q.ents, segw, toffl, min(1, t1 - t0 - 1), lane);
-        stage_store();
+        stage_store(0);
     }
     lds_barrier();  // the first tiles' entry loads stay in flight
     // bf16 mode: log1p of a set's two register entries (one v_log each) computed a tile before
@@ -555,6 +559,9 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
 
     auto tile = [&](int t, ListEntries& pend, const float (&lv)[2], const ListEntries& pnext, float (&lvnext)[2]) {
         const int tl = t - t0;
+        const int cb = NBF == 2 ? (tl & 1) : 0;  // this tile's stage buffer
+        const char* wst = wbuf(cb);
+        const float4* gst = gbuf(cb);
         // unconditional (clamped) next-stage loads: counted waits (MMVAE_VDEC_SLOAD_LATE: issued
         // after the densify instead, off the post-barrier burst of every wave's loads)
         if (!MMVAE_VDEC_SLOAD_LATE && !dbg_bit(d.dbg, 512)) stage_load(dbg_bit(d.dbg, 1024) ? t0 : min(t + 1, t1 - 1));
@@ -700,7 +707,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         }
         if (PRE && t + 1 < t1) lookup(pnext, lvnext);
         lap(1);
-        lds_barrier();
+        if (PASS || NBF == 1) lds_barrier();  // (the forward pass: its stage is double-buffered)
         lap(2);
         if (PASS) {
             for (int i = threadIdx.x; i < nq * 64; i += 256) {
@@ -711,7 +718,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
             }
         }
         lap(3);
-        if (t + 1 < t1) stage_store();
+        if (t + 1 < t1) stage_store(NBF == 2 ? ((tl + 1) & 1) : 0);
         lds_barrier();
         lap(4);
     };
@@ -1286,7 +1293,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     {
         ScopedTimer tm(e, "k_vdec_fwd");
         const dim3 gfwd(nrb * d.nsF);  // the forward pass's own split (VFwdOcc)
-        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), d.tpsF + 1, nq, 0, NPL).bytes;
+        const size_t lds = (size_t)VDecLds(KP, (int)sizeof(T), d.tpsF + 1, nq, 0, NPL, 2).bytes;
         if (ucov) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 0>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
         else if (d.C == 1) hipLaunchKernelGGL((k_vdec_fwd<PM, KP, 1>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
         else hipLaunchKernelGGL((k_vdec_fwd<PM, KP, CMAX>), gfwd, dim3(256), lds, st, Q, d, sc.epsD);
