@@ -179,7 +179,12 @@ template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
     // 64-byte rows (4 chunks): rows r and r + 8 of a transposed read (tr_frag) share their 256-byte
     // bank window, so bit 3 of the row selects the other chunk pair; the 16-lane ds_read_b128 row
     // reads stay conflict-free with it
-    const int x = NCH == 4 ? (((row >> 1) & 1) | ((row >> 2) & 2)) : ((row >> 1) & (NCH - 1));
+    // 128-byte rows (8 chunks): x = row bit 3 -> chunk bit 1, row bit 1 -> chunk bit 2 — found by
+    // exhaustive search over linear swizzles: the ds_read_b128 row reads (lane groups of 16) and
+    // the transposed 8-byte reads of rows r .. r + 3 and r + 8 .. r + 11 are both conflict-free
+    const int x = NCH == 4 ? (((row >> 1) & 1) | ((row >> 2) & 2))
+                : NCH == 8 ? ((((row >> 3) & 1) << 1) | (((row >> 1) & 1) << 2))
+                           : ((row >> 1) & (NCH - 1));
     return row * RB + (((byte >> 4) ^ x) << 4) + (byte & 15);
 }
 
