@@ -1,5 +1,7 @@
 // C-ABI implementation (include/mmvae_capi.h): handle lifecycle, parameter registry,
 // dataset upload, step orchestration, RCCL gradient all-reduce, kernel timing.
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -717,7 +719,21 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->hs_rowptr = static_cast<const int64_t*>(d);
     // integer counts below 2^16 over at most 2^16 genes: the packed copy (bit-exact values)
     if (D <= 65536 && nnz > 0 && !getenv_is("MMVAE_STREAM_PACK", "0")) {
-        HIPCHK(e, hipHostMalloc((void**)&e->hs_packed, sizeof(uint32_t) * (size_t)nnz, hipHostMallocMapped));
+        // MMVAE_STREAM_THP=1 (experiment): the copy in 2 MB transparent huge pages where the host
+        // gives them, registered, instead of hipHostMalloc — one GPU translation per 2 MB, not 4 KB
+        const size_t pbytes = (sizeof(uint32_t) * (size_t)nnz + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        if (getenv_is("MMVAE_STREAM_THP", "1")) {
+            void* m = mmap(nullptr, pbytes + (2u << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m != MAP_FAILED) {  // 2 MB-aligned start inside the mapping, the rest unmapped
+                const uintptr_t a0 = reinterpret_cast<uintptr_t>(m), al = (a0 + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+                if (al > a0) munmap(m, al - a0);
+                if (al + pbytes < a0 + pbytes + (2u << 20)) munmap(reinterpret_cast<void*>(al + pbytes), a0 + pbytes + (2u << 20) - (al + pbytes));
+                e->hs_packed = reinterpret_cast<uint32_t*>(al);
+                e->hs_packed_bytes = pbytes;
+                madvise(e->hs_packed, pbytes, MADV_HUGEPAGE);
+            }
+        }
+        if (!e->hs_packed) HIPCHK(e, hipHostMalloc((void**)&e->hs_packed, sizeof(uint32_t) * (size_t)nnz, hipHostMallocMapped));
         const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
         std::vector<char> ok(nth, 1);
@@ -736,9 +752,24 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
                 }
             });
         for (auto& x : th) x.join();
-        if (std::find(ok.begin(), ok.end(), 0) != ok.end()) {
-            hipHostFree(e->hs_packed);
+        hipError_t rer = hipSuccess;
+        if (std::find(ok.begin(), ok.end(), 0) == ok.end() && e->hs_packed_bytes) {  // written, so backed: register
+            rer = hipHostRegister(e->hs_packed, e->hs_packed_bytes, hipHostRegisterMapped);
+            void* dp = nullptr;
+            if (rer == hipSuccess && (rer = hipHostGetDevicePointer(&dp, e->hs_packed, 0)) == hipSuccess)
+                e->hs_packed_dev = static_cast<const uint32_t*>(dp);
+            else if (rer == hipSuccess)
+                hipHostUnregister(e->hs_packed);
+        } else {
+            e->hs_packed_dev = e->hs_packed;
+        }
+        if (std::find(ok.begin(), ok.end(), 0) != ok.end() || rer != hipSuccess) {
+            if (e->hs_packed_bytes) munmap(e->hs_packed, e->hs_packed_bytes);
+            else hipHostFree(e->hs_packed);
             e->hs_packed = nullptr;
+            e->hs_packed_dev = nullptr;
+            e->hs_packed_bytes = 0;
+            HIPCHK(e, rer);
         }
     }
     e->hs_col = nullptr;
@@ -775,6 +806,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     stream_bind(e, e->cur_slot);
     // the prefetched gather (stream.hip stream_prefetch); MMVAE_STREAM_SYNC=1 keeps it in the step
     e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");
+    e->stream_index_step = getenv_is("MMVAE_STREAM_INDEX_STEP", "1");
     if (e->stream_prefetch) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
         for (int s2 = 0; s2 < 2; ++s2) {

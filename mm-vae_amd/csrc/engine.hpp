@@ -110,7 +110,10 @@ struct Engine {
     // packed entries (streamed, D <= 65536, every value a 16-bit integer count): one word per
     // entry, gene << 16 | count, in engine-owned mapped pinned memory — the gather moves 4 bytes
     // per entry over PCIe instead of 8 (MMVAE_STREAM_PACK=0: the caller's arrays)
-    uint32_t* hs_packed = nullptr;
+    bool stream_index_step = false;     // prefetch mode: the batch's tile index built inside the step, not on gstream
+    uint32_t* hs_packed = nullptr;      // host address of the packed copy
+    const uint32_t* hs_packed_dev = nullptr;  // its device address
+    size_t hs_packed_bytes = 0;         // > 0: mmap'd (2 MB pages where the kernel gives them) + registered
     const int64_t* hh_rowptr = nullptr;  // the same arrays' host addresses (mmvae_get_rows)
     const int32_t* hh_col = nullptr;
     const float* hh_val = nullptr;

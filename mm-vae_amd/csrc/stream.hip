@@ -7,6 +7,8 @@
 // the rows' nonzero counts) and the batch rows' tile index (k_dataset_index), and every kernel
 // after it runs on the batch CSR as the resident path runs on the whole dataset — the batch's row
 // b is dataset row b, so the step's results are bit-identical to the resident path's.
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -20,11 +22,18 @@ namespace mmvae {
 // the batch's empty row Bp; afterwards cells[b] = b
 // gcells (prefetched gather): the batch's dataset rows from the slot's mapped row-id array, the
 // staged cells already the identity (cells is then not written).
-// A few workgroups (gather_wgs) walk the rows, each thread keeping 8 loads per array in flight:
+// A few workgroups (gather_wgs) walk the rows, each thread keeping GU loads per array (unpacked) or two 16-byte words (packed) in flight:
 // PCIe latency wants many bytes in flight, not many waves — a grid of one workgroup per row held
 // every CU's wave slots while it waited on PCIe and slowed the step it overlapped.
-static constexpr int GU = 8;
+static constexpr int GU = 6;
+// a workgroup-uniform 64-bit value into scalar registers: the row's bases then cost no VGPRs, and
+// the gather stays at <= 48 VGPRs, so its waves fit beside pass B's (2 x 232 of 512 per SIMD)
+MMVAE_DEV int64_t uni64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 // hpk (packed dataset): gene << 16 | count per entry instead of hcol / hval
+template <bool PK>
 __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict__ hrp, const int32_t* __restrict__ hcol,
                                                        const float* __restrict__ hval, const uint32_t* __restrict__ hpk,
                                                        const float* __restrict__ hcov,
@@ -42,66 +51,76 @@ __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict
             for (int c = threadIdx.x; c < C; c += 256) cov[Bp * C + c] = 0.f;
             continue;
         }
-        const int64_t g = gcells ? gcells[b] : cells[b];
+        const int64_t g = uni64(gcells ? gcells[b] : cells[b]);
         const bool real = g < Nh;
-        const int64_t s = brp[b], n = brp[b + 1] - s;
-        const int64_t src = real ? hrp[g] : 0;
-        if (hpk) {
+        const int64_t s = uni64(brp[b]);
+        const int n = (int)(uni64(brp[b + 1]) - s);  // 32-bit offsets inside the row: few live VGPRs
+        const int64_t src = real ? uni64(hrp[g]) : 0;
+        int32_t* dc = col + s;
+        float* dv = val + s;
+        if (PK) {
             // packed words: 16-byte loads from the row's first 16-byte boundary (4 entries per
             // lane, two loads in flight per lane), the unaligned head word by word
-            const int64_t head = std::min<int64_t>(n, (4 - (src & 3)) & 3);
-            if (threadIdx.x < head) {
-                const uint32_t w = hpk[src + threadIdx.x];
-                col[s + threadIdx.x] = (int32_t)(w >> 16);
-                val[s + threadIdx.x] = (float)(w & 0xffffu);
+            const uint32_t* hp = hpk + src;
+            const int head = min(n, (int)((4 - (src & 3)) & 3));
+            if ((int)threadIdx.x < head) {
+                const uint32_t w = hp[threadIdx.x];
+                dc[threadIdx.x] = (int32_t)(w >> 16);
+                dv[threadIdx.x] = (float)(w & 0xffffu);
             }
-            const uint4* p4 = reinterpret_cast<const uint4*>(hpk + src + head);
-            const int64_t n4 = (n - head) >> 2;
-            for (int64_t q0 = 0; q0 < n4; q0 += 512) {
-                uint4 w[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int64_t q = q0 + u * 256 + threadIdx.x;
-                    if (q < n4) w[u] = p4[q];
-                }
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int64_t q = q0 + u * 256 + threadIdx.x;
-                    if (q < n4) {
-                        const int64_t o = s + head + 4 * q;
-                        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            col[o + j] = (int32_t)(ww[j] >> 16);
-                            val[o + j] = (float)(ww[j] & 0xffffu);
-                        }
-                    }
-                }
+            const uint4* p4 = reinterpret_cast<const uint4*>(hp + head);
+            const int n4 = (n - head) >> 2;
+            int32_t* dc4 = dc + head;
+            float* dv4 = dv + head;
+            // two 16-byte words per lane in flight, the four stores of a word at immediate offsets
+            // of one address: <= 48 VGPRs, so the gather's waves fit beside pass B's
+            auto put = [&](int q, const uint4& w) {
+                int32_t* c4 = dc4 + 4 * (size_t)q;
+                float* v4 = dv4 + 4 * (size_t)q;
+                c4[0] = (int32_t)(w.x >> 16);
+                c4[1] = (int32_t)(w.y >> 16);
+                c4[2] = (int32_t)(w.z >> 16);
+                c4[3] = (int32_t)(w.w >> 16);
+                v4[0] = (float)(w.x & 0xffffu);
+                v4[1] = (float)(w.y & 0xffffu);
+                v4[2] = (float)(w.z & 0xffffu);
+                v4[3] = (float)(w.w & 0xffffu);
+            };
+#pragma unroll 1
+            for (int q = threadIdx.x; q < n4; q += 512) {
+                const bool two = q + 256 < n4;
+                const uint4 w0 = p4[q];
+                uint4 w1 = uint4{0u, 0u, 0u, 0u};
+                if (two) w1 = p4[q + 256];
+                put(q, w0);
+                if (two) put(q + 256, w1);
             }
-            const int64_t tail0 = head + 4 * n4;
-            if (tail0 + threadIdx.x < n) {
-                const uint32_t w = hpk[src + tail0 + threadIdx.x];
-                col[s + tail0 + threadIdx.x] = (int32_t)(w >> 16);
-                val[s + tail0 + threadIdx.x] = (float)(w & 0xffffu);
+            const int tail0 = head + 4 * n4;
+            if (tail0 + (int)threadIdx.x < n) {
+                const uint32_t w = hp[tail0 + threadIdx.x];
+                dc[tail0 + threadIdx.x] = (int32_t)(w >> 16);
+                dv[tail0 + threadIdx.x] = (float)(w & 0xffffu);
             }
         } else {
-            for (int64_t i0 = 0; i0 < n; i0 += 256 * GU) {
+            const int32_t* hc = hcol + src;
+            const float* hv = hval + src;
+            for (int i0 = 0; i0 < n; i0 += 256 * GU) {
                 int32_t cv[GU];
                 float vv[GU];
 #pragma unroll
                 for (int u = 0; u < GU; ++u) {  // every load of the group in flight before the stores
-                    const int64_t i = i0 + u * 256 + threadIdx.x;
+                    const int i = i0 + u * 256 + threadIdx.x;
                     if (i < n) {
-                        cv[u] = hcol[src + i];
-                        vv[u] = hval[src + i];
+                        cv[u] = hc[i];
+                        vv[u] = hv[i];
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < GU; ++u) {
-                    const int64_t i = i0 + u * 256 + threadIdx.x;
+                    const int i = i0 + u * 256 + threadIdx.x;
                     if (i < n) {
-                        col[s + i] = cv[u];
-                        val[s + i] = vv[u];
+                        dc[i] = cv[u];
+                        dv[i] = vv[u];
                     }
                 }
             }
@@ -134,12 +153,19 @@ void stream_bind(Engine* e, int s) {
 
 // in the step's stream (MMVAE_STREAM_SYNC=1, or a step graph's capture of it): nothing to do when
 // stream_prefetch already enqueued the gather on gstream
+// with the prefetch, the step itself only builds the batch's tile index (stream_index_step): a
+// short full-GPU launch on the step's stream instead of a second kernel on gstream's chain
 hipError_t stream_gather(Engine* e) {
-    if (!e->streamed || e->stream_prefetch) return hipSuccess;
+    if (!e->streamed) return hipSuccess;
+    if (e->stream_prefetch) {
+        if (e->wide || !e->stream_index_step) return hipSuccess;
+        ScopedTimer tm(e, "k_dataset_index");
+        return index_rows(e, e->d_rowptr, e->d_col, e->d_val, e->Bpad, e->d_rtp, e->d_cellnorm);
+    }
     ScopedTimer tm(e, "k_stream_gather");
     const int64_t Bp = e->Bpad;
-    hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, (const uint32_t*)e->hs_packed, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
+    hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
+                       e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
                        e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     hipError_t er = hipGetLastError();
     if (er != hipSuccess) return er;
@@ -157,11 +183,12 @@ hipError_t stream_prefetch(Engine* e) {
     const int64_t Bp = e->Bpad;
     hipError_t er = hipStreamWaitEvent(e->gstream, e->ev_setfree[s], 0);
     if (er != hipSuccess) return er;
-    hipLaunchKernelGGL(k_stream_gather, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, (const uint32_t*)e->hs_packed, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
+    hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
+                       e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
                        (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     if ((er = hipGetLastError()) != hipSuccess) return er;
-    if (!e->wide && (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
+    if (!e->wide && !e->stream_index_step &&
+        (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
         return er;
     if ((er = hipEventRecord(e->ev_gathered[s], e->gstream)) != hipSuccess) return er;
     return hipStreamWaitEvent(e->stream, e->ev_gathered[s], 0);
@@ -191,8 +218,15 @@ void stream_release(Engine* e) {
         q = Engine::BatchSet{};
     }
     for (void* p : e->hs_registered) hipHostUnregister(p);
-    if (e->hs_packed) hipHostFree(e->hs_packed);
+    if (e->hs_packed && e->hs_packed_bytes) {
+        hipHostUnregister(e->hs_packed);
+        munmap(e->hs_packed, e->hs_packed_bytes);
+    } else if (e->hs_packed) {
+        hipHostFree(e->hs_packed);
+    }
     e->hs_packed = nullptr;
+    e->hs_packed_dev = nullptr;
+    e->hs_packed_bytes = 0;
     e->hs_registered.clear();
     e->hs_rowptr = nullptr;
     e->hs_col = nullptr;
