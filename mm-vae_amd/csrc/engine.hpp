@@ -135,6 +135,14 @@ struct Engine {
     bool stream_prefetch = false;
     hipStream_t gstream = nullptr;
     hipEvent_t ev_gathered[2] = {nullptr, nullptr}, ev_setfree[2] = {nullptr, nullptr};
+    // MMVAE_STREAM_DMA=1 (packed copy, prefetch): the host packs the batch's rows into h_bpk[s]
+    // (worker threads), one DMA-engine copy moves them to d_bpk[s], and the unpack kernel reads
+    // HBM instead of mapped host memory
+    bool stream_dma = false;
+    uint32_t* h_bpk[2] = {nullptr, nullptr};
+    uint32_t* d_bpk[2] = {nullptr, nullptr};
+    int64_t bpk_cap[2] = {0, 0};
+    void* gpool = nullptr;  // stream.hip's host gather pool
     int64_t* h_gcells[2] = {nullptr, nullptr};
     const int64_t* d_brp = nullptr;
     size_t stage_bytes_res = 0;     // the resident path's staged block (streamed adds the rowptr)

@@ -10,7 +10,11 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 #include "common.hpp"
 #include "engine.hpp"
@@ -33,7 +37,8 @@ MMVAE_DEV int64_t uni64(int64_t v) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 // hpk (packed dataset): gene << 16 | count per entry instead of hcol / hval
-template <bool PK>
+// DEV (MMVAE_STREAM_DMA): hpk is the batch's packed rows already in HBM, row b at brp[b]
+template <bool PK, bool DEV = false>
 __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict__ hrp, const int32_t* __restrict__ hcol,
                                                        const float* __restrict__ hval, const uint32_t* __restrict__ hpk,
                                                        const float* __restrict__ hcov,
@@ -55,7 +60,7 @@ __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict
         const bool real = g < Nh;
         const int64_t s = uni64(brp[b]);
         const int n = (int)(uni64(brp[b + 1]) - s);  // 32-bit offsets inside the row: few live VGPRs
-        const int64_t src = real ? uni64(hrp[g]) : 0;
+        const int64_t src = DEV ? s : (real ? uni64(hrp[g]) : 0);
         int32_t* dc = col + s;
         float* dv = val + s;
         if (PK) {
@@ -173,6 +178,102 @@ hipError_t stream_gather(Engine* e) {
     return index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm);
 }
 
+// host gather pool (MMVAE_STREAM_DMA): persistent workers, the calling thread joins as worker 0
+struct GatherPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, cv_done;
+    std::function<void(int, int)> job;
+    int gen = 0, pending = 0, nth = 1;
+    bool stop = false;
+    explicit GatherPool(int n) : nth(n) {
+        for (int t = 1; t < n; ++t)
+            th.emplace_back([this, t] {
+                int seen = 0;
+                for (;;) {
+                    std::function<void(int, int)> j;
+                    {
+                        std::unique_lock<std::mutex> lk(m);
+                        cv.wait(lk, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        j = job;
+                    }
+                    j(t, nth);
+                    std::lock_guard<std::mutex> lk(m);
+                    if (--pending == 0) cv_done.notify_one();
+                }
+            });
+    }
+    void run(std::function<void(int, int)> f) {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            job = f;
+            pending = nth - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        f(0, nth);
+        std::unique_lock<std::mutex> lk(m);
+        cv_done.wait(lk, [&] { return pending == 0; });
+    }
+    ~GatherPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& x : th) x.join();
+    }
+};
+
+// MMVAE_STREAM_DMA: the slot's rows packed on the host, one DMA copy, the unpack kernel on HBM
+static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
+    hipError_t er;
+    const int64_t tot = e->h_brp_pin[Bp];
+    if ((er = hipEventSynchronize(e->ev_gathered[s])) != hipSuccess) return er;  // slot s's last copy has read h_bpk[s]
+    if (tot > e->bpk_cap[s]) {
+        if ((er = hipStreamSynchronize(e->gstream)) != hipSuccess) return er;
+        if (e->h_bpk[s]) hipHostFree(e->h_bpk[s]);
+        if (e->d_bpk[s]) hipFree(e->d_bpk[s]);
+        e->h_bpk[s] = nullptr;
+        e->d_bpk[s] = nullptr;
+        e->bpk_cap[s] = 0;
+        const int64_t cap = tot + tot / 4 + 1024;
+        if ((er = hipHostMalloc((void**)&e->h_bpk[s], sizeof(uint32_t) * (size_t)cap, hipHostMallocDefault)) != hipSuccess) return er;
+        if ((er = hipMalloc(&e->d_bpk[s], sizeof(uint32_t) * (size_t)cap)) != hipSuccess) return er;
+        e->bpk_cap[s] = cap;
+    }
+    if (!e->gpool) {
+        static const int env = [] { const char* v = std::getenv("MMVAE_STREAM_DMA_THREADS"); return v ? std::atoi(v) : 0; }();
+        const int n = env > 0 ? env : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        e->gpool = new GatherPool(n);
+    }
+    const int64_t* gc = e->h_gcells[s];
+    const int64_t* brp = e->h_brp_pin;
+    uint32_t* dst = e->h_bpk[s];
+    const uint32_t* src = e->hs_packed;
+    const int64_t* hrp = e->hh_rowptr;
+    const int64_t Nh = e->N_host;
+    static_cast<GatherPool*>(e->gpool)->run([&](int t, int nth) {  // contiguous row ranges of about equal entries
+        const int64_t a = tot * t / nth, z = tot * (t + 1) / nth;
+        int64_t b = std::upper_bound(brp, brp + Bp + 1, a) - brp - 1;
+        for (; b < Bp && brp[b] < z; ++b) {
+            const int64_t n = brp[b + 1] - brp[b];
+            if (n > 0 && gc[b] < Nh) {  // the part of row b inside [a, z)
+                const int64_t lo = std::max(a, brp[b]), hi = std::min(z, brp[b + 1]);
+                if (hi > lo) std::memcpy(dst + lo, src + hrp[gc[b]] + (lo - brp[b]), sizeof(uint32_t) * (size_t)(hi - lo));
+            }
+        }
+    });
+    if (tot > 0 && (er = hipMemcpyAsync(e->d_bpk[s], e->h_bpk[s], sizeof(uint32_t) * (size_t)tot, hipMemcpyHostToDevice, e->gstream)) != hipSuccess)
+        return er;
+    hipLaunchKernelGGL((k_stream_gather<true, true>), dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
+                       e->hs_val, (const uint32_t*)e->d_bpk[s], e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
+                       (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
+    return hipGetLastError();
+}
+
 // the staged step's gather on gstream, right after staging (host side, before the step's launch
 // or graph): it starts once the last step on the slot's batch set is done and runs under the
 // previous step's kernels; the step's stream waits for it.  The row ids and row offsets are read
@@ -183,10 +284,14 @@ hipError_t stream_prefetch(Engine* e) {
     const int64_t Bp = e->Bpad;
     hipError_t er = hipStreamWaitEvent(e->gstream, e->ev_setfree[s], 0);
     if (er != hipSuccess) return er;
-    hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
-                       (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
-    if ((er = hipGetLastError()) != hipSuccess) return er;
+    if (e->stream_dma && e->hs_packed) {
+        if ((er = stream_dma_gather(e, s, Bp)) != hipSuccess) return er;
+    } else {
+        hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
+                           e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
+                           (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
+        if ((er = hipGetLastError()) != hipSuccess) return er;
+    }
     if (!e->wide && !e->stream_index_step &&
         (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
         return er;
@@ -202,6 +307,16 @@ hipError_t stream_step_done(Engine* e) {
 
 void stream_release(Engine* e) {
     if (e->gstream) hipStreamSynchronize(e->gstream);
+    delete static_cast<GatherPool*>(e->gpool);
+    e->gpool = nullptr;
+    for (int s = 0; s < 2; ++s) {
+        if (e->h_bpk[s]) hipHostFree(e->h_bpk[s]);
+        if (e->d_bpk[s]) hipFree(e->d_bpk[s]);
+        e->h_bpk[s] = nullptr;
+        e->d_bpk[s] = nullptr;
+        e->bpk_cap[s] = 0;
+    }
+    e->stream_dma = false;
     for (int s = 0; s < 2; ++s) {
         if (e->ev_gathered[s]) hipEventDestroy(e->ev_gathered[s]);
         if (e->ev_setfree[s]) hipEventDestroy(e->ev_setfree[s]);
