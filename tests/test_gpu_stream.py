@@ -121,3 +121,22 @@ def test_streamed_unpacked_entries(kind):
     for s in range(3):
         cells = rng.integers(0, N, B)
         assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
+
+
+@pytest.mark.parametrize("mode", ["MMVAE_STREAM_DMA", "MMVAE_STREAM_THP", "MMVAE_STREAM_INDEX_STEP", "MMVAE_STREAM_SYNC"])
+def test_streamed_modes(mode, monkeypatch):
+    """The streamed path's alternative modes (read at stream_csr): the host gather + DMA-engine
+    copy, the huge-page packed copy, the batch index built inside the step, the in-step gather —
+    each bit-identical to the resident handle over ragged, resampled and eval steps with graphs
+    and a batch-capacity growth on the heavy cells."""
+    monkeypatch.setenv(mode, "1")
+    N, D, B = 1500, 3000, 192
+    data = _data(N, D, seed=21)
+    res, st = _pair("nb", "bf16x3", D, 32, B, data)
+    a = _drive(res, N, B, True, poison=False)
+    b = _drive(st, N, B, True, poison=True)
+    assert a[0] == b[0], (a[0], b[0])
+    for x, y in ((a[1], b[1]), (a[2], b[2])):
+        for k in x:
+            assert np.array_equal(x[k], y[k]), k
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
