@@ -807,7 +807,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     // the prefetched gather (stream.hip stream_prefetch); MMVAE_STREAM_SYNC=1 keeps it in the step
     e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");
     e->stream_index_step = getenv_is("MMVAE_STREAM_INDEX_STEP", "1");
-    e->stream_dma = getenv_is("MMVAE_STREAM_DMA", "1");
+    e->stream_dma = !getenv_is("MMVAE_STREAM_DMA", "0");  // (packed copies only)
     if (e->stream_prefetch) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
         for (int s2 = 0; s2 < 2; ++s2) {

@@ -135,10 +135,10 @@ struct Engine {
     bool stream_prefetch = false;
     hipStream_t gstream = nullptr;
     hipEvent_t ev_gathered[2] = {nullptr, nullptr}, ev_setfree[2] = {nullptr, nullptr};
-    // MMVAE_STREAM_DMA=1 (packed copy, prefetch): the host packs the batch's rows into h_bpk[s]
+    // DMA mode (packed copy, prefetch; MMVAE_STREAM_DMA=0 turns it off): the host packs the batch's rows into h_bpk[s]
     // (worker threads), one DMA-engine copy moves them to d_bpk[s], and the unpack kernel reads
     // HBM instead of mapped host memory
-    bool stream_dma = false;
+    bool stream_dma = false;  // set by mmvae_stream_csr
     uint32_t* h_bpk[2] = {nullptr, nullptr};
     uint32_t* d_bpk[2] = {nullptr, nullptr};
     int64_t bpk_cap[2] = {0, 0};

@@ -156,14 +156,20 @@ void stream_bind(Engine* e, int s) {
     e->d_cellnorm = q.cellnorm;
 }
 
-// in the step's stream (MMVAE_STREAM_SYNC=1, or a step graph's capture of it): nothing to do when
-// stream_prefetch already enqueued the gather on gstream
-// with the prefetch, the step itself only builds the batch's tile index (stream_index_step): a
-// short full-GPU launch on the step's stream instead of a second kernel on gstream's chain
+// in the step's stream (or a step graph's capture of it): the whole gather with MMVAE_STREAM_SYNC=1;
+// with the prefetch, the DMA mode's unpack (HBM to HBM) and, with it or MMVAE_STREAM_INDEX_STEP=1,
+// the batch's tile index — short full-GPU launches instead of more work on gstream's chain
+static hipError_t stream_dma_unpack(Engine* e);
+
 hipError_t stream_gather(Engine* e) {
     if (!e->streamed) return hipSuccess;
     if (e->stream_prefetch) {
-        if (e->wide || !e->stream_index_step) return hipSuccess;
+        const bool dma = e->stream_dma && e->hs_packed;
+        if (dma) {
+            hipError_t er = stream_dma_unpack(e);
+            if (er != hipSuccess) return er;
+        }
+        if (e->wide || !(e->stream_index_step || dma)) return hipSuccess;
         ScopedTimer tm(e, "k_dataset_index");
         return index_rows(e, e->d_rowptr, e->d_col, e->d_val, e->Bpad, e->d_rtp, e->d_cellnorm);
     }
@@ -266,11 +272,21 @@ static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
             }
         }
     });
+    // only the copy runs on gstream: the unpack and the tile index are the step's first kernels
+    // (stream_gather), so step n + 1's copy overlaps step n's whole kernel chain
     if (tot > 0 && (er = hipMemcpyAsync(e->d_bpk[s], e->h_bpk[s], sizeof(uint32_t) * (size_t)tot, hipMemcpyHostToDevice, e->gstream)) != hipSuccess)
         return er;
-    hipLaunchKernelGGL((k_stream_gather<true, true>), dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
-                       e->hs_val, (const uint32_t*)e->d_bpk[s], e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
-                       (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
+    return hipSuccess;
+}
+
+// the DMA mode's unpack of the slot's packed rows (HBM to HBM, one workgroup per row up to 2048)
+static hipError_t stream_dma_unpack(Engine* e) {
+    const int64_t Bp = e->Bpad;
+    const int s = e->cur_slot;
+    ScopedTimer tm(e, "k_stream_gather");
+    hipLaunchKernelGGL((k_stream_gather<true, true>), dim3((unsigned)std::min<int64_t>(Bp + 1, 2048)), dim3(256), 0, e->stream, e->hs_rowptr,
+                       e->hs_col, e->hs_val, (const uint32_t*)e->d_bpk[s], e->hs_covar, e->N_host, (int)e->C, e->d_cells,
+                       (const int64_t*)e->h_gcells[s], (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
     return hipGetLastError();
 }
 
@@ -292,7 +308,7 @@ hipError_t stream_prefetch(Engine* e) {
                            (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
         if ((er = hipGetLastError()) != hipSuccess) return er;
     }
-    if (!e->wide && !e->stream_index_step &&
+    if (!e->wide && !e->stream_index_step && !(e->stream_dma && e->hs_packed) &&
         (er = index_rows(e, e->d_rowptr, e->d_col, e->d_val, Bp, e->d_rtp, e->d_cellnorm, e->gstream)) != hipSuccess)
         return er;
     if ((er = hipEventRecord(e->ev_gathered[s], e->gstream)) != hipSuccess) return er;

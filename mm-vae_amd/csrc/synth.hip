@@ -161,14 +161,30 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
     const int32_t* cr = col + s;
     const float* vr = val + s;
     float sl2 = 0.f, sy = 0.f;
-    for (int j = lane; j < n; j += 64) {
-        const int g = cr[j];
-        const int gp = j > 0 ? cr[j - 1] : -64;
-        const float x = vr[j];
-        const float l = log1pf(x), ly = log1pf(fmaxf(x, 0.f));
-        sl2 = fmaf(l, l, sl2);
-        sy = fmaf(ly, ly + 2.f * epsD, sy);
-        for (int tt = (gp >> 6) + 1; tt <= (g >> 6); ++tt) rt[tt] = j;
+    // four entries per lane per round, every load issued first (the per-step batch index of the
+    // streamed dataset is latency-bound); each lane still sums its entries j = lane, lane + 64, ...
+    // in order, so the norms are those of one entry per round
+    constexpr int U = 4;
+    for (int j0 = lane; j0 < n; j0 += 64 * U) {
+        int g[U], gp[U];
+        float x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = min(j0 + 64 * u, n - 1);
+            g[u] = cr[j];
+            gp[u] = cr[max(j - 1, 0)];  // unconditional: a predicated load would wait on its own
+            x[u] = vr[j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + 64 * u;
+            if (j < n) {
+                const float l = log1pf(x[u]), ly = log1pf(fmaxf(x[u], 0.f));
+                sl2 = fmaf(l, l, sl2);
+                sy = fmaf(ly, ly + 2.f * epsD, sy);
+                for (int tt = (j > 0 ? gp[u] >> 6 : -1) + 1; tt <= (g[u] >> 6); ++tt) rt[tt] = j;
+            }
+        }
     }
     const int tlast = (n == 0) ? -1 : (cr[n - 1] >> 6);
     for (int tt = tlast + 1 + lane; tt <= NT; tt += 64) rt[tt] = n;

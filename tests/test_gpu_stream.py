@@ -123,13 +123,16 @@ def test_streamed_unpacked_entries(kind):
         assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
 
 
-@pytest.mark.parametrize("mode", ["MMVAE_STREAM_DMA", "MMVAE_STREAM_THP", "MMVAE_STREAM_INDEX_STEP", "MMVAE_STREAM_SYNC"])
+@pytest.mark.parametrize("mode", [("MMVAE_STREAM_DMA", "0"), ("MMVAE_STREAM_THP", "1"), ("MMVAE_STREAM_INDEX_STEP", "1"),
+                                  ("MMVAE_STREAM_SYNC", "1")])
 def test_streamed_modes(mode, monkeypatch):
-    """The streamed path's alternative modes (read at stream_csr): the host gather + DMA-engine
-    copy, the huge-page packed copy, the batch index built inside the step, the in-step gather —
-    each bit-identical to the resident handle over ragged, resampled and eval steps with graphs
-    and a batch-capacity growth on the heavy cells."""
-    monkeypatch.setenv(mode, "1")
+    """The streamed path's alternative modes (read at stream_csr): the zero-copy gather kernel
+    (no DMA copy), its huge-page packed copy, the batch index built inside the step, the in-step
+    gather — each bit-identical to the resident handle over ragged, resampled and eval steps
+    with step graphs and workspace poisoning."""
+    monkeypatch.setenv(*mode)
+    if mode[0] in ("MMVAE_STREAM_THP", "MMVAE_STREAM_INDEX_STEP"):
+        monkeypatch.setenv("MMVAE_STREAM_DMA", "0")  # (zero-copy gather options)
     N, D, B = 1500, 3000, 192
     data = _data(N, D, seed=21)
     res, st = _pair("nb", "bf16x3", D, 32, B, data)
