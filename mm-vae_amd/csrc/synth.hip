@@ -150,6 +150,11 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
                                                        int32_t* __restrict__ rtp, float2* __restrict__ cellnorm) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // log1pf of the integer counts 0 .. 511 from a workgroup table (the same log1pf values, so the
+    // norms are bit-identical): the accurate log1pf is ~150 instructions
+    __shared__ float l1tab[512];
+    for (int i = threadIdx.x; i < 512; i += 256) l1tab[i] = log1pf((float)i);
+    __syncthreads();
     if (row > N) return;
     int32_t* rt = rtp + row * (NT + 1);
     int n = 0;
@@ -179,7 +184,11 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u;
             if (j < n) {
-                const float l = log1pf(x[u]), ly = log1pf(fmaxf(x[u], 0.f));
+                const float xv = x[u];
+                const int xi = (int)fminf(fmaxf(xv, 0.f), 511.f);
+                // (x >= 0: log1pf(max(x, 0)) is l itself; else log1pf(0) = 0)
+                const float l = ((float)xi == xv) ? l1tab[xi] : log1pf(xv);
+                const float ly = xv >= 0.f ? l : 0.f;
                 sl2 = fmaf(l, l, sl2);
                 sy = fmaf(ly, ly + 2.f * epsD, sy);
                 for (int tt = (j > 0 ? gp[u] >> 6 : -1) + 1; tt <= (g[u] >> 6); ++tt) rt[tt] = j;
