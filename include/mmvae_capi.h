@@ -110,8 +110,10 @@ int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const
  * step's rows are gathered over PCIe into a per-step batch CSR in HBM (two slots, alternating with
  * the staging slots) and indexed; the gather runs on its own stream as soon as the step is staged,
  * under the previous step's kernels, and the step waits for it.  When D <= 65536 and every value
- * is a 16-bit integer count, the engine keeps a packed pinned copy (4 bytes per entry) and gathers
- * from it.  The kernels after the gather are the resident path's, on the batch's rows.  Results
+ * is a 16-bit integer count, the engine keeps a packed copy (4 bytes per entry): host threads pack
+ * the step's rows into a pinned slot buffer, one DMA-engine copy moves it to HBM and the step
+ * unpacks it (MMVAE_STREAM_DMA=0: a zero-copy gather kernel reads the copy over PCIe instead).
+ * The kernels after the gather are the resident path's, on the batch's rows.  Results
  * are bit-identical to mmvae_upload_csr of the same data.  HBM holds O(B nnz_b) of the dataset
  * instead of O(N nnz). */
 int mmvae_stream_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const float* val,
