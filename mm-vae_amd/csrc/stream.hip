@@ -249,6 +249,7 @@ static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
         if ((er = hipHostMalloc((void**)&e->h_bpk[s], sizeof(uint32_t) * (size_t)cap, hipHostMallocDefault)) != hipSuccess) return er;
         if ((er = hipMalloc(&e->d_bpk[s], sizeof(uint32_t) * (size_t)cap)) != hipSuccess) return er;
         e->bpk_cap[s] = cap;
+        ++e->graph_gen;  // the step graphs' unpack reads d_bpk[s]: re-captured with the new buffer
     }
     if (!e->gpool) {
         static const int env = [] { const char* v = std::getenv("MMVAE_STREAM_DMA_THREADS"); return v ? std::atoi(v) : 0; }();

@@ -143,3 +143,24 @@ def test_streamed_modes(mode, monkeypatch):
         for k in x:
             assert np.array_equal(x[k], y[k]), k
     assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+
+
+def test_streamed_dma_buffer_growth():
+    """The DMA mode's slot buffers grow on their own (a batch 1.25x heavier than the first one)
+    while the batch sets do not: the step graphs that read the old buffer are re-captured."""
+    from oracle import synth
+    N, D, B = 1200, 3000, 128
+    rp, col, val = synth.synth_csr(N // 2, D, lib_size=600.0, seed=5)
+    rp2, col2, val2 = synth.synth_csr(N // 2, D, lib_size=1800.0, seed=6)
+    rpx = np.concatenate([rp, rp[-1] + rp2[1:]])
+    colx = np.concatenate([col, col2])
+    valx = np.concatenate([val, val2])
+    res, st = _pair("nb", "bf16x3", D, 32, B, (rpx, colx, valx, None))
+    for eng in (res, st):
+        eng.graph(True)
+    light = np.arange(0, B, dtype=np.int64)
+    heavy = np.arange(N // 2, N // 2 + B, dtype=np.int64)
+    for s, cells in enumerate([light, light, light, heavy, heavy, light, heavy]):
+        assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
+    for k, v in res.params(registered_only=True).items():
+        assert np.array_equal(v, st.params(registered_only=True)[k]), k
