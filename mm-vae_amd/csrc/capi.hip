@@ -737,6 +737,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
         const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
         std::vector<char> ok(nth, 1);
+        std::vector<uint32_t> cmax(nth, 0);
         for (unsigned t = 0; t < nth; ++t)
             th.emplace_back([&, t] {
                 const int64_t a = nnz * t / nth, b = nnz * (t + 1) / nth;
@@ -749,9 +750,11 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
                         return;
                     }
                     e->hs_packed[i] = ((uint32_t)col[i] << 16) | c;
+                    cmax[t] = std::max(cmax[t], c);
                 }
             });
         for (auto& x : th) x.join();
+        e->hs_cmax = *std::max_element(cmax.begin(), cmax.end());
         hipError_t rer = hipSuccess;
         if (std::find(ok.begin(), ok.end(), 0) == ok.end() && e->hs_packed_bytes) {  // written, so backed: register
             rer = hipHostRegister(e->hs_packed, e->hs_packed_bytes, hipHostRegisterMapped);
@@ -808,6 +811,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");
     e->stream_index_step = getenv_is("MMVAE_STREAM_INDEX_STEP", "1");
     e->stream_dma = !getenv_is("MMVAE_STREAM_DMA", "0");  // (packed copies only)
+    e->stream_b3 = e->stream_dma && e->hs_packed && e->hs_cmax < 256 && getenv_is("MMVAE_STREAM_B3", "1");
     if (e->stream_prefetch) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
         for (int s2 = 0; s2 < 2; ++s2) {

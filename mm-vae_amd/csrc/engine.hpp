@@ -139,6 +139,8 @@ struct Engine {
     // (worker threads), one DMA-engine copy moves them to d_bpk[s], and the unpack kernel reads
     // HBM instead of mapped host memory
     bool stream_dma = false;  // set by mmvae_stream_csr
+    uint32_t hs_cmax = 0;     // the packed copy's largest count
+    bool stream_b3 = false;   // DMA mode, every count < 256 (MMVAE_STREAM_B3=1): 3-byte entries on the copy
     uint32_t* h_bpk[2] = {nullptr, nullptr};
     uint32_t* d_bpk[2] = {nullptr, nullptr};
     int64_t bpk_cap[2] = {0, 0};

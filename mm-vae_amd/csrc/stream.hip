@@ -139,6 +139,50 @@ __global__ __launch_bounds__(256) void k_stream_gather(const int64_t* __restrict
     }
 }
 
+// DMA mode with 3-byte entries (stream_b3): genes as uint16, counts as uint8, both at the rows'
+// batch offsets; four entries per lane in flight
+__global__ __launch_bounds__(256) void k_stream_unpack3(const uint16_t* __restrict__ g16, const uint8_t* __restrict__ c8,
+                                                        const float* __restrict__ hcov, int64_t Nh, int C,
+                                                        const int64_t* __restrict__ gcells, const int64_t* __restrict__ brp,
+                                                        int64_t Bp, int64_t* __restrict__ rowptr, int32_t* __restrict__ col,
+                                                        float* __restrict__ val, float* __restrict__ cov) {
+    for (int64_t b = blockIdx.x; b <= Bp; b += gridDim.x) {
+        if (b == Bp) {
+            if (threadIdx.x == 0) {
+                rowptr[Bp] = brp[Bp];
+                rowptr[Bp + 1] = brp[Bp];
+            }
+            for (int c = threadIdx.x; c < C; c += 256) cov[Bp * C + c] = 0.f;
+            continue;
+        }
+        const int64_t g = uni64(gcells[b]);
+        const bool real = g < Nh;
+        const int64_t s = uni64(brp[b]);
+        const int n = (int)(uni64(brp[b + 1]) - s);
+        const uint16_t* gs = g16 + s;
+        const uint8_t* cs = c8 + s;
+        int32_t* dc = col + s;
+        float* dv = val + s;
+        for (int i0 = threadIdx.x; i0 < n; i0 += 1024) {
+            uint32_t gg[4], cc[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = min(i0 + 256 * u, n - 1);
+                gg[u] = gs[i];
+                cc[u] = cs[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + 256 * u < n) {
+                    dc[i0 + 256 * u] = (int32_t)gg[u];
+                    dv[i0 + 256 * u] = (float)cc[u];
+                }
+        }
+        for (int c = threadIdx.x; c < C; c += 256) cov[b * C + c] = (real && hcov) ? hcov[g * C + c] : (hcov ? 0.f : (real ? 1.f : 0.f));
+        if (threadIdx.x == 0) rowptr[b] = s;
+    }
+}
+
 static unsigned gather_wgs(const Engine* e) {
     static const int env = [] { const char* v = std::getenv("MMVAE_GATHER_WGS"); return v ? std::atoi(v) : 0; }();
     const int64_t rows = e->Bpad + 1;
@@ -262,6 +306,10 @@ static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
     const uint32_t* src = e->hs_packed;
     const int64_t* hrp = e->hh_rowptr;
     const int64_t Nh = e->N_host;
+    // 3-byte entries: genes (uint16) from the buffer's start, counts (uint8) from byte 2 * cap
+    const bool b3 = e->stream_b3;
+    uint16_t* g3 = reinterpret_cast<uint16_t*>(dst);
+    uint8_t* c3 = reinterpret_cast<uint8_t*>(dst) + 2 * (size_t)e->bpk_cap[s];
     static_cast<GatherPool*>(e->gpool)->run([&](int t, int nth) {  // contiguous row ranges of about equal entries
         const int64_t a = tot * t / nth, z = tot * (t + 1) / nth;
         int64_t b = std::upper_bound(brp, brp + Bp + 1, a) - brp - 1;
@@ -269,12 +317,28 @@ static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
             const int64_t n = brp[b + 1] - brp[b];
             if (n > 0 && gc[b] < Nh) {  // the part of row b inside [a, z)
                 const int64_t lo = std::max(a, brp[b]), hi = std::min(z, brp[b + 1]);
-                if (hi > lo) std::memcpy(dst + lo, src + hrp[gc[b]] + (lo - brp[b]), sizeof(uint32_t) * (size_t)(hi - lo));
+                if (hi > lo) {
+                    const uint32_t* w = src + hrp[gc[b]] + (lo - brp[b]);
+                    if (b3) {
+                        for (int64_t i = 0; i < hi - lo; ++i) {
+                            g3[lo + i] = (uint16_t)(w[i] >> 16);
+                            c3[lo + i] = (uint8_t)w[i];
+                        }
+                    } else {
+                        std::memcpy(dst + lo, w, sizeof(uint32_t) * (size_t)(hi - lo));
+                    }
+                }
             }
         }
     });
     // only the copy runs on gstream: the unpack and the tile index are the step's first kernels
     // (stream_gather), so step n + 1's copy overlaps step n's whole kernel chain
+    if (tot > 0 && b3) {
+        if ((er = hipMemcpyAsync(e->d_bpk[s], e->h_bpk[s], 2 * (size_t)tot, hipMemcpyHostToDevice, e->gstream)) != hipSuccess) return er;
+        const size_t co = 2 * (size_t)e->bpk_cap[s];
+        return hipMemcpyAsync(reinterpret_cast<char*>(e->d_bpk[s]) + co, reinterpret_cast<char*>(e->h_bpk[s]) + co, (size_t)tot,
+                              hipMemcpyHostToDevice, e->gstream);
+    }
     if (tot > 0 && (er = hipMemcpyAsync(e->d_bpk[s], e->h_bpk[s], sizeof(uint32_t) * (size_t)tot, hipMemcpyHostToDevice, e->gstream)) != hipSuccess)
         return er;
     return hipSuccess;
@@ -285,6 +349,14 @@ static hipError_t stream_dma_unpack(Engine* e) {
     const int64_t Bp = e->Bpad;
     const int s = e->cur_slot;
     ScopedTimer tm(e, "k_stream_gather");
+    if (e->stream_b3) {
+        const uint16_t* g16 = reinterpret_cast<const uint16_t*>(e->d_bpk[s]);
+        const uint8_t* c8 = reinterpret_cast<const uint8_t*>(e->d_bpk[s]) + 2 * (size_t)e->bpk_cap[s];
+        hipLaunchKernelGGL(k_stream_unpack3, dim3((unsigned)std::min<int64_t>(Bp + 1, 2048)), dim3(256), 0, e->stream, g16, c8,
+                           e->hs_covar, e->N_host, (int)e->C, (const int64_t*)e->h_gcells[s], (const int64_t*)e->h_brp_pin, Bp,
+                           e->d_rowptr, e->d_col, e->d_val, e->d_covar);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_stream_gather<true, true>), dim3((unsigned)std::min<int64_t>(Bp + 1, 2048)), dim3(256), 0, e->stream, e->hs_rowptr,
                        e->hs_col, e->hs_val, (const uint32_t*)e->d_bpk[s], e->hs_covar, e->N_host, (int)e->C, e->d_cells,
                        (const int64_t*)e->h_gcells[s], (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
@@ -334,6 +406,8 @@ void stream_release(Engine* e) {
         e->bpk_cap[s] = 0;
     }
     e->stream_dma = false;
+    e->stream_b3 = false;
+    e->hs_cmax = 0;
     for (int s = 0; s < 2; ++s) {
         if (e->ev_gathered[s]) hipEventDestroy(e->ev_gathered[s]);
         if (e->ev_setfree[s]) hipEventDestroy(e->ev_setfree[s]);

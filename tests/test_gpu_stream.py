@@ -124,7 +124,7 @@ def test_streamed_unpacked_entries(kind):
 
 
 @pytest.mark.parametrize("mode", [("MMVAE_STREAM_DMA", "0"), ("MMVAE_STREAM_THP", "1"), ("MMVAE_STREAM_INDEX_STEP", "1"),
-                                  ("MMVAE_STREAM_SYNC", "1")])
+                                  ("MMVAE_STREAM_SYNC", "1"), ("MMVAE_STREAM_B3", "1")])
 def test_streamed_modes(mode, monkeypatch):
     """The streamed path's alternative modes (read at stream_csr): the zero-copy gather kernel
     (no DMA copy), its huge-page packed copy, the batch index built inside the step, the in-step
@@ -145,9 +145,12 @@ def test_streamed_modes(mode, monkeypatch):
     assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
 
 
-def test_streamed_dma_buffer_growth():
+@pytest.mark.parametrize("b3", ["0", "1"])
+def test_streamed_dma_buffer_growth(b3, monkeypatch):
     """The DMA mode's slot buffers grow on their own (a batch 1.25x heavier than the first one)
-    while the batch sets do not: the step graphs that read the old buffer are re-captured."""
+    while the batch sets do not: the step graphs that read the old buffer are re-captured (4-byte
+    and 3-byte entries)."""
+    monkeypatch.setenv("MMVAE_STREAM_B3", b3)
     from oracle import synth
     N, D, B = 1200, 3000, 128
     rp, col, val = synth.synth_csr(N // 2, D, lib_size=600.0, seed=5)
