@@ -109,7 +109,9 @@ def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234,
     eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dtype, device=device, seed=seed,
                            model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
     eng.init_params(seed=7)  # host-side work first: the GPU-heavy dataset synthesis runs last
-    eng.graph(graph)  # one hipGraph per step (with a communicator: the RCCL buckets captured too)
+    # one hipGraph per step; with a communicator the step graphs are used only under
+    # MMVAE_COMM_GRAPH=1 (then the RCCL buckets are captured too), else its steps run eagerly
+    eng.graph(graph)
     nnz = eng.synth_csr(cells, lib_size=lib, seed=2024)
     return eng, nnz
 

@@ -15,6 +15,18 @@
 #include "../mmvae_host.h"
 #include "options.hh"
 
+// hidden widths of --mean_encoding / --mean_decoding (NB, nb.hh:331-379) or --encoding /
+// --decoding (vMF, vmf.hh:338-385): every width up to MMVAE_MAX_HIDDEN layers per side is copied.
+// A longer list keeps its true count in n_*_hidden (widths past the array are not stored), so
+// mmvae_create rejects it with MMVAE_E_ARG instead of building a truncated model.
+template <class V>
+inline void mmvae_cfg_hidden_(mmvae_cfg& c, const V& enc, const V& dec) {
+    c.n_enc_hidden = (int32_t)enc.size();
+    c.n_dec_hidden = (int32_t)dec.size();
+    for (size_t i = 0; i < enc.size() && i < (size_t)MMVAE_MAX_HIDDEN; ++i) c.enc_hidden[i] = (int32_t)enc[i];
+    for (size_t i = 0; i < dec.size() && i < (size_t)MMVAE_MAX_HIDDEN; ++i) c.dec_hidden[i] = (int32_t)dec[i];
+}
+
 // mmvae_options_t + nbvae/vmf options + training options -> engine cfg (the constructor
 // arguments of nbvae_t, src/nb_vae_main.cc:103-112, and vmf_vae_t, src/vmf_vae_main.cc:100-107)
 inline mmvae_cfg mmvae_cfg_from_nb(const mmvae::nb::nbvae_options_t& nb, const training_options_t& tr, int64_t D, int64_t C,
@@ -29,10 +41,7 @@ inline mmvae_cfg mmvae_cfg_from_nb(const mmvae::nb::nbvae_options_t& nb, const t
     c.max_batch = batch_size;
     c.lr = tr.lr;
     c.relu = nb.do_relu ? 1 : 0;
-    c.n_enc_hidden = (int32_t)nb.mean_encoding_layers.size();
-    c.n_dec_hidden = (int32_t)nb.mean_decoding_layers.size();
-    for (size_t i = 0; i < nb.mean_encoding_layers.size() && i < 4; ++i) c.enc_hidden[i] = (int32_t)nb.mean_encoding_layers[i];
-    for (size_t i = 0; i < nb.mean_decoding_layers.size() && i < 4; ++i) c.dec_hidden[i] = (int32_t)nb.mean_decoding_layers[i];
+    mmvae_cfg_hidden_(c, nb.mean_encoding_layers, nb.mean_decoding_layers);
     return c;
 }
 
@@ -48,10 +57,7 @@ inline mmvae_cfg mmvae_cfg_from_vmf(const mmvae::vmf::vmf_options_t& v, const tr
     c.kappa_min = v.kappa_min;
     c.kappa_max = v.kappa_max;
     c.relu = v.do_relu ? 1 : 0;
-    c.n_enc_hidden = (int32_t)v.encoding_layers.size();
-    c.n_dec_hidden = (int32_t)v.decoding_layers.size();
-    for (size_t i = 0; i < v.encoding_layers.size() && i < 4; ++i) c.enc_hidden[i] = (int32_t)v.encoding_layers[i];
-    for (size_t i = 0; i < v.decoding_layers.size() && i < 4; ++i) c.dec_hidden[i] = (int32_t)v.decoding_layers[i];
+    mmvae_cfg_hidden_(c, v.encoding_layers, v.decoding_layers);
     return c;
 }
 

@@ -87,8 +87,10 @@ void mmvae_cfg_default(mmvae_cfg* cfg, int32_t model);
  * Shapes: D, K, C, H, R >= 1 and at most MMVAE_MAX_HIDDEN hidden encoder / decoder layers of any
  * width >= 1 (the reference has no limits).  Models with D <= 75,264 genes, K <= 64,
  * C, H, R <= 8, at most 4 hidden layers per side and hidden widths <= 64 run on the fused tile
- * kernels; any other shape runs on the wide path (a dense [B, D] batch in HBM and generic f32-MFMA
- * GEMMs, exact f32 whatever the dtype; mmvae_path reports which).  FP8 for the NB model only. */
+ * kernels; any other shape runs on the wide path (a dense [B, D] batch in HBM and a generic GEMM:
+ * the gene GEMMs on the bf16 MFMA as BF16X3 split operands or plain BF16 per the handle's dtype,
+ * exact f32 MFMA for F32 handles and the small layers; mmvae_path reports which).  FP8 for the NB
+ * model only. */
 int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out);
 int mmvae_destroy(mmvae_h h);
 /* Which step path the handle runs: 0 = the fused tile kernels, 1 = the wide path. */

@@ -124,3 +124,60 @@ int main(int argc, const char* argv[]) {
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["16", "2", "100", "1", "0.5", "0"]
+
+
+DEEP_TU = r'''
+#include "mmvae/mmvae.hh"
+#include <cstdio>
+int main(int argc, const char* argv[]) {
+    training_options_t tr; mmvae::nb::nbvae_options_t nb; mmvae::vmf::vmf_options_t vo;
+    parse_nbvae_options(argc, argv, nb); parse_vmf_options(argc, argv, vo); parse_training_options(argc, argv, tr);
+    const mmvae_cfg c = mmvae_cfg_from_nb(nb, tr, 500, 1, 100);
+    const mmvae_cfg v = mmvae_cfg_from_vmf(vo, tr, 500, 1, 100);
+    std::printf("nb %d", c.n_enc_hidden);
+    for (int i = 0; i < c.n_enc_hidden && i < MMVAE_MAX_HIDDEN; ++i) std::printf(" %d", c.enc_hidden[i]);
+    std::printf("\nnbdec %d", c.n_dec_hidden);
+    for (int i = 0; i < c.n_dec_hidden && i < MMVAE_MAX_HIDDEN; ++i) std::printf(" %d", c.dec_hidden[i]);
+    std::printf("\nvmf %d", v.n_enc_hidden);
+    for (int i = 0; i < v.n_enc_hidden && i < MMVAE_MAX_HIDDEN; ++i) std::printf(" %d", v.enc_hidden[i]);
+    mmvae_h h = nullptr;
+    // the shape checks of mmvae_create run before it looks for a device: a valid deep cfg gets
+    // as far as the device lookup (MMVAE_E_HIP here), a cfg over MMVAE_MAX_HIDDEN is MMVAE_E_ARG
+    const int rc = mmvae_create(&c, 0, &h);
+    std::printf("\ncreate %d %s\n", rc, rc == MMVAE_E_ARG ? mmvae_last_error(nullptr) : "");
+    if (h) mmvae_destroy(h);
+    return 0;
+}
+'''
+
+
+@pytest.mark.parametrize("n_layers", [6, 16, 17])
+def test_dropin_cfg_keeps_every_hidden_layer(tmp_path, n_layers):
+    """mmvae_cfg_from_nb / _from_vmf copy every hidden width of a reference option struct (nb.hh:331-379,
+    vmf.hh:338-385: any depth), up to MMVAE_MAX_HIDDEN; a deeper list reaches mmvae_create with its true
+    count and is rejected there (MMVAE_E_ARG), never silently truncated."""
+    src = tmp_path / "deep.cc"
+    src.write_text(DEEP_TU)
+    lib = os.path.join(ROOT, "mm-vae_amd", "lib")
+    exe = tmp_path / "deep"
+    r = subprocess.run(["g++", "-std=c++14", str(src), "-o", str(exe), "-I" + os.path.join(ROOT, "include"),
+                        "-L" + lib, "-lmmvae_host", "-lmmvae", "-Wl,-rpath," + lib], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    widths = [64 + 8 * i for i in range(n_layers)]
+    enc = ",".join(str(v) for v in widths)
+    dec = ",".join(str(v) for v in reversed(widths[:5]))
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")  # CPU container: no device in any case
+    r = subprocess.run([str(exe), "--mean_encoding", enc, "--mean_decoding", dec, "--encoding", enc],
+                       capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    out = {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines() if ln.strip()}
+    kept = widths[:16]
+    assert out["nb"] == [str(n_layers)] + [str(v) for v in kept]
+    assert out["vmf"] == [str(n_layers)] + [str(v) for v in kept]
+    assert out["nbdec"] == ["5"] + [str(v) for v in reversed(widths[:5])]
+    rc = int(out["create"][0])
+    if n_layers <= 16:
+        assert rc == -2, out  # MMVAE_E_HIP: every shape check passed
+    else:
+        assert rc == -1 and "MMVAE_MAX_HIDDEN" in " ".join(out["create"][1:]), out
+
