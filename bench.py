@@ -109,8 +109,8 @@ def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234,
     eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dtype, device=device, seed=seed,
                            model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
     eng.init_params(seed=7)  # host-side work first: the GPU-heavy dataset synthesis runs last
-    # one hipGraph per step; with a communicator the step graphs are used only under
-    # MMVAE_COMM_GRAPH=1 (then the RCCL buckets are captured too), else its steps run eagerly
+    # one hipGraph per step; with a communicator the RCCL buckets are captured too
+    # (MMVAE_COMM_GRAPH=0: its steps run eagerly)
     eng.graph(graph)
     nnz = eng.synth_csr(cells, lib_size=lib, seed=2024)
     return eng, nnz
@@ -379,6 +379,44 @@ def secondary(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=50, warmup=5, 
     return out
 
 
+def dp_exchange(mmvae_amd, D, K, B, dtype, cells, lib, steps=300, warmup=20):
+    """The data-parallel exchange's fixed cost on one GPU: the headline step with
+    a forced 1-rank RCCL communicator (MMVAE_FORCE_COMM=1, read at comm_init) runs exactly a world > 1
+    rank's exchange — the split gradient kernels, the comm-stream fork / join and the RCCL calls
+    (mmvae_alg.hh:306-310) — over one rank, where the sum is the identity.  Each mode's
+    ms/step minus the no-communicator step bounds what the N > 1 scaling must absorb besides the
+    xGMI transfer itself (0.83 MB of gradient per step)."""
+    modes = [("bucket, eager", {"MMVAE_COMM_GRAPH": "0"}), ("flat, eager", {"MMVAE_COMM_GRAPH": "0", "MMVAE_NO_OVERLAP": "1"}),
+             ("bucket, step graph (the world > 1 default)", {}),
+             ("flat, step graph", {"MMVAE_NO_OVERLAP": "1"})]
+    eng, _ = make_engine(mmvae_amd, "nb", D, K, B, dtype, cells, lib, 0)
+    batches = [(s * B + np.arange(B)) % cells for s in range(warmup + steps)]
+    base = time_steps(eng, batches, 1.0, B, 0, steps, warmup) / steps * 1e3
+    out = {"workload": f"NB {cells} x {D}, latent {K}, batch {B}, {dtype}", "steps": steps,
+           "no_comm_ms_per_step": round(base, 4), "modes": []}
+    saved = {k: os.environ.get(k) for k in ("MMVAE_FORCE_COMM", "MMVAE_COMM_GRAPH", "MMVAE_NO_OVERLAP")}
+    try:
+        for name, env in modes:
+            for k in saved:
+                os.environ.pop(k, None)
+            os.environ["MMVAE_FORCE_COMM"] = "1"
+            os.environ.update(env)
+            eng.comm_init(0, 1, mmvae_amd.Engine.comm_unique_id())
+            g0 = eng.graph_stats()
+            ms = time_steps(eng, batches, 1.0, B, 0, steps, warmup) / steps * 1e3
+            g1 = eng.graph_stats()
+            out["modes"].append({"mode": name, "ms_per_step": round(ms, 4), "delta_us": round((ms - base) * 1e3, 1),
+                                 "graph_replays": g1["replays"] - g0["replays"]})
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    eng.close()
+    return out
+
+
 def streamed(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=30, warmup=5, label=""):
     """The out-of-core mode (mmvae_stream_csr): the dataset in host memory, each step's rows gathered
     over PCIe into a batch CSR in HBM — the same synthetic dataset, copied to the host."""
@@ -493,6 +531,8 @@ def main():
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(eng, args, Ncells, K)
         eng.close()
+        if not args.no_extras and args.model == "nb":
+            out["dp_exchange"] = dp_exchange(mmvae_amd, D, K, B, args.dtype, Ncells, args.lib_size)
         if not args.no_extras:
             lines = []
             for dt_ in ("bf16", "f32"):

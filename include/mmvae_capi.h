@@ -226,10 +226,13 @@ int mmvae_debug_poison(mmvae_h h, int32_t byte);
  * replay it; the step's variable scalars (Philox step / row offset, Adam's bias corrections)
  * travel in the staged copy.  Results are identical to eager launches.  Not used while kernel
  * timing is on.  With an active communicator (world > 1, or a 1-rank one under
- * MMVAE_FORCE_COMM=1) steps run eagerly unless MMVAE_COMM_GRAPH=1 was set at mmvae_comm_init:
- * then the RCCL bucket all-reduces are captured into the step graph, after the ranks agree
- * (ncclMin over every rank's capture outcome) that every one of them captured; if any rank's
- * capture failed, all of them run that handle's communicator steps eagerly from then on.
+ * MMVAE_FORCE_COMM=1) the RCCL bucket all-reduces are captured into the step graph too (unless
+ * MMVAE_COMM_GRAPH=0 was set at mmvae_comm_init: eager steps).  Every rank then captures at the
+ * same steps: before the first such step the ranks agree (ncclMax) on the largest batch any of
+ * them can stage and size the batch-dependent buffers for it once; each capture's outcome is
+ * agreed (ncclMin) before any rank launches; if any rank's capture failed, all of them run that
+ * handle's communicator steps eagerly from then on.  Dataset and communicator calls are then
+ * collective (every rank makes them at the same point of its step sequence).
  * graph_stats: captures and replays so far. */
 int mmvae_graph_enable(mmvae_h h, int32_t on);
 int mmvae_graph_stats(mmvae_h h, int64_t* captures, int64_t* replays);

@@ -602,6 +602,7 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
                      int64_t D, const float* covar) {
     if (!e || !rowptr || N < 1) FAIL(e, MMVAE_E_ARG, "upload_csr: bad arguments");
     ++e->graph_gen;  // dataset buffers are replaced: step graphs are re-captured
+    e->cap_synced = false;
     {
         const int rc = validate_csr(e, "upload_csr", rowptr, col, N, D);
         if (rc) return rc;
@@ -680,15 +681,152 @@ extern "C" {
 int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const float* val, int64_t N, int64_t D,
                      const float* covar) {
     if (!e || !rowptr || !col || !val || N < 1) FAIL(e, MMVAE_E_ARG, "stream_csr: bad arguments");
-    ++e->graph_gen;
     {
         const int rc = validate_csr(e, "stream_csr", rowptr, col, N, D);
         if (rc) return rc;
     }
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    stream_release(e);
-    // the resident dataset (if any) is dropped
+    stream_release(e);  // a previous streamed dataset (its registrations, batch sets, buffers)
+    const int64_t nnz = rowptr[N];
+    // the DMA mode (packed copies only) rides on the prefetched gather; MMVAE_STREAM_SYNC=1 (the
+    // in-step gather) and MMVAE_STREAM_DMA=0 read the packed copy over PCIe with the gather kernel
+    const bool dma = !getenv_is("MMVAE_STREAM_SYNC", "1") && !getenv_is("MMVAE_STREAM_DMA", "0");
+    // Everything of the new dataset is set up first; the resident dataset (if any) is dropped only
+    // once it all succeeded, and a failure undoes this call's registrations.
+    std::vector<void*> regs;
+    uint32_t* packed = nullptr;
+    const uint32_t* packed_dev = nullptr;
+    size_t packed_map = 0;   // > 0: an mmap of that many bytes (else hipHostMalloc'd)
+    bool packed_reg = false;  // the mmap is registered (mapped for the zero-copy gather)
+    auto free_packed = [&]() {
+        if (!packed) return;
+        if (packed_reg) hipHostUnregister(packed);
+        if (packed_map) munmap(packed, packed_map);
+        else hipHostFree(packed);
+        packed = nullptr;
+        packed_dev = nullptr;
+        packed_map = 0;
+        packed_reg = false;
+    };
+    auto undo = [&]() {
+        for (void* h : regs) hipHostUnregister(h);
+        regs.clear();
+        free_packed();
+        (void)hipGetLastError();
+    };
+    // the caller's arrays as mapped pinned memory (read over PCIe by the gather / unpack kernels):
+    // read-only registration first (a read-only np.memmap can be pinned that way), then plain
+    auto reg = [&](const void* p, size_t bytes, const void** dev) -> hipError_t {
+        if (!bytes) {
+            *dev = p;
+            return hipSuccess;
+        }
+        void* h = const_cast<void*>(p);
+        hipError_t er = hipHostRegister(h, bytes, hipHostRegisterMapped | hipHostRegisterReadOnly);
+        if (er != hipSuccess) {
+            (void)hipGetLastError();
+            er = hipHostRegister(h, bytes, hipHostRegisterMapped);
+        }
+        if (er != hipSuccess) return er;
+        regs.push_back(h);
+        void* d = nullptr;
+        er = hipHostGetDevicePointer(&d, h, 0);
+        *dev = d;
+        return er;
+    };
+    auto failed = [&](hipError_t er, const char* what) {
+        undo();
+        FAIL(e, MMVAE_E_HIP, std::string("stream_csr: ") + what + ": " + hipGetErrorString(er));
+    };
+    const void* d = nullptr;
+    hipError_t er = reg(rowptr, sizeof(int64_t) * (size_t)(N + 1), &d);
+    if (er != hipSuccess) return failed(er, "registering rowptr");
+    const int64_t* hs_rowptr = static_cast<const int64_t*>(d);
+    // integer counts below 2^16 over at most 2^16 genes: the packed copy (bit-exact values).  In the
+    // DMA mode only host threads read it (stream_dma_gather), so it stays pageable; the zero-copy
+    // gather reads it over PCIe, so there it is mapped pinned memory.  If no such copy can be made
+    // the caller's unpacked arrays serve instead.
+    uint32_t cmax = 0;
+    if (D <= 65536 && nnz > 0 && !getenv_is("MMVAE_STREAM_PACK", "0")) {
+        const size_t bytes = sizeof(uint32_t) * (size_t)nnz;
+        // MMVAE_STREAM_THP=1 (experiment): 2 MB transparent huge pages where the host gives them
+        const bool thp = getenv_is("MMVAE_STREAM_THP", "1");
+        if (dma || thp) {
+            const size_t al2 = (size_t)(2u << 20);
+            const size_t pbytes = thp ? (bytes + al2 - 1) & ~(al2 - 1) : bytes;
+            void* m = mmap(nullptr, pbytes + (thp ? al2 : 0), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m != MAP_FAILED) {
+                if (thp) {  // 2 MB-aligned start inside the mapping, the rest unmapped
+                    const uintptr_t a0 = reinterpret_cast<uintptr_t>(m), al = (a0 + al2 - 1) & ~(uintptr_t)(al2 - 1);
+                    if (al > a0) munmap(m, al - a0);
+                    if (al + pbytes < a0 + pbytes + al2) munmap(reinterpret_cast<void*>(al + pbytes), a0 + pbytes + al2 - (al + pbytes));
+                    packed = reinterpret_cast<uint32_t*>(al);
+                    madvise(packed, pbytes, MADV_HUGEPAGE);
+                } else {
+                    packed = static_cast<uint32_t*>(m);
+                }
+                packed_map = pbytes;
+            }
+        } else if (hipHostMalloc((void**)&packed, bytes, hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            packed = nullptr;
+        }
+        if (packed) {
+            const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+            std::vector<std::thread> th;
+            std::vector<char> ok(nth, 1);
+            std::vector<uint32_t> cm(nth, 0);
+            for (unsigned t = 0; t < nth; ++t)
+                th.emplace_back([&, t] {
+                    const int64_t a = nnz * t / nth, b = nnz * (t + 1) / nth;
+                    for (int64_t i = a; i < b; ++i) {
+                        const float v = val[i];
+                        const uint32_t c = (uint32_t)(v >= 0.f && v < 65536.f ? (int)v : 0);
+                        const float back = (float)c;
+                        if (std::memcmp(&back, &v, 4) != 0) {  // non-integer, negative, -0, too large
+                            ok[t] = 0;
+                            return;
+                        }
+                        packed[i] = ((uint32_t)col[i] << 16) | c;
+                        cm[t] = std::max(cm[t], c);
+                    }
+                });
+            for (auto& x : th) x.join();
+            if (std::find(ok.begin(), ok.end(), 0) != ok.end()) {
+                free_packed();
+            } else {
+                cmax = *std::max_element(cm.begin(), cm.end());
+                if (dma) {
+                    packed_dev = nullptr;  // host-only (the pool packs the step's rows from it)
+                } else if (packed_map) {  // the zero-copy gather's THP copy: written, so backed: register
+                    void* dp = nullptr;
+                    if (hipHostRegister(packed, packed_map, hipHostRegisterMapped) == hipSuccess) {
+                        packed_reg = true;
+                        if (hipHostGetDevicePointer(&dp, packed, 0) == hipSuccess) packed_dev = static_cast<const uint32_t*>(dp);
+                    }
+                    if (!packed_dev) free_packed();
+                } else {
+                    packed_dev = packed;  // hipHostMallocMapped: one address space
+                }
+            }
+        }
+        (void)hipGetLastError();
+    }
+    const int32_t* hs_col = nullptr;
+    const float* hs_val = nullptr;
+    if (!packed) {
+        if ((er = reg(col, sizeof(int32_t) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "registering col");
+        hs_col = static_cast<const int32_t*>(d);
+        if ((er = reg(val, sizeof(float) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "registering val");
+        hs_val = static_cast<const float*>(d);
+    }
+    const float* hs_covar = nullptr;
+    if (covar) {
+        if ((er = reg(covar, sizeof(float) * (size_t)(N * e->C), &d)) != hipSuccess) return failed(er, "registering covar");
+        hs_covar = static_cast<const float*>(d);
+    }
+    // the new dataset is in place: the resident one (if any) goes
     for (void* b : {(void*)e->d_rowptr, (void*)e->d_col, (void*)e->d_val, (void*)e->d_covar, (void*)e->d_rtp,
                     (void*)e->d_cellnorm})
         if (b) hipFree(b);
@@ -698,97 +836,19 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->d_covar = nullptr;
     e->d_rtp = nullptr;
     e->d_cellnorm = nullptr;
-    const int64_t nnz = rowptr[N];
-    // the caller's arrays as mapped pinned memory: the gather kernel reads them over PCIe
-    auto reg = [&](const void* p, size_t bytes, const void** dev) -> hipError_t {
-        if (!bytes) {
-            *dev = p;
-            return hipSuccess;
-        }
-        void* h = const_cast<void*>(p);
-        hipError_t er = hipHostRegister(h, bytes, hipHostRegisterMapped);
-        if (er != hipSuccess) return er;
-        e->hs_registered.push_back(h);
-        void* d = nullptr;
-        er = hipHostGetDevicePointer(&d, h, 0);
-        *dev = d;
-        return er;
-    };
-    const void* d;
-    HIPCHK(e, reg(rowptr, sizeof(int64_t) * (size_t)(N + 1), &d));
-    e->hs_rowptr = static_cast<const int64_t*>(d);
-    // integer counts below 2^16 over at most 2^16 genes: the packed copy (bit-exact values)
-    if (D <= 65536 && nnz > 0 && !getenv_is("MMVAE_STREAM_PACK", "0")) {
-        // MMVAE_STREAM_THP=1 (experiment): the copy in 2 MB transparent huge pages where the host
-        // gives them, registered, instead of hipHostMalloc — one GPU translation per 2 MB, not 4 KB
-        const size_t pbytes = (sizeof(uint32_t) * (size_t)nnz + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-        if (getenv_is("MMVAE_STREAM_THP", "1")) {
-            void* m = mmap(nullptr, pbytes + (2u << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-            if (m != MAP_FAILED) {  // 2 MB-aligned start inside the mapping, the rest unmapped
-                const uintptr_t a0 = reinterpret_cast<uintptr_t>(m), al = (a0 + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
-                if (al > a0) munmap(m, al - a0);
-                if (al + pbytes < a0 + pbytes + (2u << 20)) munmap(reinterpret_cast<void*>(al + pbytes), a0 + pbytes + (2u << 20) - (al + pbytes));
-                e->hs_packed = reinterpret_cast<uint32_t*>(al);
-                e->hs_packed_bytes = pbytes;
-                madvise(e->hs_packed, pbytes, MADV_HUGEPAGE);
-            }
-        }
-        if (!e->hs_packed) HIPCHK(e, hipHostMalloc((void**)&e->hs_packed, sizeof(uint32_t) * (size_t)nnz, hipHostMallocMapped));
-        const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        std::vector<char> ok(nth, 1);
-        std::vector<uint32_t> cmax(nth, 0);
-        for (unsigned t = 0; t < nth; ++t)
-            th.emplace_back([&, t] {
-                const int64_t a = nnz * t / nth, b = nnz * (t + 1) / nth;
-                for (int64_t i = a; i < b; ++i) {
-                    const float v = val[i];
-                    const uint32_t c = (uint32_t)(v >= 0.f && v < 65536.f ? (int)v : 0);
-                    const float back = (float)c;
-                    if (std::memcmp(&back, &v, 4) != 0) {  // non-integer, negative, -0, too large
-                        ok[t] = 0;
-                        return;
-                    }
-                    e->hs_packed[i] = ((uint32_t)col[i] << 16) | c;
-                    cmax[t] = std::max(cmax[t], c);
-                }
-            });
-        for (auto& x : th) x.join();
-        e->hs_cmax = *std::max_element(cmax.begin(), cmax.end());
-        hipError_t rer = hipSuccess;
-        if (std::find(ok.begin(), ok.end(), 0) == ok.end() && e->hs_packed_bytes) {  // written, so backed: register
-            rer = hipHostRegister(e->hs_packed, e->hs_packed_bytes, hipHostRegisterMapped);
-            void* dp = nullptr;
-            if (rer == hipSuccess && (rer = hipHostGetDevicePointer(&dp, e->hs_packed, 0)) == hipSuccess)
-                e->hs_packed_dev = static_cast<const uint32_t*>(dp);
-            else if (rer == hipSuccess)
-                hipHostUnregister(e->hs_packed);
-        } else {
-            e->hs_packed_dev = e->hs_packed;
-        }
-        if (std::find(ok.begin(), ok.end(), 0) != ok.end() || rer != hipSuccess) {
-            if (e->hs_packed_bytes) munmap(e->hs_packed, e->hs_packed_bytes);
-            else hipHostFree(e->hs_packed);
-            e->hs_packed = nullptr;
-            e->hs_packed_dev = nullptr;
-            e->hs_packed_bytes = 0;
-            HIPCHK(e, rer);
-        }
-    }
-    e->hs_col = nullptr;
-    e->hs_val = nullptr;
-    if (!e->hs_packed) {
-        HIPCHK(e, reg(col, sizeof(int32_t) * (size_t)nnz, &d));
-        e->hs_col = static_cast<const int32_t*>(d);
-        HIPCHK(e, reg(val, sizeof(float) * (size_t)nnz, &d));
-        e->hs_val = static_cast<const float*>(d);
-    }
-    e->hs_covar = nullptr;
+    ++e->graph_gen;
+    e->cap_synced = false;
+    e->hs_registered = regs;
+    e->hs_rowptr = hs_rowptr;
+    e->hs_packed = packed;
+    e->hs_packed_dev = packed_dev;
+    e->hs_packed_bytes = packed_map;
+    e->hs_packed_reg = packed_reg;
+    e->hs_cmax = cmax;
+    e->hs_col = hs_col;
+    e->hs_val = hs_val;
+    e->hs_covar = hs_covar;
     e->unit_covar = e->C == 1 && all_ones(covar, N);
-    if (covar) {
-        HIPCHK(e, reg(covar, sizeof(float) * (size_t)(N * e->C), &d));
-        e->hs_covar = static_cast<const float*>(d);
-    }
     e->hh_rowptr = rowptr;
     e->hh_col = col;
     e->hh_val = val;
@@ -808,9 +868,9 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->stage_bytes = (e->stage_bytes_res + sizeof(int64_t) * (size_t)(e->Bpad + 1) + 15) / 16 * 16;
     stream_bind(e, e->cur_slot);
     // the prefetched gather (stream.hip stream_prefetch); MMVAE_STREAM_SYNC=1 keeps it in the step
-    e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");
+    e->stream_prefetch = !getenv_is("MMVAE_STREAM_SYNC", "1");  // (dma above implies it)
     e->stream_index_step = getenv_is("MMVAE_STREAM_INDEX_STEP", "1");
-    e->stream_dma = !getenv_is("MMVAE_STREAM_DMA", "0");  // (packed copies only)
+    e->stream_dma = dma;  // (packed copies only)
     e->stream_b3 = e->stream_dma && e->hs_packed && e->hs_cmax < 256 && getenv_is("MMVAE_STREAM_B3", "1");
     if (e->stream_prefetch) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
@@ -836,6 +896,7 @@ int mmvae_synth_csr(mmvae_h e, int64_t N, double lib_size, uint64_t seed, int64_
     if (!e || N < 1 || lib_size <= 0) FAIL(e, MMVAE_E_ARG, "synth_csr: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
     ++e->graph_gen;
+    e->cap_synced = false;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     stream_release(e);
     e->stage_bytes = e->stage_bytes_res;
@@ -1204,6 +1265,12 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     if (!e->d_rowptr) FAIL(e, MMVAE_E_STATE, "run: no dataset uploaded");
     const int64_t n_total = a->n_total > 0 ? a->n_total : a->B;
     HIPCHK(e, hipSetDevice(e->device));
+    // step graphs holding RCCL calls: the batch-dependent buffers sized for every rank's worst
+    // batch first, so that no rank's graph key changes alone (comm_sync_capacity)
+    if (e->graph_on && !e->timing && e->comm_active() && e->comm_graph && !e->comm_graph_failed && !e->cap_synced) {
+        const int crc = comm_sync_capacity(e);
+        if (crc) return crc;
+    }
     int rc = stage_rows(e, a->cell_ids, a->ridx, a->B, /*balance=*/true);
     if (rc) return rc;
     HIPCHK(e, stream_prefetch(e));  // (streamed dataset: the rows' gather on its own stream)
@@ -1216,12 +1283,13 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     // frozen operands are repacked eagerly, never inside a step graph
     if (e->frozen_dirty) HIPCHK(e, e->wide ? wide_prepare_frozen(e) : vmf ? vmf_prepare_frozen(e) : nb_prepare_frozen(e));
     // one hipGraph per step: captured on the first step of a launch shape,
-    // replayed while the shape holds; not with timers or diagnostics.  Steps with an active
-    // communicator run eagerly unless MMVAE_COMM_GRAPH=1 was set at mmvae_comm_init: then the
-    // graph holds the RCCL bucket all-reduces too (comm_bucket's event fork onto the comm stream
-    // and its join back are captured with them).  Every rank takes the same capture decision
-    // (comm_capture_agree), and a failed capture falls back to eager launches for the
-    // handle's lifetime on every rank.
+    // replayed while the shape holds; not with timers or diagnostics.  With an active
+    // communicator the graph holds the RCCL bucket all-reduces too (comm_bucket's event fork onto
+    // the comm stream and its join back are captured with them) unless MMVAE_COMM_GRAPH=0 was set
+    // at mmvae_comm_init (eager steps).  Every rank takes the same capture decisions: the graph
+    // key's batch-dependent buffers are sized for every rank's worst batch (comm_sync_capacity),
+    // the capture outcome is agreed (comm_capture_agree), and a failed capture falls back to
+    // eager launches for the handle's lifetime on every rank.
 #ifdef MMVAE_DIAG
     static const bool dbg_env = std::getenv("MMVAE_DBG") != nullptr;
 #else
@@ -1257,14 +1325,16 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
             hipError_t ie = hipSuccess;
             if (!crc && ce == hipSuccess) ie = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
             if (g) hipGraphDestroy(g);
+            const bool cap_ok = !crc && ce == hipSuccess && ie == hipSuccess;
+            // a failed capture or instantiation leaves a sticky error: cleared on every path (its
+            // code is returned below, or the eager fallback runs on a clean runtime state)
+            if (!cap_ok) (void)hipGetLastError();
             bool comm_fail = false;
             if (with_comm) {
                 // the ranks agree before any of them launches: a graph one rank captured while
                 // another fell back would pair a replayed collective with eager ones
-                const bool ok = !crc && ce == hipSuccess && ie == hipSuccess;
-                (void)hipGetLastError();
                 int agreed = 0;
-                HIPCHK(e, comm_capture_agree(e, ok, &agreed));
+                HIPCHK(e, comm_capture_agree(e, cap_ok, &agreed));
                 comm_fail = !agreed;
             }
             if (comm_fail) {
@@ -1390,6 +1460,7 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     if (!e || world < 1 || rank < 0 || rank >= world) FAIL(e, MMVAE_E_ARG, "comm_init: bad arguments");
     HIPCHK(e, hipSetDevice(e->device));
     ++e->graph_gen;  // rank-dependent launches (the vMF rank-0 term, bucket split) are re-captured
+    e->cap_synced = false;
     if (!id128) {
         // local decomposition mode (tests): this handle computes rank `rank`'s shard of a
         // world-`world` step (rank-0-only terms included) but reduces nothing — the caller sums
@@ -1414,7 +1485,10 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     e->rank = rank;
     e->world = world;
     e->comm_force = getenv_is("MMVAE_FORCE_COMM", "1");
-    e->comm_graph = getenv_is("MMVAE_COMM_GRAPH", "1");
+    // RCCL calls inside step graphs: on by default (MMVAE_COMM_GRAPH=0 opts out).  One-GPU cost of the
+    // exchange at the headline shape (bench.py dp_exchange, forced 1-rank communicator): buckets
+    // captured +4 us per step, buckets eager +34 us, flat captured +0 us
+    e->comm_graph = !getenv_is("MMVAE_COMM_GRAPH", "0");
     e->comm_graph_failed = false;
     if (!e->comm_stream) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
@@ -1495,7 +1569,7 @@ hipError_t comm_bucket(Engine* e, int b) {
 // *agreed = 1 only when every rank captured its step graph
 hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed) {
     if (!e->d_flag) {
-        hipError_t er = hipMalloc(&e->d_flag, sizeof(int32_t));
+        hipError_t er = hipMalloc(&e->d_flag, 16);  // (the int64 word at +8: comm_sync_capacity)
         if (er != hipSuccess) return er;
     }
     const int32_t v = ok ? 1 : 0;
@@ -1508,6 +1582,48 @@ hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed) {
     if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
     *agreed = r;
     return er;
+}
+
+// Step graphs with a communicator hold RCCL calls, so every rank must capture (and agree, above) at
+// the same steps.  The graph cache key is rank-invariant except for the batch-dependent buffers a
+// step graph points at: the entry lists (d_ents) and, for a streamed dataset, the batch sets and
+// DMA copy buffers, which grow when one rank's batch needs more room than it has seen (a rank
+// with a heavier batch would re-capture — and run the agreement all-reduce — alone, while its
+// peers replayed: mismatched collectives).  So before the first graph step after a
+// dataset or communicator change, the ranks agree (ncclMax, eager) on the largest batch any of
+// them can stage — Bpad rows of its largest dataset row, resampled duplicates included — and
+// size those buffers for it once; stage_rows then never grows them and every rank's key changes
+// only with the step's shape, which all ranks share.  (Every rank calls this at the same step:
+// dataset and communicator calls are collective in data-parallel use.)
+int comm_sync_capacity(Engine* e) {
+    int64_t mx = 0;
+    for (int32_t v : e->cell_nnz) mx = std::max<int64_t>(mx, v);
+    int64_t need = e->Bpad * mx;
+    if (!e->d_flag) HIPCHK(e, hipMalloc(&e->d_flag, 16));
+    int64_t* dw = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(e->d_flag) + 8);
+    HIPCHK(e, hipMemcpyAsync(dw, &need, sizeof(need), hipMemcpyHostToDevice, e->stream));
+    if (ncclAllReduce(dw, dw, 1, ncclInt64, ncclMax, e->comm, e->stream) != ncclSuccess)
+        FAIL(e, MMVAE_E_COMM, "comm_sync_capacity: ncclAllReduce failed");
+    HIPCHK(e, hipMemcpyAsync(&need, dw, sizeof(need), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->gstream) HIPCHK(e, hipStreamSynchronize(e->gstream));
+    if (!e->wide && need + 64 > e->ent_cap) {
+        if (e->d_ents) hipFree(e->d_ents);
+        e->d_ents = nullptr;
+        e->ent_cap = need + 64;
+        HIPCHK(e, hipMalloc(&e->d_ents, sizeof(uint2) * e->ent_cap));
+        HIPCHK(e, hipMemset(e->d_ents, 0, sizeof(uint2) * e->ent_cap));
+    }
+    if (e->streamed) {
+        for (int s = 0; s < 2; ++s) {
+            if (e->bset[s].cap < need) HIPCHK(e, batch_set_alloc(e, s, need));
+            if (e->stream_dma && e->hs_packed && e->bpk_cap[s] < need) HIPCHK(e, stream_bpk_alloc(e, s, need));
+        }
+        stream_bind(e, e->cur_slot);
+    }
+    ++e->graph_gen;  // on every rank at the same step
+    e->cap_synced = true;
+    return MMVAE_OK;
 }
 }  // namespace mmvae
 }  // extern "C++"

@@ -113,7 +113,8 @@ struct Engine {
     bool stream_index_step = false;     // prefetch mode: the batch's tile index built inside the step, not on gstream
     uint32_t* hs_packed = nullptr;      // host address of the packed copy
     const uint32_t* hs_packed_dev = nullptr;  // its device address
-    size_t hs_packed_bytes = 0;         // > 0: mmap'd (2 MB pages where the kernel gives them) + registered
+    size_t hs_packed_bytes = 0;         // > 0: mmap'd (pageable in the DMA mode; 2 MB pages under MMVAE_STREAM_THP=1)
+    bool hs_packed_reg = false;         // the mmap is registered as mapped pinned memory (zero-copy gather)
     const int64_t* hh_rowptr = nullptr;  // the same arrays' host addresses (mmvae_get_rows)
     const int32_t* hh_col = nullptr;
     const float* hh_val = nullptr;
@@ -263,7 +264,7 @@ struct Engine {
     // MMVAE_FORCE_COMM=1 at mmvae_comm_init: a 1-rank communicator still runs the data-parallel
     // exchange (buckets, flat all-reduce, their graph capture) — the one-GPU test of that path
     bool comm_force = false;
-    // RCCL calls inside step graphs: opt in with MMVAE_COMM_GRAPH=1 (read at mmvae_comm_init)
+    // RCCL calls inside step graphs: the default; MMVAE_COMM_GRAPH=0 opts out (read at mmvae_comm_init)
     bool comm_graph = false;
     // the gradient exchange runs (a communicator of > 1 rank, or a forced 1-rank one)
     bool comm_active() const { return comm && (world > 1 || comm_force); }
@@ -288,6 +289,11 @@ struct Engine {
     // this runtime): later steps with the communicator run eagerly
     bool comm_graph_failed = false;
     uint64_t graph_gen = 0;          // bumped when a buffer a step graph points at is replaced
+    // step graphs with a communicator (the default): the batch-dependent buffers (entry
+    // lists, streamed batch sets and DMA buffers) were sized for the worst batch of every rank
+    // (comm_sync_capacity), so no rank re-captures alone; reset when the dataset or communicator
+    // changes
+    bool cap_synced = false;
     int64_t graph_captures = 0, graph_replays = 0;
 
     // ---- timing ----
@@ -343,6 +349,11 @@ bool split_grads(const Engine* e);
 hipError_t comm_bucket(Engine* e, int b);
 // min-reduce every rank's step-graph capture outcome (eager): *agreed = 1 iff all captured
 hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed);
+// step graphs with a communicator: every batch-dependent buffer a step graph points at sized once
+// for the largest batch any rank can stage, agreed over the communicator (capi.hip)
+int comm_sync_capacity(Engine* e);
+// slot s's DMA copy buffers of the streamed dataset (stream.hip)
+hipError_t stream_bpk_alloc(Engine* e, int s, int64_t cap);
 hipError_t nb_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps);
 hipError_t nb_encode(Engine* e, int64_t B, float* d_mean, float* d_lnvar);
 // vMF launchers (vmf_kernels.hip)

@@ -219,6 +219,9 @@ hipError_t stream_gather(Engine* e) {
     }
     ScopedTimer tm(e, "k_stream_gather");
     const int64_t Bp = e->Bpad;
+    // the gather kernel reads the dataset over PCIe: the packed copy's device address, or the
+    // caller's registered arrays (a host-only packed copy belongs to the DMA mode)
+    if (e->hs_packed ? !e->hs_packed_dev : !(e->hs_col && e->hs_val)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->stream, e->hs_rowptr, e->hs_col,
                        e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)nullptr, e->d_brp, Bp,
                        e->d_rowptr, e->d_col, e->d_val, e->d_covar);
@@ -277,22 +280,29 @@ struct GatherPool {
     }
 };
 
+// slot s's DMA copy buffers (pinned host + HBM) for `cap` packed entries; the caller bumps
+// graph_gen (the step graphs' unpack reads d_bpk[s])
+hipError_t stream_bpk_alloc(Engine* e, int s, int64_t cap) {
+    hipError_t er;
+    if (e->gstream && (er = hipStreamSynchronize(e->gstream)) != hipSuccess) return er;
+    if (e->h_bpk[s]) hipHostFree(e->h_bpk[s]);
+    if (e->d_bpk[s]) hipFree(e->d_bpk[s]);
+    e->h_bpk[s] = nullptr;
+    e->d_bpk[s] = nullptr;
+    e->bpk_cap[s] = 0;
+    if ((er = hipHostMalloc((void**)&e->h_bpk[s], sizeof(uint32_t) * (size_t)cap, hipHostMallocDefault)) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_bpk[s], sizeof(uint32_t) * (size_t)cap)) != hipSuccess) return er;
+    e->bpk_cap[s] = cap;
+    return hipSuccess;
+}
+
 // MMVAE_STREAM_DMA: the slot's rows packed on the host, one DMA copy, the unpack kernel on HBM
 static hipError_t stream_dma_gather(Engine* e, int s, int64_t Bp) {
     hipError_t er;
     const int64_t tot = e->h_brp_pin[Bp];
     if ((er = hipEventSynchronize(e->ev_gathered[s])) != hipSuccess) return er;  // slot s's last copy has read h_bpk[s]
     if (tot > e->bpk_cap[s]) {
-        if ((er = hipStreamSynchronize(e->gstream)) != hipSuccess) return er;
-        if (e->h_bpk[s]) hipHostFree(e->h_bpk[s]);
-        if (e->d_bpk[s]) hipFree(e->d_bpk[s]);
-        e->h_bpk[s] = nullptr;
-        e->d_bpk[s] = nullptr;
-        e->bpk_cap[s] = 0;
-        const int64_t cap = tot + tot / 4 + 1024;
-        if ((er = hipHostMalloc((void**)&e->h_bpk[s], sizeof(uint32_t) * (size_t)cap, hipHostMallocDefault)) != hipSuccess) return er;
-        if ((er = hipMalloc(&e->d_bpk[s], sizeof(uint32_t) * (size_t)cap)) != hipSuccess) return er;
-        e->bpk_cap[s] = cap;
+        if ((er = stream_bpk_alloc(e, s, tot + tot / 4 + 1024)) != hipSuccess) return er;
         ++e->graph_gen;  // the step graphs' unpack reads d_bpk[s]: re-captured with the new buffer
     }
     if (!e->gpool) {
@@ -376,6 +386,7 @@ hipError_t stream_prefetch(Engine* e) {
     if (e->stream_dma && e->hs_packed) {
         if ((er = stream_dma_gather(e, s, Bp)) != hipSuccess) return er;
     } else {
+        if (e->hs_packed ? !e->hs_packed_dev : !(e->hs_col && e->hs_val)) return hipErrorInvalidValue;
         hipLaunchKernelGGL(e->hs_packed ? k_stream_gather<true> : k_stream_gather<false>, dim3(gather_wgs(e)), dim3(256), 0, e->gstream, e->hs_rowptr, e->hs_col,
                            e->hs_val, e->hs_packed_dev, e->hs_covar, e->N_host, (int)e->C, e->d_cells, (const int64_t*)e->h_gcells[s],
                            (const int64_t*)e->h_brp_pin, Bp, e->d_rowptr, e->d_col, e->d_val, e->d_covar);
@@ -424,12 +435,13 @@ void stream_release(Engine* e) {
         q = Engine::BatchSet{};
     }
     for (void* p : e->hs_registered) hipHostUnregister(p);
-    if (e->hs_packed && e->hs_packed_bytes) {
-        hipHostUnregister(e->hs_packed);
+    if (e->hs_packed && e->hs_packed_bytes) {  // mmap'd: pageable (DMA mode) or registered (THP zero-copy)
+        if (e->hs_packed_reg) hipHostUnregister(e->hs_packed);
         munmap(e->hs_packed, e->hs_packed_bytes);
     } else if (e->hs_packed) {
         hipHostFree(e->hs_packed);
     }
+    e->hs_packed_reg = false;
     e->hs_packed = nullptr;
     e->hs_packed_dev = nullptr;
     e->hs_packed_bytes = 0;

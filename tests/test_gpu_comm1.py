@@ -7,8 +7,9 @@ world > 1 rank runs (capi.hip comm_bucket / enqueue_run) —
 * the two overlapped buckets: split gradient kernels, an event fork onto the comm stream, one
   ncclGroupStart / ncclAllReduce-per-range / ncclGroupEnd per bucket, the join before clip + Adam;
 * the flat path (MMVAE_NO_OVERLAP=1): one ncclAllReduce of the whole gradient on the main stream;
-* both inside a captured step graph (MMVAE_COMM_GRAPH=1), after the ranks' capture agreement
-  (comm_capture_agree: an eager ncclAllReduce(min) of the capture outcome);
+* both inside a captured step graph (the default; MMVAE_COMM_GRAPH=0 runs them eagerly), after
+  the ranks' capture agreement (comm_capture_agree: an eager ncclAllReduce(min) of the capture
+  outcome) and, once, their agreement on the batch-dependent buffers' size (comm_sync_capacity);
 * a capture that fails (MMVAE_TEST_COMM_CAPTURE_FAIL=1 makes comm_bucket refuse a capturing
   stream): the eager fallback for the handle's lifetime.
 
@@ -25,11 +26,11 @@ pytestmark = pytest.mark.gpu
 D, K, B, N = 3000, 32, 384, 3000
 MODES = {
     # name: (env at comm_init / steps, graph on, expect replays)
-    "bucket": ({}, False),
-    "flat": ({"MMVAE_NO_OVERLAP": "1"}, False),
-    "bucket_graph": ({"MMVAE_COMM_GRAPH": "1"}, True),
-    "flat_graph": ({"MMVAE_COMM_GRAPH": "1", "MMVAE_NO_OVERLAP": "1"}, True),
-    "capture_fail": ({"MMVAE_COMM_GRAPH": "1", "MMVAE_TEST_COMM_CAPTURE_FAIL": "1"}, True),
+    "bucket": ({"MMVAE_COMM_GRAPH": "0"}, False),
+    "flat": ({"MMVAE_COMM_GRAPH": "0", "MMVAE_NO_OVERLAP": "1"}, False),
+    "bucket_graph": ({}, True),
+    "flat_graph": ({"MMVAE_NO_OVERLAP": "1"}, True),
+    "capture_fail": ({"MMVAE_TEST_COMM_CAPTURE_FAIL": "1"}, True),
 }
 
 
@@ -94,12 +95,12 @@ def test_forced_one_rank_comm_bit_identical(model, dtype, mode, monkeypatch):
         assert st["replays"] == 5 and st["captures"] >= 3, st
 
 
-def test_comm_graph_is_opt_in(monkeypatch):
-    """Without MMVAE_COMM_GRAPH=1 a step with an active communicator runs eagerly even with step
-    graphs enabled (capture of RCCL calls stays opt-in until measured on two GPUs)."""
+def test_comm_graph_opt_out(monkeypatch):
+    """MMVAE_COMM_GRAPH=0 (read at comm_init): a step with an active communicator runs eagerly even
+    with step graphs enabled — the fallback if RCCL calls inside graphs ever misbehave."""
     from mmvae_amd import Engine
     monkeypatch.setenv("MMVAE_FORCE_COMM", "1")
-    monkeypatch.delenv("MMVAE_COMM_GRAPH", raising=False)
+    monkeypatch.setenv("MMVAE_COMM_GRAPH", "0")
     eng = _engine("nb", "bf16x3")
     eng.comm_init(0, 1, Engine.comm_unique_id())
     eng.graph(True)
@@ -107,3 +108,54 @@ def test_comm_graph_is_opt_in(monkeypatch):
     st = eng.graph_stats()
     eng.close()
     assert st["replays"] == 0 and st["captures"] == 0, st
+
+
+@pytest.mark.parametrize("streamed", [False, True])
+def test_comm_graph_heavier_batch_keeps_its_graphs(streamed, monkeypatch):
+    """a rank whose batch needs more entry-list (or streamed batch-set / DMA) room than it
+    has seen used to re-allocate, re-capture and run the capture-agreement all-reduce alone while its
+    peers replayed.  With step graphs holding RCCL calls the engine sizes those buffers once for every
+    rank's worst batch (comm_sync_capacity), so a heavier batch replays the graphs already captured
+    (one per staging slot) — and still matches a handle without a communicator bit for bit."""
+    from mmvae_amd import Engine
+
+    def make():
+        eng = _engine("nb", "bf16x3")
+        rp, col, val = eng.get_rows(np.arange(N, dtype=np.int64))
+        if streamed:
+            eng.stream_csr(rp, col, val)
+        return eng, (rp, col, val)
+
+    def run(eng, light, heavy):
+        out = []
+        for s in range(8):
+            cells = heavy if s in (5, 6) else light
+            out.append(eng.step(cells, 0.7, step_id=s))
+        return out
+
+    monkeypatch.setenv("MMVAE_SPLIT_GRADS", "1")
+    ref, data = make()
+    nnz = np.diff(data[0])
+    order = np.argsort(nnz, kind="stable").astype(np.int64)
+    light, heavy = order[:B].copy(), order[-B:].copy()
+    assert nnz[heavy].sum() > 1.5 * nnz[light].sum()
+    ref.graph(True)
+    want = run(ref, light, heavy)
+    want_p = ref.params(registered_only=True)
+    ref.close()
+    monkeypatch.delenv("MMVAE_SPLIT_GRADS")
+
+    monkeypatch.setenv("MMVAE_FORCE_COMM", "1")
+    monkeypatch.delenv("MMVAE_COMM_GRAPH", raising=False)  # (the default: RCCL inside step graphs)
+    eng, _ = make()
+    eng.comm_init(0, 1, Engine.comm_unique_id())
+    eng.graph(True)
+    got = run(eng, light, heavy)
+    st = eng.graph_stats()
+    got_p = eng.params(registered_only=True)
+    eng.close()
+    assert got == want, (got, want)
+    for k in want_p:
+        assert np.array_equal(got_p[k], want_p[k]), k
+    # one capture per staging slot for the single launch shape; the heavy batches replayed them
+    assert st["captures"] == 2 and st["replays"] == 8, st

@@ -36,16 +36,27 @@ def _engine(model, b, device):
     return eng
 
 
-def _batches():
-    return [(np.arange(B, dtype=np.int64) * (5 + 2 * s) + 3 * s) % 3000 for s in range(STEPS)]
+def _batches(skew=False, device=0):
+    if not skew:
+        return [(np.arange(B, dtype=np.int64) * (5 + 2 * s) + 3 * s) % 3000 for s in range(STEPS)]
+    # rank 0's half from the lightest rows, rank 1's from the heaviest (only one rank's
+    # batch outgrows the buffers it has seen): the synthetic dataset is the same in every process
+    from mmvae_amd import MODEL_NB, Engine
+    probe = Engine(D=D, K=K, max_batch=8, dtype="f32", seed=9, device=device, model=MODEL_NB)
+    probe.synth_csr(3000, lib_size=1500.0, seed=4)
+    rp, _, _ = probe.get_rows(np.arange(3000, dtype=np.int64))
+    probe.close()
+    order = np.argsort(np.diff(rp), kind="stable").astype(np.int64)
+    h = B // 2
+    return [np.concatenate([order[s * h:(s + 1) * h], order[3000 - (s + 1) * h:3000 - s * h]]) for s in range(STEPS)]
 
 
-def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False):
+def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False, skew=False):
     try:
         if no_overlap:
             os.environ["MMVAE_NO_OVERLAP"] = "1"
-        if graph:  # RCCL calls inside step graphs are opt-in (read at comm_init)
-            os.environ["MMVAE_COMM_GRAPH"] = "1"
+        if not graph:  # RCCL calls inside step graphs are the default (read at comm_init)
+            os.environ["MMVAE_COMM_GRAPH"] = "0"
         from mmvae_amd import Engine
         if rank == 0:
             uid = Engine.comm_unique_id()
@@ -57,7 +68,7 @@ def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False):
         eng.comm_init(rank, 2, uid)
         eng.graph(graph)  # the step graph then holds the RCCL bucket all-reduces
         out = []
-        for s, cells in enumerate(_batches()):
+        for s, cells in enumerate(_batches(skew, device)):
             l, n = eng.step(cells[rank * b:(rank + 1) * b], 0.7, n_total=B, row_offset=rank * b, step_id=s)
             out.append((l, n))
         if graph:
@@ -68,12 +79,15 @@ def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False):
 
 
 @pytest.mark.skipif(_ndev() < 2, reason="needs two GPUs (RCCL over xGMI)")
-@pytest.mark.parametrize("no_overlap,graph", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("no_overlap,graph,skew", [(False, False, False), (True, False, False), (False, True, False),
+                                                   (False, True, True)])
 @pytest.mark.parametrize("model", ["nb", "vmf"])
-def test_rccl_world2_equals_world1(model, no_overlap, graph):
+def test_rccl_world2_equals_world1(model, no_overlap, graph, skew):
+    """skew: rank 1's shard holds the heaviest rows every step (its entry lists need more room than
+    rank 0's), with the RCCL calls inside step graphs — every rank must still replay in step."""
     ctx = mp.get_context("spawn")
     uid_q, res_q = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, model, no_overlap, uid_q, res_q, r, graph)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, model, no_overlap, uid_q, res_q, r, graph, skew)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -93,7 +107,7 @@ def test_rccl_world2_equals_world1(model, no_overlap, graph):
             assert st["replays"] == STEPS, st
     # world-1 reference in this process, on device 0
     full = _engine(model, B, 0)
-    for s, cells in enumerate(_batches()):
+    for s, cells in enumerate(_batches(skew)):
         l, n = full.step(cells, 0.7, step_id=s)
         l2 = res[0][0][s][0] + res[1][0][s][0]
         assert abs(l2 - l) <= 2e-5 * abs(l), (s, l2, l)

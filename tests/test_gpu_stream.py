@@ -167,3 +167,37 @@ def test_streamed_dma_buffer_growth(b3, monkeypatch):
         assert res.step(cells, 1.0, step_id=s) == st.step(cells, 1.0, step_id=s), s
     for k, v in res.params(registered_only=True).items():
         assert np.array_equal(v, st.params(registered_only=True)[k]), k
+
+
+@pytest.mark.parametrize("mode", [None, ("MMVAE_STREAM_DMA", "0")])
+def test_streamed_async_pipeline(mode, monkeypatch):
+    """the host runs ahead (run(sync=False)): both staging slots and both batch sets are in
+    flight while the prefetched gather (DMA copy or zero-copy kernel) of step n + 1 overlaps step n —
+    the ordering that ev_setfree, ev_gathered and the staging tickets carry — including steps whose
+    heavier batch grows the batch sets / DMA buffers mid-stream.  Parameters and gradients after the
+    run, and the closing synced step's loss, must equal the resident handle's bit for bit."""
+    if mode:
+        monkeypatch.setenv(*mode)
+    from oracle import synth
+    N, D, B = 1200, 3000, 128
+    rp, col, val = synth.synth_csr(N // 2, D, lib_size=600.0, seed=15)
+    rp2, col2, val2 = synth.synth_csr(N // 2, D, lib_size=2400.0, seed=16)
+    data = (np.concatenate([rp, rp[-1] + rp2[1:]]), np.concatenate([col, col2]), np.concatenate([val, val2]), None)
+    res, st = _pair("nb", "bf16x3", D, 32, B, data)
+    rng = np.random.default_rng(8)
+    plan = []
+    for s in range(12):
+        heavy = s in (4, 5, 9)
+        b = B - 21 if s == 7 else B
+        cells = rng.integers(N // 2, N, b) if heavy else rng.integers(0, N // 2, b)
+        plan.append((cells, s == 6, rng.integers(0, b, b) if s == 8 else None))
+    for eng in (res, st):
+        eng.graph(True)
+        for s, (cells, ev, ridx) in enumerate(plan):
+            eng.run(cells, 0.9, ridx=ridx, update=not ev, step_id=s, sync=False)
+        eng.sync()
+    for x, y in ((res.params(registered_only=True), st.params(registered_only=True)), (res.grads(), st.grads())):
+        for k in x:
+            assert np.array_equal(x[k], y[k]), k
+    cells = rng.integers(0, N, B)
+    assert res.step(cells, 0.9, step_id=99) == st.step(cells, 0.9, step_id=99)
