@@ -153,3 +153,68 @@ def test_nb_configs4_per_gpu_shape(dtype):
 def test_relu_bench_shape(model):
     """--relu at a multi-tile shape (ReLU after mu_encoding / Angular, nb.hh:345-346, vmf.hh:351-352)."""
     _run_live(model, 20000, 64 if model == "nb" else 32, 1024, "f32", N=5000, relu=True)
+
+
+def _run_live_trajectory(model, D, K, B, dtype, N, beta=0.8):
+    """Three steps of the reference loop at a bench shape against the live oracle, each side on its
+    own trajectory: an update, the eval forward of the next batch (Q12,
+    mmvae_alg.hh:277-285) and a second update (mmvae_alg.hh:300-310) — losses, gradients and clip
+    norms of both updates, the eval loss, and the parameters after each Adam step."""
+    from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
+    from helpers import assert_adam_close
+    from oracle import nb_oracle, vmf_oracle
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    vmf = model == "vmf"
+    eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=1, model=MODEL_VMF if vmf else MODEL_NB)
+    eng.synth_csr(N, lib_size=2000.0, seed=3)
+    eng.init_params(seed=7)
+    if vmf:
+        eng.set_param("ln_kappa", np.array([np.log(np.float32(4.0))], np.float32))
+    if vmf:
+        p0, f0 = vmf_oracle.init_params(D, Z=K)
+        tr = vmf_oracle.VMFTrainer(_engine_params(eng, p0), _engine_params(eng, f0))
+    else:
+        p0, f0 = nb_oracle.init_params(D, K=K)
+        tr = nb_oracle.NBTrainer(_engine_params(eng, p0), _engine_params(eng, f0))
+    tl, tg = TOL[dtype]
+    rng = np.random.default_rng(17)
+    c = torch.ones(B, 1)
+    grads_seen = []
+    for t, kind in enumerate(("update", "eval", "update")):
+        cells = (np.arange(B, dtype=np.int64) * (7 + 4 * t) + 11 + 1000 * t) % N
+        em = rng.standard_normal((B, K)).astype(np.float32)
+        en = rng.standard_normal((B, 1)).astype(np.float32)
+        eps = em.ravel() if vmf else np.concatenate([em.ravel(), en.ravel()])
+        x = _oracle_inputs(eng, cells, D)
+        oargs = (x, c, torch.from_numpy(em)) if vmf else (x, c, torch.from_numpy(em), torch.from_numpy(en))
+        if kind == "eval":
+            got = eng.eval_loss(cells, beta, eps=eps)
+            want = tr.eval_loss(*oargs, beta)
+            assert abs(got - want) <= tl * abs(want), (t, got, want)
+            continue
+        loss, norm = eng.step(cells, beta, eps=eps)
+        r = tr.step(*oargs, beta)
+        del x
+        assert abs(loss - r["loss"]) <= tl * abs(r["loss"]), (t, loss, r["loss"])
+        gold = {k: v.numpy() for k, v in r["grads"].items()}
+        got = eng.grads()
+        grads_seen.append(gold)
+        if vmf:
+            gk, wk = float(got.pop("ln_kappa")[0]), float(gold["ln_kappa"][0])
+            assert abs(gk - wk) <= 1e-6 * (0.5 * D - 1.0) + tg * abs(wk), (t, gk, wk)
+        assert_grads_close(got, {k: v for k, v in gold.items() if k in got}, tg, ctx=f"{model} {dtype} step {t}")
+        assert abs(norm - r["total_norm"]) <= 10 * tg * r["total_norm"], (t, norm, r["total_norm"])
+        # post-Adam parameters; a coordinate whose gradient sat at the noise floor in ANY update of
+        # the trajectory may have moved by lr the other way each time (assert_adam_close)
+        gmin = {k: np.minimum.reduce([np.abs(g[k]) for g in grads_seen]) for k in gold}
+        want_p = {k: v.numpy() for k, v in tr.params().items()}
+        assert_adam_close(eng.params(registered_only=True), want_p, gmin, lr=1e-3 * len(grads_seen),
+                          ctx=f"{model} {dtype} step {t}", noisy_keys=("ln_kappa",) if vmf else ())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
+@pytest.mark.parametrize("model", ["nb", "vmf"])
+def test_bench_shape_trajectory(model, dtype):
+    """configs[1] (NB, 20k genes, latent 64) / configs[2] (vMF, latent 32) at 4096 cells: update,
+    eval, update against the live oracle, parameters compared after every Adam step."""
+    _run_live_trajectory(model, 20000, 64 if model == "nb" else 32, 4096, dtype, N=12000)
