@@ -322,14 +322,15 @@ MMVAE_DEV f2 fma2(f2 a, f2 b, f2 c) { return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b
 #endif
 MMVAE_DEV f2 splat2(float v) { return f2{v, v}; }
 
-// Dense NB terms of two (cell, gene) elements at x = 0 (nb.hh:456-459, 518-528):
+// Dense NB terms of two (cell, gene) elements at x = 0 (nb.hh:456-459, 518-528) — nb_nu2 is its
+// overdispersion part, shared with the sparse pass's entry pairs (nb_kernels.hip pass B):
 //   nu = clamp(softplus(u)), nup = nu + 1e-4, sgm = d nu / d u (0 where the clamp bites),
 //   lg2 = log2((mu + nup) / nup)  (log2 units),  q = -mu / (mu + nup).
 // Five transcendentals per element: exp(-|u|), 1/(1+e), log2(1+e), 1/(nup (mu+nup)), log2(s/nup).
 // softplus' log1p uses the rounding-corrected form log1p(a) = log(z) - ((z - 1) - a) / z with
 // z = fl(1 + a) (exact z - 1): accurate for small a, as torch's log1p.  lg2 is the reference's
 // own cancelling difference log(mu + nu) - log(nu) (nb.hh:527), to the same absolute error.
-MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lg2, f2& q, f2& sgm) {
+MMVAE_DEV void nb_nu2(f2 u, f2& nup, f2& sgm) {
     constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
     f2 e, r, l;
     e.x = fexp2(-fabsf(u.x) * L2E);
@@ -345,6 +346,9 @@ MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lg2, f2& q, f2& sgm) {
     sgm.x = (nu.x == sp.x) ? ((u.x >= 0.f) ? r.x : er.x) : 0.f;
     sgm.y = (nu.y == sp.y) ? ((u.y >= 0.f) ? r.y : er.y) : 0.f;
     nup = nu + 1e-4f;
+}
+MMVAE_DEV void nb_dense2(f2 mu, f2 u, f2& nup, f2& lg2, f2& q, f2& sgm) {
+    nb_nu2(u, nup, sgm);
     const f2 sv = mu + nup;
     const f2 ns = nup * sv;
     f2 rr;
@@ -420,6 +424,42 @@ MMVAE_DEV void nb_gamma_terms(float nup, float x, float& lgd, float& dgd, const 
         lgd = a.lg + c.lg - b.lg;
         dgd = a.dg - b.dg;
     }
+}
+
+// nb_gamma_terms of two counts that are integers in 0..8 (0: lgd = dgd = 0), as packed pairs.
+// Factor i of the finite product is nup + i while i < x, else 1 — on_i = clamp(x - i, 0, 1) is one
+// v_pk_add_f32 with the clamp modifier, a_i = on_i (nup + i) + (1 - on_i) — so both counts of a
+// pair share every instruction instead of one select chain per count.  x0 / x1: the counts as ints.
+#ifndef MMVAE_F2_SCALAR
+MMVAE_DEV f2 clamp01_add2(f2 x, float c) {  // min(max(x + c, 0), 1) per half, c wave-uniform
+    f2 o;  // (a 64-bit SGPR pair operand whose low word, c, feeds both halves: op_sel_hi)
+    const uint64_t cp = (uint64_t)__float_as_uint(c);
+    asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] clamp" : "=v"(o) : "v"(x), "s"(cp));
+    return o;
+}
+#else
+MMVAE_DEV f2 clamp01_add2(f2 x, float c) {
+    return f2{fminf(fmaxf(x.x + c, 0.f), 1.f), fminf(fmaxf(x.y + c, 0.f), 1.f)};
+}
+#endif
+MMVAE_DEV void nb_gamma_terms2(f2 nup, f2 x, int x0, int x1, f2& lgd, f2& dgd, const float* ftab) {
+    constexpr float LN2 = 0.6931471805599453f;
+    f2 P = splat2(1.f), Pd = splat2(0.f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const f2 on = clamp01_add2(x, -(float)i);
+        const f2 a = fma2(on, nup + (float)i, 1.f - on);
+        Pd = fma2(Pd, a, on * P);
+        P = P * a;
+    }
+    f2 rP, l;
+    rP.x = frcp(P.x);
+    rP.y = frcp(P.y);
+    const f2 t = f2{ftab[x0], ftab[x1]} * rP;  // x! / (nup (nup+1) .. (nup+x-1))
+    l.x = flog2(t.x);
+    l.y = flog2(t.y);
+    lgd = l * LN2;
+    dgd = -Pd * rP;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1111,6 +1111,9 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         dzP[lb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     float lossacc = 0.f;
+    f2 lossacc2 = splat2(0.f);  // (the packed sparse pass's)
+    constexpr float LN2c = 0.6931471805599453f;
+    constexpr bool SPAIR = !std::is_same<P, float>::value;
     // ---- per-wave row data for the sparse pass ----
     const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
     fill_toffl(toffl, S, t0, d.NT, Q.toff, wbk, lane);
@@ -1189,7 +1192,76 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         wave_sync();
         lap(0);
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
-        if (!dbg_bit(d.dbg, 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
+        // 16-bit operand modes (x3, bf16): two entries per lane as one packed pair (entries lane
+        // and lane + 64, then + 128 / + 192 ...), packed arithmetic throughout (nb_nu2: the
+        // epilogue's own overdispersion arithmetic, so an entry's nu is the dense pass's).  The f32
+        // mode keeps one entry per lane (its pass B already spills).
+        if constexpr (SPAIR) {
+            if (!dbg_bit(d.dbg, 1)) pend.visit2(Q.ents, lane, [&](uint2 ea, uint2 eb, bool vb) {
+                const int ra = (int)(ea.x >> 6), ga = (int)(ea.x & 63);
+                const int rb = (int)(eb.x >> 6), gb2 = (int)(eb.x & 63);
+                const f2 x = f2{__uint_as_float(ea.y), vb ? __uint_as_float(eb.y) : 0.f};
+                const float* rsa = rsc + ra * NRS;
+                const float* rsb = rsc + rb * NRS;
+                const f2 p = f2{q2[ra * PS + ga], q2[rb * PS + gb2]};
+                const f2 mu = fma2(p, f2{rsa[0], rsb[0]}, splat2(1e-4f));  // nb.hh:519
+                const float4 g4a = gsb[ga], g4b = gsb[gb2];
+                f2 u = f2{g4a.y, g4b.y};
+#pragma unroll
+                for (int q = 0; q < RM; ++q) {  // nb.hh:456-457
+                    const f2 wn = q == 0 ? f2{g4a.w, g4b.w}
+                                         : ((q < R) ? f2{Q.Wnd[(int64_t)(64 * t + ga) * R + q], Q.Wnd[(int64_t)(64 * t + gb2) * R + q]}
+                                                    : splat2(0.f));
+                    u = fma2(wn, f2{rsa[3 + q], rsb[3 + q]}, u);
+                }
+                f2 nup, sgm;
+                nb_nu2(u, nup, sgm);  // nb.hh:458-459
+                const f2 sv = mu + nup;
+                f2 rsv, rmu, lr;
+                rsv.x = frcp(sv.x);
+                rsv.y = frcp(sv.y);
+                rmu.x = frcp(mu.x);
+                rmu.y = frcp(mu.y);
+                // nb.hh:522-523: the finite product for integer counts <= 8, the series otherwise
+                const bool biga = !(x.x <= 8.f && x.x == floorf(x.x)), bigb = !(x.y <= 8.f && x.y == floorf(x.y));
+                const f2 xf = f2{biga ? 0.f : x.x, bigb ? 0.f : x.y};
+                f2 lgd, dgd;
+                nb_gamma_terms2(nup, xf, (int)xf.x, (int)xf.y, lgd, dgd, ftab);
+                if (biga || bigb) {
+                    float l_, dg_;
+                    if (biga) {
+                        nb_gamma_terms<8>(nup.x, x.x, l_, dg_, ftab);
+                        lgd.x = l_;
+                        dgd.x = dg_;
+                    }
+                    if (bigb) {
+                        nb_gamma_terms<8>(nup.y, x.y, l_, dg_, ftab);
+                        lgd.y = l_;
+                        dgd.y = dg_;
+                    }
+                }
+                const f2 svm = sv * rmu;
+                lr.x = flog2(svm.x);
+                lr.y = flog2(svm.y);
+                lossacc2 = fma2(x * LN2c, lr, lossacc2 + lgd);  // nb.hh:527: x (log(mu+nu) - log(mu))
+                const f2 dq = x * (rsv - rmu);
+                const f2 ddu = fma2(x, rsv, dgd) * sgm;          // (0 where the clamp bites)
+                if constexpr (!LOSS) {
+                    const f2 pdq = p * dq;
+                    auto put = [&](int r, int gl, float a, float b) {
+                        if constexpr (PLANAR) {
+                            char* cb = reinterpret_cast<char*>(cc) + ccp(r, gl);
+                            *reinterpret_cast<float*>(cb) = a;
+                            *reinterpret_cast<float*>(cb + 1024) = b;
+                        } else {
+                            cc[cci(r, gl)] = CP::pack(a, b);
+                        }
+                    };
+                    put(ra, ga, pdq.x, ddu.x);
+                    if (vb) put(rb, gb2, pdq.y, ddu.y);
+                }
+            });
+        } else if (!dbg_bit(d.dbg, 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
             const float p = q2[r * PS + gl];
             const float mu = fmaf(p, rs_[0], 1e-4f);
@@ -1502,6 +1574,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             dp[KP] = dzP[lb][r];
         }
     }
+    lossacc += lossacc2.x + lossacc2.y;
     const float lw = wave_sum(fmaf(0.6931471805599453f, lossd2.x + lossd2.y, lossacc));
     __syncthreads();
     if (lane == 0) part[w] = lw;

@@ -128,6 +128,17 @@ struct ListEntries {
     }
     // packed position (row-in-block << 6 | gene-in-tile) of register entry k, -1 past the list
     MMVAE_DEV int pos(int k, int lane) const { return (lane + 64 * k < n) ? (int)raw[k].x : -1; }
+    // f(entry A, entry B, B valid) for the tile's entries two at a time: A = lane, B = lane + 64,
+    // then lane + 128 / + 192, ... (the packed-pair sparse passes; an invalid B holds a real entry
+    // of the tile, to be neither stored nor counted)
+    template <class F>
+    MMVAE_DEV void visit2(const uint2* __restrict__ ents, int lane, F&& f) const {
+        if (lane < n) f(raw[0], raw[1], lane + 64 < n);
+        for (int e = 128 + lane; e < n; e += 128) {
+            const bool vb = e + 64 < n;
+            f(ents[base + e], ents[base + (vb ? e + 64 : e)], vb);
+        }
+    }
     // f(row-in-block, gene-in-tile, x) for every entry of the tile
     template <class F>
     MMVAE_DEV void visit(const uint2* __restrict__ ents, int lane, F&& f) const {
