@@ -454,8 +454,76 @@ static bool use_mf(const Engine* e, const GemmOp& g) {
 
 // C = epilogue(A . B); `x` non-null: the encoder input transform on A (the f32 handles
 // materialise the normalised block instead, see enc_forward)
+// ---- narrow shapes: the column sums / small weight gradients over the batch rows and the tiny
+// Linears of the overdispersion side (H, R, C of a few units).  As GEMMs they cost a split-K
+// launch of mostly idle 64 x 64 MFMA tiles plus a reduce (~20 us each, ~15 of them per step);
+// here a column-parallel two-phase sum (fixed order: rows in RS splits, then the splits) and
+// a thread-per-output kernel.
+static constexpr int RS_SMALL = 16;  // row splits of k_w_redsmall
+// ws[s][j] = sum over split s's rows m of Y[m][j / KX] * (X ? X[m][j % KX] : 1)   (j < NJ)
+__global__ __launch_bounds__(256) void k_w_redsmall(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X,
+                                                    int64_t ldx, int KX, int M, int NJ, float* __restrict__ ws) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + lane;
+    const int per = (M + RS_SMALL - 1) / RS_SMALL;
+    const int m0 = blockIdx.y * per, m1 = min(M, m0 + per);
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (j < NJ) {
+        const int n = X ? j / KX : j, k = X ? j % KX : 0;
+        int m = m0 + w;
+        for (; m + 12 < m1; m += 16) {  // four rows in flight per lane
+            float y[4], xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                y[u] = Y[(int64_t)(m + 4 * u) * ldy + n];
+                xv[u] = X ? X[(int64_t)(m + 4 * u) * ldx + k] : 1.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] = fmaf(y[u], xv[u], s[u]);
+        }
+        for (; m < m1; m += 4) s[0] = fmaf(Y[(int64_t)m * ldy + n], X ? X[(int64_t)m * ldx + k] : 1.f, s[0]);
+    }
+    part[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (w == 0 && j < NJ) ws[(int64_t)blockIdx.y * NJ + j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+}
+// out[j] = alpha * sum_s ws[s][j]  (+ out[j])
+__global__ __launch_bounds__(256) void k_w_redsmall_fin(int NJ, float alpha, int accumulate, const float* __restrict__ ws,
+                                                        float* __restrict__ out) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= NJ) return;
+    float v = 0.f;
+#pragma unroll 4
+    for (int s = 0; s < RS_SMALL; ++s) v += ws[(int64_t)s * NJ + j];
+    v *= alpha;
+    out[j] = accumulate ? out[j] + v : v;
+}
+static hipError_t redsmall(Engine* e, int M, int N, const float* Y, int64_t ldy, const float* X, int64_t ldx, int KX,
+                           float* out, float alpha, int accumulate) {
+    const int NJ = N * (X ? KX : 1);
+    hipLaunchKernelGGL(k_w_redsmall, dim3((NJ + 63) / 64, RS_SMALL), dim3(256), 0, e->stream, Y, ldy, X, ldx, KX, M, NJ,
+                       e->wide_st->ws);
+    hipLaunchKernelGGL(k_w_redsmall_fin, dim3((NJ + 255) / 256), dim3(256), 0, e->stream, NJ, alpha, accumulate,
+                       (const float*)e->wide_st->ws, out);
+    return hipGetLastError();
+}
+// C[m][n] = act(alpha sum_k A[m][k] B[k][n] + biases) (+ C), one thread per output: K <= 16 and N <= 256
+__global__ __launch_bounds__(256) void k_w_lin_small(GemmOp g) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)g.M * g.N) return;
+    const int m = (int)(i / g.N), n = (int)(i % g.N);
+    float acc = 0.f;
+    for (int k = 0; k < g.K; ++k) acc = fmaf(g.A[(int64_t)m * g.sam + (int64_t)k * g.sak], g.B[(int64_t)k * g.sbk + (int64_t)n * g.sbn], acc);
+    gemm_epilogue(g, m, n, acc);
+}
+
 static hipError_t gemm(Engine* e, const GemmOp& g, const GemmX* x = nullptr) {
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
+    if (!x && g.K <= 16 && g.N <= 256 && g.nc == 0) {
+        hipLaunchKernelGGL(k_w_lin_small, dim3((unsigned)(((int64_t)g.M * g.N + 255) / 256)), dim3(256), 0, e->stream, g);
+        return hipGetLastError();
+    }
     WideState* w = e->wide_st;
     const int64_t MN = (int64_t)g.M * g.N;
     if (x || use_mf(e, g)) {
@@ -515,6 +583,8 @@ static hipError_t linear_dx(Engine* e, int M, int N, int K, const float* dY, int
 // dW[N][K] = dY[M][N]^T . X[M][K]  (a Linear's weight gradient over the batch rows)
 static hipError_t linear_dw(Engine* e, int M, int N, int K, const float* dY, int64_t ldy, const float* X, int64_t ldx,
                             float* dW) {
+    if ((int64_t)N * K <= 4096 && (N < 32 || K < 32))  // a few hundred dot products over the rows
+        return redsmall(e, M, N, dY, ldy, X, ldx, K, dW, 1.f, 0);
     GemmOp g;
     g.M = N; g.N = K; g.K = M;
     g.A = dY; g.sam = 1; g.sak = ldy;
@@ -523,15 +593,11 @@ static hipError_t linear_dw(Engine* e, int M, int N, int K, const float* dY, int
     return gemm(e, g);
 }
 // out[n] = sign * sum_{m < M} Y[m][n]  (column sums, fixed order)
+static hipError_t redsmall(Engine* e, int M, int N, const float* Y, int64_t ldy, const float* X, int64_t ldx, int KX,
+                           float* out, float alpha, int accumulate);
 static hipError_t colsum(Engine* e, int M, int N, const float* Y, int64_t ldy, float* out, float sign = 1.f,
                          int accumulate = 0) {
-    GemmOp g;
-    g.M = 1; g.N = N; g.K = M;
-    g.A = e->wide_st->one; g.sam = 0; g.sak = 0;
-    g.B = Y; g.sbk = ldy; g.sbn = 1;
-    g.C = out; g.scm = 0; g.scn = 1;
-    g.alpha = sign; g.accumulate = accumulate;
-    return gemm(e, g);
+    return redsmall(e, M, N, Y, ldy, nullptr, 0, 1, out, sign, accumulate);
 }
 
 // =======================================================================================
@@ -1126,6 +1192,7 @@ MMVAE_DEV float block_sum512(float v, float* red) {
     __syncthreads();
     return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
 }
+static constexpr int RCH = 5;  // float4 loads in flight per thread in the row sweeps
 __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
     extern __shared__ __attribute__((aligned(16))) float prow[];  // [D]
     __shared__ float red[8], red2[8], ftab[9];
@@ -1137,15 +1204,26 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
         for (int i = 2; i <= (int)threadIdx.x; ++i) f *= (float)i;
         ftab[threadIdx.x] = f;
     }
-    // sweep 1: the logits into LDS (log2 units), online max / sum-exp
+    // sweep 1: the logits into LDS (log2 units), online max / sum-exp.  Every sweep over the row
+    // issues RCH float4 loads per thread before it uses any (one memory latency per RCH of them,
+    // not one per float4)
     float m = -1e30f, s = 0.f;
-    for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
-        const float4 v = *reinterpret_cast<const float4*>(a.LG + o + g);
-        const float v0 = v.x * L2E, v1 = v.y * L2E, v2 = v.z * L2E, v3 = v.w * L2E;
-        *reinterpret_cast<float4*>(prow + g) = float4{v0, v1, v2, v3};
-        const float mn = fmaxf(m, fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
-        s = s * fexp2(m - mn) + ((fexp2(v0 - mn) + fexp2(v1 - mn)) + (fexp2(v2 - mn) + fexp2(v3 - mn)));
-        m = mn;
+    for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
+        float4 vv[RCH];
+#pragma unroll
+        for (int j = 0; j < RCH; ++j)
+            if (g0 + 2048 * j < a.D) vv[j] = *reinterpret_cast<const float4*>(a.LG + o + g0 + 2048 * j);
+#pragma unroll
+        for (int j = 0; j < RCH; ++j) {
+            const int g = g0 + 2048 * j;
+            if (g >= a.D) break;
+            const float4 v = vv[j];
+            const float v0 = v.x * L2E, v1 = v.y * L2E, v2 = v.z * L2E, v3 = v.w * L2E;
+            *reinterpret_cast<float4*>(prow + g) = float4{v0, v1, v2, v3};
+            const float mn = fmaxf(m, fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)));
+            s = s * fexp2(m - mn) + ((fexp2(v0 - mn) + fexp2(v1 - mn)) + (fexp2(v2 - mn) + fexp2(v3 - mn)));
+            m = mn;
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1191,7 +1269,55 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
             for (int r = 0; r < RMAX; ++r)
                 if (r < a.R) dz[r] = fmaf(q.du, a.Wnd[(int64_t)gg * a.R + r], dz[r]);
     };
-    // sweep 2: p (kept in LDS) and every gene's terms at x = 0 (branch free); U and G stored
+    // sweep 2: p (kept in LDS) and every gene's terms at x = 0 (branch free); U and G stored.
+    // With one overdispersion latent (R = 1, u inline) the gene vectors u needs (bnd, nu_bias,
+    // Wnd) are loaded RCH float4s at a time ahead of the math, as the logits are
+    auto elem4 = [&](int g, float4 uv, float4 wv) {
+        float4 lv = *reinterpret_cast<const float4*>(prow + g);
+        float* pl = reinterpret_cast<float*>(&lv);
+        const float* ul = reinterpret_cast<const float*>(&uv);
+        const float* wl = reinterpret_cast<const float*>(&wv);
+        float dus[4], gps[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float p = fexp2(pl[j] - lse2);
+            pl[j] = p;
+            const NbElem q = nb_elem(p, ul[j], d, a.inv_n);
+            lsum += q.ll;
+            S += q.gp;
+            dd += q.pg;
+            dz[0] = fmaf(q.du, wl[j], dz[0]);
+            gps[j] = q.gp;
+            dus[j] = q.du;
+        }
+        *reinterpret_cast<float4*>(prow + g) = lv;
+        if (a.with_grads) {
+            *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
+            *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+        }
+    };
+    if (a.Zn && a.R == 1) {
+        for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
+            float4 bv[RCH], nv[RCH], wv[RCH];
+#pragma unroll
+            for (int j = 0; j < RCH; ++j) {
+                const int g = g0 + 2048 * j;
+                if (g < a.D) {  // (the registered gene vectors need not be 16-byte aligned)
+                    bv[j] = float4{a.bnd[g], a.bnd[g + 1], a.bnd[g + 2], a.bnd[g + 3]};
+                    nv[j] = float4{a.nu_bias[g], a.nu_bias[g + 1], a.nu_bias[g + 2], a.nu_bias[g + 3]};
+                    wv[j] = float4{a.Wnd[g], a.Wnd[g + 1], a.Wnd[g + 2], a.Wnd[g + 3]};
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < RCH; ++j) {
+                const int g = g0 + 2048 * j;
+                if (g >= a.D) break;
+                const float4 uv = float4{fmaf(zn[0], wv[j].x, bv[j].x - nv[j].x), fmaf(zn[0], wv[j].y, bv[j].y - nv[j].y),
+                                         fmaf(zn[0], wv[j].z, bv[j].z - nv[j].z), fmaf(zn[0], wv[j].w, bv[j].w - nv[j].w)};
+                elem4(g, uv, wv[j]);
+            }
+        }
+    } else {
     for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
         float4 lv = *reinterpret_cast<const float4*>(prow + g);
         float* pl = reinterpret_cast<float*>(&lv);
@@ -1210,6 +1336,7 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
             *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
             *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
         }
+    }
     }
     // the row's nonzeros (CSR, each gene at most once): their count-dependent terms onto the
     // x = 0 values (the barrier orders the block's stores and LDS p before these reads), with
@@ -1258,14 +1385,23 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
             if (threadIdx.x == 0) a.dZn[(int64_t)b * a.R + r] = v;
         }
     // sweep 3: G = (G - p S) / n (each thread re-reads the G it stored: no barrier needed)
-    for (int g = 4 * threadIdx.x; g < a.D; g += 2048) {
-        const float4 pv = *reinterpret_cast<const float4*>(prow + g);
-        float4 gv = *reinterpret_cast<const float4*>(a.G + o + g);
-        gv.x = a.inv_n * fmaf(-pv.x, S, gv.x);
-        gv.y = a.inv_n * fmaf(-pv.y, S, gv.y);
-        gv.z = a.inv_n * fmaf(-pv.z, S, gv.z);
-        gv.w = a.inv_n * fmaf(-pv.w, S, gv.w);
-        *reinterpret_cast<float4*>(a.G + o + g) = gv;
+    for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
+        float4 gvv[RCH];
+#pragma unroll
+        for (int j = 0; j < RCH; ++j)
+            if (g0 + 2048 * j < a.D) gvv[j] = *reinterpret_cast<const float4*>(a.G + o + g0 + 2048 * j);
+#pragma unroll
+        for (int j = 0; j < RCH; ++j) {
+            const int g = g0 + 2048 * j;
+            if (g >= a.D) break;
+            const float4 pv = *reinterpret_cast<const float4*>(prow + g);
+            float4 gv = gvv[j];
+            gv.x = a.inv_n * fmaf(-pv.x, S, gv.x);
+            gv.y = a.inv_n * fmaf(-pv.y, S, gv.y);
+            gv.z = a.inv_n * fmaf(-pv.z, S, gv.z);
+            gv.w = a.inv_n * fmaf(-pv.w, S, gv.w);
+            *reinterpret_cast<float4*>(a.G + o + g) = gv;
+        }
     }
 }
 
