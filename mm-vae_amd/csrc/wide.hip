@@ -289,19 +289,39 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
     const int nch = (g.K + 31) / 32;
     const int c0 = blockIdx.z * cps, c1 = min(nch, c0 + cps);
     float4 va[2], vb[NB][2];
+    // AT: the transform's per-k vectors ride with the chunk's loads; the transform itself runs when
+    // the chunk is stored into LDS, so the next chunk's loads stay in flight under this chunk's
+    // MFMAs (applied inside load(), it made every chunk wait for its own loads: 263 us -> see
+    // DESIGN.md §4b round 5)
+    float xmv[4], isv[4], rsv[2];
+    int ktr = 0;
     auto load = [&](int ch) {
         Op::template load<AKF>(g.A, g.sam, g.sak, m0, g.M, ch * 32, g.K, vec != 0, va);
 #pragma unroll
         for (int h = 0; h < NB; ++h) Op::template load<BKF>(g.B, g.sbn, g.sbk, n0 + 64 * h, g.N, ch * 32, g.K, vec != 0, vb[h]);
-        if constexpr (AT) {  // the encoder input transform; k past K stays 0
+        if constexpr (AT) {
             const int t = threadIdx.x;
+            ktr = ch * 32 + (t & 7) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = min(ktr + j, g.K - 1);
+                xmv[j] = x.xm[k];
+                isv[j] = x.isd[k];
+            }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int r = m0 + (t >> 3) + 32 * i, k = ch * 32 + (t & 7) * 4;
-                const float rs = (x.rs && r < g.M) ? x.rs[r] : 1.f;
+                const int r = m0 + (t >> 3) + 32 * i;
+                rsv[i] = (x.rs && r < g.M) ? x.rs[r] : 1.f;
+            }
+        }
+    };
+    auto transform = [&]() {  // the encoder input transform; k past K stays 0
+        if constexpr (AT) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
                 float* e = reinterpret_cast<float*>(&va[i]);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) e[j] = (k + j < g.K) ? enc_in(e[j], rs, x.xm[k + j], x.isd[k + j]) : 0.f;
+                for (int j = 0; j < 4; ++j) e[j] = (ktr + j < g.K) ? enc_in(e[j], rsv[i], xmv[j], isv[j]) : 0.f;
             }
         }
     };
@@ -315,6 +335,7 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
     for (int ch = c0; ch < c1; ++ch) {
         const int buf = (ch - c0) & 1;
         // buffer buf was last read two chunks ago, before the previous chunk's barrier
+        transform();
         Op::template store<AKF>(lds[buf][0], PL, va);
 #pragma unroll
         for (int h = 0; h < NB; ++h) Op::template store<BKF>(lds[buf][1 + h], PL, vb[h]);
@@ -367,6 +388,21 @@ struct WLayer {
     float* act = nullptr;      // [Bpad][out] the layer's output (post-ReLU)
 };
 
+// a queued narrow column sum of the wide path (k_w_redsmall below)
+struct RedJob {
+    const float* Y;
+    const float* X;
+    float* out;
+    int64_t ldy, ldx, wsoff;
+    int KX, NJ, accumulate;
+    float alpha;
+};
+static constexpr int RJ_MAX = 12;
+struct RedJobs {
+    int n = 0, M = 0, maxnj = 0;
+    int64_t wsuse = 0;
+    RedJob j[RJ_MAX];
+};
 struct WideState {
     int64_t Bp = 0, D = 0;
     // dense [Bpad][D] blocks: the raw batch, logits, their gradient, the nu pre-activation /
@@ -399,6 +435,7 @@ struct WideState {
     std::vector<WLayer> enc, dec;  // dec: hidden layers, then the final big layer (-> D)
     float* wtil = nullptr;         // vMF: normalised Angular weights of every encoder layer
     float* lossv = nullptr;        // [2]: scratch sums
+    struct RedJobs redq;           // narrow column sums queued for one launch (red_flush)
 };
 
 static hipError_t walloc(float** p, int64_t n) { return hipMalloc(p, sizeof(float) * (size_t)(n > 0 ? n : 1)); }
@@ -460,54 +497,53 @@ static bool use_mf(const Engine* e, const GemmOp& g) {
 // here a column-parallel two-phase sum (fixed order: rows in RS splits, then the splits) and
 // a thread-per-output kernel.
 static constexpr int RS_SMALL = 16;  // row splits of k_w_redsmall
-// ws[s][j] = sum over split s's rows m of Y[m][j / KX] * (X ? X[m][j % KX] : 1)   (j < NJ)
-__global__ __launch_bounds__(256) void k_w_redsmall(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X,
-                                                    int64_t ldx, int KX, int M, int NJ, float* __restrict__ ws) {
+// A batch of such sums (RedJobs, one launch per phase): job z's ws[s][j] = sum over split s's
+// rows m of Y[m][j / KX] * (X ? X[m][j % KX] : 1)  (j < NJ), then out[j] = alpha sum_s ws[s][j]
+__global__ __launch_bounds__(256) void k_w_redsmall(RedJobs q, float* __restrict__ ws) {
     __shared__ float part[4][64];
+    const RedJob& jb = q.j[blockIdx.z];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j = blockIdx.x * 64 + lane;
-    const int per = (M + RS_SMALL - 1) / RS_SMALL;
+    if ((int)blockIdx.x * 64 >= jb.NJ) return;  // (workgroup-uniform)
+    const int M = q.M, per = (M + RS_SMALL - 1) / RS_SMALL;
     const int m0 = blockIdx.y * per, m1 = min(M, m0 + per);
+    const float* Y = jb.Y;
+    const float* X = jb.X;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    if (j < NJ) {
-        const int n = X ? j / KX : j, k = X ? j % KX : 0;
+    if (j < jb.NJ) {
+        const int n = X ? j / jb.KX : j, k = X ? j % jb.KX : 0;
         int m = m0 + w;
         for (; m + 12 < m1; m += 16) {  // four rows in flight per lane
             float y[4], xv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                y[u] = Y[(int64_t)(m + 4 * u) * ldy + n];
-                xv[u] = X ? X[(int64_t)(m + 4 * u) * ldx + k] : 1.f;
+                y[u] = Y[(int64_t)(m + 4 * u) * jb.ldy + n];
+                xv[u] = X ? X[(int64_t)(m + 4 * u) * jb.ldx + k] : 1.f;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) s[u] = fmaf(y[u], xv[u], s[u]);
         }
-        for (; m < m1; m += 4) s[0] = fmaf(Y[(int64_t)m * ldy + n], X ? X[(int64_t)m * ldx + k] : 1.f, s[0]);
+        for (; m < m1; m += 4) s[0] = fmaf(Y[(int64_t)m * jb.ldy + n], X ? X[(int64_t)m * jb.ldx + k] : 1.f, s[0]);
     }
     part[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
     __syncthreads();
-    if (w == 0 && j < NJ) ws[(int64_t)blockIdx.y * NJ + j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (w == 0 && j < jb.NJ)
+        ws[jb.wsoff + (int64_t)blockIdx.y * jb.NJ + j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
-// out[j] = alpha * sum_s ws[s][j]  (+ out[j])
-__global__ __launch_bounds__(256) void k_w_redsmall_fin(int NJ, float alpha, int accumulate, const float* __restrict__ ws,
-                                                        float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_w_redsmall_fin(RedJobs q, const float* __restrict__ ws) {
+    const RedJob& jb = q.j[blockIdx.z];
     const int j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= NJ) return;
+    if (j >= jb.NJ) return;
     float v = 0.f;
 #pragma unroll 4
-    for (int s = 0; s < RS_SMALL; ++s) v += ws[(int64_t)s * NJ + j];
-    v *= alpha;
-    out[j] = accumulate ? out[j] + v : v;
+    for (int s = 0; s < RS_SMALL; ++s) v += ws[jb.wsoff + (int64_t)s * jb.NJ + j];
+    v *= jb.alpha;
+    jb.out[j] = jb.accumulate ? jb.out[j] + v : v;
 }
+static hipError_t red_flush(Engine* e);
 static hipError_t redsmall(Engine* e, int M, int N, const float* Y, int64_t ldy, const float* X, int64_t ldx, int KX,
-                           float* out, float alpha, int accumulate) {
-    const int NJ = N * (X ? KX : 1);
-    hipLaunchKernelGGL(k_w_redsmall, dim3((NJ + 63) / 64, RS_SMALL), dim3(256), 0, e->stream, Y, ldy, X, ldx, KX, M, NJ,
-                       e->wide_st->ws);
-    hipLaunchKernelGGL(k_w_redsmall_fin, dim3((NJ + 255) / 256), dim3(256), 0, e->stream, NJ, alpha, accumulate,
-                       (const float*)e->wide_st->ws, out);
-    return hipGetLastError();
-}
+                           float* out, float alpha, int accumulate);
+
 // C[m][n] = act(alpha sum_k A[m][k] B[k][n] + biases) (+ C), one thread per output: K <= 16 and N <= 256
 __global__ __launch_bounds__(256) void k_w_lin_small(GemmOp g) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -593,8 +629,40 @@ static hipError_t linear_dw(Engine* e, int M, int N, int K, const float* dY, int
     return gemm(e, g);
 }
 // out[n] = sign * sum_{m < M} Y[m][n]  (column sums, fixed order)
+// queue one narrow sum; red_flush launches the queued group (two launches for all of them)
 static hipError_t redsmall(Engine* e, int M, int N, const float* Y, int64_t ldy, const float* X, int64_t ldx, int KX,
-                           float* out, float alpha, int accumulate);
+                           float* out, float alpha, int accumulate) {
+    RedJobs& q = e->wide_st->redq;
+    const int NJ = N * (X ? KX : 1);
+    if (q.n == RJ_MAX || (q.n > 0 && q.M != M) || q.wsuse + (int64_t)RS_SMALL * NJ > e->wide_st->ws_cap) {
+        const hipError_t er = red_flush(e);
+        if (er != hipSuccess) return er;
+    }
+    RedJob& jb = q.j[q.n++];
+    jb.Y = Y;
+    jb.X = X;
+    jb.out = out;
+    jb.ldy = ldy;
+    jb.ldx = ldx;
+    jb.KX = KX;
+    jb.NJ = NJ;
+    jb.alpha = alpha;
+    jb.accumulate = accumulate;
+    jb.wsoff = q.wsuse;
+    q.wsuse += (int64_t)RS_SMALL * NJ;
+    q.M = M;
+    q.maxnj = std::max(q.maxnj, NJ);
+    return hipSuccess;
+}
+static hipError_t red_flush(Engine* e) {
+    RedJobs& q = e->wide_st->redq;
+    if (q.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_w_redsmall, dim3((q.maxnj + 63) / 64, RS_SMALL, q.n), dim3(256), 0, e->stream, q, e->wide_st->ws);
+    hipLaunchKernelGGL(k_w_redsmall_fin, dim3((q.maxnj + 255) / 256, 1, q.n), dim3(256), 0, e->stream, q,
+                       (const float*)e->wide_st->ws);
+    q = RedJobs{};
+    return hipGetLastError();
+}
 static hipError_t colsum(Engine* e, int M, int N, const float* Y, int64_t ldy, float* out, float sign = 1.f,
                          int accumulate = 0) {
     return redsmall(e, M, N, Y, ldy, nullptr, 0, 1, out, sign, accumulate);
@@ -1967,6 +2035,7 @@ static hipError_t heads_bwd(Engine* e, int B, const float* h, const std::string&
     WCHK(colsum(e, B, K, w->dA, K, e->greg(wl + ".bias")));
     WCHK(linear_dw(e, B, K, C, w->dM, K, w->Cb, C, e->greg("covar_encoding.weight")));
     WCHK(colsum(e, B, K, w->dM, K, e->greg("covar_encoding.bias")));
+    WCHK(red_flush(e));  // (the group's sums in two launches)
     WCHK(linear_dx(e, B, K, E, w->dM, K, e->preg(wm + ".weight"), w->dT0, E));
     WCHK(linear_dx(e, B, K, E, w->dA, K, e->preg(wl + ".weight"), w->dT0, E, 1));
     return hipSuccess;
@@ -2107,6 +2176,7 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     }
     WCHK(colsum(e, B, 1, r_ddpre, 1, e->greg("depth.bias")));
     WCHK(colsum(e, B, H, w->dHn, H, e->greg("nu_encoding.bias")));
+    WCHK(red_flush(e));
     // encoder chain -> dXn (into G: the decoder's gradient block is consumed), x_mean / ln_x_sd
     WCHK(enc_backward(e, B, w->G));
     {
