@@ -165,12 +165,6 @@ def roofline(model, dtype, D, K, B, nnz_per_cell, per_kernel):
     """The dominant kernel against SURVEY §8(d)'s bound: Q quarter-rate VALU ops per (cell,
     gene) at P_q; its HBM and MFMA fractions beside."""
     dom, fpe = DOMINANT[model]
-    if dom not in per_kernel:  # the wide path: one timed region, the algorithmic GEMM flops on the f32 MFMA
-        t = per_kernel["wide_step"] * 1e-3
-        flops = 8.0 * D * K * B
-        return {"bound": "mfma", "kernel": "wide_step", "kernel_ms": round(t * 1e3, 4),
-                "achieved": round(flops / t / 1e12, 3), "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-                "frac": round(flops / t / PEAK_F32_MFMA, 4), "traffic": None}
     t = per_kernel[dom] * 1e-3
     q_ops = float(Q_PER_ELEM[model]) * B * D
     esz = {"bf16": 2, "bf16x3": 4, "f32": 4, "fp8": 2}[dtype]
@@ -375,8 +369,43 @@ def secondary(mmvae_amd, model, D, K, B, dtype, cells, lib, steps=50, warmup=5, 
         pk, _ = kernel_times(eng, batches, 1.0, B, 0, 5)
         out["dominant_kernel_ms"] = round(pk[DOMINANT[model][0]], 4)
         out["roofline_frac"] = roofline(model, dtype, D, K, B, nnz / cells, pk)["frac"]
+    else:
+        out.update(wide_roofline(eng, batches, B, D, K, dtype, dt / steps))
     eng.close()
     return out
+
+
+def wide_roofline(eng, batches, B, D, K, dtype, t_step, steps=5):
+    """The wide path (dense [B, D] blocks in HBM, generic GEMMs): per-kernel ms per step (HIP events
+    around its launch groups) and two bounds.  MFMA: the four gene GEMMs of the reference's op
+    sequence (encoder forward, logits, dz, the encoder input gradient), 8 B D K algorithmic flops a
+    step, issued MFMA_PASSES times on the bf16 MFMA (x3: three products) — against their own time
+    and against the step.  HBM: the dense blocks the path moves, 15 passes of 4 B D bytes a step
+    (densify write; encoder read; logits write; row kernel read + U, G writes + G rewrite; the column
+    reductions' reads of G, U and X twice; dz GEMM read; the encoder input gradient write)."""
+    eng.timing(True)
+    eng.timing_reset()
+    for s in range(steps):
+        eng.run(batches[s % len(batches)], 1.0, update=True, n_total=B, step_id=s, sync=False)
+    eng.sync()
+    tm = eng.timings()
+    eng.timing(False)
+    per_step = {k: v[0] / steps for k, v in tm.items()}
+    flops = 8.0 * B * D * K
+    issued = flops * MFMA_PASSES[dtype]
+    peak = PEAK_F32_MFMA if dtype == "f32" else PEAK_BF16
+    t_gemm = per_step.get("w_gemm_gene", 0.0) * 1e-3
+    dense_bytes = 15.0 * 4 * B * D
+    return {"kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per_step.items(), key=lambda kv: -kv[1])},
+            "roofline": {"bound": "mfma", "kernel": "w_gemm_gene (4 gene GEMMs)",
+                         "achieved": round(issued / t_gemm / 1e12, 2) if t_gemm else None,
+                         "peak": peak / 1e12, "unit": "issued TFLOP/s",
+                         "frac": round(issued / t_gemm / peak, 4) if t_gemm else None,
+                         "step_frac": round(issued / t_step / peak, 4),
+                         "hbm": {"dense_bytes_per_step": dense_bytes,
+                                 "achieved_gbs": round(dense_bytes / t_step / 1e9, 1),
+                                 "frac": round(dense_bytes / t_step / PEAK_HBM, 4)}},
+            "roofline_frac": round(issued / t_gemm / peak, 4) if t_gemm else None}
 
 
 def dp_exchange(mmvae_amd, D, K, B, dtype, cells, lib, steps=300, warmup=20):
@@ -481,6 +510,8 @@ def main():
     gst = eng.graph_stats()  # replays > 0: the timed steps ran as step graphs (RCCL buckets included)
     per_kernel, step_dev_ms = kernel_times(eng, batches, beta, n_total, rank * B, args.kernel_steps)
     loss, _ = eng.run(batches[0], beta, update=False, n_total=n_total, row_offset=rank * B, step_id=0)
+    # the wide path's per-launch-group timings run steps too: every rank takes part (collectives)
+    wide_rf = wide_roofline(eng, batches, B, D, K, args.dtype, dt / args.steps) if eng.path() == "wide" else None
 
     if rank != 0:
         if world > 1:
@@ -516,10 +547,12 @@ def main():
                    "nnz_per_cell": round(npc, 1), "parallelism": f"dp{world}",
                    "step_graph": gst["replays"] > 0 and not args.no_graph,
                    "graph_stats": gst},
-        "roofline": roofline(args.model, args.dtype, D, K, B, npc, per_kernel),
+        "roofline": (roofline(args.model, args.dtype, D, K, B, npc, per_kernel) if eng.path() == "fused" else
+                     wide_rf["roofline"]),
         "composite": composite(args.model, args.dtype, D, K, B, npc, P_reg, ms),
         "device_ms_per_step": round(step_dev_ms, 4),
-        "kernel_ms": {k: round(v, 4) for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1])},
+        "kernel_ms": ({k: round(v, 4) for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1])} if wide_rf is None
+                      else wide_rf["kernel_ms_per_step"]),
         "eval_loss": loss,
         "setup_s": round(t_setup, 2),
     }

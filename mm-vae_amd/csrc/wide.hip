@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -35,6 +36,11 @@ namespace mmvae {
 // Generic GEMM: C(m, n) [+]= act(alpha * sum_k A(m, k) B(k, n) + bias[n])
 //   A(m, k) = A[m * sam + k * sak], B(k, n) = B[k * sbk + n * sbn], C(m, n) = C[m * scm + n * scn]
 // =======================================================================================
+struct GemmX {
+    const float* xm = nullptr;   // x_mean [K]
+    const float* isd = nullptr;  // 1 / (softplus(ln_x_sd) + eps) [K]
+    const float* rs = nullptr;   // per-row scale of log1p(x) (vMF: 1 / |log1p(x_b)|), null: 1
+};
 struct GemmOp {
     int M = 0, N = 0, K = 0;
     const float* A = nullptr;
@@ -55,6 +61,14 @@ struct GemmOp {
     int nc = 0;
     int act = 0;                  // 1: ReLU
     int accumulate = 0;           // C += result
+    // the column-sum epilogue (k_gemm_mf, one split): C is not stored; per 64-row tile mt,
+    // cpart[(mt * 2 + 0) * N + n] = sum_m C(m, n) and [(mt * 2 + 1) * N + n] =
+    // sum_m C(m, n) enc_in(cx(m, n)) with cxf's transform — the x_mean / ln_x_sd sums over the
+    // encoder's input gradient straight from its GEMM (k_colred's XPROD pair, chunks = row tiles)
+    float* cpart = nullptr;
+    const float* cx = nullptr;
+    int64_t ldcx = 0;
+    GemmX cxf;
 };
 
 static constexpr int GT = 64, GK = 16, GLD = GT + 4;
@@ -180,11 +194,6 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmOp g, int S, const floa
 // loaded, A(m, k) = (log1p(x) rs[m] - x_mean[k]) / sd[k] from the raw dense batch x, so the
 // normalised input block is never stored.
 // =======================================================================================
-struct GemmX {
-    const float* xm = nullptr;   // x_mean [K]
-    const float* isd = nullptr;  // 1 / (softplus(ln_x_sd) + eps) [K]
-    const float* rs = nullptr;   // per-row scale of log1p(x) (vMF: 1 / |log1p(x_b)|), null: 1
-};
 
 MMVAE_DEV float enc_in(float v, float rs, float xm, float isd) { return (log1p_pos(v) * rs - xm) * isd; }
 // the same with libm log1pf (the f32 handles' input block, the ln_x_sd gradient's column sum)
@@ -200,40 +209,36 @@ template <class P>
 struct MfOperand {
     static constexpr bool X = IsX3<P>::value;
     // one 64-row x 32-k slice: KF (k contiguous in HBM) -> image [64][32] (64-byte rows);
-    // otherwise -> image [32][64] (128-byte rows); four f32 per thread per half
+    // otherwise -> image [32][64] (128-byte rows); four f32 per thread per half.  Every load is
+    // issued (indices clamped into the operand, out-of-range values zeroed after the load): the
+    // count of loads in flight is then static and the compiler's waits let the next chunks'
+    // loads stay outstanding (a bounds branch around a load made it wait for all of them).
+    // The host routes here only float4-aligned operands whose contiguous extent is a multiple of 4.
     template <bool KF>
-    static MMVAE_DEV void load(const float* base, int64_t srow, int64_t sk, int r0, int nrow, int k0, int K, bool vec,
+    static MMVAE_DEV void load(const float* base, int64_t srow, int64_t sk, int r0, int nrow, int k0, int K,
                                float4 (&v)[2]) {
         const int t = threadIdx.x;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            int r, k;
+            bool ok;
+            int64_t o;
             if constexpr (KF) {
-                const int r = (t >> 3) + 32 * i, k = k0 + (t & 7) * 4;
-                const int64_t o = (int64_t)(r0 + r) * srow + k;
-                if (r0 + r >= nrow) {
-                    v[i] = float4{0.f, 0.f, 0.f, 0.f};
-                } else if (vec && k + 3 < K) {
-                    v[i] = *reinterpret_cast<const float4*>(base + o);
-                } else {
-                    v[i].x = k < K ? base[o] : 0.f;
-                    v[i].y = k + 1 < K ? base[o + 1] : 0.f;
-                    v[i].z = k + 2 < K ? base[o + 2] : 0.f;
-                    v[i].w = k + 3 < K ? base[o + 3] : 0.f;
-                }
+                r = r0 + (t >> 3) + 32 * i;
+                k = k0 + (t & 7) * 4;
+                ok = r < nrow && k < K;
+                o = (int64_t)min(r, nrow - 1) * srow + min(k, K - 4);
             } else {
-                const int k = k0 + (t >> 4) + 16 * i, r = r0 + (t & 15) * 4;
-                const int64_t o = (int64_t)k * sk + r;
-                if (k >= K) {
-                    v[i] = float4{0.f, 0.f, 0.f, 0.f};
-                } else if (vec && r + 3 < nrow) {
-                    v[i] = *reinterpret_cast<const float4*>(base + o);
-                } else {
-                    v[i].x = r < nrow ? base[o] : 0.f;
-                    v[i].y = r + 1 < nrow ? base[o + 1] : 0.f;
-                    v[i].z = r + 2 < nrow ? base[o + 2] : 0.f;
-                    v[i].w = r + 3 < nrow ? base[o + 3] : 0.f;
-                }
+                k = k0 + (t >> 4) + 16 * i;
+                r = r0 + (t & 15) * 4;
+                ok = k < K && r < nrow;
+                o = (int64_t)min(k, K - 1) * sk + min(r, nrow - 4);
             }
+            const float4 u = *reinterpret_cast<const float4*>(base + o);
+            v[i].x = ok ? u.x : 0.f;
+            v[i].y = ok ? u.y : 0.f;
+            v[i].z = ok ? u.z : 0.f;
+            v[i].w = ok ? u.w : 0.f;
         }
     }
     // the slice's bf16 planes (hi [, lo at +PL bytes]) into the image
@@ -273,7 +278,30 @@ struct MfOperand {
 
 // NT: 64 or 128 output columns per workgroup (the four waves 32 x NT / 2 each); 128 halves
 // the A re-reads of the K = D GEMMs whose N is the latent width
-template <class P, bool AKF, bool BKF, bool AT, int NT>
+// XCD-aware tile order: blocks b and b + 8 share an XCD (its L2), so block b takes tile
+// xcd * per + b / 8 of the (m fastest, then n, then split) order — an XCD walks the m tiles of
+// its own n tiles / k splits and keeps their B slice in its L2 instead of every XCD cycling
+// through all of B (MI355X_MICROARCH.md, workgroup dispatch; for speed only: any placement
+// computes the same tiles)
+MMVAE_DEV void mf_tile(int& tn, int& tm, int& tz) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int T = gx * gy * (int)gridDim.z;
+    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int c = (T + 7) / 8, r = T % 8, xcd = L % 8, idx = L / 8;
+    const int t = (r == 0 || xcd < r) ? xcd * c + idx : r * c + (xcd - r) * (c - 1) + idx;
+    tm = t % gy;
+    tn = (t / gy) % gx;
+    tz = t / (gy * gx);
+}
+
+// NT: 64 or 128 output columns per workgroup (the four waves 32 x NT / 2 each); 128 halves
+// the A re-reads of the K = D GEMMs whose N is the latent width.  PF: chunks whose loads are in
+// flight in registers.  PF = 2 (the long-K GEMMs: K = D): two register stages, the loop unrolled
+// by two so every register index is static — the chunk being stored into LDS and the next one
+// load under the MFMAs of the current one; PF = 1 (a few chunks, K = a latent / hidden width):
+// one stage, fewer registers and more workgroups per CU (two stages measured 272 -> 336 us on
+// the logit GEMM, 4 chunks).
+template <class P, bool AKF, bool BKF, bool AT, int NT, int PF>
 __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, float* __restrict__ ws, int vec) {
     static_assert(!AT || AKF, "the input transform follows the k-contiguous slice layout");
     using M = MM<P>;
@@ -285,43 +313,37 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
     constexpr int WJ = NT / 32;             // 16-column blocks per wave
     __shared__ __attribute__((aligned(16))) char lds[2][1 + NB][IMG];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * NT;
+    int btn, btm, btz;
+    if (vec & 2) mf_tile(btn, btm, btz);
+    else btn = blockIdx.x, btm = blockIdx.y, btz = blockIdx.z;
+    const int m0 = btm * 64, n0 = btn * NT;
     const int nch = (g.K + 31) / 32;
-    const int c0 = blockIdx.z * cps, c1 = min(nch, c0 + cps);
-    float4 va[2], vb[NB][2];
+    const int c0 = btz * cps, c1 = min(nch, c0 + cps);
+    float4 va[PF][2], vb[PF][NB][2];
     // AT: the transform's per-k vectors ride with the chunk's loads; the transform itself runs when
     // the chunk is stored into LDS, so the next chunk's loads stay in flight under this chunk's
     // MFMAs (applied inside load(), it made every chunk wait for its own loads: 263 us -> see
     // DESIGN.md §4b round 5)
-    float xmv[4], isv[4], rsv[2];
-    int ktr = 0;
-    auto load = [&](int ch) {
-        Op::template load<AKF>(g.A, g.sam, g.sak, m0, g.M, ch * 32, g.K, vec != 0, va);
+    float xmv[PF][4], isv[PF][4], rsv[PF][2];
+    int ktr[PF] = {};
+    auto load = [&](auto S, int ch) {
+        constexpr int st = decltype(S)::value;
+        Op::template load<AKF>(g.A, g.sam, g.sak, m0, g.M, ch * 32, g.K, va[st]);
 #pragma unroll
-        for (int h = 0; h < NB; ++h) Op::template load<BKF>(g.B, g.sbn, g.sbk, n0 + 64 * h, g.N, ch * 32, g.K, vec != 0, vb[h]);
+        for (int h = 0; h < NB; ++h) Op::template load<BKF>(g.B, g.sbn, g.sbk, n0 + 64 * h, g.N, ch * 32, g.K, vb[st][h]);
         if constexpr (AT) {
             const int t = threadIdx.x;
-            ktr = ch * 32 + (t & 7) * 4;
+            ktr[st] = ch * 32 + (t & 7) * 4;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int k = min(ktr + j, g.K - 1);
-                xmv[j] = x.xm[k];
-                isv[j] = x.isd[k];
+                const int k = min(ktr[st] + j, g.K - 1);
+                xmv[st][j] = x.xm[k];
+                isv[st][j] = x.isd[k];
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int r = m0 + (t >> 3) + 32 * i;
-                rsv[i] = (x.rs && r < g.M) ? x.rs[r] : 1.f;
-            }
-        }
-    };
-    auto transform = [&]() {  // the encoder input transform; k past K stays 0
-        if constexpr (AT) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                float* e = reinterpret_cast<float*>(&va[i]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) e[j] = (ktr + j < g.K) ? enc_in(e[j], rsv[i], xmv[j], isv[j]) : 0.f;
+                rsv[st][i] = x.rs ? x.rs[min(r, g.M - 1)] : 1.f;  // (x.rs: uniform)
             }
         }
     };
@@ -331,16 +353,32 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (c0 < c1) load(c0);
-    for (int ch = c0; ch < c1; ++ch) {
-        const int buf = (ch - c0) & 1;
-        // buffer buf was last read two chunks ago, before the previous chunk's barrier
-        transform();
-        Op::template store<AKF>(lds[buf][0], PL, va);
+    // chunk ch in register stage / LDS buffer st = (ch - c0) & 1; buffer st was last read two
+    // chunks ago, before the previous chunk's barrier
+    auto chunk = [&](auto S, int buf, int ch) {
+        constexpr int st = decltype(S)::value;
+        if constexpr (AT) {  // the encoder input transform; k past K stays 0
 #pragma unroll
-        for (int h = 0; h < NB; ++h) Op::template store<BKF>(lds[buf][1 + h], PL, vb[h]);
+            for (int i = 0; i < 2; ++i) {
+                float* e = reinterpret_cast<float*>(&va[st][i]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    // (computed on every lane, the clamped k's loads are finite; pinned so the
+                    // select stays a v_cndmask instead of a branch with its own load waits)
+                    float tv = enc_in(e[j], rsv[st][i], xmv[st][j], isv[st][j]);
+                    asm volatile("" : "+v"(tv));
+                    e[j] = (ktr[st] + j < g.K) ? tv : 0.f;
+                }
+            }
+        }
+        Op::template store<AKF>(lds[buf][0], PL, va[st]);
+#pragma unroll
+        for (int h = 0; h < NB; ++h) Op::template store<BKF>(lds[buf][1 + h], PL, vb[st][h]);
         __syncthreads();
-        if (ch + 1 < c1) load(ch + 1);  // in flight under this chunk's MFMAs
+        // in flight under the MFMAs of this chunk (and with PF = 2 the next one).  PF = 2 issues
+        // them unconditionally (past the split's end: its last chunk again, unused) so the loads
+        // in flight are a static count; PF = 1 waits for all of them anyway and skips the spare
+        if (PF == 2 || ch + 1 < c1) load(S, min(ch + PF, c1 - 1));
         typename M::frag fa[2], fb[WJ];
 #pragma unroll
         for (int i = 0; i < 2; ++i) fa[i] = Op::template frag<AKF>(lds[buf][0], PL, wm + 16 * i);
@@ -353,6 +391,66 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < WJ; ++j) acc[i][j] = M::mma(fa[i], fb[j], acc[i][j]);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    load(S0{}, c0);
+    if constexpr (PF == 2) {
+        load(S1{}, min(c0 + 1, max(c1 - 1, c0)));
+        int ch = c0;
+        for (; ch + 1 < c1; ch += 2) {  // (both stages every trip: the waits see one load pattern)
+            chunk(S0{}, 0, ch);
+            chunk(S1{}, 1, ch + 1);
+        }
+        if (ch < c1) chunk(S0{}, 0, ch);
+    } else {
+        for (int ch = c0; ch < c1; ++ch) chunk(S0{}, (ch - c0) & 1, ch);
+    }
+    if (g.cpart) {  // the column-sum epilogue (uniform; the host launches it with one split)
+        __syncthreads();  // every wave's last fragment reads are done: the images are free
+        float* red = reinterpret_cast<float*>(&lds[0][0][0]);  // [row half][2][NT]
+        float xv[WJ][2][4];
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+            const int n = min(n0 + wn + 16 * j + (lane & 15), g.N - 1);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = min(m0 + wm + 16 * i + 4 * (lane >> 4) + r, g.M - 1);
+                    xv[j][i][r] = g.cx[(int64_t)m * g.ldcx + n];
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+            const int n = n0 + wn + 16 * j + (lane & 15), nn = min(n, g.N - 1);
+            const float xm = g.cxf.xm[nn], isd = g.cxf.isd[nn];
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+                    const float rs = g.cxf.rs ? g.cxf.rs[min(m, g.M - 1)] : 1.f;
+                    const float v = (m < g.M && n < g.N) ? acc[i][j][r] : 0.f;
+                    s0 += v;
+                    s1 = fmaf(v, enc_in_acc(xv[j][i][r], rs, xm, isd), s1);
+                }
+            s0 += __shfl_xor(s0, 16, 64);
+            s1 += __shfl_xor(s1, 16, 64);
+            s0 += __shfl_xor(s0, 32, 64);
+            s1 += __shfl_xor(s1, 32, 64);
+            if (lane < 16) {
+                red[((w >> 1) * 2 + 0) * NT + wn + 16 * j + lane] = s0;
+                red[((w >> 1) * 2 + 1) * NT + wn + 16 * j + lane] = s1;
+            }
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < 2 * NT; t += 256) {
+            const int q = t / NT, c = t % NT, n = n0 + c;
+            if (n < g.N) g.cpart[((int64_t)btm * 2 + q) * g.N + n] = red[q * NT + c] + red[(2 + q) * NT + c];
+        }
+        return;
     }
     const bool split = gridDim.z > 1;
 #pragma unroll
@@ -370,7 +468,7 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
             for (int r = 0; r < 4; ++r) {
                 const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
                 if (m >= g.M) continue;
-                if (split) ws[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+                if (split) ws[((int64_t)btz * g.M + m) * g.N + n] = acc[i][j][r];
                 else gemm_store(g, m, n, acc[i][j][r], colc, cwn);
             }
     }
@@ -459,33 +557,65 @@ static void launch_reduce(Engine* e, const GemmOp& g, int S) {
     hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, e->stream, g, S, (const float*)e->wide_st->ws);
 }
 
-template <class P, bool AT, int NT>
+template <class P, bool AT, int NT, int PF>
 static void launch_mf(Engine* e, const GemmOp& g, const GemmX& x, dim3 grid, int cps, int vec) {
     float* ws = e->wide_st->ws;
     const bool akf = g.sak == 1, bkf = g.sbk == 1;
     if constexpr (AT) {
-        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, true, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
-        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, true, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, true, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, true, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
     } else if (akf) {
-        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
-        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, true, true, false, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, true, false, false, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
     } else {
-        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, false, true, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
-        else hipLaunchKernelGGL((k_gemm_mf<P, false, false, false, NT>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        if (bkf) hipLaunchKernelGGL((k_gemm_mf<P, false, true, false, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
+        else hipLaunchKernelGGL((k_gemm_mf<P, false, false, false, NT, PF>), grid, dim3(256), 0, e->stream, g, x, cps, ws, vec);
     }
 }
+// the input transform's GEMM runs over K = D (two stages); the others by their chunks per split
 template <class P, bool AT>
 static void launch_mf_nt(Engine* e, const GemmOp& g, const GemmX& x, dim3 grid, int cps, int vec, int nt) {
-    if (nt == 128) launch_mf<P, AT, 128>(e, g, x, grid, cps, vec);
-    else launch_mf<P, AT, 64>(e, g, x, grid, cps, vec);
+    if constexpr (AT) {
+        if (nt == 128) launch_mf<P, true, 128, 2>(e, g, x, grid, cps, vec);
+        else launch_mf<P, true, 64, 2>(e, g, x, grid, cps, vec);
+    } else {
+        const bool pf2 = cps >= 16;
+        if (nt == 128) {
+            if (pf2) launch_mf<P, false, 128, 2>(e, g, x, grid, cps, vec);
+            else launch_mf<P, false, 128, 1>(e, g, x, grid, cps, vec);
+        } else {
+            if (pf2) launch_mf<P, false, 64, 2>(e, g, x, grid, cps, vec);
+            else launch_mf<P, false, 64, 1>(e, g, x, grid, cps, vec);
+        }
+    }
 }
 
-// the bf16-MFMA kernel takes the handle's non-f32 modes, operands with a unit stride on one side
-// each, and shapes big enough to fill its 64 x 64 x 32 tiles
+// float4 operands: 16-byte aligned bases, strides and contiguous extents multiples of 4 floats
+// (k_gemm_mf's loads are unconditional float4s with clamped indices)
+static bool mf_vec(const GemmOp& g) {
+    auto al = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool akf = g.sak == 1, bkf = g.sbk == 1;
+    const int64_t sa = akf ? g.sam : g.sak, sb = bkf ? g.sbn : g.sbk;
+    return al(g.A) && al(g.B) && sa % 4 == 0 && sb % 4 == 0 && (akf ? g.K : g.M) % 4 == 0 &&
+           (bkf ? g.K : g.N) % 4 == 0;
+}
+static bool mf_modes(const Engine* e) {
+    return e->cfg.dtype != MMVAE_DTYPE_F32 && !getenv_is("MMVAE_WIDE_F32GEMM", "1");
+}
+// the encoder input transform inside the first encoder GEMM (its A operand is the raw [B][D]
+// batch, its B the [out][D] weight); otherwise the normalised block Xn is materialised
+static bool at_in_gemm(const Engine* e) {
+    if (!mf_modes(e) || e->D % 4 != 0) return false;
+    if (e->cfg.model == MMVAE_MODEL_VMF) return true;  // layer 0 reads its Angular copy from wtil's start
+    // (parameter slots are packed: the frozen weight's offset decides its alignment)
+    const ParamSlot* sl = e->slot(e->fz_enc_w);
+    return sl && sl->off % 4 == 0;
+}
 static bool use_mf(const Engine* e, const GemmOp& g) {
-    if (e->cfg.dtype == MMVAE_DTYPE_F32 || getenv_is("MMVAE_WIDE_F32GEMM", "1")) return false;
+    if (!mf_modes(e)) return false;
     if (!(g.sak == 1 || g.sam == 1) || !(g.sbk == 1 || g.sbn == 1)) return false;
     if (g.sam == 0 || g.sbn == 0) return false;  // broadcast operands (column sums): the f32 kernel
+    if (!mf_vec(g)) return false;
     return g.M >= 32 && g.N >= 32 && g.K >= 32 && (int64_t)g.M * g.N * (int64_t)g.K >= ((int64_t)1 << 22);
 }
 
@@ -556,6 +686,8 @@ __global__ __launch_bounds__(256) void k_w_lin_small(GemmOp g) {
 
 static hipError_t gemm(Engine* e, const GemmOp& g, const GemmX* x = nullptr) {
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
+    // per-kernel timers (bench.py's wide lines): the gene GEMMs apart from the small ones
+    ScopedTimer tmg(e, (int64_t)g.M * g.N * g.K >= ((int64_t)1 << 26) ? "w_gemm_gene" : "w_gemm_small");
     if (!x && g.K <= 16 && g.N <= 256 && g.nc == 0) {
         hipLaunchKernelGGL(k_w_lin_small, dim3((unsigned)(((int64_t)g.M * g.N + 255) / 256)), dim3(256), 0, e->stream, g);
         return hipGetLastError();
@@ -565,13 +697,12 @@ static hipError_t gemm(Engine* e, const GemmOp& g, const GemmX* x = nullptr) {
     if (x || use_mf(e, g)) {
         const int nt = g.N >= 96 ? 128 : 64;
         const int tm = (g.M + 63) / 64, tn = (g.N + nt - 1) / nt, nch = (g.K + 31) / 32;
-        int S = split_count(w, MN, tm * tn, nch, 8);
+        int S = g.cpart ? 1 : split_count(w, MN, tm * tn, nch, 8);
         const int cps = (nch + S - 1) / S;
         S = std::max(1, (nch + cps - 1) / cps);
-        // float4 loads: 16-byte aligned bases and strides on the strided side
-        auto al = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-        const int64_t sa = g.sak == 1 ? g.sam : g.sak, sb = g.sbk == 1 ? g.sbn : g.sbk;
-        const int vec = al(g.A) && al(g.B) && sa % 4 == 0 && sb % 4 == 0;
+        if (x && !mf_vec(g)) return hipErrorInvalidValue;  // (at_in_gemm routes these to Xn)
+        // (the XCD-aware tile order measured slower on every wide GEMM shape: opt-in only)
+        const int vec = getenv_is("MMVAE_WIDE_XCD", "1") ? 2 : 0;
         const GemmX gx = x ? *x : GemmX{};
         const dim3 grid(tn, tm, S);
         if (e->cfg.dtype == MMVAE_DTYPE_BF16X3) {
@@ -657,6 +788,7 @@ static hipError_t redsmall(Engine* e, int M, int N, const float* Y, int64_t ldy,
 static hipError_t red_flush(Engine* e) {
     RedJobs& q = e->wide_st->redq;
     if (q.n == 0) return hipSuccess;
+    ScopedTimer tm(e, "w_colsum_small");
     hipLaunchKernelGGL(k_w_redsmall, dim3((q.maxnj + 63) / 64, RS_SMALL, q.n), dim3(256), 0, e->stream, q, e->wide_st->ws);
     hipLaunchKernelGGL(k_w_redsmall_fin, dim3((q.maxnj + 255) / 256, 1, q.n), dim3(256), 0, e->stream, q,
                        (const float*)e->wide_st->ws);
@@ -720,11 +852,13 @@ struct WDens {
 };
 // The row is built in LDS segments of WSEG genes (zeroed, the segment's nonzeros scattered, then
 // written out with coalesced 16-byte stores), so every byte of the dense row is written once.
-static constexpr int WSEG = 4096;
+// The segments' first entries come from one parallel pass over the row's entries (genes sorted:
+// entry i starts every segment after its predecessor's, up to its own) — no serial search.
+static constexpr int WSEG = 4096, WSEG_MAX = 64;
 __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
     __shared__ __attribute__((aligned(16))) float seg[WSEG];
     __shared__ float red[4];
-    __shared__ int64_t bnd[2];
+    __shared__ int64_t bnd[WSEG_MAX + 1];
     const int b = blockIdx.x;
     const int64_t cell = a.cells[b];
     float* xr = a.X + (int64_t)b * a.D;
@@ -750,23 +884,24 @@ __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
         }
     }
     const bool v4 = (a.D & 3) == 0;
-    int64_t e = r0;  // the first entry of the current segment (genes sorted in the row)
-    for (int s0 = 0; s0 < a.D; s0 += WSEG) {
-        const int len = min(WSEG, a.D - s0);
-        // this segment's entries: [e, first entry with gene >= s0 + len)
-        if (threadIdx.x == 0) {
-            int64_t lo = e, hi = r1;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (cr[mid] < s0 + len) lo = mid + 1;
-                else hi = mid;
-            }
-            bnd[0] = lo;
-        }
+    const int nseg = (a.D + WSEG - 1) / WSEG;
+    for (int sgi = 0; sgi < nseg; ++sgi) {
+        const int s0 = sgi * WSEG, len = min(WSEG, a.D - s0);
+        const int g0 = sgi % WSEG_MAX == 0 ? sgi : -1;  // the first segment of a group of WSEG_MAX
+        if (g0 >= 0)
+            for (int t = threadIdx.x; t <= WSEG_MAX; t += 256) bnd[t] = r1;
         for (int i = threadIdx.x; i < WSEG / 4; i += 256) reinterpret_cast<float4*>(seg)[i] = float4{0.f, 0.f, 0.f, 0.f};
         __syncthreads();
-        const int64_t e1 = bnd[0];
-        for (int64_t i = e + threadIdx.x; i < e1; i += 256) seg[cr[i] - s0] = a.val[i];
+        if (g0 >= 0) {  // bnd[t]: the first entry of the group's segment t (t = WSEG_MAX: the next group's)
+            for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+                const int sg = cr[i] / WSEG, sp = i == r0 ? -1 : cr[i - 1] / WSEG;
+                for (int t = max(sp + 1, g0); t <= min(sg, g0 + WSEG_MAX); ++t) bnd[t - g0] = i;
+            }
+            __syncthreads();
+        }
+        // this segment's entries: [bnd[j], bnd[j + 1])
+        const int j = sgi % WSEG_MAX;
+        for (int64_t i = bnd[j] + threadIdx.x; i < bnd[j + 1]; i += 256) seg[cr[i] - s0] = a.val[i];
         __syncthreads();
         if (v4) {
             for (int i = threadIdx.x; i < len / 4; i += 256)
@@ -774,8 +909,7 @@ __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
         } else {
             for (int i = threadIdx.x; i < len; i += 256) xr[s0 + i] = seg[i];
         }
-        e = e1;
-        __syncthreads();  // seg and bnd are rewritten by the next segment
+        __syncthreads();  // seg is rewritten by the next segment
     }
     for (int c = threadIdx.x; c < a.C; c += 256) a.Cb[(int64_t)b * a.C + c] = a.covar[cell * a.C + c];
     if (a.dpre) {
@@ -1728,7 +1862,7 @@ hipError_t wide_create(Engine* e) {
     hipError_t er;
 #define WA(p, n) if ((er = walloc(&(p), (n))) != hipSuccess) return er
     WA(w->X, Bp * D);
-    if (e->cfg.dtype == MMVAE_DTYPE_F32) WA(w->Xn, Bp * D);
+    if (!at_in_gemm(e)) WA(w->Xn, Bp * D);
     if (e->cfg.model == MMVAE_MODEL_NB && R > RMAX) WA(w->Uin, Bp * D);
     WA(w->LG, Bp * D);
     WA(w->G, Bp * D);
@@ -1859,6 +1993,7 @@ static hipError_t wide_input(Engine* e, int64_t B) {
         a.Hn = w->Hn;
         if (e->H > HMAX) a.H = 0;  // (the wide nu encoder runs as a GEMM)
     }
+    ScopedTimer tm(e, "w_densify");
     hipLaunchKernelGGL(k_w_densify2, dim3((unsigned)B), dim3(256), 0, e->stream, a);
     return hipGetLastError();
 }
@@ -1889,7 +2024,7 @@ static const float* enc_forward(Engine* e, int B, hipError_t& er) {
         g.B = L.W; g.sbk = 1; g.sbn = L.in;
         g.C = L.act; g.scm = L.out; g.scn = 1;
         g.bias = L.b; g.act = L.relu ? 1 : 0;
-        if (l == 0 && e->cfg.dtype != MMVAE_DTYPE_F32) {
+        if (l == 0 && at_in_gemm(e)) {
             g.A = w->X;
             er = gemm(e, g, &gx);
         } else {
@@ -1912,7 +2047,7 @@ static const float* enc_forward(Engine* e, int B, hipError_t& er) {
 // column sums of Y [M][N] (row stride ly) into `o`: column 0 = a0 (null: ones) when has0, then
 // the n1 columns of A1 (row stride la1), at most CR_QMAX per launch; X2: the XPROD pair
 // (sum Y, sum Y enc_in(X2)) for the encoder's ln_x_sd gradient
-static hipError_t colred(Engine* e, int M, int N, const float* Y, int64_t ly, bool has0, const float* a0,
+static hipError_t colred_(Engine* e, int M, int N, const float* Y, int64_t ly, bool has0, const float* a0,
                          const float* A1, int64_t la1, int n1, ColOut o, const float* X2 = nullptr,
                          const GemmX* xf = nullptr) {
     WideState* w = e->wide_st;
@@ -1952,10 +2087,20 @@ static hipError_t colred(Engine* e, int M, int N, const float* Y, int64_t ly, bo
     }
     return hipGetLastError();
 }
+static hipError_t colred(Engine* e, int M, int N, const float* Y, int64_t ly, bool has0, const float* a0,
+                         const float* A1, int64_t la1, int n1, ColOut o, const float* X2 = nullptr,
+                         const GemmX* xf = nullptr) {
+    ScopedTimer tm(e, "w_colred");
+    return colred_(e, M, N, Y, ly, has0, a0, A1, la1, n1, o, X2, xf);
+}
 
-// back through the encoder chain from dh [B][E] (in dT0) to dXn [B][D] (into out)
-static hipError_t enc_backward(Engine* e, int B, float* out) {
+// back through the encoder chain from dh [B][E] (in dT0) to the input gradient dXn [B][D] and
+// its x_mean / ln_x_sd column sums (o: sum_b dXn, sum_b dXn Xn).  On the MFMA path the first
+// layer's GEMM sums its output tiles itself (GemmOp::cpart) and dXn is never stored; otherwise
+// dXn goes into G (the decoder's gradient block is consumed by then) and k_colred sums it.
+static hipError_t enc_backward(Engine* e, int B, const ColOut& o) {
     WideState* w = e->wide_st;
+    const int D = (int)e->D;
     float *cur = w->dT0, *nxt = w->dT1;
     for (int l = (int)w->enc.size() - 1; l >= 0; --l) {
         const WLayer& L = w->enc[l];
@@ -1964,9 +2109,31 @@ static hipError_t enc_backward(Engine* e, int B, float* out) {
             hipLaunchKernelGGL(k_w_relu_bwd, dim3(grid_for((int64_t)B * L.out)), dim3(256), 0, e->stream,
                                (int64_t)B * L.out, (const float*)L.act, cur);
         }
-        float* dst = (l == 0) ? out : nxt;
-        if ((er = linear_dx(e, B, L.out, L.in, cur, L.out, L.W, dst, L.in)) != hipSuccess) return er;
-        std::swap(cur, nxt);
+        if (l > 0) {
+            if ((er = linear_dx(e, B, L.out, L.in, cur, L.out, L.W, nxt, L.in)) != hipSuccess) return er;
+            std::swap(cur, nxt);
+            continue;
+        }
+        const GemmX gx = enc_x(e);
+        GemmOp g;  // dXn = dT . W0 (linear_dx's operands)
+        g.M = B; g.N = L.in; g.K = L.out;
+        g.A = cur; g.sam = L.out; g.sak = 1;
+        g.B = L.W; g.sbk = L.in; g.sbn = 1;
+        const int tm = (B + 63) / 64;
+        if (use_mf(e, g) && (int64_t)tm * 2 * D <= w->cr_cap && !getenv_is("MMVAE_WIDE_UNFUSED", "1")) {
+            g.cpart = w->cr_part;
+            g.cx = w->X;
+            g.ldcx = D;
+            g.cxf = gx;
+            if ((er = gemm(e, g)) != hipSuccess) return er;
+            ScopedTimer tm_(e, "w_colred");
+            hipLaunchKernelGGL(k_colred_fin, dim3((unsigned)((2 * (int64_t)D + 255) / 256)), dim3(256), 0, e->stream, D, 2,
+                               1, tm, (const float*)w->cr_part, o);
+            return hipGetLastError();
+        }
+        g.C = w->G; g.scm = D; g.scn = 1;
+        if ((er = gemm(e, g)) != hipSuccess) return er;
+        return colred(e, B, D, w->G, D, true, nullptr, nullptr, 0, 1, o, w->X, &gx);
     }
     return hipGetLastError();
 }
@@ -2120,10 +2287,13 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     rw.nu_bias = e->preg("nu_bias");
     rw.dv = r_d; rw.dpre = r_dpre; rw.lossr = r_loss; rw.ddpre = r_ddpre;
     rw.with_grads = update ? 1 : 0;
-    if (D % 4 == 0 && (size_t)D * 4 <= 150 * 1024)  // the row in LDS (2 workgroups per CU up to 20k genes)
-        hipLaunchKernelGGL(k_w_nb_row_lds, dim3(B), dim3(512), (size_t)D * 4, e->stream, rw);
-    else
-        hipLaunchKernelGGL(k_w_nb_row, dim3(B), dim3(256), 0, e->stream, rw);
+    {
+        ScopedTimer tmr(e, "w_nb_row");
+        if (D % 4 == 0 && (size_t)D * 4 <= 150 * 1024)  // the row in LDS (2 workgroups per CU up to 20k genes)
+            hipLaunchKernelGGL(k_w_nb_row_lds, dim3(B), dim3(512), (size_t)D * 4, e->stream, rw);
+        else
+            hipLaunchKernelGGL(k_w_nb_row, dim3(B), dim3(256), 0, e->stream, rw);
+    }
     hipLaunchKernelGGL(k_w_loss, dim3(1), dim3(256), 0, e->stream, B, (const float*)r_loss, (const float*)r_kl, beta,
                        inv_n, 0.f, e->d_out);
     if (!update) return hipGetLastError();
@@ -2177,14 +2347,12 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     WCHK(colsum(e, B, 1, r_ddpre, 1, e->greg("depth.bias")));
     WCHK(colsum(e, B, H, w->dHn, H, e->greg("nu_encoding.bias")));
     WCHK(red_flush(e));
-    // encoder chain -> dXn (into G: the decoder's gradient block is consumed), x_mean / ln_x_sd
-    WCHK(enc_backward(e, B, w->G));
+    // encoder chain -> dXn and its column sums -> x_mean / ln_x_sd
     {
-        const GemmX gx = enc_x(e);
         ColOut o;
         o.o0 = w->gvec + 2 * D;
         o.o1 = w->gvec + 3 * D;
-        WCHK(colred(e, B, D, w->G, D, true, nullptr, nullptr, 0, 1, o, w->X, &gx));
+        WCHK(enc_backward(e, B, o));
     }
     hipLaunchKernelGGL(k_w_xgrad, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)(w->gvec + 2 * D),
                        (const float*)w->gvec, e->greg("x_mean"), e->greg("ln_x_sd"));
@@ -2255,7 +2423,10 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     }
     rw.vk = vk; rw.cosr = r_cos;
     rw.with_grads = update ? 1 : 0;
-    hipLaunchKernelGGL(k_w_vmf_row, dim3(B), dim3(256), 0, e->stream, rw);
+    {
+        ScopedTimer tmr(e, "w_vmf_row");
+        hipLaunchKernelGGL(k_w_vmf_row, dim3(B), dim3(256), 0, e->stream, rw);
+    }
     hipLaunchKernelGGL(k_w_vloss, dim3(1), dim3(256), 0, e->stream, B, (const float*)r_cos, (const float*)r_kl,
                        (const float*)vk, sc, beta, inv_n, e->d_out, e->greg("ln_kappa"), update ? 1 : 0);
     if (!update) return hipGetLastError();
@@ -2275,13 +2446,11 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     lb.Mn = w->Mn; lb.Ar = w->Ar; lb.Ep = w->Ep; lb.dZ = w->dZ; lb.dM = w->dM; lb.dA = w->dA;
     hipLaunchKernelGGL(k_w_latent_bwd, dim3(B), dim3(256), 0, e->stream, lb);
     WCHK(heads_bwd(e, B, h, "representation_mean", "representation_logvariance"));
-    WCHK(enc_backward(e, B, w->G));
     {
-        const GemmX gx = enc_x(e);
         ColOut o;
         o.o0 = w->gvec + 2 * D;
         o.o1 = w->gvec + 3 * D;
-        WCHK(colred(e, B, D, w->G, D, true, nullptr, nullptr, 0, 1, o, w->X, &gx));
+        WCHK(enc_backward(e, B, o));
     }
     hipLaunchKernelGGL(k_w_xgrad, dim3((D + 255) / 256), dim3(256), 0, e->stream, D, (const float*)(w->gvec + 2 * D),
                        (const float*)w->gvec, e->greg("x_mean"), e->greg("ln_x_sd"));
@@ -2289,7 +2458,8 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
 }
 
 hipError_t wide_forward_backward(Engine* e, int64_t B, int64_t n_total, float beta, bool update, bool use_eps) {
-    ScopedTimer tm(e, "wide_step");
+    // (per-kernel timers inside: w_gemm_gene, w_nb_row, w_colred, w_densify, ...; the rest of the
+    // step's small kernels are untimed)
     if (e->cfg.model == MMVAE_MODEL_VMF) return vmf_step(e, (int)B, n_total, beta, update, use_eps);
     return nb_step(e, (int)B, n_total, beta, update, use_eps);
 }

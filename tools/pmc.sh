@@ -5,7 +5,7 @@
 #        TAG_traffic.json ({"MODEL/DTYPE/kernel": HBM bytes per launch})
 TAG=${1:-pmc}; MODEL=${2:-nb}; DT=${3:-bf16}
 R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out; cd /tmp; export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu --no-extras --model $MODEL --dtype $DT --steps 20 --warmup 20 --kernel-steps 2 ${CELLS:+--cells $CELLS}"
+B="python3 $R/bench.py --no-cpu --no-extras --model $MODEL --dtype $DT --steps 20 --warmup 20 --kernel-steps 2 ${CELLS:+--cells $CELLS} ${LATENT:+--latent $LATENT}"
 run() { timeout -k 10 300 rocprofv3 "$@" -o run --output-format csv -- $B > /dev/null 2>>$R/gpurun_out/${TAG}.err; }
 run --kernel-trace --stats -d $R/gpurun_out/${TAG}_trace || exit 1
 run --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU -d $R/gpurun_out/${TAG}_p1 || exit 2
