@@ -69,6 +69,11 @@ struct GemmOp {
     const float* cx = nullptr;
     int64_t ldcx = 0;
     GemmX cxf;
+    // a frozen B operand's bf16 planes for k_gemm_skf (null: none): bpl[n * bkp + k], lo at + bplane
+    const __bf16* bpl = nullptr;
+    int bkp = 0;
+    int64_t bplane = 0;
+    const float* colv = nullptr;  // k_gemm_skf: gemm_colc of every column, combined by the host's launch
 };
 
 static constexpr int GT = 64, GK = 16, GLD = GT + 4;
@@ -475,6 +480,232 @@ __global__ __launch_bounds__(256) void k_gemm_mf(GemmOp g, GemmX x, int cps, flo
 }
 
 // =======================================================================================
+// k_gemm_skf — the short-K, wide-output GEMMs against a frozen weight (K <= 128, N = D: the
+// logit GEMM z W^T and the encoder input gradient dT W0, [B, D] outputs).  Their B operand is a
+// frozen Linear weight, so it is kept pre-split as bf16 planes (hi [, lo]) in k-contiguous
+// [N][Kp] layout (WideState::pl_*, rebuilt with the frozen parameters), and a lane reads its MFMA
+// fragments straight from them (16-byte loads, no LDS, no per-tile conversion).  One wave per
+// workgroup: it converts its 64 A rows (all of K) into fragments held in registers once, then
+// walks the n tiles nt = blockIdx.x, + gridDim.x, ... (32 columns each) with the next tile's B
+// fragments in flight under the current tile's MFMAs and epilogue — no barriers, no LDS.
+// grid (G, row tiles), G a multiple of 8: blocks b and b + 8 share an XCD and walk the same
+// columns, so a B tile is read from HBM about once per XCD.
+// CS: the column-sum epilogue of GemmOp::cpart (chunks = 64-row tiles).
+// =======================================================================================
+template <class P>
+MMVAE_DEV typename MM<P>::frag skf_split(const float4& a, const float4& b) {
+    const float e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = pk_bf16(e[2 * i], e[2 * i + 1]);
+    if constexpr (IsX3<P>::value) {
+        uint32_t l[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            l[i] = pk_bf16(e[2 * i] - __uint_as_float(h[i] << 16), e[2 * i + 1] - __uint_as_float(h[i] & 0xffff0000u));
+        return typename MM<P>::frag{__builtin_bit_cast(bf16x8, uint4{h[0], h[1], h[2], h[3]}),
+                                    __builtin_bit_cast(bf16x8, uint4{l[0], l[1], l[2], l[3]})};
+    } else {
+        return __builtin_bit_cast(bf16x8, uint4{h[0], h[1], h[2], h[3]});
+    }
+}
+template <class P>
+MMVAE_DEV typename MM<P>::frag skf_bfrag(const __bf16* p, int64_t plane) {
+    if constexpr (IsX3<P>::value)
+        return typename MM<P>::frag{*reinterpret_cast<const bf16x8*>(p), *reinterpret_cast<const bf16x8*>(p + plane)};
+    else
+        return *reinterpret_cast<const bf16x8*>(p);
+}
+template <class P, bool CS>
+__global__ __launch_bounds__(64) void k_gemm_skf(GemmOp g) {
+    using M = MM<P>;
+    using Fr = typename M::frag;
+    const int lane = threadIdx.x;
+    const int mt = blockIdx.y, m0 = mt * 64;
+    const int KC = g.bkp / 32;  // <= 4 (host)
+    const int ntiles = (g.N + 31) / 32;
+    // the wave's A fragments: rows m0 + 16 i + (lane & 15), k = 32 kc + 8 (lane >> 4) .. + 7
+    Fr fa[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 16 * i + (lane & 15);
+        const float* ar = g.A + (int64_t)min(m, g.M - 1) * g.sam;
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            if (kc >= KC) break;
+            const int k0 = 32 * kc + 8 * (lane >> 4);
+            const float4 u = *reinterpret_cast<const float4*>(ar + min(k0, g.K - 4));
+            const float4 v = *reinterpret_cast<const float4*>(ar + min(k0 + 4, g.K - 4));
+            const bool ok = m < g.M;
+            const float4 z4 = float4{0.f, 0.f, 0.f, 0.f};
+            fa[i][kc] = skf_split<P>((ok && k0 < g.K) ? u : z4, (ok && k0 + 4 < g.K) ? v : z4);
+        }
+    }
+    // the lane's rows m0 + 16 i + 4 (lane >> 4) + r: store, the covariate rows (nc <= 2); CS, the row scale
+    float car[4][4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = min(m0 + 16 * i + 4 * (lane >> 4) + r, g.M - 1);
+            if constexpr (CS) {
+                car[i][r][0] = g.cxf.rs ? g.cxf.rs[m] : 1.f;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) car[i][r][c] = c < g.nc ? g.ca[(int64_t)m * g.lca + c] : 0.f;
+            }
+        }
+    // one n tile's operands, all issued together one tile ahead (tile t + 1's under tile t's MFMAs
+    // and stores): the column constants (CS: the raw inputs and the transform's vectors) first,
+    // then the B fragments (columns nt * 32 + 16 j + (lane & 15), k = 32 kc + 8 (lane >> 4)).  The
+    // loop is unrolled by two over a ping-pong pair, so nothing is copied between registers.
+    struct Tile {
+        Fr fb[2][4];
+        float cc[2], cw2[2][2], xv[CS ? 2 : 1][4][4];
+    };
+    auto fetch = [&](int nt, Tile& T) {
+        const int n0 = nt * 32;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = min(n0 + 16 * j + (lane & 15), g.N - 1);
+            if constexpr (CS) {
+                T.cc[j] = g.cxf.xm[n];
+                T.cw2[j][0] = g.cxf.isd[n];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int m = min(m0 + 16 * i + 4 * (lane >> 4) + r, g.M - 1);
+                        T.xv[j][i][r] = g.cx[(int64_t)m * g.ldcx + n];
+                    }
+            } else {
+                // unconditional loads (the host's combined column vector; the covariate columns past
+                // nc re-read the last one, or the column vector, and meet zero rows): a load behind a
+                // pointer test is consumed at once, and its wait would drain everything in flight
+                T.cc[j] = g.colv[n];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) T.cw2[j][c] = g.cw[(int64_t)n * g.lcw + min(c, max(g.nc - 1, 0))];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // (issue order: the constants before the B fragments)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = min(n0 + 16 * j + (lane & 15), g.N - 1);
+            const __bf16* bp = g.bpl + (int64_t)n * g.bkp + 8 * (lane >> 4);
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc)  // (all four: k chunks past KC reload the last, unused)
+                T.fb[j][kc] = skf_bfrag<P>(bp + 32 * min(kc, KC - 1), g.bplane);
+        }
+    };
+    auto compute = [&](int nt, const Tile& T) {
+        const int n0 = nt * 32;
+        f32x4 acc[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            if (kc >= KC) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = M::mma(fa[i][kc], T.fb[j][kc], acc[i][j]);
+        }
+        if constexpr (CS) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = n0 + 16 * j + (lane & 15);
+                float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int m = m0 + 16 * i + 4 * (lane >> 4) + r;
+                        const float v = (m < g.M && n < g.N) ? acc[i][j][r] : 0.f;
+                        s0 += v;
+                        s1 = fmaf(v, enc_in_acc(T.xv[j][i][r], car[i][r][0], T.cc[j], T.cw2[j][0]), s1);
+                    }
+                s0 += __shfl_xor(s0, 16, 64);
+                s1 += __shfl_xor(s1, 16, 64);
+                s0 += __shfl_xor(s0, 32, 64);
+                s1 += __shfl_xor(s1, 32, 64);
+                if (lane < 16 && n < g.N) {
+                    g.cpart[((int64_t)mt * 2 + 0) * g.N + n] = s0;
+                    g.cpart[((int64_t)mt * 2 + 1) * g.N + n] = s1;
+                }
+            }
+        } else {
+            // (plain row-major stores, no read-modify-write: a load among the stores would make the
+            // next tile's wait for its operands a wait for every store before it)
+            float* cb = g.C + (int64_t)(m0 + 4 * (lane >> 4)) * g.scm + n0 + (lane & 15);
+            float vv[4][4][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        float v = fmaf(g.alpha, acc[i][j][r], T.cc[j]);
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) v = fmaf(car[i][r][c], T.cw2[j][c], v);  // (car = 0 past nc)
+                        vv[i][r][j] = g.act == 1 ? fmaxf(v, 0.f) : v;
+                    }
+            if (m0 + 64 <= g.M && n0 + 32 <= g.N) {  // (uniform) a full tile: plain stores
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) cb[(int64_t)(16 * i + r) * g.scm + 16 * j] = vv[i][r][j];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            if (m0 + 16 * i + 4 * (lane >> 4) + r < g.M && n0 + 16 * j + (lane & 15) < g.N)
+                                cb[(int64_t)(16 * i + r) * g.scm + 16 * j] = vv[i][r][j];
+            }
+        }
+    };
+    const int G = gridDim.x;
+    // every fetch is issued unconditionally (past the end: the last tile again, unused) so the
+    // loads in flight are a static count and each tile waits for its own operands only
+    Tile t0, t1;
+    const int last = ntiles - 1;
+    int nt = blockIdx.x;
+    fetch(min(nt, last), t0);
+    for (; nt < ntiles; nt += 2 * G) {
+        fetch(min(nt + G, last), t1);
+        compute(nt, t0);
+        if (nt + G >= ntiles) break;
+        fetch(min(nt + 2 * G, last), t0);
+        compute(nt + G, t1);
+    }
+}
+
+// every column's gemm_colc (the GEMM's biases, summed in its fixed order) into one vector
+__global__ __launch_bounds__(256) void k_w_colc(GemmOp g, float* __restrict__ out) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < g.N) out[n] = gemm_colc(g, n);
+}
+
+// bf16 planes (hi at out, lo at out + plane) of a frozen weight, B(k, n) = W[k sk + n sn], in
+// the [N][Kp] k-contiguous layout of k_gemm_skf (k >= K: zero)
+__global__ __launch_bounds__(256) void k_w_planes(const float* __restrict__ W, int64_t sk, int64_t sn, int N, int K,
+                                                  int Kp, __bf16* __restrict__ out, int64_t plane) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)N * Kp) return;
+    const int n = (int)(i % N), k = (int)(i / N);  // n fastest: coalesced reads when sn == 1
+    const float v = k < K ? W[(int64_t)k * sk + (int64_t)n * sn] : 0.f;
+    const __bf16 h = (__bf16)v;
+    out[(int64_t)n * Kp + k] = h;
+    out[plane + (int64_t)n * Kp + k] = (__bf16)(v - (float)h);
+}
+
+// =======================================================================================
 // Wide-path state (device buffers sized at create, so a step allocates nothing and can be
 // captured into a step graph)
 // =======================================================================================
@@ -534,6 +765,12 @@ struct WideState {
     float* wtil = nullptr;         // vMF: normalised Angular weights of every encoder layer
     float* lossv = nullptr;        // [2]: scratch sums
     struct RedJobs redq;           // narrow column sums queued for one launch (red_flush)
+    // bf16 planes of the frozen B operands of the two short-K GEMMs (k_gemm_skf, null: not
+    // eligible): the decoder's final weight (logits) and the first encoder weight, transposed
+    // (the encoder input gradient); [D][kp] each, the lo plane after the hi one
+    __bf16 *pl_F = nullptr, *pl_E = nullptr;
+    int kp_F = 0, kp_E = 0;
+    float* colv = nullptr;  // [D] the short-K GEMM's combined column constants
 };
 
 static hipError_t walloc(float** p, int64_t n) { return hipMalloc(p, sizeof(float) * (size_t)(n > 0 ? n : 1)); }
@@ -619,6 +856,16 @@ static bool use_mf(const Engine* e, const GemmOp& g) {
     return g.M >= 32 && g.N >= 32 && g.K >= 32 && (int64_t)g.M * g.N * (int64_t)g.K >= ((int64_t)1 << 22);
 }
 
+// the short-K kernel: a frozen B operand with planes, k-contiguous float4 A rows, K <= 128, at
+// most two covariate columns in the epilogue
+static bool use_sk(const Engine* e, const GemmOp& g) {
+    if (!g.bpl || getenv_is("MMVAE_WIDE_NOSK", "1") || !mf_modes(e)) return false;
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return g.sak == 1 && al(g.A) && g.sam % 4 == 0 && g.K % 4 == 0 && g.K <= 128 && g.bkp >= g.K &&
+           g.bkp % 32 == 0 && g.bkp <= 128 && g.nc <= 2 && g.M >= 1 && g.N >= 32 && !g.accumulate &&
+           (g.cpart || g.scn == 1);
+}
+
 // C = epilogue(A . B); `x` non-null: the encoder input transform on A (the f32 handles
 // materialise the normalised block instead, see enc_forward)
 // ---- narrow shapes: the column sums / small weight gradients over the batch rows and the tiny
@@ -694,6 +941,30 @@ static hipError_t gemm(Engine* e, const GemmOp& g, const GemmX* x = nullptr) {
     }
     WideState* w = e->wide_st;
     const int64_t MN = (int64_t)g.M * g.N;
+    if (!x && use_sk(e, g)) {
+        GemmOp gs = g;
+        if (!g.cpart) {  // the column constants as one vector; cw pointed at something valid
+            hipLaunchKernelGGL(k_w_colc, dim3((g.N + 255) / 256), dim3(256), 0, e->stream, g, w->colv);
+            gs.colv = w->colv;
+            if (g.nc == 0) {
+                gs.cw = w->colv;  // (read, times the zero covariate rows)
+                gs.lcw = 0;
+            }
+        }
+        const int tmr = (g.M + 63) / 64, ntl = (g.N + 31) / 32;
+        // one wave per SIMD over the chip (1024 SIMDs; ~400 registers a lane), G a multiple of 8
+        int G = std::max(8, (1024 / std::max(1, tmr)) / 8 * 8);
+        G = std::min(G, (ntl + 7) / 8 * 8);
+        const dim3 grid((unsigned)G, (unsigned)tmr);
+        if (e->cfg.dtype == MMVAE_DTYPE_BF16X3) {
+            if (g.cpart) hipLaunchKernelGGL((k_gemm_skf<X3, true>), grid, dim3(64), 0, e->stream, gs);
+            else hipLaunchKernelGGL((k_gemm_skf<X3, false>), grid, dim3(64), 0, e->stream, gs);
+        } else {
+            if (g.cpart) hipLaunchKernelGGL((k_gemm_skf<__bf16, true>), grid, dim3(64), 0, e->stream, gs);
+            else hipLaunchKernelGGL((k_gemm_skf<__bf16, false>), grid, dim3(64), 0, e->stream, gs);
+        }
+        return hipGetLastError();
+    }
     if (x || use_mf(e, g)) {
         const int nt = g.N >= 96 ? 128 : 64;
         const int tm = (g.M + 63) / 64, tn = (g.N + nt - 1) / nt, nch = (g.K + 31) / 32;
@@ -1868,6 +2139,7 @@ hipError_t wide_create(Engine* e) {
     WA(w->G, Bp * D);
     WA(w->U, Bp * D);
     WA(w->gvec, 5 * D);
+    WA(w->colv, D);
     WA(w->one, 1);
     w->ws_cap = std::max<int64_t>(int64_t(8) << 20, 4 * D);
     WA(w->ws, w->ws_cap);
@@ -1898,6 +2170,16 @@ hipError_t wide_create(Engine* e) {
 #undef WA
     const float one = 1.f;
     if ((er = hipMemcpy(w->one, &one, sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) return er;
+    if (mf_modes(e)) {  // the short-K GEMMs' weight planes (filled by wide_prepare_frozen)
+        const int kf = w->dec.back().in, ke = w->enc[0].out;
+        auto pl = [&](__bf16** p, int* kp, int k) -> hipError_t {
+            if (k > 128 || k % 4 != 0) return hipSuccess;
+            *kp = (k + 31) / 32 * 32;
+            return hipMalloc(p, sizeof(__bf16) * 2 * (size_t)D * *kp);
+        };
+        if ((er = pl(&w->pl_F, &w->kp_F, kf)) != hipSuccess) return er;
+        if ((er = pl(&w->pl_E, &w->kp_E, ke)) != hipSuccess) return er;
+    }
     bind_layers(e, w);
     return hipSuccess;
 }
@@ -1905,7 +2187,7 @@ hipError_t wide_create(Engine* e) {
 void wide_destroy(Engine* e) {
     WideState* w = e->wide_st;
     if (!w) return;
-    for (float* p : {w->X, w->Xn, w->Uin, w->LG, w->G, w->U, w->gvec, w->one, w->ws, w->cr_part, w->Cb, w->rowv, w->Mr, w->Ar, w->Ce,
+    for (float* p : {w->X, w->Xn, w->Uin, w->LG, w->G, w->U, w->gvec, w->colv, w->one, w->ws, w->cr_part, w->Cb, w->rowv, w->Mr, w->Ar, w->Ce,
                      w->Mn, w->Z, w->Ep, w->dZ, w->dM, w->dA, w->Hn, w->dHn, w->NMr, w->NAr, w->Zn, w->En, w->dZn,
                      w->dNM, w->dNA, w->dT0, w->dT1, w->wtil, w->lossv})
         if (p) hipFree(p);
@@ -1913,6 +2195,8 @@ void wide_destroy(Engine* e) {
         if (L.act) hipFree(L.act);
     for (auto& L : w->dec)
         if (L.act) hipFree(L.act);
+    if (w->pl_F) hipFree(w->pl_F);
+    if (w->pl_E) hipFree(w->pl_E);
     delete w;
     e->wide_st = nullptr;
 }
@@ -1927,6 +2211,19 @@ hipError_t wide_prepare_frozen(Engine* e) {
             hipLaunchKernelGGL(k_w_angular, dim3(w->enc[l].out), dim3(256), 0, e->stream, w->enc[l].in,
                                (const float*)e->pfrz(base + ".weight"), const_cast<float*>(w->enc[l].W));
         }
+    }
+    const int D = (int)e->D;
+    if (w->pl_F) {  // B(k, n) = W_F[n][k]
+        const WLayer& F = w->dec.back();
+        const int64_t n = (int64_t)D * w->kp_F;
+        hipLaunchKernelGGL(k_w_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, F.W, (int64_t)1,
+                           (int64_t)F.in, D, F.in, w->kp_F, w->pl_F, n);
+    }
+    if (w->pl_E) {  // B(k, n) = W0[k][n]
+        const WLayer& L = w->enc[0];
+        const int64_t n = (int64_t)D * w->kp_E;
+        hipLaunchKernelGGL(k_w_planes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, L.W, (int64_t)L.in,
+                           (int64_t)1, D, L.out, w->kp_E, w->pl_E, n);
     }
     e->frozen_dirty = false;
     ++e->graph_gen;
@@ -2119,7 +2416,12 @@ static hipError_t enc_backward(Engine* e, int B, const ColOut& o) {
         g.M = B; g.N = L.in; g.K = L.out;
         g.A = cur; g.sam = L.out; g.sak = 1;
         g.B = L.W; g.sbk = L.in; g.sbn = 1;
-        const int tm = (B + 63) / 64;
+        if (w->pl_E) {
+            g.bpl = w->pl_E;
+            g.bkp = w->kp_E;
+            g.bplane = (int64_t)D * w->kp_E;
+        }
+        const int tm = (B + 63) / 64;  // the 64-row tiles = the partial chunks (both kernels)
         if (use_mf(e, g) && (int64_t)tm * 2 * D <= w->cr_cap && !getenv_is("MMVAE_WIDE_UNFUSED", "1")) {
             g.cpart = w->cr_part;
             g.cx = w->X;
@@ -2257,6 +2559,11 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
         g.C = w->LG; g.scm = D; g.scn = 1;
         g.bias = F.b;
         g.bias2 = e->preg("mu_bias");
+        if (w->pl_F) {
+            g.bpl = w->pl_F;
+            g.bkp = w->kp_F;
+            g.bplane = (int64_t)D * w->kp_F;
+        }
         if (c_in) {
             g.ca = w->Cb; g.lca = C;
             g.cw = e->preg("covar_decoding.weight"); g.lcw = C;
@@ -2409,7 +2716,20 @@ static hipError_t vmf_step(Engine* e, int B, int64_t n_total, float beta, bool u
     const float* zd = dec_hidden_fwd(e, B, er);
     WCHK(er);
     const WLayer& F = w->dec.back();
-    WCHK(linear_fwd(e, B, D, F.in, zd, F.in, F.W, F.b, w->LG, D));
+    {  // linear_fwd's operands, with the frozen weight's planes for the short-K kernel
+        GemmOp g;
+        g.M = B; g.N = D; g.K = F.in;
+        g.A = zd; g.sam = F.in; g.sak = 1;
+        g.B = F.W; g.sbk = 1; g.sbn = F.in;
+        g.C = w->LG; g.scm = D; g.scn = 1;
+        g.bias = F.b;
+        if (w->pl_F) {
+            g.bpl = w->pl_F;
+            g.bkp = w->kp_F;
+            g.bplane = (int64_t)D * w->kp_F;
+        }
+        WCHK(gemm(e, g));
+    }
     if (!c_in)
         WCHK(linear_fwd(e, B, D, C, w->Cb, C, e->preg("covar_decoding_.weight"), e->preg("covar_decoding_.bias"), w->U, D));
     WVRow rw;
