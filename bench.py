@@ -408,6 +408,21 @@ def wide_roofline(eng, batches, B, D, K, dtype, t_step, steps=5):
             "roofline_frac": round(issued / t_gemm / peak, 4) if t_gemm else None}
 
 
+class _StdoutToStderr:
+    """fd 1 -> fd 2 for the enclosed native calls (RCCL prints its version banner to stdout at
+    communicator init; the bench's stdout is its one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def dp_exchange(mmvae_amd, D, K, B, dtype, cells, lib, steps=300, warmup=20):
     """The data-parallel exchange's fixed cost on one GPU: the headline step with
     a forced 1-rank RCCL communicator (MMVAE_FORCE_COMM=1, read at comm_init) runs exactly a world > 1
@@ -430,9 +445,11 @@ def dp_exchange(mmvae_amd, D, K, B, dtype, cells, lib, steps=300, warmup=20):
                 os.environ.pop(k, None)
             os.environ["MMVAE_FORCE_COMM"] = "1"
             os.environ.update(env)
-            eng.comm_init(0, 1, mmvae_amd.Engine.comm_unique_id())
+            with _StdoutToStderr():
+                eng.comm_init(0, 1, mmvae_amd.Engine.comm_unique_id())
             g0 = eng.graph_stats()
-            ms = time_steps(eng, batches, 1.0, B, 0, steps, warmup) / steps * 1e3
+            with _StdoutToStderr():  # (the first step after init may print too)
+                ms = time_steps(eng, batches, 1.0, B, 0, steps, warmup) / steps * 1e3
             g1 = eng.graph_stats()
             out["modes"].append({"mode": name, "ms_per_step": round(ms, 4), "delta_us": round((ms - base) * 1e3, 1),
                                  "graph_replays": g1["replays"] - g0["replays"]})
@@ -491,9 +508,11 @@ def main():
                            graph=not args.no_graph)
     t_setup = time.perf_counter() - t_setup
     if world > 1:
-        obj = [mmvae_amd.Engine.comm_unique_id() if rank == 0 else None]
+        with _StdoutToStderr():
+            obj = [mmvae_amd.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        eng.comm_init(rank, world, obj[0])
+        with _StdoutToStderr():
+            eng.comm_init(rank, world, obj[0])
 
     beta = 1.0
     n_total = B * world

@@ -202,11 +202,14 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmOp g, int S, const floa
 
 MMVAE_DEV float enc_in(float v, float rs, float xm, float isd) { return (log1p_pos(v) * rs - xm) * isd; }
 // the same with libm log1pf (the f32 handles' input block, the ln_x_sd gradient's column sum)
+__device__ __attribute__((noinline)) float log1p_libm(float v) { return log1pf(v); }
 MMVAE_DEV float log1p_acc(float v) {
-    // integer counts: 1 + v is exact and v_log's error is ~1 ulp of the result; others libm
-    if (v == 0.f) return 0.f;
-    if (v >= 1.f && v < 16777216.f && v == floorf(v)) return flog(1.f + v);
-    return log1pf(v);
+    // integer counts (0 included): 1 + v is exact and v_log's error is ~1 ulp of the result;
+    // others libm, out of line (the branch is skipped by waves of counts, and the inlined libm
+    // body would multiply the register use of every caller's unrolled loop)
+    float r = flog(1.f + v);
+    if (!(v >= 0.f && v < 16777216.f && v == floorf(v))) r = log1p_libm(v);
+    return r;
 }
 MMVAE_DEV float enc_in_acc(float v, float rs, float xm, float isd) { return (log1p_acc(v) * rs - xm) * isd; }
 
@@ -1120,6 +1123,7 @@ struct WDens {
     // vMF row scales (null: NB)
     float *rs1, *rs2;
     float epsD;
+    int seg;  // 1: the LDS segment build; 0: the store pass (MMVAE_WIDE_DENSSTORE=1)
 };
 // The row is built in LDS segments of WSEG genes (zeroed, the segment's nonzeros scattered, then
 // written out with coalesced 16-byte stores), so every byte of the dense row is written once.
@@ -1155,6 +1159,14 @@ __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
         }
     }
     const bool v4 = (a.D & 3) == 0;
+    if (v4 && !a.seg) {
+        // the row zeroed with 16-byte stores, then, after the barrier (its workgroup fence completes
+        // those stores), the nonzeros written over it: one pass of stores, no LDS, one barrier —
+        // the LDS segment build below is bound by its chain of per-segment barriers
+        for (int i = threadIdx.x; i < a.D / 4; i += 256) reinterpret_cast<float4*>(xr)[i] = float4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) xr[cr[i]] = a.val[i];
+    } else {
     const int nseg = (a.D + WSEG - 1) / WSEG;
     for (int sgi = 0; sgi < nseg; ++sgi) {
         const int s0 = sgi * WSEG, len = min(WSEG, a.D - s0);
@@ -1181,6 +1193,7 @@ __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
             for (int i = threadIdx.x; i < len; i += 256) xr[s0 + i] = seg[i];
         }
         __syncthreads();  // seg is rewritten by the next segment
+    }
     }
     for (int c = threadIdx.x; c < a.C; c += 256) a.Cb[(int64_t)b * a.C + c] = a.covar[cell * a.C + c];
     if (a.dpre) {
@@ -1222,7 +1235,7 @@ struct ColRed {
     float* part;  // [chunks][Q][N]
 };
 template <bool XPROD>
-__global__ __launch_bounds__(256) void k_colred(ColRed c) {
+__global__ __launch_bounds__(256) void k_colred_gen(ColRed c) {
     constexpr int RG = 8;  // rows per group: their loads are all issued before the sums
     const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (n >= c.N) return;
@@ -1289,6 +1302,99 @@ __global__ __launch_bounds__(256) void k_colred(ColRed c) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (n + j < c.N) c.part[((int64_t)blockIdx.y * c.Q + q) * c.N + n + j] = acc[q][j];
+}
+// The float4 form (N and the row strides multiples of 4): a workgroup's rows in 64-row blocks,
+// whose Q coefficient columns are staged into LDS first (block-uniform reads, no scalar load
+// on the way to each fma), and the block's eight 8-row groups streamed through two register
+// buffers — the next group's loads in flight under the current group's sums (ping-pong, fully
+// unrolled, every load issued: rows past the chunk re-read its last row and meet a zero weight).
+template <bool XPROD>
+__global__ __launch_bounds__(256) void k_colred(ColRed c) {
+    constexpr int RG = 8;
+    __shared__ float cf[CR_QMAX][64];
+    const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int r0 = blockIdx.y * c.rows_per, r1 = min(c.M, r0 + c.rows_per);
+    const int nq = XPROD ? 2 : c.Q;
+    const int nc = min(n, c.N - 4);  // (threads past N load a valid column and store nothing)
+    float acc[CR_QMAX][4];
+#pragma unroll
+    for (int q = 0; q < CR_QMAX; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[q][j] = 0.f;
+    float xm[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (XPROD)  // (x_mean is a packed parameter slot: no 16-byte alignment assumed)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xm[j] = c.xf.xm[nc + j];
+            isd[j] = c.xf.isd[nc + j];
+        }
+    float4 yb[2][RG], xb[XPROD ? 2 : 1][RG];
+    auto load = [&](int buf, int m0) {
+#pragma unroll
+        for (int i = 0; i < RG; ++i) {
+            const int m = min(m0 + i, r1 - 1);
+            yb[buf][i] = *reinterpret_cast<const float4*>(c.Y + (int64_t)m * c.ly + nc);
+            if constexpr (XPROD) xb[buf][i] = *reinterpret_cast<const float4*>(c.X2 + (int64_t)m * c.ly + nc);
+        }
+    };
+    auto sum = [&](int buf, int i0) {  // rows i0 .. i0 + RG - 1 of the block
+#pragma unroll
+        for (int i = 0; i < RG; ++i) {
+            const float* y = reinterpret_cast<const float*>(&yb[buf][i]);
+            if constexpr (XPROD) {
+                const float* x = reinterpret_cast<const float*>(&xb[buf][i]);
+                const float w = cf[0][i0 + i], rs = cf[1][i0 + i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float yv = w * y[j];
+                    acc[0][j] += yv;
+                    acc[1][j] = fmaf(yv, enc_in_acc(x[j], rs, xm[j], isd[j]), acc[1][j]);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < CR_QMAX; ++q)
+                    if (q < nq) {
+                        const float a = cf[q][i0 + i];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[q][j] = fmaf(a, y[j], acc[q][j]);
+                    }
+            }
+        }
+    };
+    for (int b0 = r0; b0 < r1; b0 += 64) {
+        __syncthreads();  // the previous block's coefficient reads are done
+        for (int t = threadIdx.x; t < nq * 64; t += 256) {
+            const int q = t >> 6, m = b0 + (t & 63);
+            float v = 0.f;
+            if (m < r1) {
+                if constexpr (XPROD) v = q == 0 ? 1.f : (c.xf.rs ? c.xf.rs[m] : 1.f);
+                else v = (c.has0 && q == 0) ? (c.a0 ? c.a0[m] : 1.f) : c.A1[(int64_t)m * c.la1 + q - c.has0];
+            }
+            cf[q][t & 63] = v;
+        }
+        __syncthreads();
+        // (sched barriers: each group's loads stay issued together, ahead of the sums that wait
+        // for the other buffer — left alone, the scheduler sinks every load next to its use)
+        load(0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+        for (int gq = 0; gq < 64 / RG; gq += 2) {
+            load(1, b0 + (gq + 1) * RG);
+            __builtin_amdgcn_sched_barrier(0);
+            sum(0, gq * RG);
+            __builtin_amdgcn_sched_barrier(0);
+            load(0, b0 + min(gq + 2, 64 / RG - 1) * RG);  // (the last trip: a spare re-read, unused)
+            __builtin_amdgcn_sched_barrier(0);
+            sum(1, (gq + 1) * RG);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (n >= c.N) return;
+#pragma unroll
+    for (int q = 0; q < CR_QMAX; ++q)
+        if (q < nq)
+            *reinterpret_cast<float4*>(c.part + ((int64_t)blockIdx.y * nq + q) * c.N + n) =
+                float4{acc[q][0], acc[q][1], acc[q][2], acc[q][3]};
 }
 // outputs: column 0 -> o0[n s0] = alpha0 s (and o0b[n s0] = beta0 s); the A1 columns j ->
 // o1[j q1 + n s1] = alpha1 s (the XPROD sum: o1[n s1])
@@ -1680,12 +1786,15 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
     // sweep 1: the logits into LDS (log2 units), online max / sum-exp.  Every sweep over the row
     // issues RCH float4 loads per thread before it uses any (one memory latency per RCH of them,
     // not one per float4)
+    // (every batch's loads are issued unconditionally — clamped into the row, the spares unused —
+    // and fenced from the math by a sched barrier: conditional or scheduler-sunk loads were
+    // each waited for alone)
     float m = -1e30f, s = 0.f;
     for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
         float4 vv[RCH];
 #pragma unroll
-        for (int j = 0; j < RCH; ++j)
-            if (g0 + 2048 * j < a.D) vv[j] = *reinterpret_cast<const float4*>(a.LG + o + g0 + 2048 * j);
+        for (int j = 0; j < RCH; ++j) vv[j] = *reinterpret_cast<const float4*>(a.LG + o + min(g0 + 2048 * j, a.D - 4));
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < RCH; ++j) {
             const int g = g0 + 2048 * j;
@@ -1774,13 +1883,12 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
             float4 bv[RCH], nv[RCH], wv[RCH];
 #pragma unroll
             for (int j = 0; j < RCH; ++j) {
-                const int g = g0 + 2048 * j;
-                if (g < a.D) {  // (the registered gene vectors need not be 16-byte aligned)
-                    bv[j] = float4{a.bnd[g], a.bnd[g + 1], a.bnd[g + 2], a.bnd[g + 3]};
-                    nv[j] = float4{a.nu_bias[g], a.nu_bias[g + 1], a.nu_bias[g + 2], a.nu_bias[g + 3]};
-                    wv[j] = float4{a.Wnd[g], a.Wnd[g + 1], a.Wnd[g + 2], a.Wnd[g + 3]};
-                }
+                const int g = min(g0 + 2048 * j, a.D - 4);  // (the registered gene vectors need not be 16-byte aligned)
+                bv[j] = float4{a.bnd[g], a.bnd[g + 1], a.bnd[g + 2], a.bnd[g + 3]};
+                nv[j] = float4{a.nu_bias[g], a.nu_bias[g + 1], a.nu_bias[g + 2], a.nu_bias[g + 3]};
+                wv[j] = float4{a.Wnd[g], a.Wnd[g + 1], a.Wnd[g + 2], a.Wnd[g + 3]};
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < RCH; ++j) {
                 const int g = g0 + 2048 * j;
@@ -1861,8 +1969,8 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
     for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
         float4 gvv[RCH];
 #pragma unroll
-        for (int j = 0; j < RCH; ++j)
-            if (g0 + 2048 * j < a.D) gvv[j] = *reinterpret_cast<const float4*>(a.G + o + g0 + 2048 * j);
+        for (int j = 0; j < RCH; ++j) gvv[j] = *reinterpret_cast<const float4*>(a.G + o + min(g0 + 2048 * j, a.D - 4));
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < RCH; ++j) {
             const int g = g0 + 2048 * j;
@@ -2291,6 +2399,7 @@ static hipError_t wide_input(Engine* e, int64_t B) {
         if (e->H > HMAX) a.H = 0;  // (the wide nu encoder runs as a GEMM)
     }
     ScopedTimer tm(e, "w_densify");
+    a.seg = getenv_is("MMVAE_WIDE_DENSSTORE", "1") ? 0 : 1;
     hipLaunchKernelGGL(k_w_densify2, dim3((unsigned)B), dim3(256), 0, e->stream, a);
     return hipGetLastError();
 }
@@ -2372,8 +2481,15 @@ static hipError_t colred_(Engine* e, int M, int N, const float* Y, int64_t ly, b
         c.rows_per = (M + chunks - 1) / chunks;
         chunks = (M + c.rows_per - 1) / c.rows_per;
         const dim3 grid((unsigned)((N + 1023) / 1024), (unsigned)chunks);
-        if (X2) hipLaunchKernelGGL(k_colred<true>, grid, dim3(256), 0, e->stream, c);
-        else hipLaunchKernelGGL(k_colred<false>, grid, dim3(256), 0, e->stream, c);
+        const bool f4 = N % 4 == 0 && ly % 4 == 0 && N >= 4 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0 &&
+                        (!X2 || (reinterpret_cast<uintptr_t>(X2) & 15) == 0);
+        if (f4) {
+            if (X2) hipLaunchKernelGGL(k_colred<true>, grid, dim3(256), 0, e->stream, c);
+            else hipLaunchKernelGGL(k_colred<false>, grid, dim3(256), 0, e->stream, c);
+        } else {
+            if (X2) hipLaunchKernelGGL(k_colred_gen<true>, grid, dim3(256), 0, e->stream, c);
+            else hipLaunchKernelGGL(k_colred_gen<false>, grid, dim3(256), 0, e->stream, c);
+        }
         ColOut oc = o;
         if (done) oc.o1 = o.o1 + done * o.q1;
         const int64_t nq = (int64_t)N * c.Q;
