@@ -178,8 +178,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmOp g, int cps, float* __restri
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemmOp g, int S, const float* __restrict__ ws) {
     const int64_t MN = (int64_t)g.M * g.N;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
-        float s = 0.f;
-        for (int q = 0; q < S; ++q) s += ws[q * MN + i];
+        float s = 0.f;  // (the splits in order, 8 loads issued at a time)
+        int q = 0;
+        for (; q + 8 <= S; q += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = ws[(q + u) * MN + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; q < S; ++q) s += ws[q * MN + i];
         gemm_epilogue(g, (int)(i / g.N), (int)(i % g.N), s);
     }
 }
@@ -1129,7 +1137,10 @@ struct WDens {
 // written out with coalesced 16-byte stores), so every byte of the dense row is written once.
 // The segments' first entries come from one parallel pass over the row's entries (genes sorted:
 // entry i starts every segment after its predecessor's, up to its own) — no serial search.
-static constexpr int WSEG = 4096, WSEG_MAX = 64;
+#ifndef MMVAE_WSEG
+#define MMVAE_WSEG 4096
+#endif
+static constexpr int WSEG = MMVAE_WSEG, WSEG_MAX = 64;
 __global__ __launch_bounds__(256) void k_w_densify2(WDens a) {
     __shared__ __attribute__((aligned(16))) float seg[WSEG];
     __shared__ float red[4];
@@ -1308,8 +1319,12 @@ __global__ __launch_bounds__(256) void k_colred_gen(ColRed c) {
 // on the way to each fma), and the block's eight 8-row groups streamed through two register
 // buffers — the next group's loads in flight under the current group's sums (ping-pong, fully
 // unrolled, every load issued: rows past the chunk re-read its last row and meet a zero weight).
+struct ColRed2 {
+    ColRed c[2];  // blockIdx.z selects one (two independent sums over blocks of one shape in one launch)
+};
 template <bool XPROD>
-__global__ __launch_bounds__(256) void k_colred(ColRed c) {
+__global__ __launch_bounds__(256) void k_colred(ColRed2 cc) {
+    const ColRed& c = cc.c[blockIdx.z];
     constexpr int RG = 8;
     __shared__ float cf[CR_QMAX][64];
     const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
@@ -1412,8 +1427,18 @@ __global__ __launch_bounds__(256) void k_colred_fin(int N, int Q, int has0, int 
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)N * Q) return;
     const int q = (int)(i / N), n = (int)(i % N);
+    // the chunks in order, 16 loads issued at a time (one thread per output: a serial loop
+    // waited for each load alone, ~17 us a launch)
     float s = 0.f;
-    for (int c = 0; c < chunks; ++c) s += part[((int64_t)c * Q + q) * N + n];
+    int c = 0;
+    for (; c + 16 <= chunks; c += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = part[((int64_t)(c + u) * Q + q) * N + n];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; c < chunks; ++c) s += part[((int64_t)c * Q + q) * N + n];
     if (has0 && q == 0) {
         o.o0[n * o.s0] = o.alpha0 * s;
         if (o.o0b) o.o0b[n * o.s0] = o.beta0 * s;
@@ -2484,8 +2509,10 @@ static hipError_t colred_(Engine* e, int M, int N, const float* Y, int64_t ly, b
         const bool f4 = N % 4 == 0 && ly % 4 == 0 && N >= 4 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0 &&
                         (!X2 || (reinterpret_cast<uintptr_t>(X2) & 15) == 0);
         if (f4) {
-            if (X2) hipLaunchKernelGGL(k_colred<true>, grid, dim3(256), 0, e->stream, c);
-            else hipLaunchKernelGGL(k_colred<false>, grid, dim3(256), 0, e->stream, c);
+            ColRed2 cc;
+            cc.c[0] = c;
+            if (X2) hipLaunchKernelGGL(k_colred<true>, grid, dim3(256), 0, e->stream, cc);
+            else hipLaunchKernelGGL(k_colred<false>, grid, dim3(256), 0, e->stream, cc);
         } else {
             if (X2) hipLaunchKernelGGL(k_colred_gen<true>, grid, dim3(256), 0, e->stream, c);
             else hipLaunchKernelGGL(k_colred_gen<false>, grid, dim3(256), 0, e->stream, c);
@@ -2505,6 +2532,54 @@ static hipError_t colred(Engine* e, int M, int N, const float* Y, int64_t ly, bo
                          const GemmX* xf = nullptr) {
     ScopedTimer tm(e, "w_colred");
     return colred_(e, M, N, Y, ly, has0, a0, A1, la1, n1, o, X2, xf);
+}
+// two such sums (ones + A1 columns each, one launch each alone) over [M][N] blocks in one launch:
+// the decoder's G and U sums, whose tails then overlap (falls back to two colred calls)
+struct ColJob {
+    const float* Y;
+    const float* A1;
+    int64_t la1;
+    int n1;
+    ColOut o;
+};
+static hipError_t colred_pair(Engine* e, int M, int N, const ColJob& j0, const ColJob& j1) {
+    WideState* w = e->wide_st;
+    const int64_t N4 = (N + 3) / 4 * 4;
+    const int q0 = 1 + j0.n1, q1 = 1 + j1.n1;
+    const int chunks = std::max(1, std::min(64, M / 64));
+    auto al = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (q0 > CR_QMAX || q1 > CR_QMAX || N % 4 != 0 || N < 4 || !al(j0.Y) || !al(j1.Y) ||
+        (int64_t)chunks * (q0 + q1) * N4 > w->cr_cap || getenv_is("MMVAE_WIDE_COLRED1", "1")) {
+        hipError_t er = colred(e, M, N, j0.Y, N, true, nullptr, j0.A1, j0.la1, j0.n1, j0.o);
+        if (er == hipSuccess) er = colred(e, M, N, j1.Y, N, true, nullptr, j1.A1, j1.la1, j1.n1, j1.o);
+        return er;
+    }
+    ScopedTimer tm(e, "w_colred");
+    ColRed2 cc;
+    std::memset(&cc, 0, sizeof(cc));
+    const int rows_per = (M + chunks - 1) / chunks;
+    const ColJob* js[2] = {&j0, &j1};
+    for (int z = 0; z < 2; ++z) {
+        ColRed& c = cc.c[z];
+        c.M = M;
+        c.N = N;
+        c.has0 = 1;
+        c.Q = 1 + js[z]->n1;
+        c.A1 = js[z]->A1;
+        c.la1 = js[z]->la1;
+        c.Y = js[z]->Y;
+        c.ly = N;
+        c.rows_per = rows_per;
+        c.part = w->cr_part + (z ? (int64_t)chunks * q0 * N : 0);
+    }
+    const int ch = (M + rows_per - 1) / rows_per;
+    hipLaunchKernelGGL(k_colred<false>, dim3((unsigned)((N + 1023) / 1024), (unsigned)ch, 2), dim3(256), 0, e->stream, cc);
+    for (int z = 0; z < 2; ++z) {
+        const int64_t nq = (int64_t)N * cc.c[z].Q;
+        hipLaunchKernelGGL(k_colred_fin, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, e->stream, N, cc.c[z].Q, 1, ch,
+                           (const float*)cc.c[z].part, js[z]->o);
+    }
+    return hipGetLastError();
 }
 
 // back through the encoder chain from dh [B][E] (in dT0) to the input gradient dXn [B][D] and
@@ -2723,23 +2798,27 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     // ---- backward ----
     // decoder-side gene vectors from the batch sums of dL/dlogit (G) and dL/du (U)
     {
-        ColOut o;
-        o.o0 = e->greg("mu_bias");
-        o.o0b = e->greg("covar_decoding.bias");
-        o.o1 = e->greg("covar_decoding.weight");
-        o.q1 = 1;
-        o.s1 = C;
-        WCHK(colred(e, B, D, w->G, D, true, nullptr, w->Cb, C, C, o));
-    }
-    {
-        ColOut o;
-        o.o0 = e->greg("nu_decoding.bias");
-        o.o0b = e->greg("nu_bias");
-        o.beta0 = -1.f;  // u = nu_dec(z_nu) - nu_bias
-        o.o1 = e->greg("nu_decoding.weight");
-        o.q1 = 1;
-        o.s1 = R;
-        WCHK(colred(e, B, D, w->U, D, true, nullptr, w->Zn, R, R, o));
+        ColJob jg, ju;
+        jg.Y = w->G;
+        jg.A1 = w->Cb;
+        jg.la1 = C;
+        jg.n1 = C;
+        jg.o.o0 = e->greg("mu_bias");
+        jg.o.o0b = e->greg("covar_decoding.bias");
+        jg.o.o1 = e->greg("covar_decoding.weight");
+        jg.o.q1 = 1;
+        jg.o.s1 = C;
+        ju.Y = w->U;
+        ju.A1 = w->Zn;
+        ju.la1 = R;
+        ju.n1 = R;
+        ju.o.o0 = e->greg("nu_decoding.bias");
+        ju.o.o0b = e->greg("nu_bias");
+        ju.o.beta0 = -1.f;  // u = nu_dec(z_nu) - nu_bias
+        ju.o.o1 = e->greg("nu_decoding.weight");
+        ju.o.q1 = 1;
+        ju.o.s1 = R;
+        WCHK(colred_pair(e, B, D, jg, ju));
     }
     if (!r_in) WCHK(linear_dx(e, B, D, R, w->U, D, e->preg("nu_decoding.weight"), w->dZn, R));
     // decoder chain -> dz, then the latent
