@@ -488,6 +488,10 @@ int mmvae_destroy(mmvae_h e) {
     if (!e) return MMVAE_OK;
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
+    if (e->comm_stream) hipStreamSynchronize(e->comm_stream);
+    // the gather stream first (its kernels read the slots' mapped pinned blocks: h_gcells,
+    // h_brp_pin), then the slots
+    stream_release(e);
     for (auto& sl : e->slots2) {
         for (auto& g : sl.graphs) hipGraphExecDestroy(g.second);
         if (sl.block) hipHostFree(sl.block);
@@ -495,7 +499,6 @@ int mmvae_destroy(mmvae_h e) {
         if (sl.ev) hipEventDestroy(sl.ev);
     }
     if (e->comm) ncclCommDestroy(e->comm);
-    stream_release(e);
     wide_destroy(e);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
