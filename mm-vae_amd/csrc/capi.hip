@@ -713,26 +713,34 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
         packed_reg = false;
     };
     auto undo = [&]() {
-        for (void* h : regs) hipHostUnregister(h);
+        for (void* h : regs) hipHostFree(h);
         regs.clear();
         free_packed();
         (void)hipGetLastError();
     };
-    // the caller's arrays as mapped pinned memory (read over PCIe by the gather / unpack kernels):
-    // read-only registration first (a read-only np.memmap can be pinned that way), then plain
+    // the arrays the gather / unpack kernels read over PCIe, as engine-owned mapped pinned copies.
+    // The caller's memory itself is never registered: a registration outliving (or not fully
+    // undone before) the caller's free let a later host -> device copy from a new array at the
+    // same addresses go through the stale mapping (an illegal access in the next upload).
     auto reg = [&](const void* p, size_t bytes, const void** dev) -> hipError_t {
         if (!bytes) {
             *dev = p;
             return hipSuccess;
         }
-        void* h = const_cast<void*>(p);
-        hipError_t er = hipHostRegister(h, bytes, hipHostRegisterMapped | hipHostRegisterReadOnly);
-        if (er != hipSuccess) {
-            (void)hipGetLastError();
-            er = hipHostRegister(h, bytes, hipHostRegisterMapped);
-        }
+        void* h = nullptr;
+        hipError_t er = hipHostMalloc(&h, bytes, hipHostMallocMapped);
         if (er != hipSuccess) return er;
         regs.push_back(h);
+        {  // host threads for the large ones
+            const unsigned nth = bytes >= ((size_t)64 << 20) ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nth; ++t)
+                th.emplace_back([&, t] {
+                    const size_t a = bytes * t / nth, b = bytes * (t + 1) / nth;
+                    std::memcpy(static_cast<char*>(h) + a, static_cast<const char*>(p) + a, b - a);
+                });
+            for (auto& x : th) x.join();
+        }
         void* d = nullptr;
         er = hipHostGetDevicePointer(&d, h, 0);
         *dev = d;
@@ -744,7 +752,7 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     };
     const void* d = nullptr;
     hipError_t er = reg(rowptr, sizeof(int64_t) * (size_t)(N + 1), &d);
-    if (er != hipSuccess) return failed(er, "registering rowptr");
+    if (er != hipSuccess) return failed(er, "pinning rowptr");
     const int64_t* hs_rowptr = static_cast<const int64_t*>(d);
     // integer counts below 2^16 over at most 2^16 genes: the packed copy (bit-exact values).  In the
     // DMA mode only host threads read it (stream_dma_gather), so it stays pageable; the zero-copy
@@ -819,14 +827,14 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     const int32_t* hs_col = nullptr;
     const float* hs_val = nullptr;
     if (!packed) {
-        if ((er = reg(col, sizeof(int32_t) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "registering col");
+        if ((er = reg(col, sizeof(int32_t) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "pinning col");
         hs_col = static_cast<const int32_t*>(d);
-        if ((er = reg(val, sizeof(float) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "registering val");
+        if ((er = reg(val, sizeof(float) * (size_t)nnz, &d)) != hipSuccess) return failed(er, "pinning val");
         hs_val = static_cast<const float*>(d);
     }
     const float* hs_covar = nullptr;
     if (covar) {
-        if ((er = reg(covar, sizeof(float) * (size_t)(N * e->C), &d)) != hipSuccess) return failed(er, "registering covar");
+        if ((er = reg(covar, sizeof(float) * (size_t)(N * e->C), &d)) != hipSuccess) return failed(er, "pinning covar");
         hs_covar = static_cast<const float*>(d);
     }
     // the new dataset is in place: the resident one (if any) goes

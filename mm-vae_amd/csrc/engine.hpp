@@ -106,7 +106,7 @@ struct Engine {
     const int32_t* hs_col = nullptr;
     const float* hs_val = nullptr;
     const float* hs_covar = nullptr;
-    std::vector<void*> hs_registered;  // host ranges to hipHostUnregister
+    std::vector<void*> hs_registered;  // the engine's mapped pinned copies of the streamed arrays (hipHostFree)
     // packed entries (streamed, D <= 65536, every value a 16-bit integer count): one word per
     // entry, gene << 16 | count, in engine-owned mapped pinned memory — the gather moves 4 bytes
     // per entry over PCIe instead of 8 (MMVAE_STREAM_PACK=0: the caller's arrays)

@@ -434,7 +434,7 @@ void stream_release(Engine* e) {
             if (p) hipFree(p);
         q = Engine::BatchSet{};
     }
-    for (void* p : e->hs_registered) hipHostUnregister(p);
+    for (void* p : e->hs_registered) hipHostFree(p);  // (the engine's pinned copies)
     if (e->hs_packed && e->hs_packed_bytes) {  // mmap'd: pageable (DMA mode) or registered (THP zero-copy)
         if (e->hs_packed_reg) hipHostUnregister(e->hs_packed);
         munmap(e->hs_packed, e->hs_packed_bytes);
