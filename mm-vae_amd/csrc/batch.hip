@@ -144,10 +144,16 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
 #pragma unroll
             for (int u = 0; u < U; ++u) wv[u] = dotw[(unsigned)g[u] < (unsigned)D ? g[u] : 0];
         }
+        // every tile-base lookup first (the clamped loads give real gene ids, so each index is in
+        // range), then the masked stores: a lookup inside each store's branch waited for its own
+        // LDS round trip, sixteen in a row
+        int pos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pos[u] = sb[min(g[u] >> 6, NT - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u + lane;
-            if (j < jB) stage[sb[g[u] >> 6] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+            if (j < jB) stage[pos[u] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
         }
         if (dots) {
 #pragma unroll

@@ -1797,8 +1797,14 @@ MMVAE_DEV float block_sum512(float v, float* red) {
     return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
 }
 static constexpr int RCH = 5;  // float4 loads in flight per thread in the row sweeps
+// GL: the row's G = p dL/dmu' d (+ the nonzeros' terms) is kept in LDS beside p (2 D floats, one
+// workgroup per CU up to ~20k genes) instead of being stored, read back and stored again: the
+// kernel is HBM-bound (≈ 2.4 GB a step at K = 128, D = 20k, B = 4096: logits in, U and G out,
+// G in and out again, the sparse read-modify-writes), and G's round trip is 0.66 GB of it.
+template <bool GL>
 __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
-    extern __shared__ __attribute__((aligned(16))) float prow[];  // [D]
+    extern __shared__ __attribute__((aligned(16))) float prow[];  // [D] (GL: + [D] the row's G)
+    float* grow = prow + a.D;  // (GL; D % 4 == 0 keeps it 16-byte aligned)
     __shared__ float red[8], red2[8], ftab[9];
     constexpr float L2E = 1.4426950408889634f;
     const int b = blockIdx.x;
@@ -1900,7 +1906,8 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
         *reinterpret_cast<float4*>(prow + g) = lv;
         if (a.with_grads) {
             *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
-            *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+            if (GL) *reinterpret_cast<float4*>(grow + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+            else *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
         }
     };
     if (a.Zn && a.R == 1) {
@@ -1940,7 +1947,8 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
         *reinterpret_cast<float4*>(prow + g) = lv;
         if (a.with_grads) {
             *reinterpret_cast<float4*>(a.U + o + g) = float4{dus[0], dus[1], dus[2], dus[3]};
-            *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+            if (GL) *reinterpret_cast<float4*>(grow + g) = float4{gps[0], gps[1], gps[2], gps[3]};
+            else *reinterpret_cast<float4*>(a.G + o + g) = float4{gps[0], gps[1], gps[2], gps[3]};
         }
     }
     }
@@ -1963,7 +1971,7 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
             if (a.with_grads)
 #pragma unroll
                 for (int k = 0; k < NE; ++k) {
-                    gpo[k] = xs[k] != 0.f ? a.G[o + gs[k]] : 0.f;
+                    gpo[k] = xs[k] != 0.f ? (GL ? grow[gs[k]] : a.G[o + gs[k]]) : 0.f;
                     duo[k] = xs[k] != 0.f ? a.U[o + gs[k]] : 0.f;
                 }
 #pragma unroll
@@ -1973,7 +1981,8 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
                 const NbElem q = nb_delta(prow[gg], u_of(gg), d, xs[k], a.inv_n, ftab);
                 take(gg, q);
                 if (a.with_grads) {
-                    a.G[o + gg] = gpo[k] + q.gp;
+                    if (GL) grow[gg] = gpo[k] + q.gp;
+                    else a.G[o + gg] = gpo[k] + q.gp;
                     a.U[o + gg] = duo[k] + q.du;
                 }
             }
@@ -1994,7 +2003,10 @@ __global__ __launch_bounds__(512) void k_w_nb_row_lds(WNbRow a) {
     for (int g0 = 4 * threadIdx.x; g0 < a.D; g0 += 2048 * RCH) {
         float4 gvv[RCH];
 #pragma unroll
-        for (int j = 0; j < RCH; ++j) gvv[j] = *reinterpret_cast<const float4*>(a.G + o + min(g0 + 2048 * j, a.D - 4));
+        for (int j = 0; j < RCH; ++j) {
+            const int gj = min(g0 + 2048 * j, a.D - 4);
+            gvv[j] = GL ? *reinterpret_cast<const float4*>(grow + gj) : *reinterpret_cast<const float4*>(a.G + o + gj);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < RCH; ++j) {
@@ -2787,8 +2799,11 @@ static hipError_t nb_step(Engine* e, int B, int64_t n_total, float beta, bool up
     rw.with_grads = update ? 1 : 0;
     {
         ScopedTimer tmr(e, "w_nb_row");
-        if (D % 4 == 0 && (size_t)D * 4 <= 150 * 1024)  // the row in LDS (2 workgroups per CU up to 20k genes)
-            hipLaunchKernelGGL(k_w_nb_row_lds, dim3(B), dim3(512), (size_t)D * 4, e->stream, rw);
+        if (D % 4 == 0 && (size_t)D * 8 <= 158 * 1024 && update && !getenv_is("MMVAE_WIDE_ROWG", "0"))
+            // p and G in LDS (one workgroup per CU up to ~20k genes)
+            hipLaunchKernelGGL(k_w_nb_row_lds<true>, dim3(B), dim3(512), (size_t)D * 8, e->stream, rw);
+        else if (D % 4 == 0 && (size_t)D * 4 <= 150 * 1024)  // the row in LDS (2 workgroups per CU up to 20k genes)
+            hipLaunchKernelGGL(k_w_nb_row_lds<false>, dim3(B), dim3(512), (size_t)D * 4, e->stream, rw);
         else
             hipLaunchKernelGGL(k_w_nb_row, dim3(B), dim3(256), 0, e->stream, rw);
     }

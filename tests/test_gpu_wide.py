@@ -72,11 +72,15 @@ def test_wide_fixture_trajectory(path):
     _check_trajectory(z, eng)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
 @pytest.mark.parametrize("path", FUSED, ids=os.path.basename)
-def test_forced_wide_path_on_every_fixture(monkeypatch, path):
+def test_forced_wide_path_on_every_fixture(monkeypatch, path, dtype):
+    """Every fused-shape fixture on the wide path: exact f32 (k_gemm), and bf16x3, which runs the
+    MFMA kernels at every fixture's odd shapes — the short-K frozen-weight GEMM (k_gemm_skf) with
+    0-2 covariates in its epilogue (3: k_gemm_mf), its column-sum epilogue, ragged row / column tiles."""
     monkeypatch.setenv("MMVAE_WIDE", "1")
     z = load(path)
-    eng = engine_from_fixture(z, "f32")
+    eng = engine_from_fixture(z, dtype)
     assert eng.path() == "wide"
     _check_trajectory(z, eng)
 
@@ -146,15 +150,16 @@ def test_wide_genes_above_fused_limit():
     _live("nb", 80000, 16, 128, N=600)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16x3"])
 @pytest.mark.parametrize("model", ["nb", "vmf"])
-def test_wide_graph_equals_eager_under_poison(model):
+def test_wide_graph_equals_eager_under_poison(model, dtype):
     """Step graphs on the wide path replay bit-identically to eager launches, with the whole
     workspace (dense blocks, GEMM split partials, latent blocks) poisoned before every step."""
     from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
     D, K, B = 3000, 96, 256
     res = []
     for graph, poison in ((False, None), (True, 0xFF)):
-        eng = Engine(D=D, K=K, max_batch=B, dtype="f32", seed=5, model=MODEL_VMF if model == "vmf" else MODEL_NB)
+        eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=5, model=MODEL_VMF if model == "vmf" else MODEL_NB)
         assert eng.path() == "wide"
         eng.synth_csr(2000, lib_size=1500.0, seed=4)
         eng.init_params(seed=13)
@@ -172,3 +177,30 @@ def test_wide_graph_equals_eager_under_poison(model):
     assert res[0][0] == res[1][0]
     for k in res[0][1]:
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_wide_bf16_operands_latent128():
+    """The plain bf16 operand mode on the wide path (k_gemm_mf / k_gemm_skf single-plane
+    instances): loss within the bf16 tolerance of the fp32 oracle (2e-3, as the fused bf16 mode)."""
+    from mmvae_amd import MODEL_NB, Engine
+    from oracle import nb_oracle, synth
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    D, K, B, N = 4000, 128, 512, 1500
+    eng = Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1, model=MODEL_NB)
+    assert eng.path() == "wide"
+    eng.synth_csr(N, lib_size=2000.0, seed=3)
+    eng.init_params(seed=7)
+    cells = (np.arange(B, dtype=np.int64) * 7 + 11) % N
+    rng = np.random.default_rng(5)
+    em = rng.standard_normal((B, K)).astype(np.float32)
+    en = rng.standard_normal((B, 1)).astype(np.float32)
+    info = {n: k for n, k, _ in eng.param_info()}
+    p0, f0 = nb_oracle.init_params(D, C=1, K=K, H=1, R=1)
+    pull = {n: torch.from_numpy(eng.get_param(n, info[n]).reshape(v.shape)) for n, v in p0.items()}
+    pullf = {n: torch.from_numpy(eng.get_param(n, info[n]).reshape(v.shape)) for n, v in f0.items()}
+    tr = nb_oracle.NBTrainer(pull, pullf)
+    loss, _ = eng.step(cells, 0.8, eps=np.concatenate([em.ravel(), en.ravel()]))
+    rp, col, val = eng.get_rows(cells)
+    x = torch.from_numpy(synth.densify(rp, col, val, np.arange(B), D))
+    r = tr.step(x, torch.ones(B, 1), torch.from_numpy(em), torch.from_numpy(en), 0.8)
+    assert np.isfinite(loss) and abs(loss - r["loss"]) <= 2e-3 * abs(r["loss"]), (loss, r["loss"])
