@@ -9,5 +9,5 @@ for dt in $DTS; do
 for spec in base "$KNOB"; do
   if [ "$spec" == base ]; then envs=""; else envs="$spec"; fi
   env $envs timeout -k 10 200 python bench.py --no-extras --no-cpu --dtype $dt --steps 300 > gpurun_out/$TAG.json 2>gpurun_out/$TAG.err || { tail -3 gpurun_out/$TAG.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/$TAG.json'));print('$dt', '$spec', round(d['value']), d['ms_per_step'], {k: round(v*1e3,1) for k, v in d['kernel_ms'].items() if k.startswith('k_dec') or k.startswith('k_enc')})"
+  python -c "import json;d=json.load(open('gpurun_out/$TAG.json'));print('$dt', '$spec', round(d['value']), d['ms_per_step'], {k: round(v*1e3,1) for k, v in d['kernel_ms'].items()})"
 done; done
