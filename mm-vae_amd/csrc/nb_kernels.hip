@@ -322,32 +322,41 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
 }
 
 // =======================================================================================
-// k_latent_fwd — the K x K heads and the reparameterisation for 64 cells per workgroup
-// (wave w owns cells 16w..16w+15, lane = latent k):
+// k_latent_fwd — the K x K heads and the reparameterisation for LAT_CELLS = 16 cells per
+// workgroup (lane = latent k; NW waves, each owning 16 / NW cells):
 //   h = mu_enc(x~) (+ frozen bias), mean = mu_repr_mean(h) + covar_enc(c) (nb.hh:412-416),
 //   lnvar = clamp(mu_repr_lnvar(h), -4, 4), z = mean + eps*exp(lnvar/2) (nb.hh:462-472),
 //   nu path (nb.hh:444-451, 489-492), depth d = softplus(pre) (nb.hh:498), KL terms (nb.hh:533-537).
-// The heads are [64 cells x K] x [K x K] products: W rows from LDS (lane-distinct), h from an
-// LDS [cell][k] image read as wave-uniform broadcasts.
+// The heads are [16 cells x K] x [K x K] products on f32 MFMA (waves 0..3), h from an LDS
+// [cell][k] image.
 //   mode 1 = recorder encode_mu(x) (nb.hh:419-431): no covariate, writes mean/lnvar out.
+// NW = 16 (one cell per wave, 1024 threads): the kernel is a chain of memory rounds, and one
+// wave per SIMD with 4 cells each leaves most of each round's loads queued behind the wave's
+// load counter; 16 waves per CU keep every cell's loads in flight at once.  It has no frozen
+// hidden chains (those run the NW = 4 instance, whose chain layers assume 256 threads).  Every
+// global load is issued before the first global store (one in-order counter covers both).
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_latent_fwd(
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_latent_fwd(
     NBPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float* __restrict__ rowxp,
     float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
     const StepScalars* __restrict__ ss,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
+    constexpr int CPW = LAT_CELLS / NW;  // cells per wave
+    constexpr bool CHAINS = NW == 4;     // the frozen chains' layers run on 256 threads
     const int K = d.K, KE = d.KE, E = d.E;
     const uint64_t step = (uint64_t)ss->step_id;  // the noise key (staged with the batch)
     const int64_t row_offset = ss->row_offset;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];  // [cell][k]
-    __shared__ float sred[4];
+    __shared__ float sred[NW];
     __shared__ float sRX[LAT_CELLS][1 + HMAX];  // depth pre-activation, nu_enc(x)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // first cell of this wave (4 cells per wave)
+    const int cw = CPW * w;                     // this wave's first cell in the workgroup
+    const int bw = blockIdx.x * LAT_CELLS + cw;  // ... in the batch
     // diagnostic (MMVAE_DBG & 2048): realtime stamps of the phases into P.dbg_out (outputs invalid)
     const bool rts = dbg_bit(d.dbg, 2048) && mode == 0;
     uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -357,83 +366,99 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     mark(0);
     // every global input first, waits in issue order (one memory round, plus one for the loads
     // that depend on a cell id); the per-cell loop below then only stores
-    HeadsStage hst;
+    HeadsStage<64 * NW> hst;
     hst.issue(P.Wm, P.Wl, K, E);
     const int nqx = 1 + d.H;
-    float xs[4];  // raw-count dots (k_batch_lists), lanes < 1 + H
-    split_sum4(rowxp, 1, (int64_t)d.Bpad * nqx, (int64_t)bw * nqx + (k < nqx ? k : 0), nqx, k < nqx, xs);
-    float hs[4];  // the encoder's gene-split partials of h
-    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
+    float xs[CPW];  // raw-count dots (k_batch_lists), lanes < 1 + H
+    split_sum<CPW>(rowxp, 1, (int64_t)d.Bpad * nqx, (int64_t)bw * nqx + (k < nqx ? k : 0), nqx, k < nqx, xs);
+    float hs[CPW];  // the encoder's gene-split partials of h
+    split_sum<CPW>(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
+    // per-lane parameters (clamped, unconditional loads)
+    const int kk = min(k, K - 1), kr = min(k, d.R - 1), ke = min(k, KE - 1);
+    const float p_bx = (k == 0) ? P.bdp[0] : P.bne[min(max(k - 1, 0), d.H - 1)];  // raw-count dot bias
+    const float p_be = P.be[ke], p_bm = P.bm[kk], p_bl = P.bl[kk];
+    const float p_bce = P.bce[kk], p_wce = P.Wce[(int64_t)kk * d.C];
+    const float p_bnm = P.bnm[kr], p_bnl = P.bnl[kr];
+    float p_wnm[HMAX], p_wnl[HMAX];
+#pragma unroll
+    for (int hh = 0; hh < HMAX; ++hh) {
+        p_wnm[hh] = P.Wnm[kr * d.H + min(hh, d.H - 1)];
+        p_wnl[hh] = P.Wnl[kr * d.H + min(hh, d.H - 1)];
+    }
     // rows past this batch (b >= B): the handle-wide grid covers them, but the lists / encoder
     // wrote their partials only up to pad_rows(B) — whatever the buffers hold there is dropped
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < CPW; ++c)
         if (bw + c >= d.B) hs[c] = xs[c] = 0.f;
-    int pbv[4];
-    float cmv[4], epv[4], enp[4];
+    int pbv[CPW];
+    float cmv[CPW], epv[CPW], enp[CPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
         const bool valid = b < d.B;
         pbv[c] = (perm && valid) ? perm[b] : b;  // original batch position: the noise key
         float cm = 0.f;
         if (k < K && mode == 0) {
-            cm = P.bce[k];
-            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
+            cm = p_bce;
+            if (!covar) {  // unit covariate (Engine::unit_covar): c = 1, padding rows (row N) 0
+                cm += valid ? p_wce : 0.f;
+            } else {
+                const int64_t cell = cells[b];  // padding rows hold the empty row N
+                for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
+            }
         }
         cmv[c] = cm;
         epv[c] = (eps_in && k < K && valid) ? eps_in[(int64_t)pbv[c] * K + k] : 0.f;
         enp[c] = (eps_in && k < d.R && valid) ? eps_in[(int64_t)d.B * K + (int64_t)pbv[c] * d.R + k] : 0.f;
     }
-    if (d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
+    // h = sum of the encoder's gene-split partials - mvec + bias (mvec: all threads, LDS combine)
+    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);
+    if (!CHAINS || d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
     mark(1);
     {
         // raw-count dots (+ bias) -> sRX, and rowx for k_latent_bwd
-        const int nq = nqx;
-        if (k < nq) {
-            const float bias = (k == 0) ? P.bdp[0] : P.bne[k - 1];
+        if (k < nqx) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float v = xs[c] + bias;
-                sRX[4 * w + c][k] = v;
+            for (int c = 0; c < CPW; ++c) {
+                const float v = xs[c] + p_bx;
+                sRX[cw + c][k] = v;
                 if (mode == 0) rowx[(int64_t)(bw + c) * d.rowx_stride + (k == 0 ? 0 : 1 + k)] = v;
             }
         }
     }
-    // h = sum of the encoder's gene-split partials - mvec + bias
-    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
-    const float hb = (k < KE) ? P.be[k] - mvk : 0.f;
+    const float hb = (k < KE) ? p_be - mvk : 0.f;
     mark(2);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const float hv = hb + hs[c];  // mu_enc Linear output; --relu appends ReLU(inplace) (nb.hh:345-346)
-        sH[(4 * w + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
+        sH[(cw + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
     }
     __syncthreads();
     // the frozen encoder chain (hidden mu_encoding_l, l >= 2: nb.hh:331-340) -> the heads' input
-    __shared__ float sZ[2][LAT_CELLS * 68];
+    __shared__ float sZ[CHAINS ? 2 : 1][LAT_CELLS * 68];
     const float* hin = sH;
-    if (d.nce > 0) {
-        hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[1], false, sWm, w, lane);
-        hst.store(K, E, sWm, sWl);
-        __syncthreads();
+    if constexpr (CHAINS) {
+        if (d.nce > 0) {
+            hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[CHAINS ? 1 : 0], false, sWm, w, lane);
+            hst.store(K, E, sWm, sWl);
+            __syncthreads();
+        }
     }
     // heads on f32 MFMA (nb.hh:412-416), transposed back to lane = latent through LDS
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
-    heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
+    if (w < 4) heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
     __syncthreads();
     mark(3);
-    float mean[4], av[4];
-    const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
+    float mean[CPW], av[CPW];
+    const float bm = (k < K) ? p_bm : 0.f, bl = (k < K) ? p_bl : 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        mean[c] = bm + sM[(4 * w + c) * 68 + k];
-        av[c] = bl + sA[(4 * w + c) * 68 + k];
+    for (int c = 0; c < CPW; ++c) {
+        mean[c] = bm + sM[(cw + c) * 68 + k];
+        av[c] = bl + sA[(cw + c) * 68 + k];
     }
     float kl = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
         const bool valid = b < d.B;
         const int pb = pbv[c];
@@ -452,28 +477,30 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         if (k < K && b < d.B)
             eps = eps_in ? epv[c] : (dbg_bit(d.dbg, 4096) ? 0.f : philox_normal(seed, step, row_offset + pb, k));  // 4096: diagnostic
         const float z = mn + eps * sig;
-        if (k < KE) L[d.LAT_H + k] = sH[(4 * w + c) * 68 + k];
+        if (k < KE) L[d.LAT_H + k] = sH[(cw + c) * 68 + k];
         if (k < K) {
             L[d.LAT_MEAN + k] = mn;
             L[d.LAT_A + k] = a;
             L[d.LAT_EPS + k] = eps;
             if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
         }
-        if (d.ncd > 0) {
-            sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
+        if (CHAINS && d.ncd > 0) {
+            sZ[0][(cw + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
         } else if (k < d.KP && b < d.Bpad) {  // rows past this batch's padded size: none
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
             put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);  // hi plane (+ the x3 lo plane)
         }
         // ---- overdispersion latent (lanes r < R) ----
-        const float* rx = &sRX[4 * w + c][0];  // [0] = depth pre-activation, [1 + h] = nu_enc_h
+        const float* rx = &sRX[cw + c][0];  // [0] = depth pre-activation, [1 + h] = nu_enc_h
         if (k < d.R) {
-            float nm = P.bnm[k], an = P.bnl[k];
-            for (int hh = 0; hh < d.H; ++hh) {
-                nm += P.Wnm[k * d.H + hh] * rx[1 + hh];
-                an += P.Wnl[k * d.H + hh] * rx[1 + hh];
-            }
+            float nm = p_bnm, an = p_bnl;
+#pragma unroll
+            for (int hh = 0; hh < HMAX; ++hh)
+                if (hh < d.H) {
+                    nm += p_wnm[hh] * rx[1 + hh];
+                    an += p_wnl[hh] * rx[1 + hh];
+                }
             const float nlv = fminf(fmaxf(an, -4.f), 4.f);
             float en = 0.f;
             if (b < d.B)
@@ -494,19 +521,21 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
         }
     }
     if (mode == 1) return;
-    if (d.ncd > 0) {
-        // the frozen decoder chain (mu_decoding_l + ReLU with --relu, nb.hh:362-379): z -> zd,
-        // the big decoder GEMM's input
-        __syncthreads();
-        // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
-        const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[1], sM, false, sWm, w, lane);
+    if constexpr (CHAINS) {
+        if (d.ncd > 0) {
+            // the frozen decoder chain (mu_decoding_l + ReLU with --relu, nb.hh:362-379): z -> zd,
+            // the big decoder GEMM's input
+            __syncthreads();
+            // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
+            const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[CHAINS ? 1 : 0], sM, false, sWm, w, lane);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = bw + c;
-            if (k < d.KP && b < d.Bpad) {
-                const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
-                zf[(int64_t)b * d.KP + k] = zz;
-                put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+            for (int c = 0; c < CPW; ++c) {
+                const int b = bw + c;
+                if (k < d.KP && b < d.Bpad) {
+                    const float zz = (k < d.KD && b < d.B) ? zd[(cw + c) * 68 + k] : 0.f;
+                    zf[(int64_t)b * d.KP + k] = zz;
+                    put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+                }
             }
         }
     }
@@ -514,12 +543,21 @@ __global__ __launch_bounds__(256) void k_latent_fwd(
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
-    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * ((sred[0] + sred[1]) + (sred[2] + sred[3]));
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        if constexpr (NW == 4) {
+            t = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NW; i += 4) t += (sred[i] + sred[i + 1]) + (sred[i + 2] + sred[i + 3]);
+        }
+        klpart[blockIdx.x] = -0.5f * t;
+    }
     if (rts) {
         vm_wait_all();
         mark(5);
         if (lane == 0) {
-            float* o = P.dbg_out + ((int64_t)blockIdx.x * 4 + w) * 8;
+            float* o = P.dbg_out + ((int64_t)blockIdx.x * NW + w) * 8;
             for (int i = 0; i < 6; ++i) o[i] = (float)(rt_[i] & 0xffffffu);
             o[6] = o[5];
             o[7] = (float)wave_place();
@@ -1596,13 +1634,16 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
 // from LDS images with wave-uniform broadcast reads.  Every per-workgroup partial is a plain
 // store (fixed-order sums, no atomics); k_grad_small reduces the partials.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_latent_bwd(NBPtrs P, Dims d, const int64_t* __restrict__ cells,
                                                     const float* __restrict__ covar,
                                                     float* __restrict__ lat, const float* __restrict__ rowx,
                                                     const float* __restrict__ rowB,
                                                     const float* __restrict__ dzp, float* __restrict__ dh,
                                                     float* __restrict__ dhT_f, __bf16* __restrict__ dhT_b,
                                                     float* __restrict__ small) {
+    constexpr int CPW = LAT_CELLS / NW;  // cells per wave
+    constexpr bool CHAINS = NW == 4;     // the frozen chains' layers run on 256 threads
     const int K = d.K, C = d.C, H = d.H, R = d.R, KP = d.KP, E = d.E, KE = d.KE;
     const int SMALL = small_len(K, E, KE, C, 2 * R * H + 2 * R + H + 1);
     extern __shared__ __attribute__((aligned(16))) float lsm[];
@@ -1611,11 +1652,11 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     float* sDM = sWl + 64 * 65;       // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;  // [cell][68] dlnvar-pre-clamp (a)
     float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h0
-    float* wpart = sH + LAT_CELLS * 68; // [4][NSM] per-wave small partials
+    float* wpart = sH + LAT_CELLS * 68; // [NW][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
     // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
     // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
-    float* sCW = wpart + 4 * NSM;
+    float* sCW = wpart + NW * NSM;
     float* const sG0 = sCW + 64 * 65;  // gradient images sG(0), sG(1)
     auto sG = [&](int i) { return sG0 + i * (LAT_CELLS * 68); };
     float* cimg = sG0 + 2 * LAT_CELLS * 68;  // [nce + ncd + 1][LAT_CELLS * 68]
@@ -1628,15 +1669,17 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     mark(0);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * LAT_CELLS + 4 * w;  // 4 cells per wave
+    const int cw = CPW * w;                     // this wave's first cell in the workgroup
+    const int bw = blockIdx.x * LAT_CELLS + cw;  // ... in the batch
     // ---- every global input first (the waits are in issue order: one memory round) ----
     const int kk = min(k, K - 1), kr = min(k, R - 1), ke = min(k, KE - 1);
-    float vval[4], vw[4], vmean[4], va[4], veps[4], vh[4], vnm[4], van[4], ven[4], vpre[4], vrx[4][HMAX];
-    int64_t vcell[4];
+    float vval[CPW], vw[CPW], vmean[CPW], va[CPW], veps[CPW], vh[CPW], vnm[CPW], van[CPW], ven[CPW], vpre[CPW],
+        vrx[CPW][HMAX];
+    int64_t vcell[CPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
-        vcell[c] = cells[b];  // padding rows hold the empty row N
+        vcell[c] = covar ? cells[b] : 0;  // padding rows hold the empty row N (unit covariate: unread)
         const float* L = lat + (int64_t)b * d.lat_stride;
         vval[c] = L[d.LAT_VALID];
         vw[c] = L[d.LAT_W];
@@ -1652,28 +1695,35 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
 #pragma unroll
         for (int hh = 0; hh < HMAX; ++hh) vrx[c][hh] = (hh < H) ? rx[2 + hh] : 0.f;
     }
-    HeadsStage hst;
+    HeadsStage<64 * NW> hst;
     hst.issue(P.Wm, P.Wl, K, E);
-    float dzA4[4], dzP4[4];  // the decoder GEMM input's gradient terms (KD wide)
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < d.KD, dzA4);
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < d.KD, dzP4);
-    float E4[4], dzn4[4];  // pass B's per-split row sums: E_b and dL/dznu_b (lanes < R)
-    split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R), 2 + R, true, E4);
-    split_sum4(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R) + 2 + kr, 2 + R, k < R, dzn4);
+    // the nu heads' weights (lanes k < H: dh_nu = sum_q Wnm[q][k] dnm_q + Wnl[q][k] dan_q)
+    float p_wnm[RMAX], p_wnl[RMAX];
+#pragma unroll
+    for (int q = 0; q < RMAX; ++q) {
+        p_wnm[q] = P.Wnm[min(q, R - 1) * H + min(k, H - 1)];
+        p_wnl[q] = P.Wnl[min(q, R - 1) * H + min(k, H - 1)];
+    }
+    float dzA4[CPW], dzP4[CPW];  // the decoder GEMM input's gradient terms (KD wide)
+    split_sum<CPW>(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + k, 2 * KP, k < d.KD, dzA4);
+    split_sum<CPW>(dzp, d.nsD, (int64_t)d.Bpad * 2 * KP, (int64_t)bw * 2 * KP + KP + k, 2 * KP, k < d.KD, dzP4);
+    float E4[CPW], dzn4[CPW];  // pass B's per-split row sums: E_b and dL/dznu_b (lanes < R)
+    split_sum<CPW>(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R), 2 + R, true, E4);
+    split_sum<CPW>(rowB, d.nsD, (int64_t)d.Bpad * (2 + R), (int64_t)bw * (2 + R) + 2 + kr, 2 + R, k < R, dzn4);
     hst.store(K, E, sWm, sWl);
     mark(1);
     // with a decoder chain: dz at the latent = the chain's backward from dzd (z recomputed, the
     // chain outputs kept for the ReLU masks)
     const float* dzimg = nullptr;
-    if (d.ncd > 0) {
+    if (CHAINS && d.ncd > 0) {
         float* zimg = cimg + d.nce * LAT_CELLS * 68;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < CPW; ++c) {
             const int b = bw + c;
             const bool valid = (b < d.Bpad) && vval[c] > 0.f;
             const float lnvar = fminf(fmaxf(va[c], -4.f), 4.f);
-            zimg[(4 * w + c) * 68 + k] = (k < K) ? vmean[c] + veps[c] * expf(lnvar / 2.f) : 0.f;
-            sG(0)[(4 * w + c) * 68 + k] = (k < d.KD && valid) ? vw[c] * (dzA4[c] - E4[c] * dzP4[c]) : 0.f;
+            zimg[(cw + c) * 68 + k] = (k < K) ? vmean[c] + veps[c] * expf(lnvar / 2.f) : 0.f;
+            sG(0)[(cw + c) * 68 + k] = (k < d.KD && valid) ? vw[c] * (dzA4[c] - E4[c] * dzP4[c]) : 0.f;
         }
         __syncthreads();
         float* outs = zimg + LAT_CELLS * 68;  // decoder chain outputs [ncd]
@@ -1713,17 +1763,17 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         rdnl[h] = 0.f;
     }
     // ---- per cell: dmean, da (lane = k); the per-cell outputs to lat are stored after the loop ----
-    float o_dhn[4], o_dpre[4];
-    bool o_valid[4];
+    float o_dhn[CPW], o_dpre[CPW];
+    bool o_valid[CPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
         const bool valid = (b < d.Bpad) && vval[c] > 0.f;
         const float E = E4[c];
         const float wb = vw[c];
         float dmean = 0.f, da = 0.f;
         if (k < K) {
-            const float dz = dzimg ? dzimg[(4 * w + c) * 68 + k] : wb * (dzA4[c] - E * dzP4[c]);
+            const float dz = dzimg ? dzimg[(cw + c) * 68 + k] : wb * (dzA4[c] - E * dzP4[c]);
             const float mean = vmean[c], a = va[c], eps = veps[c];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
             const float sig = expf(lnvar / 2.f);
@@ -1735,14 +1785,14 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
                 da = 0.f;
             }
         }
-        sDM[(4 * w + c) * 68 + k] = dmean;
-        sDA[(4 * w + c) * 68 + k] = da;
-        sH[(4 * w + c) * 68 + k] = (k < KE && valid) ? vh[c] : 0.f;  // dW = dmean^T h: 0 * h must be 0
+        sDM[(cw + c) * 68 + k] = dmean;
+        sDA[(cw + c) * 68 + k] = da;
+        sH[(cw + c) * 68 + k] = (k < KE && valid) ? vh[c] : 0.f;  // dW = dmean^T h: 0 * h must be 0
         rbm += dmean;
         rbl += da;
 #pragma unroll
         for (int q = 0; q < CMAX; ++q)
-            if (q < C) rWce[q] += dmean * covar[vcell[c] * C + q];
+            if (q < C) rWce[q] += covar ? dmean * covar[vcell[c] * C + q] : dmean;  // unit: c = 1 (dmean 0 if invalid)
         // ---- overdispersion path (lanes < R) and depth (lane 0) ----
         float dnm = 0.f, dan = 0.f;
         if (k < R && valid) {
@@ -1762,10 +1812,12 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
             rbnl += dan;
         }
         float dhn = 0.f;
-        for (int q = 0; q < R; ++q) {
-            const float a1 = __shfl(dnm, q, 64), a2 = __shfl(dan, q, 64);
-            if (k < H) dhn += P.Wnm[q * H + k] * a1 + P.Wnl[q * H + k] * a2;
-        }
+#pragma unroll
+        for (int q = 0; q < RMAX; ++q)
+            if (q < R) {
+                const float a1 = __shfl(dnm, q, 64), a2 = __shfl(dan, q, 64);
+                if (k < H) dhn += p_wnm[q] * a1 + p_wnl[q] * a2;
+            }
         o_valid[c] = valid;
         o_dhn[c] = dhn;
         if (k < H && b < d.Bpad && valid) rbne += dhn;
@@ -1776,7 +1828,7 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
         }
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
         float* L = lat + (int64_t)b * d.lat_stride;
         if (k < H && b < d.Bpad) L[d.LAT_DHNU + k] = o_valid[c] ? o_dhn[c] : 0.f;
@@ -1786,13 +1838,13 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     __syncthreads();
     // the heads' input: h0, or the frozen encoder chain's output (recomputed, outputs kept)
     const float* hin = sH;
-    if (d.nce > 0) {
+    if (CHAINS && d.nce > 0) {
         hin = chain_run(d, 0, d.nce, sH, cimg, nullptr, true, sCW, w, lane);
     }
     // ---- dh0[16 cells][KE] on f32 MFMA (wave w: columns 16w..16w+15) ----
-    {
+    if (w < 4) {  // (NW = 16: waves 4.. have no head columns)
         f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, E, w, lane);
-        if (d.nce > 0) {  // back through the encoder chain
+        if (CHAINS && d.nce > 0) {  // back through the encoder chain
             img_store(sG(0), acc, w, lane);
             __syncthreads();
             int g = 0;
@@ -1842,39 +1894,43 @@ __global__ __launch_bounds__(256) void k_latent_bwd(NBPtrs P, Dims d, const int6
     // ---- dWm, dWl = [dmean | da]^T h over the workgroup's cells on f32 MFMA ----
     float* out = small + (int64_t)blockIdx.x * SMALL;
     mark(4);
-    heads_dW(sDM, sDA, hin, K, E, w, lane, out);
+    if (w < 4) heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     mark(5);
     __syncthreads();
     // ---- the small vectors: fixed-order sum of the four waves' partials ----
     const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + KE,
               o_bnm = o_nm + R * H, o_nl = o_bnm + R, o_bnl = o_nl + R * H, o_bne = o_bnl + R, o_bdp = o_bne + H;
-    auto wsum = [&](int off) {
-        return (wpart[0 * NSM + off] + wpart[1 * NSM + off]) + (wpart[2 * NSM + off] + wpart[3 * NSM + off]);
+    auto wsum = [&](int off) {  // fixed order over the waves, four at a time
+        float t = (wpart[0 * NSM + off] + wpart[1 * NSM + off]) + (wpart[2 * NSM + off] + wpart[3 * NSM + off]);
+#pragma unroll
+        for (int i = 4; i < NW; i += 4)
+            t += (wpart[i * NSM + off] + wpart[(i + 1) * NSM + off]) + (wpart[(i + 2) * NSM + off] + wpart[(i + 3) * NSM + off]);
+        return t;
     };
-    for (int i = threadIdx.x; i < K; i += 256) {
+    for (int i = threadIdx.x; i < K; i += 64 * NW) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
         for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
     }
-    for (int i = threadIdx.x; i < KE; i += 256) out[o_dhs + i] = wsum(128 + i);
+    for (int i = threadIdx.x; i < KE; i += 64 * NW) out[o_dhs + i] = wsum(128 + i);
     const int b_nm = 192 + 64 * CMAX, b_nl = b_nm + RMAX * HMAX, b_bnm = b_nl + RMAX * HMAX, b_bnl = b_bnm + RMAX,
               b_bne = b_bnl + RMAX, b_bdp = b_bne + HMAX;
-    for (int i = threadIdx.x; i < R * H; i += 256) {
+    for (int i = threadIdx.x; i < R * H; i += 64 * NW) {
         const int r2 = i / H, h2 = i % H;
         out[o_nm + i] = wsum(b_nm + r2 * HMAX + h2);
         out[o_nl + i] = wsum(b_nl + r2 * HMAX + h2);
     }
-    for (int i = threadIdx.x; i < R; i += 256) {
+    for (int i = threadIdx.x; i < R; i += 64 * NW) {
         out[o_bnm + i] = wsum(b_bnm + i);
         out[o_bnl + i] = wsum(b_bnl + i);
     }
-    for (int i = threadIdx.x; i < H; i += 256) out[o_bne + i] = wsum(b_bne + i);
+    for (int i = threadIdx.x; i < H; i += 64 * NW) out[o_bne + i] = wsum(b_bne + i);
     if (threadIdx.x == 0) out[o_bdp] = wsum(b_bdp);
     if (rts) {
         vm_wait_all();
         mark(6);
         if (lane == 0) {
-            float* o = P.dbg_out + ((int64_t)blockIdx.x * 4 + w) * 8;
+            float* o = P.dbg_out + ((int64_t)blockIdx.x * NW + w) * 8;
             for (int i = 0; i < 7; ++i) o[i] = (float)(rt_[i] & 0xffffffu);
             o[7] = (float)wave_place();
         }
@@ -2390,11 +2446,29 @@ static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     return Q;
 }
 
+// k_latent_fwd: one cell per wave (16 waves, 1024 threads) when there are no frozen hidden
+// chains; MMVAE_LAT_NW=4 forces the 4-wave instance (4 cells per wave)
+static bool latent_nw16(const Dims& d) {
+    static const bool nw4 = getenv_is("MMVAE_LAT_NW", "4");
+    return !nw4 && d.nce == 0 && d.ncd == 0;
+}
+static void latent_fwd_launch(Engine* e, const NBPtrs& P, const Dims& d, const float* covar, const float* eps,
+                              const int32_t* perm, int mode, float* out_mean, float* out_lnvar, hipStream_t st) {
+    const bool nw16 = latent_nw16(d);
+    auto go = [&](auto kern, int nth) {
+        hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), 0, st, P, d, e->d_cells, covar, e->d_hpart, e->d_mvec,
+                           e->d_rowxp, e->d_rowx, eps, perm, e->cfg.seed, e->d_ss, e->d_lat, e->d_zf, e->d_zb,
+                           e->d_lossp + e->klp_off, mode, out_mean, out_lnvar);
+    };
+    if (nw16) go(k_latent_fwd<16>, 1024);
+    else go(k_latent_fwd<4>, 256);
+}
+
 // k_latent_bwd's LDS: head weights, 3 cell images, the per-wave partials; with hidden layers
 // also the chain W stage, 2 gradient images and the recomputed chain outputs
-static size_t latent_bwd_lds(const Engine* e) {
+static size_t latent_bwd_lds(const Engine* e, int nw) {
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * NSM;
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + (size_t)nw * NSM;
     if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
     return f * 4;
 }
@@ -2411,20 +2485,21 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     hipStream_t st = e->stream;
     const int nrb = d.nrb;
     float* gene = e->d_gene;  // k_prep ran before the batch lists (nb_prep)
+    // unit covariate (no covariate file): the CM = 0 decoder instances fold it into per-gene
+    // constants, and the latent kernels skip the covariate gather (a null pointer: c = 1)
+    const bool ucov = d.C == 1 && e->unit_covar;
+    const float* lat_covar = ucov ? nullptr : e->d_covar;
     {
         ScopedTimer tm(e, "k_enc_fwd");
         enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);  // fp8 mode: the e4m3 encoder GEMM (PM = F8)
     }
     {
         ScopedTimer tm(e, "k_latent_fwd");
-        hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                           e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, use_eps ? e->d_eps : nullptr,
-                           e->perm_active ? e->d_perm : nullptr, e->cfg.seed, e->d_ss, e->d_lat, e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 0, nullptr, nullptr);
+        latent_fwd_launch(e, P, d, lat_covar, use_eps ? e->d_eps : nullptr, e->perm_active ? e->d_perm : nullptr, 0,
+                          nullptr, nullptr, st);
     }
     const DecPtrs Q = dec_ptrs(e, d, P, bf);
     const bool small_cr = (d.C == 1 && d.R == 1);
-    // unit covariate (no covariate file): the CM = 0 instances fold it into per-gene constants
-    const bool ucov = d.C == 1 && e->unit_covar;
     // pass B: 16 NW rows per workgroup.  bf16: NW = 8 with double-buffered stages (one barrier
     // per tile); x3: NW = 8 single-buffered (the hi + lo images of double buffers exceed the
     // 160 KB LDS); f32 or MMVAE_DEC_NW=4: NW = 4 (64 rows, two workgroups per CU)
@@ -2516,9 +2591,14 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     {
         ScopedTimer tm(e, "k_latent_bwd");
-        const size_t lds = latent_bwd_lds(e);
-        hipLaunchKernelGGL(k_latent_bwd, dim3(e->n_lat_wg), dim3(256), lds, st, P, d, e->d_cells, e->d_covar,
-                           e->d_lat, e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
+        const bool nw16 = latent_nw16(d);
+        const size_t lds = latent_bwd_lds(e, nw16 ? 16 : 4);
+        auto go = [&](auto kern, int nth) {
+            hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), lds, st, P, d, e->d_cells, lat_covar, e->d_lat,
+                               e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
+        };
+        if (nw16) go(k_latent_bwd<16>, 1024);
+        else go(k_latent_bwd<4>, 256);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     // (one double per block, fixed order), so k_adam folds them and k_sumsq is skipped
@@ -2610,10 +2690,7 @@ template <class PM, int KP>
 static hipError_t nb_encode_t(Engine* e, const Dims& d, const NBPtrs& P, float* d_mean, float* d_lnvar) {
     hipStream_t st = e->stream;
     enc_fwd_run<PM, KP>(e, d, e->d_hpart, st);
-    hipLaunchKernelGGL(k_latent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar,
-                       e->d_hpart, e->d_mvec, e->d_rowxp, e->d_rowx, nullptr, (const int32_t*)nullptr, e->cfg.seed, e->d_ss,
-                       e->d_lat,
-                       e->d_zf, e->d_zb, e->d_lossp + e->klp_off, 1, d_mean, d_lnvar);
+    latent_fwd_launch(e, P, d, e->d_covar, nullptr, nullptr, 1, d_mean, d_lnvar, st);
     return hipGetLastError();
 }
 

@@ -67,26 +67,46 @@ MMVAE_DEV void stage_copy_part(const StageCopy& sc) {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < sc.n16; i += gridDim.x * 256) sc.dst[i] = sc.src[i];
 }
 
-// out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c = 0..3: the split
-// partials of four cells, loads issued four splits at a time (independent, then summed)
-MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, int64_t off, int64_t cstride, bool on,
-                          float (&out)[4]) {
+// out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c < NC (NC = 4 or 1 cells):
+// the split partials, loads issued 16 / NC splits at a time (independent, then summed).  The
+// summation order is the same for any NC — groups of four splits, (v0 + v1) + (v2 + v3), added in
+// split order, then the single splits — so a cell's sum does not depend on the cells per wave.
+template <int NC>
+MMVAE_DEV void split_sum(const float* __restrict__ p, int ns, int64_t sstride, int64_t off, int64_t cstride, bool on,
+                         float (&out)[NC]) {
+    static_assert(NC == 1 || NC == 2 || NC == 4, "split_sum: 1, 2 or 4 cells");
+    constexpr int G = 16 / NC;  // splits per batch of loads
 #pragma unroll
-    for (int c = 0; c < 4; ++c) out[c] = 0.f;
+    for (int c = 0; c < NC; ++c) out[c] = 0.f;
     if (!on) return;
     int s = 0;
+    for (; s + G <= ns; s += G) {
+        float v[G][NC];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[u][c] = p[(int64_t)(s + u) * sstride + off + c * cstride];
+#pragma unroll
+        for (int g = 0; g < G / 4; ++g)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) out[c] += (v[4 * g][c] + v[4 * g + 1][c]) + (v[4 * g + 2][c] + v[4 * g + 3][c]);
+    }
     for (; s + 4 <= ns; s += 4) {
-        float v[4][4];
+        float v[4][NC];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) v[u][c] = p[(int64_t)(s + u) * sstride + off + c * cstride];
+            for (int c = 0; c < NC; ++c) v[u][c] = p[(int64_t)(s + u) * sstride + off + c * cstride];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) out[c] += (v[0][c] + v[1][c]) + (v[2][c] + v[3][c]);
+        for (int c = 0; c < NC; ++c) out[c] += (v[0][c] + v[1][c]) + (v[2][c] + v[3][c]);
     }
     for (; s < ns; ++s)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) out[c] += p[(int64_t)s * sstride + off + c * cstride];
+        for (int c = 0; c < NC; ++c) out[c] += p[(int64_t)s * sstride + off + c * cstride];
+}
+MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, int64_t off, int64_t cstride, bool on,
+                          float (&out)[4]) {
+    split_sum<4>(p, ns, sstride, off, cstride, on, out);
 }
 
 MMVAE_DEV void wave_sync() {
@@ -243,16 +263,27 @@ template <class P> MMVAE_DEV void put_op(typename Elem<P>::type* t, int idx, int
 }
 
 // mvec[k] from the per-256-gene-block partials [nblk][KP] written by k_prep / k_vprep: the
-// workgroup's 256 threads each sum a quarter of the blocks of one latent (fixed order), the
-// quarters are combined in order through LDS.  All threads call it; valid for k < 64.
+// workgroup's first 256 threads each sum a quarter of the blocks of one latent (fixed order,
+// loads issued 16 at a time), the quarters are combined in order through LDS.  All threads of
+// the block call it; valid for k < 64.
 MMVAE_DEV float mvec_sum(const float* __restrict__ mvecp, int nblk, int KP, int k) {
     __shared__ float smv[4][64];
     const int kk = threadIdx.x & 63, part = threadIdx.x >> 6;
-    float s = 0.f;
-    if (kk < KP)
-#pragma unroll 8
-        for (int i = part; i < nblk; i += 4) s += mvecp[(int64_t)i * KP + kk];
-    smv[part][kk] = s;
+    if (part < 4) {
+        float s = 0.f;
+        if (kk < KP) {
+            int i = part;
+            for (; i + 4 * 15 < nblk; i += 64) {
+                float v[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = mvecp[(int64_t)(i + 4 * j) * KP + kk];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) s += v[j];
+            }
+            for (; i < nblk; i += 4) s += mvecp[(int64_t)i * KP + kk];
+        }
+        smv[part][kk] = s;
+    }
     __syncthreads();
     return (smv[0][k] + smv[1][k]) + (smv[2][k] + smv[3][k]);
 }
@@ -295,13 +326,15 @@ MMVAE_DEV float sum_partials(const float* __restrict__ small, int nwg, int SMALL
 // The K x E head weights (Wm, Wl; K, E <= 64) into LDS [k][65]: issue() loads into registers
 // (clamped, unconditional addresses: counted waits), store() writes LDS — other loads issued
 // between the two share the same memory round.
+template <int NTH = 256>
 struct HeadsStage {
-    float tm[16], tl[16];
+    static constexpr int NU = 4096 / NTH;  // K * E <= 64 * 64 values per thread group
+    float tm[NU], tl[NU];
     MMVAE_DEV void issue(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, int E) {
         const int KK = K * E;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int i = min((int)threadIdx.x + 256 * u, KK - 1);
+        for (int u = 0; u < NU; ++u) {
+            const int i = min((int)threadIdx.x + NTH * u, KK - 1);
             tm[u] = Wm[i];
             tl[u] = Wl[i];
         }
@@ -309,8 +342,8 @@ struct HeadsStage {
     MMVAE_DEV void store(int K, int E, float* sWm, float* sWl) const {
         const int KK = K * E;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int i = (int)threadIdx.x + 256 * u;
+        for (int u = 0; u < NU; ++u) {
+            const int i = (int)threadIdx.x + NTH * u;
             if (i < KK) {
                 sWm[(i / E) * 65 + i % E] = tm[u];
                 sWl[(i / E) * 65 + i % E] = tl[u];
@@ -320,7 +353,7 @@ struct HeadsStage {
 };
 MMVAE_DEV void load_heads_lds(const float* __restrict__ Wm, const float* __restrict__ Wl, int K, int E, float* sWm,
                               float* sWl) {
-    HeadsStage hs;
+    HeadsStage<> hs;
     hs.issue(Wm, Wl, K, E);
     hs.store(K, E, sWm, sWl);
 }

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
     __shared__ float sred[4];
-    HeadsStage hst;
+    HeadsStage<> hst;
     hst.issue(P.Wm, P.Wl, K, E);
     if (d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -215,14 +215,18 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int b = bw + c;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
         const bool valid = b < d.B;
         float* L = lat + (int64_t)b * d.lat_stride;
         float mn = mean[c];
         const float a = av[c];
         if (k < K && mode == 0) {
             float cm = P.bce[k];
-            for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
+            if (!covar) {  // unit covariate (Engine::unit_covar): c = 1, padding rows (row N) 0
+                cm += valid ? P.Wce[k] : 0.f;
+            } else {
+                const int64_t cell = cells[b];  // padding rows hold the empty row N
+                for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
+            }
             mn += cm;
         }
         const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
@@ -883,10 +887,14 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         if (k == 0) sH[(4 * w + c) * 68 + 64] = inx[c];  // 1/||l|| beside the cell's h
         rbm += dmean;
         rbl += da;
-        const int64_t cell = cells[b];  // padding rows hold the empty row N
+        if (!covar) {  // unit covariate (Engine::unit_covar): c = 1 (dmean is 0 on padding rows)
+            rWce[0] += dmean;
+        } else {
+            const int64_t cell = cells[b];  // padding rows hold the empty row N
 #pragma unroll
-        for (int q = 0; q < CMAX; ++q)
-            if (q < C) rWce[q] += dmean * covar[cell * C + q];
+            for (int q = 0; q < CMAX; ++q)
+                if (q < C) rWce[q] += dmean * covar[cell * C + q];
+        }
     }
     for (int i = lane; i < NSM; i += 64) wpart[w][i] = 0.f;
     __syncthreads();
@@ -1251,6 +1259,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     hipStream_t st = e->stream;
     const int nrb = d.nrb;
     float* gene = e->d_gene;  // k_vprep ran before the batch lists (vmf_prep)
+    const bool ucov = d.C == 1 && e->unit_covar;  // the CM = 0 decoder instances
+    const float* lat_covar = ucov ? nullptr : e->d_covar;  // latent kernels: no covariate gather
     {
         ScopedTimer tm(e, "k_enc_fwd");
         hipError_t er = enc_forward_launch(e, d, e->d_hpart);
@@ -1258,7 +1268,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_fwd");
-        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, e->d_covar, e->d_hpart,
+        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, mode == 1 ? e->d_covar : lat_covar, e->d_hpart,
                            e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr,
                            (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, e->d_ss,
                            e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
@@ -1287,7 +1297,6 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.zplane = (int64_t)d.Bpad * d.KP;
     Q.wplane = (int64_t)e->KP * e->DP;
     const dim3 gdec(nrb * d.nsD);
-    const bool ucov = d.C == 1 && e->unit_covar;  // the CM = 0 decoder instances
     const int nq = 1 + d.C;
     const int S = d.tpsD + 1;
     {
@@ -1328,7 +1337,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");
-        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), vlat_bwd_lds(e), st, P, d, e->d_cells, e->d_covar, e->d_lat,
+        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), vlat_bwd_lds(e), st, P, d, e->d_cells, lat_covar, e->d_lat,
                            e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials

@@ -6,7 +6,7 @@ KER = os.environ.get("KER", "bwd")
 os.environ["MMVAE_DBG"] = str((1024 if KER == "bwd" else 2048) | int(os.environ.get("EXTRA", "0")))
 import mmvae_amd
 B, D, K = 4096, 20000, 64
-eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype="bf16", seed=1)
+eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=os.environ.get("DTYPE", "bf16x3"), seed=1)
 eng.synth_csr(100000, lib_size=2000.0, seed=3)
 eng.init_params(seed=7)
 for i in range(3):  # fwd: eval path (pass C, which also writes slabC, does not run)
