@@ -154,75 +154,95 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
 //   mode 1 = recorder encode(x) (vmf.hh:267-281): no covariate, writes mean/lnvar out.
 // Per-row state kept for the backward: h, mean, pre-clamp a, eps, 1/||l|| (LAT_D), valid.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_vlatent_fwd(
+// NW = 16 (one cell per wave, 1024 threads; no frozen chains): see k_latent_fwd (nb_kernels.hip).
+// Every global load is issued before the first global store.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_vlatent_fwd(
     VPtrs P, Dims d, const int64_t* __restrict__ cells, const float* __restrict__ covar,
     const float* __restrict__ hpart, const float* __restrict__ mvec, const float2* __restrict__ cellnorm,
     float* __restrict__ rowx, const float* __restrict__ eps_in, const int32_t* __restrict__ perm, uint64_t seed,
     const StepScalars* __restrict__ ss,
     float* __restrict__ lat, float* __restrict__ zf, __bf16* __restrict__ zb,
     float* __restrict__ klpart, int mode, float* __restrict__ out_mean, float* __restrict__ out_lnvar) {
+    constexpr int CPW = LAT_CELLS / NW;  // cells per wave
+    constexpr bool CHAINS = NW == 4;     // the frozen chains' layers run on 256 threads
     const int K = d.K, KE = d.KE, E = d.E;
     const uint64_t step = (uint64_t)ss->step_id;  // the noise key (staged with the batch)
     const int64_t row_offset = ss->row_offset;
     __shared__ float sWm[64 * 65], sWl[64 * 65];
     __shared__ __attribute__((aligned(16))) float sH[LAT_CELLS * 68];
-    __shared__ float sred[4];
-    HeadsStage<> hst;
+    __shared__ float sred[NW];
+    HeadsStage<64 * NW> hst;
     hst.issue(P.Wm, P.Wl, K, E);
-    if (d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * LAT_CELLS + 4 * w;
-    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
-    const float mk = (k < KE) ? mvk : 0.f;
-    float inx[4], hs[4];
-    split_sum4(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
+    const int cw = CPW * w;                     // this wave's first cell in the workgroup
+    const int bw = blockIdx.x * LAT_CELLS + cw;  // ... in the batch
+    float hs[CPW];
+    split_sum<CPW>(hpart, d.nsE, (int64_t)d.Bpad * d.KP, (int64_t)bw * d.KP + k, d.KP, k < KE, hs);
+    // per-lane parameters and per-cell inputs (clamped, unconditional loads where possible)
+    const int kk = min(k, K - 1);
+    const float p_bm = P.bm[kk], p_bl = P.bl[kk], p_bce = P.bce[kk], p_wce = P.Wce[(int64_t)kk * d.C];
+    float2 cn[CPW];
+    int pbv[CPW];
+    float epv[CPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
+        const int b = bw + c;
+        cn[c] = cellnorm[cells[b]];  // row norms from the dataset index (row Ncells = the empty padding row)
+        pbv[c] = (perm && b < d.B) ? perm[b] : b;  // original batch position: the noise key
+        epv[c] = (eps_in && k < K && b < d.B) ? eps_in[(int64_t)pbv[c] * K + k] : 0.f;
+    }
+    const float mvk = mvec_sum(mvec, d.nmv, d.KP, k);  // all threads (LDS combine)
+    if (!CHAINS || d.nce == 0) hst.store(K, E, sWm, sWl);  // (with an encoder chain: after it, sWm stages its W)
+    const float mk = (k < KE) ? mvk : 0.f;
+    float inx[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
         if (b >= d.B) hs[c] = 0.f;  // past this batch: partials unwritten this step (NB k_latent_fwd)
-        // row norms from the dataset index (row Ncells = the empty padding row)
-        const float2 cn = cellnorm[cells[b]];
-        inx[c] = 1.f / fmaxf(sqrtf(cn.x), 1e-12f);  // F::normalize
+        inx[c] = 1.f / fmaxf(sqrtf(cn[c].x), 1e-12f);  // F::normalize
         if (mode == 0 && k == 0) {
-            rowx[(int64_t)b * d.rowx_stride] = cn.x;
-            rowx[(int64_t)b * d.rowx_stride + 1] = cn.y;
+            rowx[(int64_t)b * d.rowx_stride] = cn[c].x;
+            rowx[(int64_t)b * d.rowx_stride + 1] = cn[c].y;
         }
         const float hv = hs[c] * inx[c] - mk;  // Angular output; --relu appends ReLU (vmf.hh:351-352)
-        sH[(4 * w + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
+        sH[(cw + c) * 68 + k] = (k < KE) ? (d.relu ? fmaxf(hv, 0.f) : hv) : 0.f;
     }
     __syncthreads();
     // the frozen Angular chain (encoding_l, l >= 2, + ReLU with --relu: vmf.hh:338-347)
-    __shared__ float sZ[2][LAT_CELLS * 68];
+    __shared__ float sZ[CHAINS ? 2 : 1][LAT_CELLS * 68];
     const float* hin = sH;
-    if (d.nce > 0) {
-        hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[1], false, sWm, w, lane);
-        hst.store(K, E, sWm, sWl);
-        __syncthreads();
+    if constexpr (CHAINS) {
+        if (d.nce > 0) {
+            hin = chain_run(d, 0, d.nce, sH, sZ[0], sZ[CHAINS ? 1 : 0], false, sWm, w, lane);
+            hst.store(K, E, sWm, sWl);
+            __syncthreads();
+        }
     }
     // heads on f32 MFMA (vmf.hh:259-264), transposed back to lane = latent through LDS
     __shared__ float sM[LAT_CELLS * 68], sA[LAT_CELLS * 68];
-    heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
+    if (w < 4) heads_fwd(hin, sWm, sWl, K, E, w, lane, sM, sA);
     __syncthreads();
-    float mean[4], av[4];
-    const float bm = (k < K) ? P.bm[k] : 0.f, bl = (k < K) ? P.bl[k] : 0.f;
+    float mean[CPW], av[CPW];
+    const float bm = (k < K) ? p_bm : 0.f, bl = (k < K) ? p_bl : 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        mean[c] = bm + sM[(4 * w + c) * 68 + k];
-        av[c] = bl + sA[(4 * w + c) * 68 + k];
+    for (int c = 0; c < CPW; ++c) {
+        mean[c] = bm + sM[(cw + c) * 68 + k];
+        av[c] = bl + sA[(cw + c) * 68 + k];
     }
     float kl = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
         const bool valid = b < d.B;
         float* L = lat + (int64_t)b * d.lat_stride;
         float mn = mean[c];
         const float a = av[c];
         if (k < K && mode == 0) {
-            float cm = P.bce[k];
+            float cm = p_bce;
             if (!covar) {  // unit covariate (Engine::unit_covar): c = 1, padding rows (row N) 0
-                cm += valid ? P.Wce[k] : 0.f;
+                cm += valid ? p_wce : 0.f;
             } else {
                 const int64_t cell = cells[b];  // padding rows hold the empty row N
                 for (int q = 0; q < d.C; ++q) cm += P.Wce[k * d.C + q] * covar[cell * d.C + q];
@@ -239,19 +259,18 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         }
         const float sig = expf(lnvar / 2.f);
         float eps = 0.f;
-        const int pb = (perm && b < d.B) ? perm[b] : b;  // original batch position: the noise key
-        if (k < K && b < d.B)
-            eps = eps_in ? eps_in[(int64_t)pb * K + k] : philox_normal(seed, step, row_offset + pb, k);
+        const int pb = pbv[c];
+        if (k < K && b < d.B) eps = eps_in ? epv[c] : philox_normal(seed, step, row_offset + pb, k);
         const float z = mn + eps * sig;
-        if (k < KE) L[d.LAT_H + k] = sH[(4 * w + c) * 68 + k];
+        if (k < KE) L[d.LAT_H + k] = sH[(cw + c) * 68 + k];
         if (k < K) {
             L[d.LAT_MEAN + k] = mn;
             L[d.LAT_A + k] = a;
             L[d.LAT_EPS + k] = eps;
             if (valid) kl += 1.f + lnvar - mn * mn - expf(lnvar);
         }
-        if (d.ncd > 0) {
-            sZ[0][(4 * w + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
+        if (CHAINS && d.ncd > 0) {
+            sZ[0][(cw + c) * 68 + k] = (k < K) ? z : 0.f;  // the decoder chain's input (below)
         } else if (k < d.KP && b < d.Bpad) {  // rows past this batch's padded size: none
             const float zz = (k < K && valid) ? z : 0.f;
             zf[(int64_t)b * d.KP + k] = zz;
@@ -263,25 +282,32 @@ __global__ __launch_bounds__(256) void k_vlatent_fwd(
         }
     }
     if (mode == 1) return;
-    if (d.ncd > 0) {
-        // the frozen decoder chain (decoding_l + ReLU with --relu, vmf.hh:374-381): z -> zd
-        __syncthreads();
-        // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
-        const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[1], sM, false, sWm, w, lane);
+    if constexpr (CHAINS) {
+        if (d.ncd > 0) {
+            // the frozen decoder chain (decoding_l + ReLU with --relu, vmf.hh:374-381): z -> zd
+            __syncthreads();
+            // ping-pong sZ[1] / sM (free: the means were read before the cell loop)
+            const float* zd = chain_run(d, d.nce, d.nce + d.ncd, sZ[0], sZ[CHAINS ? 1 : 0], sM, false, sWm, w, lane);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = bw + c;
-            if (k < d.KP && b < d.Bpad) {
-                const float zz = (k < d.KD && b < d.B) ? zd[(4 * w + c) * 68 + k] : 0.f;
-                zf[(int64_t)b * d.KP + k] = zz;
-                put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+            for (int c = 0; c < CPW; ++c) {
+                const int b = bw + c;
+                if (k < d.KP && b < d.Bpad) {
+                    const float zz = (k < d.KD && b < d.B) ? zd[(cw + c) * 68 + k] : 0.f;
+                    zf[(int64_t)b * d.KP + k] = zz;
+                    put_op<X3>(zb, b * d.KP + k, d.Bpad * d.KP, zz);
+                }
             }
         }
     }
     kl = wave_sum(kl);
     if (lane == 0) sred[w] = kl;
     __syncthreads();
-    if (threadIdx.x == 0) klpart[blockIdx.x] = -0.5f * ((sred[0] + sred[1]) + (sred[2] + sred[3]));
+    if (threadIdx.x == 0) {
+        float t = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+#pragma unroll
+        for (int i = 4; i < NW; i += 4) t += (sred[i] + sred[i + 1]) + (sred[i + 2] + sred[i + 3]);
+        klpart[blockIdx.x] = -0.5f * t;
+    }
 }
 
 // =======================================================================================
@@ -801,10 +827,13 @@ __global__ __launch_bounds__(256) void k_vrowfin(Dims d, float epsD, const float
 //   dh = dmean Wm + da Wl;  dWm += dmean^T h, dWl += da^T h (per-workgroup partials)
 // dhT (encoder backward operand) = dh / ||l||; the x_mean gradient needs the unscaled sum.
 // =======================================================================================
-__global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int64_t* __restrict__ cells,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_vlatent_bwd(VPtrs P, Dims d, const int64_t* __restrict__ cells,
                                                      const float* __restrict__ covar, const float* __restrict__ lat,
                                                      const float* __restrict__ dzp, float* __restrict__ dhT_f,
                                                      __bf16* __restrict__ dhT_b, float* __restrict__ small) {
+    constexpr int CPW = LAT_CELLS / NW;  // cells per wave (NW = 16: no frozen chains)
+    constexpr bool CHAINS = NW == 4;
     const int K = d.K, C = d.C, KP = d.KP, E = d.E, KE = d.KE;
     const int SMALL = small_len(K, E, KE, C, 0);
     constexpr int NSM = 3 * 64 + 64 * CMAX;
@@ -814,32 +843,45 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
     float* sDM = sWl + 64 * 65;            // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;     // [cell][68] d(pre-clamp lnvar)
     float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h0 (column 64: 1/||l||)
-    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [4][NSM]
+    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [NW][NSM]
     // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
     // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
-    float* sCW = &wpart[4][0];
+    float* sCW = &wpart[NW][0];
     float* const sG0 = sCW + 64 * 65;  // gradient images sG(0), sG(1)
     auto sG = [&](int i) { return sG0 + i * (LAT_CELLS * 68); };
     float* cimg = sG0 + 2 * LAT_CELLS * 68;
-    load_heads_lds(P.Wm, P.Wl, K, E, sWm, sWl);
+    // every global input first (one memory round): head weights, dz split partials, the cells' latent records
+    HeadsStage<64 * NW> hst;
+    hst.issue(P.Wm, P.Wl, K, E);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = lane;
-    const int bw = blockIdx.x * LAT_CELLS + 4 * w;
-    float dz4[4];  // the decoder GEMM input's gradient (KD wide)
-    split_sum4(dzp, d.nsD, (int64_t)d.Bpad * KP, (int64_t)bw * KP + k, KP, k < d.KD, dz4);
+    const int cw = CPW * w;                     // this wave's first cell in the workgroup
+    const int bw = blockIdx.x * LAT_CELLS + cw;  // ... in the batch
+    float dz4[CPW];  // the decoder GEMM input's gradient (KD wide)
+    split_sum<CPW>(dzp, d.nsD, (int64_t)d.Bpad * KP, (int64_t)bw * KP + k, KP, k < d.KD, dz4);
+    const int kk = min(k, K - 1), ke = min(k, KE - 1);
+    float vval[CPW], vinx[CPW], vh[CPW], vmean[CPW], va[CPW], veps[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const float* L = lat + (int64_t)(bw + c) * d.lat_stride;
+        vval[c] = L[d.LAT_VALID];
+        vinx[c] = L[d.LAT_D];
+        vh[c] = L[d.LAT_H + ke];
+        vmean[c] = L[d.LAT_MEAN + kk];
+        va[c] = L[d.LAT_A + kk];
+        veps[c] = L[d.LAT_EPS + kk];
+    }
+    hst.store(K, E, sWm, sWl);
     // with a decoder chain: dz at the latent = the chain's backward from dzd (z recomputed, the
     // chain outputs kept for the ReLU masks)
     const float* dzimg = nullptr;
-    if (d.ncd > 0) {
+    if (CHAINS && d.ncd > 0) {
         float* zimg = cimg + d.nce * LAT_CELLS * 68;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = bw + c;
-            const float* L = lat + (int64_t)b * d.lat_stride;
-            const int kk = min(k, K - 1);
-            const float lnvar = fminf(fmaxf(L[d.LAT_A + kk], -4.f), 4.f);
-            zimg[(4 * w + c) * 68 + k] = (k < K) ? L[d.LAT_MEAN + kk] + L[d.LAT_EPS + kk] * expf(lnvar / 2.f) : 0.f;
-            sG(0)[(4 * w + c) * 68 + k] = (k < d.KD && L[d.LAT_VALID] > 0.f) ? dz4[c] : 0.f;
+        for (int c = 0; c < CPW; ++c) {
+            const float lnvar = fminf(fmaxf(va[c], -4.f), 4.f);
+            zimg[(cw + c) * 68 + k] = (k < K) ? vmean[c] + veps[c] * expf(lnvar / 2.f) : 0.f;
+            sG(0)[(cw + c) * 68 + k] = (k < d.KD && vval[c] > 0.f) ? dz4[c] : 0.f;
         }
         __syncthreads();
         float* outs = zimg + LAT_CELLS * 68;  // decoder chain outputs [ncd]
@@ -856,21 +898,18 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
         dzimg = sG(g);
     }
     const float bn = d.beta * d.inv_n;
-    float rbm = 0.f, rbl = 0.f, rWce[CMAX], inx[4];
+    float rbm = 0.f, rbl = 0.f, rWce[CMAX];
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) rWce[c] = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPW; ++c) {
         const int b = bw + c;
-        const float* L = lat + (int64_t)b * d.lat_stride;
-        const bool valid = L[d.LAT_VALID] > 0.f;
-        inx[c] = L[d.LAT_D];
+        const bool valid = vval[c] > 0.f;
         float dmean = 0.f, da = 0.f;
-        const float h = (k < KE && valid) ? L[d.LAT_H + k] : 0.f;  // dW = dmean^T h: 0 * h must be 0
+        const float h = (k < KE && valid) ? vh[c] : 0.f;  // dW = dmean^T h: 0 * h must be 0
         if (k < K) {
-            const float dz = dzimg ? dzimg[(4 * w + c) * 68 + k]
-                                   : (c == 0) ? dz4[0] : (c == 1) ? dz4[1] : (c == 2) ? dz4[2] : dz4[3];
-            const float mean = L[d.LAT_MEAN + k], a = L[d.LAT_A + k], eps = L[d.LAT_EPS + k];
+            const float dz = dzimg ? dzimg[(cw + c) * 68 + k] : dz4[c];
+            const float mean = vmean[c], a = va[c], eps = veps[c];
             const float lnvar = fminf(fmaxf(a, -4.f), 4.f);
             const float sig = expf(lnvar / 2.f);
             dmean = dz + bn * mean;
@@ -881,10 +920,10 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
                 da = 0.f;
             }
         }
-        sDM[(4 * w + c) * 68 + k] = dmean;
-        sDA[(4 * w + c) * 68 + k] = da;
-        sH[(4 * w + c) * 68 + k] = h;
-        if (k == 0) sH[(4 * w + c) * 68 + 64] = inx[c];  // 1/||l|| beside the cell's h
+        sDM[(cw + c) * 68 + k] = dmean;
+        sDA[(cw + c) * 68 + k] = da;
+        sH[(cw + c) * 68 + k] = h;
+        if (k == 0) sH[(cw + c) * 68 + 64] = vinx[c];  // 1/||l|| beside the cell's h
         rbm += dmean;
         rbl += da;
         if (!covar) {  // unit covariate (Engine::unit_covar): c = 1 (dmean is 0 on padding rows)
@@ -901,12 +940,12 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
     float* wp = wpart[w];
     // the heads' input: h0, or the Angular chain's output (recomputed, outputs kept)
     const float* hin = sH;
-    if (d.nce > 0) {
+    if (CHAINS && d.nce > 0) {
         hin = chain_run(d, 0, d.nce, sH, cimg, nullptr, true, sCW, w, lane);
     }
-    {  // dh0[16 cells][KE] on f32 MFMA (wave w: columns 16w..16w+15), scaled by 1/||l|| for k_enc_bwd
+    if (w < 4) {  // dh0[16 cells][KE] on f32 MFMA (wave w: columns 16w..16w+15), scaled by 1/||l|| for k_enc_bwd
         f32x4 acc = heads_dh(sDM, sDA, sWm, sWl, K, E, w, lane);
-        if (d.nce > 0) {  // back through the Angular chain
+        if (CHAINS && d.nce > 0) {  // back through the Angular chain
             img_store(sG(0), acc, w, lane);
             __syncthreads();
             int g = 0;
@@ -944,20 +983,25 @@ __global__ __launch_bounds__(256) void k_vlatent_bwd(VPtrs P, Dims d, const int6
 #pragma unroll
     for (int q = 0; q < CMAX; ++q) wp[192 + k * CMAX + q] = rWce[q];
     float* out = small + (int64_t)blockIdx.x * SMALL;
-    heads_dW(sDM, sDA, hin, K, E, w, lane, out);
+    if (w < 4) heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     __syncthreads();
     const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
-    auto wsum = [&](int off) { return (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]); };
-    for (int i = threadIdx.x; i < K; i += 256) {
+    auto wsum = [&](int off) {  // fixed order over the waves, four at a time
+        float t = (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]);
+#pragma unroll
+        for (int i = 4; i < NW; i += 4) t += (wpart[i][off] + wpart[i + 1][off]) + (wpart[i + 2][off] + wpart[i + 3][off]);
+        return t;
+    };
+    for (int i = threadIdx.x; i < K; i += 64 * NW) {
         out[o_bm + i] = wsum(i);
         out[o_bl + i] = wsum(64 + i);
         for (int q = 0; q < C; ++q) out[o_ce + i * C + q] = wsum(192 + i * CMAX + q);
     }
-    for (int i = threadIdx.x; i < KE; i += 256) out[o_dhs + i] = wsum(128 + i);
+    for (int i = threadIdx.x; i < KE; i += 64 * NW) out[o_dhs + i] = wsum(128 + i);
 }
 // k_vlatent_bwd's LDS (+ the chain W stage, 2 gradient images and the chain outputs with hidden layers)
-static size_t vlat_bwd_lds(const Engine* e) {
-    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 4 * (3 * 64 + 64 * CMAX);
+static size_t vlat_bwd_lds(const Engine* e, int nw) {
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + (size_t)nw * (3 * 64 + 64 * CMAX);
     if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
     return f * 4;
 }
@@ -1261,6 +1305,9 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     float* gene = e->d_gene;  // k_vprep ran before the batch lists (vmf_prep)
     const bool ucov = d.C == 1 && e->unit_covar;  // the CM = 0 decoder instances
     const float* lat_covar = ucov ? nullptr : e->d_covar;  // latent kernels: no covariate gather
+    // latent kernels: one cell per wave (16 waves) without frozen chains (k_latent_fwd, NB)
+    static const bool lat_nw4 = getenv_is("MMVAE_LAT_NW", "4");
+    const bool lat16 = !lat_nw4 && d.nce == 0 && d.ncd == 0;
     {
         ScopedTimer tm(e, "k_enc_fwd");
         hipError_t er = enc_forward_launch(e, d, e->d_hpart);
@@ -1268,10 +1315,15 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_fwd");
-        hipLaunchKernelGGL(k_vlatent_fwd, dim3(e->n_lat_wg), dim3(256), 0, st, P, d, e->d_cells, mode == 1 ? e->d_covar : lat_covar, e->d_hpart,
-                           e->d_mvec, (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr,
-                           (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, e->d_ss,
-                           e->d_lat, e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
+        auto go = [&](auto kern, int nth) {
+            hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), 0, st, P, d, e->d_cells,
+                               mode == 1 ? e->d_covar : lat_covar, e->d_hpart, e->d_mvec,
+                               (const float2*)e->d_cellnorm, e->d_rowx, use_eps ? e->d_eps : nullptr,
+                               (mode == 0 && e->perm_active) ? e->d_perm : nullptr, e->cfg.seed, e->d_ss, e->d_lat,
+                               e->d_zf, e->d_zb, e->d_lossp, mode, out_mean, out_lnvar);
+        };
+        if (lat16) go(k_vlatent_fwd<16>, 1024);
+        else go(k_vlatent_fwd<4>, 256);
     }
     if (mode == 1) return hipGetLastError();
     VDecPtrs Q;
@@ -1337,8 +1389,12 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     }
     {
         ScopedTimer tm(e, "k_vlatent_bwd");
-        hipLaunchKernelGGL(k_vlatent_bwd, dim3(e->n_lat_wg), dim3(256), vlat_bwd_lds(e), st, P, d, e->d_cells, lat_covar, e->d_lat,
-                           e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
+        auto go = [&](auto kern, int nth) {
+            hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), vlat_bwd_lds(e, lat16 ? 16 : 4), st, P, d, e->d_cells,
+                               lat_covar, e->d_lat, e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
+        };
+        if (lat16) go(k_vlatent_bwd<16>, 1024);
+        else go(k_vlatent_bwd<4>, 256);
     }
     // world 1 (no split): the gradient kernels also write the clip norm's sum-of-squares partials
     const bool fuse_sq = !split && !(e->comm_active());
