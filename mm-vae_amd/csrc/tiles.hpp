@@ -62,10 +62,25 @@ struct StageCopy {
     uint4* dst;
     int n16;           // 16-byte chunks
 };
-MMVAE_DEV void stage_copy_part(const StageCopy& sc) {
-    if (blockIdx.y != 0 || !sc.src) return;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < sc.n16; i += gridDim.x * 256) sc.dst[i] = sc.src[i];
-}
+// The copy, split in two: load() issues this thread's first chunk (an unconditional load:
+// blocks with y != 0, or with no staged block, read `dummy` instead), store() writes it and
+// copies any further chunks.  A kernel issues load() after its own loads, so waiting for those
+// never waits for the slower host-memory read (loads retire in issue order).
+struct StageHold {
+    uint4 v;
+    int i;
+    bool on;
+    MMVAE_DEV void load(const StageCopy& sc, const void* dummy) {
+        on = blockIdx.y == 0 && sc.src && sc.n16 > 0;
+        i = blockIdx.x * 256 + threadIdx.x;
+        v = *(on ? sc.src + min(i, sc.n16 - 1) : reinterpret_cast<const uint4*>(dummy));
+    }
+    MMVAE_DEV void store(const StageCopy& sc) const {
+        if (!on) return;
+        if (i < sc.n16) sc.dst[i] = v;
+        for (int j = i + gridDim.x * 256; j < sc.n16; j += gridDim.x * 256) sc.dst[j] = sc.src[j];
+    }
+};
 
 // out[c] = sum over splits s < ns of p[s * sstride + off + c * cstride], c < NC (NC = 4 or 1 cells):
 // the split partials, loads issued 16 / NC splits at a time (independent, then summed).  The

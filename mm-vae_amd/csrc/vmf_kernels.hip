@@ -113,29 +113,41 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
                                                const float* __restrict__ WeP_f, float* __restrict__ WeS_f,
                                                __bf16* __restrict__ WeS_b, float* __restrict__ mvecp, VScal sc,
                                                float* __restrict__ vk, StageCopy scp) {
-    stage_copy_part(scp);
+    // every load before the first store (see k_prep, nb_kernels.hip), the staged block's
+    // host-memory chunk last
+    StageHold sh;
     if (blockIdx.x == gridDim.x - 1) {
+        sh.load(scp, P.lsd);
         if (blockIdx.y == 0) vkappa_body(P, sc, vk);
+        sh.store(scp);
         return;
     }
     const int g0 = blockIdx.x * 256 + threadIdx.x;
     const bool in = g0 < d.DP;
     const int g = in ? g0 : d.DP - 1;
     const bool v = in && g < d.D;
-    const float inv = v ? 1.f / (softplus_acc(P.lsd[g]) + epsD) : 0.f;
+    const int gl = min(g, d.D - 1);
+    const float lsd = P.lsd[gl];
+    float wp[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wp[kk] = WeP_f[(int64_t)(blockIdx.y * 8 + kk) * d.DP + g];
+    const float xm = P.xm[gl], bd = P.bd[gl], bcd = P.bcd[gl], wcd = P.Wcd[(int64_t)gl * d.C];
+    __builtin_amdgcn_sched_barrier(0);  // the host-memory load stays behind the others
+    sh.load(scp, P.lsd);
+    __builtin_amdgcn_sched_barrier(0);
+    const float inv = v ? 1.f / (softplus_acc(lsd) + epsD) : 0.f;
     if (blockIdx.y == 0 && in) {
         gene[g] = inv;
-        gene[3 * d.DP + g] = v ? P.xm[g] * inv : 0.f;
+        gene[3 * d.DP + g] = v ? xm * inv : 0.f;
         reinterpret_cast<float4*>(gene + 4 * d.DP)[g] =
-            float4{v ? P.bd[g] * 1.4426950408889634f : -INFINITY, v ? P.bcd[g] : 0.f, v ? P.Wcd[(int64_t)g * d.C] : 0.f,
-                   v ? epsD : 0.f};
+            float4{v ? bd * 1.4426950408889634f : -INFINITY, v ? bcd : 0.f, v ? wcd : 0.f, v ? epsD : 0.f};
     }
-    const float xmv = v ? P.xm[g] : 0.f;
+    const float xmv = v ? xm : 0.f;
     float mp[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
         const int k = blockIdx.y * 8 + kk;
-        const float ws = inv * WeP_f[(int64_t)k * d.DP + g];
+        const float ws = inv * wp[kk];
         if (in) {  // bf16 image: hi plane, and the x3 mode's lo plane KP * DP elements after it
             if (WeS_b) put_op<X3>(WeS_b, (int)((int64_t)k * d.DP + g), d.KP * d.DP, ws);
             else WeS_f[(int64_t)k * d.DP + g] = ws;
@@ -143,6 +155,7 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
         mp[kk] = xmv * ws;  // xmi_g W~[k][g]
     }
     mvec_partial(mp, mvecp, d.KP, blockIdx.y * 8);  // summed by k_vlatent_fwd
+    sh.store(scp);
 }
 
 // =======================================================================================
