@@ -1127,21 +1127,21 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
     __shared__ float cdh[64];
     __shared__ float red[NPART][NQ][VGG_GENES];
     const int C = d.C, nqB = 1 + C;
-    for (int k = threadIdx.x; k < d.KE; k += 256) cdh[k] = smallg[k];
     const int part = threadIdx.x >> 4, gq = (threadIdx.x & 15) * GPT;
     const int g0 = blockIdx.x * VGG_GENES;  // DP is a multiple of 64: every slab / W read is in bounds
+    auto ld = [&](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
+    // every load first (clamped, unconditional; one memory round): the column dot's W rows
+    // (latent rows part, part + NPART, ...), dh's column sums, the final phase's gene parameters
+    // (threads < 64), then the slab rows
+    f32x4 wv[64 / NPART];
+#pragma unroll
+    for (int i = 0; i < 64 / NPART; ++i) wv[i] = ld(WeP_f + (int64_t)min(part + NPART * i, d.KE - 1) * d.DP + g0 + gq);
+    const float cdv = smallg[min((int)threadIdx.x, d.KE - 1)];
+    const int gf = min(g0 + (int)threadIdx.x, d.D - 1);
+    const float f_inv = gene[gf], f_xm = P.xm[gf], f_lsd = P.lsd[gf];
     f32x4 acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto ld = [&](const float* p) { return *reinterpret_cast<const f32x4*>(p); };
-    if (PART != 1) {  // the column dot's loads first (latent rows part, part + NPART, ...)
-        __syncthreads();  // cdh
-        for (int k = part; k < d.KE; k += NPART) {
-            const f32x4 wv = ld(WeP_f + (int64_t)k * d.DP + g0 + gq);
-#pragma unroll
-            for (int i = 0; i < GPT; ++i) acc[NQ - 1][i] = fmaf(cdh[k], wv[i], acc[NQ - 1][i]);
-        }
-    }
 #pragma unroll 4
     for (int rb = part; rb < nrb; rb += NPART) {
         const float* sB = slabB + (int64_t)rb * nqB * d.DP + g0 + gq;
@@ -1149,6 +1149,15 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
         for (int q = 0; q < 1 + CMAX; ++q)
             if (PART != 2 && q < nqB) acc[q] += ld(sB + (int64_t)q * d.DP);
         if (PART != 1) acc[NQ - 2] += ld(slabE + (int64_t)rb * d.DP + g0 + gq);
+    }
+    if (threadIdx.x < d.KE) cdh[threadIdx.x] = cdv;
+    __syncthreads();
+    if (PART != 1) {  // sum_k cdh[k] W~[k][g] in latent order
+#pragma unroll
+        for (int i = 0; i < 64 / NPART; ++i)
+            if (part + NPART * i < d.KE)
+#pragma unroll
+                for (int e = 0; e < GPT; ++e) acc[NQ - 1][e] = fmaf(cdh[part + NPART * i], wv[i][e], acc[NQ - 1][e]);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
@@ -1173,9 +1182,9 @@ __global__ __launch_bounds__(256) void k_vgrad_genes(VPtrs P, Dims d, VGrads G, 
         }
         if (PART != 1) {
             const float Gl = t[NQ - 2], gs = t[NQ - 1];
-            const float inv = gene[g];
+            const float inv = f_inv;
             put(&G.xm[g], -inv * gs);
-            put(&G.lsd[g], -(inv * inv) * (Gl - P.xm[g] * gs) * dsoftplus(P.lsd[g]));
+            put(&G.lsd[g], -(inv * inv) * (Gl - f_xm * gs) * dsoftplus(f_lsd));
         }
     }
     if (sqpart && threadIdx.x < 64) {  // wave 0 holds every writer (threads 0..63)
