@@ -1664,7 +1664,8 @@ __global__ __launch_bounds__(64 * NW) void k_latent_bwd(NBPtrs P, Dims d, const 
     float* sDM = sWl + 64 * 65;       // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;  // [cell][68] dlnvar-pre-clamp (a)
     float* sH = sDA + LAT_CELLS * 68;   // [cell][68] h0
-    float* wpart = sH + LAT_CELLS * 68; // [NW][NSM] per-wave small partials
+    float* sT = sH + LAT_CELLS * 68;    // [64][17] dh0, transposed (latent-major)
+    float* wpart = sT + 64 * 17;        // [NW][NSM] per-wave small partials
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
     // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
     // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
@@ -1880,9 +1881,7 @@ __global__ __launch_bounds__(64 * NW) void k_latent_bwd(NBPtrs P, Dims d, const 
                 // ReLU backward: the gradient passes where the (stored, post-ReLU) h0 is > 0
                 const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
-                dh[(int64_t)b * KP + j] = v;
-                dhT_f[(int64_t)j * d.Bpad + b] = v;
-                put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, v);  // hi plane (+ the x3 lo plane)
+                sT[j * 17 + cl] = v;  // stored transposed below, 16 cells of a latent per 16 lanes
                 rdhs += v;
             }
         }
@@ -1909,6 +1908,16 @@ __global__ __launch_bounds__(64 * NW) void k_latent_bwd(NBPtrs P, Dims d, const 
     if (w < 4) heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     mark(5);
     __syncthreads();
+    // dh^T [KP][Bpad] (the encoder backward's A operand: f32 image, or the bf16 hi [+ lo] planes)
+    // from the transposed LDS tile: 16 consecutive cells of one latent per 16 lanes
+    for (int i = threadIdx.x; i < KP * LAT_CELLS; i += 64 * NW) {
+        const int j = i >> 4, cl = i & 15, b = blockIdx.x * LAT_CELLS + cl;
+        const float v = sT[j * 17 + cl];
+        if (b < d.Bpad) {
+            if (dhT_f) dhT_f[(int64_t)j * d.Bpad + b] = v;
+            if (dhT_b) put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, v);  // hi plane (+ the x3 lo plane)
+        }
+    }
     // ---- the small vectors: fixed-order sum of the four waves' partials ----
     const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C, o_nm = o_dhs + KE,
               o_bnm = o_nm + R * H, o_nl = o_bnm + R, o_bnl = o_nl + R * H, o_bne = o_bnl + R, o_bdp = o_bne + H;
@@ -2480,7 +2489,7 @@ static void latent_fwd_launch(Engine* e, const NBPtrs& P, const Dims& d, const f
 // also the chain W stage, 2 gradient images and the recomputed chain outputs
 static size_t latent_bwd_lds(const Engine* e, int nw) {
     const int NSM = 3 * 64 + 64 * CMAX + 2 * RMAX * HMAX + 2 * RMAX + HMAX + 1;
-    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + (size_t)nw * NSM;
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 64 * 17 + (size_t)nw * NSM;
     if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
     return f * 4;
 }
@@ -2606,8 +2615,10 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         const bool nw16 = latent_nw16(d);
         const size_t lds = latent_bwd_lds(e, nw16 ? 16 : 4);
         auto go = [&](auto kern, int nth) {
+            // the encoder backward reads one dh^T image: bf16 planes (bf16, x3 and fp8 modes) or f32
             hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), lds, st, P, d, e->d_cells, lat_covar, e->d_lat,
-                               e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b, e->d_small);
+                               e->d_rowx, e->d_rowB, e->d_dzp, e->d_dh, bf ? nullptr : e->d_dhT_f,
+                               bf ? e->d_dhT_b : nullptr, e->d_small);
         };
         if (nw16) go(k_latent_bwd<16>, 1024);
         else go(k_latent_bwd<4>, 256);

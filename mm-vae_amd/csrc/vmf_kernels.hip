@@ -856,7 +856,8 @@ __global__ __launch_bounds__(64 * NW) void k_vlatent_bwd(VPtrs P, Dims d, const 
     float* sDM = sWl + 64 * 65;            // [cell][68] dmean
     float* sDA = sDM + LAT_CELLS * 68;     // [cell][68] d(pre-clamp lnvar)
     float* sH = sDA + LAT_CELLS * 68;      // [cell][68] h0 (column 64: 1/||l||)
-    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sH + LAT_CELLS * 68);  // [NW][NSM]
+    float* sT = sH + LAT_CELLS * 68;       // [64][17] dh0 / ||l||, transposed (latent-major)
+    float (*wpart)[NSM] = reinterpret_cast<float (*)[NSM]>(sT + 64 * 17);  // [NW][NSM]
     // frozen chains (only with hidden layers): W stage, two gradient images, the recomputed
     // chain outputs (ReLU masks): encoder [nce], decoder z + [ncd]
     float* sCW = &wpart[NW][0];
@@ -982,9 +983,7 @@ __global__ __launch_bounds__(64 * NW) void k_vlatent_bwd(VPtrs P, Dims d, const 
                 // ReLU backward: the gradient passes where the (stored, post-ReLU) h is > 0
                 const bool pass = j < KE && (!d.relu || sH[cl * 68 + j] > 0.f);
                 const float v = pass ? acc[r] : 0.f;
-                const float vs = v * sH[cl * 68 + 64];
-                dhT_f[(int64_t)j * d.Bpad + b] = vs;
-                put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, vs);  // hi plane (+ the x3 lo plane)
+                sT[j * 17 + cl] = v * sH[cl * 68 + 64];  // stored transposed below
                 rdhs += v;
             }
         }
@@ -998,6 +997,16 @@ __global__ __launch_bounds__(64 * NW) void k_vlatent_bwd(VPtrs P, Dims d, const 
     float* out = small + (int64_t)blockIdx.x * SMALL;
     if (w < 4) heads_dW(sDM, sDA, hin, K, E, w, lane, out);
     __syncthreads();
+    // dh^T / ||l|| [KP][Bpad] (the encoder backward's A operand: f32 image, or the bf16 hi [+ lo]
+    // planes) from the transposed LDS tile: 16 consecutive cells of one latent per 16 lanes
+    for (int i = threadIdx.x; i < KP * LAT_CELLS; i += 64 * NW) {
+        const int j = i >> 4, cl = i & 15, b = blockIdx.x * LAT_CELLS + cl;
+        const float vs = sT[j * 17 + cl];
+        if (b < d.Bpad) {
+            if (dhT_f) dhT_f[(int64_t)j * d.Bpad + b] = vs;
+            if (dhT_b) put_op<X3>(dhT_b, j * d.Bpad + b, KP * d.Bpad, vs);  // hi plane (+ the x3 lo plane)
+        }
+    }
     const int o_bm = 2 * K * E, o_bl = o_bm + K, o_ce = o_bl + K, o_dhs = o_ce + K * C;
     auto wsum = [&](int off) {  // fixed order over the waves, four at a time
         float t = (wpart[0][off] + wpart[1][off]) + (wpart[2][off] + wpart[3][off]);
@@ -1014,7 +1023,7 @@ __global__ __launch_bounds__(64 * NW) void k_vlatent_bwd(VPtrs P, Dims d, const 
 }
 // k_vlatent_bwd's LDS (+ the chain W stage, 2 gradient images and the chain outputs with hidden layers)
 static size_t vlat_bwd_lds(const Engine* e, int nw) {
-    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + (size_t)nw * (3 * 64 + 64 * CMAX);
+    size_t f = 2 * 64 * 65 + 3 * LAT_CELLS * 68 + 64 * 17 + (size_t)nw * (3 * 64 + 64 * CMAX);
     if (e->nce + e->ncd > 0) f += 64 * 65 + (size_t)(2 + e->nce + e->ncd + 1) * LAT_CELLS * 68;
     return f * 4;
 }
@@ -1413,7 +1422,8 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         ScopedTimer tm(e, "k_vlatent_bwd");
         auto go = [&](auto kern, int nth) {
             hipLaunchKernelGGL(kern, dim3(e->n_lat_wg), dim3(nth), vlat_bwd_lds(e, lat16 ? 16 : 4), st, P, d, e->d_cells,
-                               lat_covar, e->d_lat, e->d_dzp, e->d_dhT_f, e->d_dhT_b, e->d_small);
+                               lat_covar, e->d_lat, e->d_dzp, bf ? nullptr : e->d_dhT_f, bf ? e->d_dhT_b : nullptr,
+                               e->d_small);
         };
         if (lat16) go(k_vlatent_bwd<16>, 1024);
         else go(k_vlatent_bwd<4>, 256);
