@@ -208,8 +208,8 @@ int mmvae_timing_count(mmvae_h h, int32_t* n);
 int mmvae_timing_get(mmvae_h h, int32_t idx, const char** name, double* total_ms, int64_t* launches);
 int mmvae_timing_reset(mmvae_h h);
 /* Diagnostics: copy n floats of an internal workspace (0 = encoder partials, 1 = decoder dz, 2 = pass-C slab
- * partials; the MMVAE_DBG stamp builds write per-wave phase cycles there; 3 = the last step's latent
- * noise eps [Bpad][K], rows in the staged order) to the host. */
+ * partials, 4 = encoder-backward slab; the MMVAE_DBG stamp builds write per-wave phase cycles there;
+ * 3 = the last step's latent noise eps [Bpad][K], rows in the staged order) to the host. */
 int mmvae_debug_copy(mmvae_h h, int32_t which, float* host, int64_t n);
 /* Gene tiling of the handle's tile kernels (tests assert that a split walks many tiles):
  * out[0] = 64-gene tiles NT, out[1..3] = gene splits of the encoder forward / decoder pass B /

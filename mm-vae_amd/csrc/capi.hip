@@ -1680,10 +1680,10 @@ int mmvae_timing_get(mmvae_h e, int32_t idx, const char** name, double* total_ms
 }
 
 int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
-    if (!e || !host || n < 0 || which < 0 || which > 3) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
+    if (!e || !host || n < 0 || which < 0 || which > 4) FAIL(e, MMVAE_E_ARG, "debug_copy: bad arguments");
     // 0: encoder split partials (k_enc_fwd stamps), 1: decoder dz partials (k_dec_nb stamps),
     // 2: pass-C column slab (k_dec_lse / latent stamps), 3: the last step's latent noise eps
-    //    [Bpad][K] (rows in the step's staged order)
+    //    [Bpad][K] (rows in the step's staged order), 4: the encoder-backward slab (its stamps)
     if (which == 3) {
         if (n > e->Bpad * e->K) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds Bpad * K");
         HIPCHK(e, hipSetDevice(e->device));
@@ -1695,11 +1695,12 @@ int mmvae_debug_copy(mmvae_h e, int32_t which, float* host, int64_t n) {
     }
     const int64_t cap = which == 0   ? (int64_t)e->nsplit_e * e->Bpad * e->KP
                         : which == 1 ? (int64_t)e->nsplit_d * e->Bpad * 2 * e->KP
+                        : which == 4 ? (int64_t)e->nrb_max * (2 + e->H) * e->DP
                                      : (int64_t)e->nrb_max * (1 + e->C) * e->DP;
     if (n > cap) FAIL(e, MMVAE_E_ARG, "debug_copy: n exceeds the workspace");
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    const float* src = which == 0 ? e->d_hpart : which == 1 ? e->d_dzp : e->d_slabC;
+    const float* src = which == 0 ? e->d_hpart : which == 1 ? e->d_dzp : which == 4 ? e->d_slabE : e->d_slabC;
     HIPCHK(e, hipMemcpy(host, src, sizeof(float) * n, hipMemcpyDeviceToHost));
     return MMVAE_OK;
 }

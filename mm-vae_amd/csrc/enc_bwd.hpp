@@ -180,6 +180,18 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
         keep(first);
     }
     lds_barrier();
+    // diagnostic (MMVAE_DBG & 16384, -DMMVAE_DIAG builds): per-wave phase cycles into slabE
+    // (outputs invalid): raw sums, M + W dot, barrier 1, slab store + scatter, fetch + barrier 2
+    const bool stamps = dbg_bit(d.dbg, 16384);
+    uint64_t st_[6] = {0, 0, 0, 0, 0, 0}, tp_ = stamps ? stamp_now() : 0;
+    const uint64_t t_start = tp_;
+    auto lap = [&](int i_) {
+        if (stamps) {
+            const uint64_t tn = stamp_now();
+            st_[i_] += tn - tp_;
+            tp_ = tn;
+        }
+    };
     // q: tile t + 1's entries; wc / wx: this / the next tile's W registers (WREG)
     auto tile = [&](int t, ListEntries& q, float (&wc)[4][4], float (&wx)[4][4]) {
         const int tl = t - t0;
@@ -201,9 +213,10 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
                     v = fmaf(xv[c].x, a.x, fmaf(xv[c].y, a.y, fmaf(xv[c].z, a.z, fmaf(xv[c].w, a.w, v))));
                 }
                 v = sum_rowgroups(v);
-                if (lane < 16) slabE[((int64_t)rb * nq + 1 + h) * d.DP + 64 * t + gl] = v;
+                if (lane < 16 && !stamps) slabE[((int64_t)rb * nq + 1 + h) * d.DP + 64 * t + gl] = v;
             }
         }
+        lap(0);
         // ---- M block w on MFMA, then Gl partial = sum over the block's latents of W M ----
         if (lb < KP / 16) {
             if constexpr (GSPLIT)  // the other waves' gene blocks: zero partials from this wave
@@ -236,8 +249,10 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
 #pragma unroll
             for (int gb = 0; gb < 4; ++gb) part[w * 64 + 16 * gb + lane] = 0.f;
         }
+        lap(1);
         lds_barrier();
-        if (threadIdx.x < 64) {
+        lap(2);
+        if (threadIdx.x < 64 && !stamps) {
             const int g = threadIdx.x;
             slabE[((int64_t)rb * nq) * d.DP + 64 * t + g] = part[g] + part[64 + g] + part[128 + g] + part[192 + g];
         }
@@ -247,12 +262,20 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
             keep(q);
             if constexpr (!WREG) wreg.store(wst);
         }
+        lap(3);
         q.fetch(ents, segw, toffl, min(tl + 3, nt - 1), lane);
         lds_barrier();
+        lap(4);
     };
     for (int t = t0; t < t1; t += 2) {
         tile(t, qA, wr, wn);
         if (t + 1 < t1) tile(t + 1, qB, wn, wr);
+    }
+    if (stamps && lane == 0) {
+        float* o = slabE + ((int64_t)bid * 4 + w) * 8;
+        for (int i = 0; i < 5; ++i) o[i] = (float)st_[i];
+        o[5] = (float)(stamp_now() - t_start);
+        o[6] = (float)nt;
     }
 }
 
