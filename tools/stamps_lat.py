@@ -15,7 +15,8 @@ for i in range(3):  # fwd: eval path (pass C, which also writes slabC, does not 
     else:
         eng.eval_loss(np.arange(B), 1.0, step_id=i)
 nwg = B // 16
-buf = np.zeros(nwg * 4 * 8, np.float32)
+NWV = int(os.environ.get("NWV", "16"))  # waves per latent workgroup (MMVAE_LAT_NW=4: 4)
+buf = np.zeros(nwg * NWV * 8, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 2, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
 assert rc == 0
 f = buf.reshape(-1, 8).astype(np.float64)
