@@ -160,6 +160,11 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 // W stage is rewritten between two barriers — so x3 fits 4 workgroups per CU (39 KB) instead of 2.
 // NW waves (16 rows each) per workgroup: 8 in the x3 mode (the staged W tile serves 128 rows,
 // two workgroups per CU), 4 otherwise
+// W stage buffers of k_enc_fwd: 2 (double-buffered, one barrier per tile) in every mode; the x3
+// mode's single-buffered x tiles keep its two 8-wave workgroups per CU with both W stages (75 KB)
+#ifndef MMVAE_ENC_NBW
+#define MMVAE_ENC_NBW 2
+#endif
 template <class P, int KP, bool SB = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
                                                  const int32_t* __restrict__ toff,
@@ -174,7 +179,8 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
     constexpr int RB = 64 * (int)sizeof(T);        // staged W row = 64 genes of one latent
     constexpr int STB = KP * RB;
     constexpr int XT = 16 * XS;                    // elements of one x tile plane
-    constexpr int NB = SB ? 1 : 2;                 // x tiles / W stages
+    constexpr int NB = SB ? 1 : 2;                 // x tiles per wave
+    constexpr int NBW = MMVAE_ENC_NBW;             // W stage buffers (2: one barrier per tile)
     constexpr int XB = NB * NPL * XT * (int)sizeof(T);  // per wave: x tiles [hi 0][hi 1][lo 0][lo 1]
     constexpr int XPL = NB * XT;                   // x plane stride (elements)
     using Tab = Log1pTab<P, SB ? 512 : LTAB>;
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
     const int row0 = rb * 16 * NW + 16 * w;
     const int t0 = sp * d.tpsE, t1 = min(d.NT, t0 + d.tpsE);
     const int S = d.tpsE + 1;
-    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Tab::BYTES, NB, NW);
+    const EncLds L(KP, (int)sizeof(T), S, XB, 0, NPL, Tab::BYTES, NBW, NW);
     char* wst = smem;
     uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.o_tab);
     Tab::fill(ltab);
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
         first.fetch(ents, segw, toffl, 0, lane);
         qA.fetch(ents, segw, toffl, min(1, nt - 1), lane);
         qB.fetch(ents, segw, toffl, min(2, nt - 1), lane);
-        wreg.store(wst, NB * STB);
+        wreg.store(wst, NBW * STB);
         scatter(first, xt);
         keep(first, 0);
     }
@@ -266,8 +272,8 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
             tp = tn;
         }
     };
-    // q: tile t + 1's entries; buf: the x tile buffer holding tile t
-    auto tile = [&](int t, ListEntries& q, int buf) {
+    // q: tile t + 1's entries; buf: the x tile buffer holding tile t; wb: the W stage holding it
+    auto tile = [&](int t, ListEntries& q, int buf, int wb) {
         const int tl = t - t0;
         // unconditional (clamped) prefetch of the next weight tile: counted vmcnt waits
         wreg.load(wsrc(min(t + 1, t1 - 1)), (int64_t)d.DP * sizeof(T), wplane * (int64_t)sizeof(T));
@@ -278,8 +284,8 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
 #pragma unroll
             for (int lb = 0; lb < KP / 16; ++lb) {
                 const Fr bw = M::load(reinterpret_cast<const T*>(
-                    wst + buf * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
-                    NB * STB / (int)sizeof(T));
+                    wst + wb * STB + swz_off<RB>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
+                    NBW * STB / (int)sizeof(T));
                 acc[lb] = M::mma(a, bw, acc[lb]);
             }
         }
@@ -294,19 +300,20 @@ __global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ e
         }
         lap(sb);
         q.fetch(ents, segw, toffl, min(tl + 3, nt - 1), lane);  // the loads stay in flight across the barriers
-        if constexpr (SB) {
+        if constexpr (NBW == 1) {
             lds_barrier();  // every wave's reads of this W stage done
             if (t + 1 < t1) wreg.store(wst, STB);
         } else if (t + 1 < t1) {
-            wreg.store(wst + (buf ^ 1) * STB, 2 * STB);
+            // the other stage: every wave read it in tile t - 1, before that tile's last barrier
+            wreg.store(wst + (wb ^ 1) * STB, NBW * STB);
         }
         lap(sc);
         lds_barrier();
         lap(sd);
     };
     for (int t = t0; t < t1; t += 2) {
-        tile(t, qA, 0);
-        if (t + 1 < t1) tile(t + 1, qB, SB ? 0 : 1);
+        tile(t, qA, 0, 0);
+        if (t + 1 < t1) tile(t + 1, qB, SB ? 0 : 1, NBW == 2 ? 1 : 0);
     }
     if (stamps) {  // diagnostic build: per-wave phase cycles into hpart (outputs invalid)
         const uint64_t t_loop_end = stamp_now();
@@ -2410,7 +2417,7 @@ static size_t enc_fwd_lds(const Dims& d) {
     constexpr bool SB = EncSB<P>::value;
     constexpr int NB = SB ? 1 : 2;
     return (size_t)EncLds(KP, (int)sizeof(T), d.tpsE + 1, NB * NPL * 16 * XS * (int)sizeof(T), 0, NPL,
-                          Log1pTab<P, SB ? 512 : LTAB>::BYTES, NB, EncNW<P>::value).bytes;
+                          Log1pTab<P, SB ? 512 : LTAB>::BYTES, MMVAE_ENC_NBW, EncNW<P>::value).bytes;
 }
 // the encoder operand images of mode P: bf16 planes (bf16, x3) or f32
 template <class P> static const typename Elem<P>::type* op_img(const float* f, const __bf16* b) {
