@@ -109,8 +109,8 @@ def make_engine(mmvae_amd, model, D, K, B, dtype, cells, lib, device, seed=1234,
     eng = mmvae_amd.Engine(D=D, K=K, max_batch=B, dtype=dtype, device=device, seed=seed,
                            model=mmvae_amd.MODEL_VMF if model == "vmf" else mmvae_amd.MODEL_NB)
     eng.init_params(seed=7)  # host-side work first: the GPU-heavy dataset synthesis runs last
-    # one hipGraph per step; with a communicator the RCCL buckets are captured too
-    # (MMVAE_COMM_GRAPH=0: its steps run eagerly)
+    # one hipGraph per step; with a communicator the steps run eagerly with one flat all-reduce
+    # unless MMVAE_COMM_GRAPH=1 (RCCL buckets captured into the step graphs)
     eng.graph(graph)
     nnz = eng.synth_csr(cells, lib_size=lib, seed=2024)
     return eng, nnz
@@ -430,15 +430,15 @@ def dp_exchange(mmvae_amd, D, K, B, dtype, cells, lib, steps=300, warmup=20):
     (mmvae_alg.hh:306-310) — over one rank, where the sum is the identity.  Each mode's
     ms/step minus the no-communicator step bounds what the N > 1 scaling must absorb besides the
     xGMI transfer itself (0.83 MB of gradient per step)."""
-    modes = [("bucket, eager", {"MMVAE_COMM_GRAPH": "0"}), ("flat, eager", {"MMVAE_COMM_GRAPH": "0", "MMVAE_NO_OVERLAP": "1"}),
-             ("bucket, step graph (the world > 1 default)", {}),
-             ("flat, step graph", {"MMVAE_NO_OVERLAP": "1"})]
+    modes = [("bucket, eager", {"MMVAE_OVERLAP": "1"}), ("flat, eager (the world > 1 default)", {}),
+             ("bucket, step graph", {"MMVAE_COMM_GRAPH": "1"}),
+             ("flat, step graph", {"MMVAE_COMM_GRAPH": "1", "MMVAE_NO_OVERLAP": "1"})]
     eng, _ = make_engine(mmvae_amd, "nb", D, K, B, dtype, cells, lib, 0)
     batches = [(s * B + np.arange(B)) % cells for s in range(warmup + steps)]
     base = time_steps(eng, batches, 1.0, B, 0, steps, warmup) / steps * 1e3
     out = {"workload": f"NB {cells} x {D}, latent {K}, batch {B}, {dtype}", "steps": steps,
            "no_comm_ms_per_step": round(base, 4), "modes": []}
-    saved = {k: os.environ.get(k) for k in ("MMVAE_FORCE_COMM", "MMVAE_COMM_GRAPH", "MMVAE_NO_OVERLAP")}
+    saved = {k: os.environ.get(k) for k in ("MMVAE_FORCE_COMM", "MMVAE_COMM_GRAPH", "MMVAE_NO_OVERLAP", "MMVAE_OVERLAP")}
     try:
         for name, env in modes:
             for k in saved:

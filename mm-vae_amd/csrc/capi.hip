@@ -288,6 +288,7 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
         FAIL((Engine*)nullptr, MMVAE_E_HIP, "no HIP device " + std::to_string(device));
     mmvae_engine* e = new mmvae_engine();
     e->cfg = *cfg;
+    e->no_balance = std::getenv("MMVAE_NO_BALANCE") != nullptr;  // (read once: a graph-key input, graph_key.hpp)
     e->device = device;
     e->wide = wide;
     HIPCHK(e, hipSetDevice(device));
@@ -1159,8 +1160,7 @@ static int stage_rows(Engine* e, const int64_t* cell_ids, const int64_t* ridx, i
         e->h_cells_pin[j] = c;
     }
     const int64_t Nv = e->N_host;  // the caller's cells (the padding marker: Nv)
-    e->perm_active = balance && !e->wide && B % 16 == 0 && B >= 32 && (int64_t)e->cell_nnz.size() == Nv &&
-                     !std::getenv("MMVAE_NO_BALANCE");
+    e->perm_active = balance && balance_rule(B, e->wide, (int64_t)e->cell_nnz.size() == Nv, e->no_balance);
     if (e->perm_active) {
         balance_rows(e, B);
     }
@@ -1278,7 +1278,10 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     HIPCHK(e, hipSetDevice(e->device));
     // step graphs holding RCCL calls: the batch-dependent buffers sized for every rank's worst
     // batch first, so that no rank's graph key changes alone (comm_sync_capacity)
-    if (e->graph_on && !e->timing && e->comm_active() && e->comm_graph && !e->comm_graph_failed && !e->cap_synced) {
+    const bool comm_graph_step = e->graph_on && !e->timing && e->comm_active() && e->comm_graph && !e->comm_graph_failed;
+    if (comm_graph_step && a->B * (int64_t)e->world != n_total)  // (before any collective: graph_key.hpp)
+        FAIL(e, MMVAE_E_ARG, "run: step graphs with RCCL calls (MMVAE_COMM_GRAPH=1) need B * world == n_total");
+    if (comm_graph_step && !e->cap_synced) {
         const int crc = comm_sync_capacity(e);
         if (crc) return crc;
     }
@@ -1296,8 +1299,8 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
     // one hipGraph per step: captured on the first step of a launch shape,
     // replayed while the shape holds; not with timers or diagnostics.  With an active
     // communicator the graph holds the RCCL bucket all-reduces too (comm_bucket's event fork onto
-    // the comm stream and its join back are captured with them) unless MMVAE_COMM_GRAPH=0 was set
-    // at mmvae_comm_init (eager steps).  Every rank takes the same capture decisions: the graph
+    // the comm stream and its join back are captured with them) when MMVAE_COMM_GRAPH=1 was set
+    // at mmvae_comm_init (otherwise: eager steps).  Every rank takes the same capture decisions: the graph
     // key's batch-dependent buffers are sized for every rank's worst batch (comm_sync_capacity),
     // the capture outcome is agreed (comm_capture_agree), and a failed capture falls back to
     // eager launches for the handle's lifetime on every rank.
@@ -1311,14 +1314,18 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
                            (!with_comm || (e->comm_graph && !e->comm_graph_failed));
     if (use_graph) {
         GraphKey k;
-        k.B = a->B;
-        k.n_total = n_total;
-        std::memcpy(&k.beta_bits, &a->beta, 4);
-        k.update = a->update != 0;
-        k.use_eps = a->eps != nullptr;
-        k.perm = e->perm_active;
-        k.ents = e->d_ents;
-        k.gen = e->graph_gen;
+        KeyInputs ki;
+        ki.B = a->B;
+        ki.n_total = n_total;
+        ki.beta = a->beta;
+        ki.update = a->update != 0;
+        ki.use_eps = a->eps != nullptr;
+        ki.perm = e->perm_active;
+        ki.world = e->world;
+        ki.comm_graph = with_comm;
+        ki.ents = e->d_ents;
+        ki.gen = e->graph_gen;
+        if (derive_graph_key(ki, &k)) FAIL(e, MMVAE_E_ARG, "run: graph key (B * world != n_total)");
         Engine::StageSlot& sl = e->slots2[e->cur_slot];
         hipGraphExec_t gx = nullptr;
         for (auto& g : sl.graphs)
@@ -1345,7 +1352,7 @@ int mmvae_run(mmvae_h e, const mmvae_step_args* a, float* loss_out, double* tota
                 // the ranks agree before any of them launches: a graph one rank captured while
                 // another fell back would pair a replayed collective with eager ones
                 int agreed = 0;
-                HIPCHK(e, comm_capture_agree(e, cap_ok, &agreed));
+                HIPCHK(e, comm_capture_agree(e, cap_ok, k, &agreed));
                 comm_fail = !agreed;
             }
             if (comm_fail) {
@@ -1496,10 +1503,11 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
     e->rank = rank;
     e->world = world;
     e->comm_force = getenv_is("MMVAE_FORCE_COMM", "1");
-    // RCCL calls inside step graphs: on by default (MMVAE_COMM_GRAPH=0 opts out).  One-GPU cost of the
-    // exchange at the headline shape (bench.py dp_exchange, forced 1-rank communicator): buckets
-    // captured +4 us per step, buckets eager +34 us, flat captured +0 us
-    e->comm_graph = !getenv_is("MMVAE_COMM_GRAPH", "0");
+    // RCCL calls inside step graphs: opt-in (MMVAE_COMM_GRAPH=1).  No multi-rank run of captured
+    // collectives has been made yet (one-GPU pool), so the default is the eager exchange.
+    // One-GPU cost of the exchange at the headline shape (bench.py dp_exchange, forced 1-rank
+    // communicator): flat eager -4 us per step, buckets eager +33 us, buckets captured +5 us
+    e->comm_graph = getenv_is("MMVAE_COMM_GRAPH", "1");
     e->comm_graph_failed = false;
     if (!e->comm_stream) {
         HIPCHK(e, hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
@@ -1513,10 +1521,16 @@ int mmvae_comm_init(mmvae_h e, int32_t rank, int32_t world, const void* id128) {
 extern "C++" {
 namespace mmvae {
 bool split_grads(const Engine* e) {
-    // MMVAE_NO_OVERLAP=1: one all-reduce of the whole flat gradient on the main stream after the
-    // backward (no comm-stream events) instead of the two overlapped buckets
-    const char* no = std::getenv("MMVAE_NO_OVERLAP");
-    if (e->comm_active()) return !(no && no[0] == '1');
+    // With a communicator: the two overlapped buckets when the step is captured into a graph
+    // (their comm-stream fork / join is cheap there), otherwise one all-reduce of the whole flat
+    // gradient on the main stream after the backward (eager fork / join costs more than the bucket
+    // hides, bench.py dp_exchange).  MMVAE_NO_OVERLAP=1 forces the flat path, MMVAE_OVERLAP=1 the
+    // buckets.
+    if (e->comm_active()) {
+        if (getenv_is("MMVAE_NO_OVERLAP", "1")) return false;
+        if (getenv_is("MMVAE_OVERLAP", "1")) return true;
+        return e->comm_graph && !e->comm_graph_failed;
+    }
     const char* v = std::getenv("MMVAE_SPLIT_GRADS");
     return v && v[0] == '1';
 }
@@ -1576,22 +1590,33 @@ hipError_t comm_bucket(Engine* e, int b) {
     return hipSuccess;
 }
 
-// every rank's capture outcome, min-reduced over the communicator (eager, outside any capture):
-// *agreed = 1 only when every rank captured its step graph
-hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed) {
+constexpr size_t AGREE_BYTES = 16 * sizeof(int64_t);  // d_flag: the agreement words
+
+// every rank's capture outcome and graph key, min-reduced over the communicator (eager, outside
+// any capture; the key's max as the min of its negation): *agreed = 1 only when every rank
+// captured its step graph and every rank's key words are equal (graph_key.hpp) — a rank whose key
+// diverged makes all ranks fall back to eager steps instead of pairing mismatched graphs
+hipError_t comm_capture_agree(Engine* e, bool ok, const GraphKey& k, int* agreed) {
     if (!e->d_flag) {
-        hipError_t er = hipMalloc(&e->d_flag, 16);  // (the int64 word at +8: comm_sync_capacity)
+        hipError_t er = hipMalloc(&e->d_flag, AGREE_BYTES);
         if (er != hipSuccess) return er;
     }
-    const int32_t v = ok ? 1 : 0;
-    hipError_t er = hipMemcpyAsync(e->d_flag, &v, sizeof(v), hipMemcpyHostToDevice, e->stream);
+    int64_t w[6], v[13];
+    key_words(k, w);
+    v[0] = ok ? 1 : 0;
+    for (int i = 0; i < 6; ++i) {
+        v[1 + i] = w[i];
+        v[7 + i] = -w[i];
+    }
+    int64_t* dw = reinterpret_cast<int64_t*>(e->d_flag);
+    hipError_t er = hipMemcpyAsync(dw, v, sizeof(v), hipMemcpyHostToDevice, e->stream);
     if (er != hipSuccess) return er;
-    if (ncclAllReduce(e->d_flag, e->d_flag, 1, ncclInt32, ncclMin, e->comm, e->stream) != ncclSuccess)
-        return hipErrorUnknown;
-    int32_t r = 0;
-    er = hipMemcpyAsync(&r, e->d_flag, sizeof(r), hipMemcpyDeviceToHost, e->stream);
+    if (ncclAllReduce(dw, dw, 13, ncclInt64, ncclMin, e->comm, e->stream) != ncclSuccess) return hipErrorUnknown;
+    er = hipMemcpyAsync(v, dw, sizeof(v), hipMemcpyDeviceToHost, e->stream);
     if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
-    *agreed = r;
+    bool same = v[0] == 1;
+    for (int i = 0; i < 6; ++i) same = same && v[1 + i] == -v[7 + i];
+    *agreed = same ? 1 : 0;
     return er;
 }
 
@@ -1609,14 +1634,18 @@ hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed) {
 int comm_sync_capacity(Engine* e) {
     int64_t mx = 0;
     for (int32_t v : e->cell_nnz) mx = std::max<int64_t>(mx, v);
-    int64_t need = e->Bpad * mx;
-    if (!e->d_flag) HIPCHK(e, hipMalloc(&e->d_flag, 16));
-    int64_t* dw = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(e->d_flag) + 8);
-    HIPCHK(e, hipMemcpyAsync(dw, &need, sizeof(need), hipMemcpyHostToDevice, e->stream));
-    if (ncclAllReduce(dw, dw, 1, ncclInt64, ncclMax, e->comm, e->stream) != ncclSuccess)
+    // [0] the batch capacity, [1] MMVAE_NO_BALANCE on any rank (so the permutation rule, a graph
+    // key field, is the same function of B on every rank)
+    int64_t w[2] = {e->Bpad * mx, e->no_balance ? 1 : 0};
+    if (!e->d_flag) HIPCHK(e, hipMalloc(&e->d_flag, AGREE_BYTES));
+    int64_t* dw = reinterpret_cast<int64_t*>(e->d_flag);
+    HIPCHK(e, hipMemcpyAsync(dw, w, sizeof(w), hipMemcpyHostToDevice, e->stream));
+    if (ncclAllReduce(dw, dw, 2, ncclInt64, ncclMax, e->comm, e->stream) != ncclSuccess)
         FAIL(e, MMVAE_E_COMM, "comm_sync_capacity: ncclAllReduce failed");
-    HIPCHK(e, hipMemcpyAsync(&need, dw, sizeof(need), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(w, dw, sizeof(w), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t need = w[0];
+    e->no_balance = w[1] != 0;
     if (e->gstream) HIPCHK(e, hipStreamSynchronize(e->gstream));
     if (!e->wide && need + 64 > e->ent_cap) {
         if (e->d_ents) hipFree(e->d_ents);

@@ -13,6 +13,7 @@
 
 #include "../../include/mmvae_capi.h"
 #include "common.hpp"
+#include "graph_key.hpp"
 
 namespace mmvae {
 
@@ -45,17 +46,6 @@ struct StepScalars {
 };
 
 // launch shape of a captured step graph: replayed while every field matches
-struct GraphKey {
-    int64_t B = -1, n_total = 0;
-    uint32_t beta_bits = 0;
-    int update = 0, use_eps = 0, perm = 0;
-    const void* ents = nullptr;
-    uint64_t gen = 0;
-    bool operator==(const GraphKey& o) const {
-        return B == o.B && n_total == o.n_total && beta_bits == o.beta_bits && update == o.update &&
-               use_eps == o.use_eps && perm == o.perm && ents == o.ents && gen == o.gen;
-    }
-};
 
 struct TimerRec {
     std::string name;
@@ -184,6 +174,7 @@ struct Engine {
     StepScalars* h_ss = nullptr;     // pinned: this step's scalars (end of the staging block)
     const StepScalars* d_ss = nullptr;
     bool perm_active = false;        // the last staged batch was reordered (noise keyed by d_perm)
+    bool no_balance = false;         // MMVAE_NO_BALANCE at create (max-agreed over the ranks, comm_sync_capacity)
     std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing, lists)
     // per-step batch entry lists (batch.hip)
     uint2* d_ents = nullptr;         // [ent_cap]
@@ -255,7 +246,7 @@ struct Engine {
     int cur_slot = 0;
     float* d_tmp = nullptr;          // encode outputs
     float* d_tmp_ar = nullptr;       // host-value all-reduce staging
-    int32_t* d_flag = nullptr;       // the ranks' capture-agreement word (comm_capture_agree)
+    int32_t* d_flag = nullptr;       // the ranks' agreement words (comm_capture_agree, comm_sync_capacity)
     int64_t n_tmp_ar = 0;
 
     // ---- comm ----
@@ -264,7 +255,7 @@ struct Engine {
     // MMVAE_FORCE_COMM=1 at mmvae_comm_init: a 1-rank communicator still runs the data-parallel
     // exchange (buckets, flat all-reduce, their graph capture) — the one-GPU test of that path
     bool comm_force = false;
-    // RCCL calls inside step graphs: the default; MMVAE_COMM_GRAPH=0 opts out (read at mmvae_comm_init)
+    // RCCL calls inside step graphs: opt-in, MMVAE_COMM_GRAPH=1 (read at mmvae_comm_init)
     bool comm_graph = false;
     // the gradient exchange runs (a communicator of > 1 rank, or a forced 1-rank one)
     bool comm_active() const { return comm && (world > 1 || comm_force); }
@@ -348,7 +339,7 @@ bool split_grads(const Engine* e);
 // bucket 1 also makes e->stream wait for both buckets.  No-op without a communicator.
 hipError_t comm_bucket(Engine* e, int b);
 // min-reduce every rank's step-graph capture outcome (eager): *agreed = 1 iff all captured
-hipError_t comm_capture_agree(Engine* e, bool ok, int* agreed);
+hipError_t comm_capture_agree(Engine* e, bool ok, const GraphKey& k, int* agreed);
 // step graphs with a communicator: every batch-dependent buffer a step graph points at sized once
 // for the largest batch any rank can stage, agreed over the communicator (capi.hip)
 int comm_sync_capacity(Engine* e);

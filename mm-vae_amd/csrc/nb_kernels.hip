@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
     const float esc = WeS8 ? escale[0] : 1.f;
     StageHold sh;
     __builtin_amdgcn_sched_barrier(0);  // the host-memory load stays behind the others
-    sh.load(scp, P.lsd);
+    sh.load(scp);
     __builtin_amdgcn_sched_barrier(0);
     const float inv = v ? 1.f / (softplus_acc(lsd) + 1e-4f) : 0.f;
     if (blockIdx.y == 0 && in) {

@@ -63,17 +63,19 @@ struct StageCopy {
     int n16;           // 16-byte chunks
 };
 // The copy, split in two: load() issues this thread's first chunk (an unconditional load:
-// blocks with y != 0, or with no staged block, read `dummy` instead), store() writes it and
-// copies any further chunks.  A kernel issues load() after its own loads, so waiting for those
-// never waits for the slower host-memory read (loads retire in issue order).
+// blocks with y != 0, or with no staged block, read the first chunk of the destination block
+// instead — engine-owned device memory, 16-byte aligned, at least one chunk long; the value is
+// unused), store() writes it and copies any further chunks.  A kernel issues load() after its
+// own loads, so waiting for those never waits for the slower host-memory read (loads retire in
+// issue order).
 struct StageHold {
     uint4 v;
     int i;
     bool on;
-    MMVAE_DEV void load(const StageCopy& sc, const void* dummy) {
+    MMVAE_DEV void load(const StageCopy& sc) {
         on = blockIdx.y == 0 && sc.src && sc.n16 > 0;
         i = blockIdx.x * 256 + threadIdx.x;
-        v = *(on ? sc.src + min(i, sc.n16 - 1) : reinterpret_cast<const uint4*>(dummy));
+        v = *(on ? sc.src + min(i, sc.n16 - 1) : sc.dst);
     }
     MMVAE_DEV void store(const StageCopy& sc) const {
         if (!on) return;

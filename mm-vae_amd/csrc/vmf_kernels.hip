@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
     // host-memory chunk last
     StageHold sh;
     if (blockIdx.x == gridDim.x - 1) {
-        sh.load(scp, P.lsd);
+        sh.load(scp);
         if (blockIdx.y == 0) vkappa_body(P, sc, vk);
         sh.store(scp);
         return;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void k_vprep(VPtrs P, Dims d, float epsD, floa
     for (int kk = 0; kk < 8; ++kk) wp[kk] = WeP_f[(int64_t)(blockIdx.y * 8 + kk) * d.DP + g];
     const float xm = P.xm[gl], bd = P.bd[gl], bcd = P.bcd[gl], wcd = P.Wcd[(int64_t)gl * d.C];
     __builtin_amdgcn_sched_barrier(0);  // the host-memory load stays behind the others
-    sh.load(scp, P.lsd);
+    sh.load(scp);
     __builtin_amdgcn_sched_barrier(0);
     const float inv = v ? 1.f / (softplus_acc(lsd) + epsD) : 0.f;
     if (blockIdx.y == 0 && in) {

@@ -103,3 +103,93 @@ def test_wide_shapes_accepted(kw):
         pytest.skip("GPU present")
     with pytest.raises(mmvae_amd.MMVAEError, match="no HIP device"):
         mmvae_amd.Engine(**kw)
+
+
+GRAPH_KEY_PROBE = r"""
+#include "graph_key.hpp"
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+using namespace mmvae;
+// argv: world n_total comm_graph no_balance_mask(per rank bits) seed
+int main(int argc, char** argv) {
+    const int world = atoi(argv[1]);
+    const long n_total = atol(argv[2]);
+    const bool comm_graph = atoi(argv[3]) != 0;
+    const int nb_mask = atoi(argv[4]);
+    std::mt19937 rng(atoi(argv[5]));
+    // comm_sync_capacity: MMVAE_NO_BALANCE max-agreed over the ranks
+    bool no_balance = false;
+    for (int r = 0; r < world; ++r) no_balance = no_balance || ((nb_mask >> r) & 1);
+    for (int r = 0; r < world; ++r) {
+        // the rank's slice of the global batch (trainer.cc / bench.py: B = n_total / world, the
+        // last rank taking any remainder) and a rank-local batch: its own cells and nonzero counts
+        const long B = r < world - 1 ? n_total / world : n_total - (world - 1) * (n_total / world);
+        long nnz = 0;
+        for (long j = 0; j < B; ++j) nnz += rng() % 4000;
+        KeyInputs in;
+        in.B = B;
+        in.n_total = n_total;
+        in.beta = 0.5f;
+        in.update = true;
+        in.world = world;
+        in.comm_graph = comm_graph;
+        in.perm = balance_rule(B, false, true, no_balance);
+        in.ents = (const void*)(0x1000 + 64 * r);  // a rank-local device pointer
+        in.gen = 3;
+        GraphKey k;
+        const int rc = derive_graph_key(in, &k);
+        int64_t w[6];
+        key_words(k, w);
+        printf("%d %d", r, rc);
+        for (int i = 0; i < 6; ++i) printf(" %lld", (long long)w[i]);
+        printf(" %ld\n", nnz);
+    }
+    return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def graph_key_probe(tmp_path_factory):
+    import subprocess
+    d = tmp_path_factory.mktemp("gk")
+    src = d / "probe.cc"
+    src.write_text(GRAPH_KEY_PROBE)
+    exe = d / "probe"
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mm-vae_amd", "csrc")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", csrc, str(src), "-o", str(exe)], check=True)
+
+    def run(world, n_total, comm_graph, nb_mask=0, seed=1):
+        out = subprocess.run([str(exe), str(world), str(n_total), str(int(comm_graph)), str(nb_mask), str(seed)],
+                             check=True, capture_output=True, text=True).stdout
+        return [tuple(int(v) for v in line.split()) for line in out.strip().splitlines()]
+    return run
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_graph_key_rank_invariant_under_differing_batches(graph_key_probe, world):
+    """VERDICT r5 item 7 (capi.hip mmvae_run, graph_key.hpp): with RCCL calls inside step graphs
+    every rank must derive the same key words at every step, whatever rows and nonzero counts its
+    own batch holds, so all ranks capture (and run the capture agreement) at the same steps."""
+    for seed in range(3):
+        rows = graph_key_probe(world, 4096 * world, True, seed=seed)
+        assert all(r[1] == 0 for r in rows)
+        assert len({r[2:8] for r in rows}) == 1, rows          # identical key words
+        assert len({r[8] for r in rows}) == world              # from different batches
+        # MMVAE_NO_BALANCE set on one rank only: agreed (max) before the rule, still one key
+        rows = graph_key_probe(world, 4096 * world, True, nb_mask=1 << (world - 1), seed=seed)
+        assert len({r[2:8] for r in rows}) == 1 and (rows[0][5] >> 2) & 1 == 0, rows
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_graph_key_uneven_slices_refused_before_any_collective(graph_key_probe, world):
+    """Uneven slices (n_total % world != 0) would give the ranks different B — and B % 16 decides
+    the permutation flag — so their keys could diverge and one rank would capture alone.  The key
+    derivation refuses it on the ranks whose slice differs (a rank-local MMVAE_E_ARG before the
+    step issues any collective), and eager steps (no comm graph) are unaffected."""
+    n_total = 4096 * world + 1
+    rows = graph_key_probe(world, n_total, True)
+    assert any(r[1] == -1 for r in rows), rows
+    assert all(r[1] == -1 or r[2] * world == n_total for r in rows)
+    assert all(r[1] == 0 for r in graph_key_probe(world, n_total, False))

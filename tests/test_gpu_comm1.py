@@ -6,8 +6,9 @@ world > 1 rank runs (capi.hip comm_bucket / enqueue_run) —
 
 * the two overlapped buckets: split gradient kernels, an event fork onto the comm stream, one
   ncclGroupStart / ncclAllReduce-per-range / ncclGroupEnd per bucket, the join before clip + Adam;
-* the flat path (MMVAE_NO_OVERLAP=1): one ncclAllReduce of the whole gradient on the main stream;
-* both inside a captured step graph (the default; MMVAE_COMM_GRAPH=0 runs them eagerly), after
+* the flat path (the eager default; MMVAE_NO_OVERLAP=1 forces it): one ncclAllReduce of the whole
+  gradient on the main stream;
+* both inside a captured step graph (opt-in, MMVAE_COMM_GRAPH=1; the default runs them eagerly), after
   the ranks' capture agreement (comm_capture_agree: an eager ncclAllReduce(min) of the capture
   outcome) and, once, their agreement on the batch-dependent buffers' size (comm_sync_capacity);
 * a capture that fails (MMVAE_TEST_COMM_CAPTURE_FAIL=1 makes comm_bucket refuse a capturing
@@ -26,11 +27,11 @@ pytestmark = pytest.mark.gpu
 D, K, B, N = 3000, 32, 384, 3000
 MODES = {
     # name: (env at comm_init / steps, graph on, expect replays)
-    "bucket": ({"MMVAE_COMM_GRAPH": "0"}, False),
-    "flat": ({"MMVAE_COMM_GRAPH": "0", "MMVAE_NO_OVERLAP": "1"}, False),
-    "bucket_graph": ({}, True),
-    "flat_graph": ({"MMVAE_NO_OVERLAP": "1"}, True),
-    "capture_fail": ({"MMVAE_TEST_COMM_CAPTURE_FAIL": "1"}, True),
+    "bucket": ({"MMVAE_OVERLAP": "1"}, False),
+    "flat": ({}, False),  # (the default: eager steps, one flat all-reduce)
+    "bucket_graph": ({"MMVAE_COMM_GRAPH": "1"}, True),
+    "flat_graph": ({"MMVAE_COMM_GRAPH": "1", "MMVAE_NO_OVERLAP": "1"}, True),
+    "capture_fail": ({"MMVAE_COMM_GRAPH": "1", "MMVAE_TEST_COMM_CAPTURE_FAIL": "1"}, True),
 }
 
 
@@ -95,12 +96,13 @@ def test_forced_one_rank_comm_bit_identical(model, dtype, mode, monkeypatch):
         assert st["replays"] == 5 and st["captures"] >= 3, st
 
 
-def test_comm_graph_opt_out(monkeypatch):
-    """MMVAE_COMM_GRAPH=0 (read at comm_init): a step with an active communicator runs eagerly even
-    with step graphs enabled — the fallback if RCCL calls inside graphs ever misbehave."""
+def test_comm_graph_is_opt_in(monkeypatch):
+    """Without MMVAE_COMM_GRAPH=1 (read at comm_init) a step with an active communicator runs
+    eagerly even with step graphs enabled (captured collectives stay opt-in until a
+    multi-rank run has exercised them)."""
     from mmvae_amd import Engine
     monkeypatch.setenv("MMVAE_FORCE_COMM", "1")
-    monkeypatch.setenv("MMVAE_COMM_GRAPH", "0")
+    monkeypatch.delenv("MMVAE_COMM_GRAPH", raising=False)
     eng = _engine("nb", "bf16x3")
     eng.comm_init(0, 1, Engine.comm_unique_id())
     eng.graph(True)
@@ -146,7 +148,7 @@ def test_comm_graph_heavier_batch_keeps_its_graphs(streamed, monkeypatch):
     monkeypatch.delenv("MMVAE_SPLIT_GRADS")
 
     monkeypatch.setenv("MMVAE_FORCE_COMM", "1")
-    monkeypatch.delenv("MMVAE_COMM_GRAPH", raising=False)  # (the default: RCCL inside step graphs)
+    monkeypatch.setenv("MMVAE_COMM_GRAPH", "1")  # (RCCL inside step graphs)
     eng, _ = make()
     eng.comm_init(0, 1, Engine.comm_unique_id())
     eng.graph(True)
@@ -159,3 +161,20 @@ def test_comm_graph_heavier_batch_keeps_its_graphs(streamed, monkeypatch):
         assert np.array_equal(got_p[k], want_p[k]), k
     # one capture per staging slot for the single launch shape; the heavy batches replayed them
     assert st["captures"] == 2 and st["replays"] == 8, st
+
+
+def test_comm_graph_uneven_slice_refused(monkeypatch):
+    """With RCCL calls inside step graphs the key must follow from n_total (graph_key.hpp): a step
+    whose B * world != n_total is refused before it issues any collective."""
+    from mmvae_amd import Engine, MMVAEError
+    monkeypatch.setenv("MMVAE_FORCE_COMM", "1")
+    monkeypatch.setenv("MMVAE_COMM_GRAPH", "1")
+    eng = _engine("nb", "bf16x3")
+    eng.comm_init(0, 1, Engine.comm_unique_id())
+    eng.graph(True)
+    cells = np.arange(B, dtype=np.int64)
+    with pytest.raises(MMVAEError):
+        eng.step(cells, 0.7, n_total=B + 16, step_id=0)
+    l, _ = eng.step(cells, 0.7, n_total=B, step_id=1)
+    assert np.isfinite(l)
+    eng.close()

@@ -53,10 +53,11 @@ def _batches(skew=False, device=0):
 
 def _worker(rank, model, no_overlap, uid_q, res_q, device, graph=False, skew=False):
     try:
-        if no_overlap:
-            os.environ["MMVAE_NO_OVERLAP"] = "1"
-        if not graph:  # RCCL calls inside step graphs are the default (read at comm_init)
-            os.environ["MMVAE_COMM_GRAPH"] = "0"
+        # no_overlap: the flat all-reduce; otherwise the two buckets (the default with graphs;
+        # forced by MMVAE_OVERLAP=1 for eager steps, whose default is flat)
+        os.environ["MMVAE_NO_OVERLAP" if no_overlap else "MMVAE_OVERLAP"] = "1"
+        if graph:  # RCCL calls inside step graphs are opt-in (read at comm_init)
+            os.environ["MMVAE_COMM_GRAPH"] = "1"
         from mmvae_amd import Engine
         if rank == 0:
             uid = Engine.comm_unique_id()

@@ -201,3 +201,64 @@ def test_streamed_async_pipeline(mode, monkeypatch):
             assert np.array_equal(x[k], y[k]), k
     cells = rng.integers(0, N, B)
     assert res.step(cells, 0.9, step_id=99) == st.step(cells, 0.9, step_id=99)
+
+
+@pytest.mark.parametrize("kind", ["packed", "unpacked"])
+def test_released_stream_arrays_reused_by_a_resident_upload(kind):
+    """The round-5 fault's sequence, made deterministic.  Until 3a24d7a the streamed
+    handle page-locked the caller's own arrays (hipHostRegister) and unregistered them at release.
+    In the suite, a streamed test's arrays were freed while its handle was still alive (the handle
+    went later, with the garbage collector); the next test allocated same-size arrays at the same
+    addresses, and its resident upload's plain host-to-device copy of `col` faulted ("illegal
+    memory access" in upload_chunked(d_col)).  Here: a streamed handle takes arrays A; A is freed
+    while the handle lives; new arrays A' are allocated (same sizes, typically the same addresses)
+    and a resident handle uploads from A' and trains; the streamed handle is then destroyed and a
+    second resident handle uploads from A' again.  Every result must equal a clean handle's, bit
+    for bit, with the streamed handle stepping in between (it must still read its own copies)."""
+    import gc
+    from mmvae_amd import MODEL_NB, Engine
+    N, D, B, K = 2500, 3000 if kind == "packed" else 70000, 256, 32
+    rp0, col0, val0, _ = _data(N, min(D, 3000), seed=21)
+    if kind == "unpacked":
+        val0 = val0 + np.float32(0.25)  # fractional values: the unpacked col / val pinned copies
+
+    def fresh():
+        return rp0.copy(), col0.copy(), val0.copy()
+
+    def run(eng):
+        eng.init_params(seed=5)
+        rng = np.random.default_rng(8)
+        return [eng.step(rng.integers(0, N, B), 0.8, step_id=s) for s in range(3)], eng.params(registered_only=True)
+
+    def make():
+        return Engine(D=D, K=K, max_batch=B, dtype="bf16x3", seed=11, model=MODEL_NB)
+
+    clean = make()
+    clean.upload_csr(*fresh())
+    want, want_p = run(clean)
+    clean.close()
+
+    a = fresh()
+    old_addr = [x.ctypes.data for x in a]
+    streamed = make()
+    streamed.stream_csr(*a)
+    s_res = run(streamed)
+    del a
+    gc.collect()
+    a2 = fresh()  # same sizes: the allocator hands back the freed ranges as a rule
+    reused = sum(x.ctypes.data == o for x, o in zip(a2, old_addr))
+    r1 = make()
+    r1.upload_csr(*a2)
+    got1, got1_p = run(r1)
+    # the streamed handle still reads its own (engine-owned) copies of the freed arrays
+    s_again = run(streamed)
+    streamed.close()
+    r1.close()
+    r2 = make()
+    r2.upload_csr(*a2)
+    got2, got2_p = run(r2)
+    r2.close()
+    assert got1 == want and got2 == want, (reused, got1, got2, want)
+    assert s_res[0] == want and s_again[0] == want, (s_res[0], s_again[0], want)
+    for k in want_p:
+        assert np.array_equal(got1_p[k], want_p[k]) and np.array_equal(got2_p[k], want_p[k]), k

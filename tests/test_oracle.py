@@ -2,7 +2,10 @@
 
 * fast-math helpers vs the reference's own fastlog.h/fastgamma.h (oracle/_ref, built from
   /root/reference when present) — bit-exact;
-* the oracle reproduces every golden fixture exactly (determinism of the pinned vectors);
+* every NB golden fixture is an output of the reference's own nb.hh model + Adam loop
+  (oracle/ref_nb_harness.cc); where the harness is built, it is re-run on each fixture's
+  inputs and must reproduce the fixture bit for bit (parity pinned to the reference);
+* the oracle reproduces every NB golden fixture — i.e. the reference's numbers — bit for bit;
 * the float64 restatement of the kernel algebra (oracle/nb_analytic.py) equals the
   oracle's LibTorch-autograd loss and gradients.
 """
@@ -14,7 +17,7 @@ import pytest
 import torch
 
 from helpers import GOLDEN, dims, golden_files, load, params_of, relu_of
-from oracle import fastmath, nb_analytic, nb_oracle, synth
+from oracle import fastmath, nb_analytic, nb_oracle, ref_nb, synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_fastmath.so")
@@ -39,6 +42,35 @@ def test_fastmath_known_constants():
     assert abs(float(fastmath.fasterlgamma(np.float32(25.0))) - 54.4777) < 1e-3
 
 
+def test_nb_fixtures_come_from_the_reference():
+    for p in golden_files("nb_"):
+        assert str(load(p)["source"]).startswith("reference nb.hh:1-563"), p
+
+
+@pytest.mark.skipif(not ref_nb.available(), reason="oracle/_ref/ref_nb_harness not built (needs /root/reference)")
+@pytest.mark.parametrize("path", golden_files("nb_"), ids=os.path.basename)
+def test_reference_reproduces_golden(path):
+    """Re-run the reference (nb.hh:1-563, mmvae_alg.hh:234-310 on LibTorch) on the fixture's
+    parameters, rows and seeds: every stored number must come back bit for bit."""
+    z = load(path)
+    d = dims(z)
+    enc, dec = (tuple(int(v) for v in z[k]) for k in ("enc_layers", "dec_layers"))
+    params = {**params_of(z, "init/"), **params_of(z, "frozen/")}
+    def rows(cells):
+        return synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]), z["covar"][cells]
+    sched = []
+    for t in range(int(z["steps"])):
+        x, c = rows(z[f"s{t}/cells"])
+        sched.append(dict(x=x, c=c, ridx=np.arange(d["B"]), beta=float(z[f"s{t}/beta"]),
+                          seed=int(z[f"s{t}/torch_seed"])))
+    x, c = rows(z["eval/cells"])
+    evalb = dict(x=x, c=c, beta=float(z["eval/beta"]), seed=int(z["eval/torch_seed"]))
+    ref = ref_nb.run(d["D"], d["C"], d["K"], d["H"], d["R"], relu_of(z), 0, enc, dec, sched, evalb,
+                     params_in={k.replace("frozen/", ""): v for k, v in params.items()})
+    for k, v in ref.items():
+        np.testing.assert_array_equal(np.asarray(v, z[k].dtype).reshape(z[k].shape), z[k], err_msg=k)
+
+
 @pytest.mark.parametrize("path", golden_files("nb_"), ids=os.path.basename)
 def test_oracle_reproduces_golden(path):
     z = load(path)
@@ -57,6 +89,14 @@ def test_oracle_reproduces_golden(path):
             np.testing.assert_array_equal(v.numpy(), z[f"s{t}/grad/{k}"])
         for k, v in tr.params().items():
             np.testing.assert_array_equal(v.numpy(), z[f"s{t}/param/{k}"])
+    cells = z["eval/cells"]
+    x = torch.from_numpy(synth.densify(z["rowptr"], z["col"], z["val"], cells, d["D"]))
+    el = tr.eval_loss(x, torch.from_numpy(z["covar"][cells]), torch.from_numpy(z["eval/eps_mu"]),
+                      torch.from_numpy(z["eval/eps_nu"]), float(z["eval/beta"]))
+    assert np.float32(el) == z["eval/loss"]
+    m, lv = tr.encode(x)
+    np.testing.assert_array_equal(m.numpy(), z["eval/enc_mean"])
+    np.testing.assert_array_equal(lv.numpy(), z["eval/enc_lnvar"])
 
 
 @pytest.mark.parametrize("path", golden_files("nb_"), ids=os.path.basename)
