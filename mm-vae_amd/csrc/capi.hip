@@ -337,8 +337,10 @@ int mmvae_create(const mmvae_cfg* cfg, int device, mmvae_h* out) {
     const bool vmf_model = cfg->model == MMVAE_MODEL_VMF;
     const bool bf_ops = cfg->dtype == MMVAE_DTYPE_BF16 || cfg->dtype == MMVAE_DTYPE_FP8;  // fp8: bf16 encoders / dz
     // vMF x3 at K <= 32: ~48 KB of LDS per decoder workgroup (no WdT image): 3 per CU
+    // NB x3 with MMVAE_DEC3=1: pass B at three 4-wave workgroups per CU (k_dec_nb D3)
+    e->dec3 = !vmf_model && cfg->dtype == MMVAE_DTYPE_BF16X3 && getenv_is("MMVAE_DEC3", "1");
     const int dec_cu = vmf_model ? (bf_ops ? 4 : (cfg->dtype == MMVAE_DTYPE_BF16X3 && e->KP == 32 ? 3 : 2))
-                                 : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : 2);
+                                 : (cfg->dtype == MMVAE_DTYPE_F32 ? 1 : e->dec3 ? 3 : 2);
     e->nsplit_d = pick_split(dec_cu);
     // vMF forward decoder pass: ~29 KB of LDS and <= 128 VGPRs in the 16-bit operand modes at
     // K <= 32 with one covariate (VFwdOcc, vmf_kernels.hip): 4 per CU instead of the backward's 3

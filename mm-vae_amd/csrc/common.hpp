@@ -195,8 +195,7 @@ template <int RB> MMVAE_DEV int swz_off(int row, int byte) {
 // receives column i of the 4 rows (cdna_hip_programming.md T10).  The 8-byte pieces stay whole
 // under swz_off's 16-byte chunk XOR.  EXEC must be all ones.
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0) {
-    const int lane = threadIdx.x & 63;
+template <int RB> MMVAE_DEV bf16x8 tr_frag(const char* img, int r0, int c0, int lane = (int)threadIdx.x & 63) {
     const int row = r0 + 8 * (lane >> 4) + ((lane >> 2) & 3);
     const int byte = (c0 + 4 * (lane & 3)) * 2;
     typedef __attribute__((address_space(3))) bf16x4 lds_v4;
@@ -218,8 +217,7 @@ MMVAE_DEV uint32_t pk_bf16(float a, float b) { return __builtin_bit_cast(uint32_
 template <int BS = 2048> MMVAE_DEV int pqt_off(int g, int r) {
     return (g >> 4) * BS + (g & 15) * 32 + (((r >> 2) ^ ((g >> 2) & 3)) << 3) + (r & 3) * 2;
 }
-template <int BS = 2048> MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0) {
-    const int lane = threadIdx.x & 63;
+template <int BS = 2048> MMVAE_DEV bf16x8 pqt_frag(const char* img, int k0, int lane = (int)threadIdx.x & 63) {
     const int k = k0 + 8 * (lane >> 4) + ((lane >> 2) & 3), r = 4 * (lane & 3);
     typedef __attribute__((address_space(3))) bf16x4 lds_v4;
     const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + pqt_off<BS>(k, r)));
@@ -240,12 +238,15 @@ template <int BS, bool SPLIT> MMVAE_DEV void pqt_put(char* img, int PO, int g, i
 }
 
 template <class P, int RB> struct TrFrag;
+// (lane: threadIdx.x & 63, or a kernel's per-tile opaque copy of it — see k_dec_nb D3)
 template <int RB> struct TrFrag<__bf16, RB> {
-    static MMVAE_DEV bf16x8 load(const char* img, int r0, int c0, int) { return tr_frag<RB>(img, r0, c0); }
+    static MMVAE_DEV bf16x8 load(const char* img, int r0, int c0, int, int lane = (int)threadIdx.x & 63) {
+        return tr_frag<RB>(img, r0, c0, lane);
+    }
 };
 template <int RB> struct TrFrag<X3, RB> {  // hi and lo planes, plane_bytes apart
-    static MMVAE_DEV MM<X3>::frag load(const char* img, int r0, int c0, int plane_bytes) {
-        return MM<X3>::frag{tr_frag<RB>(img, r0, c0), tr_frag<RB>(img + plane_bytes, r0, c0)};
+    static MMVAE_DEV MM<X3>::frag load(const char* img, int r0, int c0, int plane_bytes, int lane = (int)threadIdx.x & 63) {
+        return MM<X3>::frag{tr_frag<RB>(img, r0, c0, lane), tr_frag<RB>(img + plane_bytes, r0, c0, lane)};
     }
 };
 

@@ -217,6 +217,7 @@ struct Engine {
     float* h_out_pin = nullptr;
 
     int nsplit_e = 1, nsplit_d = 1;  // D-splits of encoder / decoder pass-B grids
+    bool dec3 = false;               // NB x3: the three-waves-per-SIMD pass B (MMVAE_DEC3=1)
     int nsplit_f = 1;                // vMF decoder forward pass (4 workgroups per CU where it fits)
     int nsplit_b = 1;                // D-split of the encoder backward
     int nsplit_a = 1;                // D-split of decoder passes A / C

@@ -971,15 +971,40 @@ template <> struct CorrPair<__bf16> {  // bf16 mode: both corrections rounded to
 // the tile is re-zeroed after the dz GEMM has read pq — saving the separate 4.6 KB pq tile per
 // wave that would not fit 8 waves of x3 images in 160 KB.
 struct DecNBLds {
-    int o_gst, o_tst, o_part, o_fact, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, bytes;
+    int o_gst, o_tst, o_part, o_fact, o_wave, wave_bytes, o_q1, o_q2, o_cc, o_toff, o_rsc, o_du = 0, bytes;
     int sw, st, sp;     // per-buffer strides: W tile, WdT tile (bytes, all planes), column partials (floats)
     int swp, stp;       // one plane of the W / WdT images (bytes)
     // eszw: element size of the staged logit operand (1 in the fp8 mode), esz: the dz operands'.
     // loss: the eval instance (no WdT stage, column partials, correction or pq tiles)
     // no_wdt: the dz GEMM reads its W operand transposed from the logit GEMM's W image (the
     // staggered x3 instance), so there is no WdT stage
+    // d3: the three-waves-per-SIMD instance (k_dec_nb D3, x3): one stage buffer, no column
+    // partial buffer (each wave's partials go into its own p tile after the dz GEMM), the p tile
+    // unpadded (gene index XOR-swizzled by row), the correction tile holds p dq only (d du is
+    // summed by the sparse pass into the wave's du accumulators), so 4 waves fit in 53 KB
     MMVAE_HOSTDEV DecNBLds(int KP, int esz, int S, int nq, int NRS, int csz, int NW, int nbuf, int planes, int eszw,
-                           bool loss = false, bool no_wdt = false) {
+                           bool loss = false, bool no_wdt = false, bool d3 = false) {
+        if (d3) {
+            swp = 64 * KP * eszw;
+            stp = 0;
+            sw = planes * swp;
+            st = 0;
+            sp = 0;
+            o_gst = sw;
+            o_tst = o_gst + 1024;
+            o_part = o_tst;
+            o_fact = o_part;
+            o_wave = o_fact + 64;
+            o_q2 = 0;                 // p tile [16][64] f32 (x3: column partials [nq][64] after the dz GEMM)
+            o_cc = 16 * 64 * 4;       // p dq plane per 16-gene block, 1 KB blocks (pq hi / lo aliased)
+            o_q1 = o_cc;
+            o_du = o_cc + 16 * 64 * 4;  // du sums: [64] genes, [64] genes x z_nu, [16] rows x w_nu
+            o_toff = o_du + (64 + 64 + 16) * 4;
+            o_rsc = o_toff + ((S * 4 + 15) / 16) * 16;
+            wave_bytes = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
+            bytes = o_wave + NW * wave_bytes;
+            return;
+        }
         const bool alias = planes == 2 && !loss;
         swp = 64 * KP * eszw;
         stp = (loss || no_wdt) ? 0 : KP * 64 * esz;
@@ -1012,9 +1037,15 @@ struct DecNBLds {
 // (below), the W stage is double-buffered and serves the dz GEMM transposed (no WdT stage)
 // TRW: no WdT stage, the dz GEMM reads W transposed (as SG does) — with DB, the x3 8-wave instance
 // then double-buffers its stage and meets one barrier per tile (the default x3 training instance)
+// D3: three waves per SIMD — 4-wave / 64-row workgroups, three per CU (<= 168 VGPRs, <= 53 KB of
+// LDS: DecNBLds d3), so each SIMD holds waves of three independent workgroups and one wave's
+// barrier wait leaves two others issuing.  The sparse pass stores only p dq per nonzero and
+// adds its d du terms straight into the wave's LDS du sums (per-wave arrays, one wave's ds_add
+// in program order: no cross-wave races); each wave's column partials go into its own p tile
+// after the dz GEMM; one stage buffer, two barriers per tile.
 template <class P, int KP, int CM, int RM, int NW, bool DB, class PL = P, bool LOSS = false, bool SG = false,
-          bool TRW = false>
-__global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec_nb(DecPtrs Q, Dims d) {
+          bool TRW = false, bool D3 = false>
+__global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW)) void k_dec_nb(DecPtrs Q, Dims d) {
     using T = typename Elem<P>::type;
     using M = MM<P>;
     using Fr = typename M::frag;
@@ -1039,7 +1070,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     // ran 6 % slower with the planes)
     constexpr bool PLANAR = X;
     // (16-byte row quads XOR-swizzled by gene so the 16 genes of a lane group hit distinct banks)
-    auto ccp = [](int r, int g) { return (g >> 4) * 2048 + (g & 15) * 64 + (((r >> 2) ^ ((g >> 2) & 3)) << 4) + (r & 3) * 4; };
+    constexpr int PQBS = D3 ? 1024 : 2048;  // x3: bytes per 16-gene block of the correction / pq tile
+    auto ccp = [](int r, int g) { return (g >> 4) * PQBS + (g & 15) * 64 + (((r >> 2) ^ ((g >> 2) & 3)) << 4) + (r & 3) * 4; };
     constexpr int PS = 68;
     // CM = 0: unit covariate (Engine::unit_covar, C = 1): the covariate Linear folds into the
     // gene's bias, and its weight gradient's column sums are the bias gradient's
@@ -1049,7 +1081,11 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     constexpr int RBT = 64 * (int)sizeof(T);  // staged WdT row (one latent, 64 genes)
     constexpr float L2E = 1.4426950408889634f;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // (D3: lane is re-made opaque every tile, so the lane-derived LDS addresses are recomputed
+    // instead of being hoisted out of the tile loop and spilled)
+    int lane = threadIdx.x & 63;
+    int tido = threadIdx.x;  // (D3: opaque per tile, as lane)
+    const int w = threadIdx.x >> 6;
     constexpr int NTH = 64 * NW;
     const int sp = blockIdx.x % d.nsD, rbw = blockIdx.x / d.nsD;
     const int row0 = rbw * 16 * NW + 16 * w;
@@ -1058,11 +1094,14 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     const int C = (CM <= 1) ? 1 : d.C, R = (RM == 1) ? 1 : d.R;
     const int nq = (1 + C) + 1 + R;
     static_assert(!SG || (X && DB && NW == 8 && !LOSS), "the staggered pass B is the x3 training instance");
-    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG || TRW);
+    static_assert(!D3 || (X && NW == 4 && !DB && TRW && !LOSS && !SG && CM <= 1 && RM == 1 && !F8M),
+                  "the three-waves-per-SIMD pass B is the x3 training instance for C = R = 1");
+    const DecNBLds L(KP, (int)sizeof(T), S, nq, NRS, (int)sizeof(CT), NW, DB ? 2 : 1, NPL, (int)sizeof(TL), LOSS, SG || TRW, D3);
     char* wst = smem;
     const float4* gst = reinterpret_cast<const float4*>(smem + L.o_gst);
     char* tst = smem + L.o_tst;
-    float* part = reinterpret_cast<float*>(smem + L.o_part);  // [4][nq][64]
+    // [4][nq][64] column partials; D3: prologue / loss scratch in wave 0's p tile
+    float* part = reinterpret_cast<float*>(smem + (D3 ? L.o_wave + L.o_q2 : L.o_part));
     float* ftab = reinterpret_cast<float*>(smem + L.o_fact);
     if (threadIdx.x < 9) {  // published by the barrier of the row lse block below
         float f = 1.f;
@@ -1075,6 +1114,11 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     CT* cc = reinterpret_cast<CT*>(wp + L.o_cc);
     int32_t* toffl = reinterpret_cast<int32_t*>(wp + L.o_toff);
     float* rsc = reinterpret_cast<float*>(wp + L.o_rsc);
+    float* duacc = reinterpret_cast<float*>(wp + L.o_du);  // D3: [64] sum du, [64] sum du z_nu, [16] sum du w_nu
+    // the p tile's element (r, g): D3 unpadded with the gene XOR-swizzled by row (8-gene groups
+    // stay contiguous for the dz GEMM's fragment reads), else a 68-float row stride
+    auto qx = [](int r, int g) { return D3 ? r * 64 + (g ^ ((r & 7) << 3)) : r * 68 + g; };
+    constexpr int CCBYTES = D3 ? 16 * 64 * 4 : 16 * 64 * (int)sizeof(CT);  // correction tile bytes
     const T* Z = BF ? reinterpret_cast<const T*>(Q.zb) : reinterpret_cast<const T*>(Q.zf);
     const char* WdPc = reinterpret_cast<const char*>(Q.WdP);
     const char* WdTc = reinterpret_cast<const char*>(Q.WdT);
@@ -1094,18 +1138,20 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     constexpr int NST = SG ? NTH / 2 : NTH;
     const bool lag = SG && w >= NW / 2;
     const bool stager = !SG || lag;
-    const int stid = (int)threadIdx.x & (NST - 1);
+    auto stid_ = [&]() { return (D3 ? tido : (int)threadIdx.x) & (NST - 1); };
     DualStage<64, RBW, NST, X> wreg;
     DualStage<KP, RBT, NTH, X> treg;
     float4 greg = float4{0.f, 0.f, 0.f, 0.f};
     const int64_t wplb = Q.wplane * (int64_t)sizeof(T);
     auto stage_load = [&](int t) {
-        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb);
+        const int stid = stid_();
+        wreg.load(WdPc + (int64_t)64 * t * RBW, RBW, wplb, D3 ? tido : (int)threadIdx.x);
         if constexpr (!LOSS && !SG && !TRW) treg.load(WdTc + (int64_t)64 * t * sizeof(T), (int64_t)d.DP * sizeof(T), wplb);
         if (stid < 64) greg = grec[64 * t + stid];
     };
     auto stage_store = [&](int b_) {
-        wreg.store(wst + b_ * L.sw, L.swp);
+        const int stid = stid_();
+        wreg.store(wst + b_ * L.sw, L.swp, D3 ? tido : (int)threadIdx.x);
         if constexpr (!LOSS && !SG && !TRW) treg.store(tst + b_ * L.st, L.stp);
         if (stid < 64) reinterpret_cast<float4*>(smem + L.o_gst)[64 * b_ + stid] = greg;
     };
@@ -1187,7 +1233,9 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         for (int c = 0; c < CM; ++c) rs[3 + RM + c] = (c < C) ? Q.covar[cell * C + c] : 0.f;
     }
     if constexpr (!LOSS)
-        for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        for (int i = lane; i < CCBYTES / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+    if constexpr (D3)
+        for (int i = lane; i < 64 + 64 + 16; i += 64) duacc[i] = 0.f;
 
     wave_sync();  // toffl
     ListEntries pend;
@@ -1243,11 +1291,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 float lg = fmaf(acc[r], ainv, gx);
 #pragma unroll
                 for (int c2 = 0; c2 < CM; ++c2) lg = fmaf(crow2[r >> 1][c2][r & 1], wcd[c2], lg);
-                q2[(4 * (lane >> 4) + r) * PS + gl] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
+                q2[qx(4 * (lane >> 4) + r, gl)] = fexp2(fmaf(lg, L2E, -lse2[r]));  // nb.hh:440-441
             }
         }
         wave_sync();
         lap(0);
+        if constexpr (D3) __builtin_amdgcn_sched_barrier(0);  // (phases not interleaved: register budget)
         // ---- 2. sparse pass: x-dependent terms of the tile's nonzeros ----
         // 16-bit operand modes (x3, bf16): two entries per lane as one packed pair (entries lane
         // and lane + 64, then + 128 / + 192 ...), packed arithmetic throughout (nb_nu2: the
@@ -1260,7 +1309,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 const f2 x = f2{__uint_as_float(ea.y), vb ? __uint_as_float(eb.y) : 0.f};
                 const float* rsa = rsc + ra * NRS;
                 const float* rsb = rsc + rb * NRS;
-                const f2 p = f2{q2[ra * PS + ga], q2[rb * PS + gb2]};
+                const f2 p = f2{q2[qx(ra, ga)], q2[qx(rb, gb2)]};
                 const f2 mu = fma2(p, f2{rsa[0], rsb[0]}, splat2(1e-4f));  // nb.hh:519
                 const float4 g4a = gsb[ga], g4b = gsb[gb2];
                 f2 u = f2{g4a.y, g4b.y};
@@ -1306,7 +1355,9 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 if constexpr (!LOSS) {
                     const f2 pdq = p * dq;
                     auto put = [&](int r, int gl, float a, float b) {
-                        if constexpr (PLANAR) {
+                        if constexpr (D3) {
+                            *reinterpret_cast<float*>(reinterpret_cast<char*>(cc) + ccp(r, gl)) = a;
+                        } else if constexpr (PLANAR) {
                             char* cb = reinterpret_cast<char*>(cc) + ccp(r, gl);
                             *reinterpret_cast<float*>(cb) = a;
                             *reinterpret_cast<float*>(cb + 1024) = b;
@@ -1316,11 +1367,23 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                     };
                     put(ra, ga, pdq.x, ddu.x);
                     if (vb) put(rb, gb2, pdq.y, ddu.y);
+                    if constexpr (D3) {  // the d du terms into the wave's du sums (R = 1)
+                        const f2 dz = ddu * f2{rsa[3], rsb[3]};  // x z_nu of the entry's row
+                        const f2 dw = ddu * f2{g4a.w, g4b.w};    // x w_nu of the entry's gene
+                        atomicAdd(&duacc[ga], ddu.x);
+                        atomicAdd(&duacc[64 + ga], dz.x);
+                        atomicAdd(&duacc[128 + ra], dw.x);
+                        if (vb) {
+                            atomicAdd(&duacc[gb2], ddu.y);
+                            atomicAdd(&duacc[64 + gb2], dz.y);
+                            atomicAdd(&duacc[128 + rb], dw.y);
+                        }
+                    }
                 }
             });
         } else if (!dbg_bit(d.dbg, 1)) pend.visit(Q.ents, lane, [&](int r, int gl, float x) {
             const float* rs_ = rsc + r * NRS;
-            const float p = q2[r * PS + gl];
+            const float p = q2[qx(r, gl)];
             const float mu = fmaf(p, rs_[0], 1e-4f);
             const float4 g4 = gsb[gl];
             float wnd[RM];
@@ -1354,9 +1417,11 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         });
         wave_sync();
         lap(1);
+        if constexpr (D3) __builtin_amdgcn_sched_barrier(0);  // (phases not interleaved: register budget)
         // ---- prefetch the next tile's entries (rinc reused; loads stay in flight) ----
         pend.fetch(Q.ents, segw, toffl, min(tl + 1, t1 - t0 - 1), lane);
         lap(2);
+        if constexpr (D3) __builtin_amdgcn_sched_barrier(0);  // (phases not interleaved: register budget)
     };
     // ---- phases E + Z of tile c.t: dense epilogue, dz GEMM ----
     auto phase_ez = [&](const TileCtx& c) {
@@ -1366,10 +1431,12 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         // ---- 3. dense epilogue in the owner lanes ----
         // MASK: some of the wave's rows (last row block) or the tile's genes (last tile) are
         // padding; the common case runs without the validity products.
+        float colv[4];  // D3: the lane's column partial of each gene block (stored after the dz GEMM)
         auto epilogue = [&](auto mask_c) {
             constexpr bool MASK = decltype(mask_c)::value;
             constexpr float LN2 = 0.6931471805599453f;
-            constexpr int GBU = (CM <= 1 && RM == 1) ? 4 : 1;  // the general variant stays rolled
+            // (the general variant stays rolled; D3 too, for its register budget)
+            constexpr int GBU = (CM <= 1 && RM == 1 && !D3) ? 4 : 1;
 #pragma unroll GBU
             for (int gb = 0; gb < 4; ++gb) {
                 const int gl = 16 * gb + (lane & 15);
@@ -1396,7 +1463,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         for (int h = 0; h < 2; ++h) {
                             const char* cb = reinterpret_cast<const char*>(cc) + ccp(4 * (lane >> 4) + 2 * h, gl);
                             cpv[h] = *reinterpret_cast<const f2*>(cb);
-                            cdv[h] = *reinterpret_cast<const f2*>(cb + 1024);
+                            if constexpr (!D3) cdv[h] = *reinterpret_cast<const f2*>(cb + 1024);
                         }
                     } else {
 #pragma unroll
@@ -1407,7 +1474,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {  // rows rl, rl + 1 as one packed pair
                     const int rl = 4 * (lane >> 4) + 2 * h;
-                    const f2 p = f2{q2[rl * PS + gl], q2[(rl + 1) * PS + gl]};
+                    const f2 p = f2{q2[qx(rl, gl)], q2[qx(rl + 1, gl)]};
                     const f2 mu = fma2(p, dv2[h], splat2(1e-4f));                // nb.hh:519
                     f2 u = splat2(cn);
 #pragma unroll
@@ -1434,7 +1501,8 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         cdp = f2{cda, cdb};
                     }
                     const f2 pq = fma2(p, qv, cpp);                              // qv = n dL/dmu' - 1 at x = 0
-                    const f2 du = fma2(fma2(lg2, splat2(LN2), qv), sgm, cdp);
+                    // (D3: the nonzeros' d du terms went into the du sums in the sparse pass)
+                    const f2 du = D3 ? fma2(lg2, splat2(LN2), qv) * sgm : fma2(fma2(lg2, splat2(LN2), qv), sgm, cdp);
                     Eacc2[h] += pq;
                     cs1[0] = fma2(wv2[h], pq, cs1[0]);
 #pragma unroll
@@ -1446,7 +1514,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                         dzn2[h][qq] = fma2(du, splat2(wnd[qq]), dzn2[h][qq]);
                     }
                     if constexpr (X) {  // hi / lo planes of the row pair, one word each
-                        pqt_put<2048, true>(reinterpret_cast<char*>(q1), 512, gl, rl, pq.x, pq.y);
+                        pqt_put<PQBS, true>(reinterpret_cast<char*>(q1), 512, gl, rl, pq.x, pq.y);
                     } else if constexpr (BF) {  // bf16: the separate q1 tile, compact blocks
                         pqt_put<512, false>(reinterpret_cast<char*>(q1), 0, gl, rl, pq.x, pq.y);
                     } else {
@@ -1459,8 +1527,13 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 // (CM = 0: the covariate column sums sum_b w_b c_b pq with c_b = 1 are cs1[0])
                 const f2 cs1c = (CM == 0) ? cs1[0] : cs1[1];
                 if (CM <= 1 && RM == 1) {  // nq = 4: one transposed reduction, every lane stores
-                    pw[(lane >> 4) * 64] = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1c.x + cs1c.y, csdu.x + csdu.y,
-                                                          csduz[0].x + csduz[0].y);
+                    const float v = sum_rowgroups4(cs1[0].x + cs1[0].y, cs1c.x + cs1c.y, csdu.x + csdu.y,
+                                                   csduz[0].x + csduz[0].y);
+                    if constexpr (D3) {  // (rolled loop: selects keep colv in registers)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) colv[k] = (gb == k) ? v : colv[k];
+                    }
+                    else pw[(lane >> 4) * 64] = v;
                 } else {
 #pragma unroll
                     for (int c2 = 0; c2 < 1 + CA; ++c2)
@@ -1490,6 +1563,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
         if constexpr (!X && !LOSS)
             for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
         lap(3);
+        if constexpr (D3) __builtin_amdgcn_sched_barrier(0);  // (phases not interleaved: register budget)
         // ---- 4. dz partial = sum_g Q[cell][g] W[g][latent] on MFMA ----
         if (!LOSS && !dbg_bit(d.dbg, 4))
 #pragma unroll
@@ -1497,18 +1571,18 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
                 Fr a1;
                 if constexpr (X) {
                     const char* qb = reinterpret_cast<const char*>(q1);
-                    a1 = Fr{pqt_frag(qb, s * M::KSTEP), pqt_frag(qb + 512, s * M::KSTEP)};
+                    a1 = Fr{pqt_frag<PQBS>(qb, s * M::KSTEP, lane), pqt_frag<PQBS>(qb + 512, s * M::KSTEP, lane)};
                 } else if constexpr (BF) {
                     a1 = pqt_frag<512>(reinterpret_cast<const char*>(q1), s * M::KSTEP);
                 } else {
                     a1 = M::load(&q1[q1i(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)], Q1PL);
                 }
-                const Fr a2 = M::load_f32(&q2[(lane & 15) * PS + s * M::KSTEP + (lane >> 4) * M::EPL]);
+                const Fr a2 = M::load_f32(&q2[qx(lane & 15, s * M::KSTEP + (lane >> 4) * M::EPL)]);
 #pragma unroll
                 for (int lb = 0; lb < KP / 16; ++lb) {
                     Fr bw;
                     if constexpr (SG || TRW)  // transposed from the logit GEMM's W image (genes = k)
-                        bw = TrFrag<P, RBW>::load(c.wsb, s * M::KSTEP, 16 * lb, L.swp);
+                        bw = TrFrag<P, RBW>::load(c.wsb, s * M::KSTEP, 16 * lb, L.swp, lane);
                     else
                         bw = M::load(reinterpret_cast<const T*>(
                             c.tsb + swz_off<RBT>(16 * lb + (lane & 15), (s * M::KSTEP + (lane >> 4) * M::EPL) * (int)sizeof(T))),
@@ -1519,7 +1593,22 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             }
         if constexpr (X && !LOSS) {  // pq consumed: re-zero the correction tile it aliased
             wave_sync();
-            for (int i = lane; i < 16 * 64 * (int)sizeof(CT) / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+            for (int i = lane; i < CCBYTES / 16; i += 64) reinterpret_cast<uint4*>(cc)[i] = uint4{0, 0, 0, 0};
+        }
+        if constexpr (D3) {
+            // the p tile is consumed: the wave's column partials [nq][64] go there (read by the
+            // combine after the barrier), the du sums of the sparse pass added to theirs; the
+            // per-tile du sums are cleared (the row sums at 128.. accumulate over the tiles)
+            wave_sync();
+            const int q = lane >> 4;
+#pragma unroll
+            for (int gb = 0; gb < 4; ++gb) {
+                const int gl = 16 * gb + (lane & 15);
+                q2[q * 64 + gl] = colv[gb] + (q >= 2 ? duacc[(q - 2) * 64 + gl] : 0.f);
+            }
+            wave_sync();
+            duacc[lane] = 0.f;
+            duacc[64 + lane] = 0.f;
         }
         lap(4);
     };
@@ -1527,11 +1616,17 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     //      [th0, th0 + nth) ----
     auto combine = [&](const TileCtx& c, int th0, int nth) {
         if (LOSS || dbg_bit(d.dbg, 16384)) return;  // 16384: diagnostic, slab stores skipped
-        for (int i = (int)threadIdx.x - th0; i < (NW / 4) * nq * 64; i += nth) {  // per 64-row slab block h
+        for (int i = (D3 ? tido : (int)threadIdx.x) - th0; i < (NW / 4) * nq * 64; i += nth) {  // per 64-row slab block h
             const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
-            const float* ph = c.pb + 4 * h * nq * 64;
-            const float v = ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
-                            ph[(3 * nq + q) * 64 + g];
+            float v;
+            if constexpr (D3) {  // each wave's partials in its p tile
+                auto pw_ = [&](int wv) { return reinterpret_cast<const float*>(smem + L.o_wave + wv * L.wave_bytes + L.o_q2); };
+                v = pw_(0)[q * 64 + g] + pw_(1)[q * 64 + g] + pw_(2)[q * 64 + g] + pw_(3)[q * 64 + g];
+            } else {
+                const float* ph = c.pb + 4 * h * nq * 64;
+                v = ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
+                    ph[(3 * nq + q) * 64 + g];
+            }
             Q.slabB[((int64_t)(rbw * (NW / 4) + h) * nq + q) * d.DP + 64 * c.t + g] = v;
         }
     };
@@ -1574,7 +1669,10 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
     } else {
         for (int t = t0; t < t1; ++t) {
             const int tl = t - t0;
-            stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
+            // (D3: the next stage is loaded after the tile's barrier, right before it is stored, so
+            // its registers are not live across the tile; the latency is the other workgroups')
+            if constexpr (!D3) stage_load(min(t + 1, t1 - 1));  // unconditional (clamped): counted waits, not vmcnt(0)
+            if constexpr (D3) asm volatile("" : "+v"(lane), "+v"(tido));
             const TileCtx c = ctx(t);
             phase_ls(c);
             phase_ez(c);
@@ -1586,7 +1684,14 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             combine(c, 0, NTH);
             lap(5);
             if (!DB) {
-                if (t + 1 < t1) stage_store(0);
+                if constexpr (D3) {
+                    if (t + 1 < t1) {
+                        stage_load(t + 1);
+                        stage_store(0);
+                    }
+                } else if (t + 1 < t1) {
+                    stage_store(0);
+                }
                 lds_barrier();
             }
             lap(6);
@@ -1618,6 +1723,7 @@ __global__ __launch_bounds__(64 * NW, (LOSS && NW == 8) ? 2 : 8 / NW) void k_dec
             for (int q = 0; q < RM; ++q) dz2[q] += __shfl_xor(dz2[q], o, 64);
         }
         const int b = row0 + 4 * (lane >> 4) + r;
+        if constexpr (D3) dz2[0] += duacc[128 + 4 * (lane >> 4) + r];  // the nonzeros' d du w_nu terms
         if ((lane & 15) == 0) {
             float* rp = Q.rowB + ((int64_t)sp * d.Bpad + b) * (2 + R);
             rp[0] = E;
@@ -2535,7 +2641,11 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const int csz = (bf && !X) ? 4 : 8;
     const bool nw4 = getenv_is("MMVAE_DEC_NW", "4");
     const size_t ldsB8 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL, (int)sizeof(TL)).bytes;
-    const int nwB = (small_cr && bf && ldsB8 <= 160 * 1024 && !nw4) ? 8 : 4;
+    // x3 with MMVAE_DEC3=1 (read at create, Engine::dec3): the three-waves-per-SIMD instance
+    // (4-wave workgroups, three per CU; the gene split was sized for three at create)
+    const size_t lds3 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL), false, true, true).bytes;
+    const bool use_d3 = X && e->dec3 && small_cr && lds3 <= 160 * 1024 / 3;
+    const int nwB = use_d3 ? 4 : (small_cr && bf && ldsB8 <= 160 * 1024 && !nw4) ? 8 : 4;
     const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
     const dim3 gdecA(nrb / 2 * d.nsA);  // passes A / C: 128 rows per workgroup
     const size_t ldsA = dec_lds(d, 0, (int)sizeof(TL), NPL), ldsC = dec_lds(d, 2, (int)sizeof(TL), NPL);
@@ -2558,6 +2668,13 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     const bool use_trwdb = X && nwB == 8 && trwdb_on && !use_sg && ldsSG <= 160 * 1024;
     auto launch_b = [&](auto loss_c) {
         constexpr bool LS = decltype(loss_c)::value;
+        if constexpr (X && !LS && std::is_same<PB, PM>::value) {
+            if (use_d3) {
+                if (ucov) hipLaunchKernelGGL((k_dec_nb<PB, KP, 0, 1, 4, false, PM, false, false, true, true>), gdecB, dim3(256), lds3, st, Q, d);
+                else hipLaunchKernelGGL((k_dec_nb<PB, KP, 1, 1, 4, false, PM, false, false, true, true>), gdecB, dim3(256), lds3, st, Q, d);
+                return;
+            }
+        }
         if (nwB == 8) {
             const size_t lds = LS ? DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 8, X ? 1 : 2, NPL, (int)sizeof(TL), true).bytes
                                   : ldsB8;

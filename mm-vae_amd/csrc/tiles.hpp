@@ -541,28 +541,30 @@ struct RegStage {
     static_assert((NTH & (NTH - 1)) == 0, "RegStage: a power-of-two thread group");
     // the staging threads are NTH consecutive threads of the block (a whole block, or one
     // aligned half of it): thread index within the group
-    static MMVAE_DEV int tid() { return (int)threadIdx.x & (NTH - 1); }
+    // (tx: the block's thread index — threadIdx.x, or a copy a kernel keeps opaque per tile so the
+    // addresses derived from it are recomputed rather than held across its loop)
+    static MMVAE_DEV int tid(int tx) { return tx & (NTH - 1); }
     u32x4 v0, v1, v2, v3;
-    MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i) const {
-        const int c = PART ? min(tid(), CH - 1) : tid() + NTH * i;
+    MMVAE_DEV u32x4 ld1(const char* src, int64_t ld, int i, int tx) const {
+        const int c = PART ? min(tid(tx), CH - 1) : tid(tx) + NTH * i;
         return *reinterpret_cast<const u32x4*>(src + (int64_t)(c / (RB / 16)) * ld + (c % (RB / 16)) * 16);
     }
-    MMVAE_DEV void st1(char* dst, int i, u32x4 x) const {
-        const int c = tid() + NTH * i;
+    MMVAE_DEV void st1(char* dst, int i, u32x4 x, int tx) const {
+        const int c = tid(tx) + NTH * i;
         if (PART && c >= CH) return;
         *reinterpret_cast<u32x4*>(dst + swz_off<RB>(c / (RB / 16), (c % (RB / 16)) * 16)) = x;
     }
-    MMVAE_DEV void load(const char* src, int64_t ld) {
-        v0 = ld1(src, ld, 0);
-        if constexpr (NC > 1) v1 = ld1(src, ld, 1);
-        if constexpr (NC > 2) v2 = ld1(src, ld, 2);
-        if constexpr (NC > 3) v3 = ld1(src, ld, 3);
+    MMVAE_DEV void load(const char* src, int64_t ld, int tx = (int)threadIdx.x) {
+        v0 = ld1(src, ld, 0, tx);
+        if constexpr (NC > 1) v1 = ld1(src, ld, 1, tx);
+        if constexpr (NC > 2) v2 = ld1(src, ld, 2, tx);
+        if constexpr (NC > 3) v3 = ld1(src, ld, 3, tx);
     }
-    MMVAE_DEV void store(char* dst) const {
-        st1(dst, 0, v0);
-        if constexpr (NC > 1) st1(dst, 1, v1);
-        if constexpr (NC > 2) st1(dst, 2, v2);
-        if constexpr (NC > 3) st1(dst, 3, v3);
+    MMVAE_DEV void store(char* dst, int tx = (int)threadIdx.x) const {
+        st1(dst, 0, v0, tx);
+        if constexpr (NC > 1) st1(dst, 1, v1, tx);
+        if constexpr (NC > 2) st1(dst, 2, v2, tx);
+        if constexpr (NC > 3) st1(dst, 3, v3, tx);
     }
 };
 
@@ -571,13 +573,13 @@ struct RegStage {
 template <int NR, int RB, int NTH, bool X>
 struct DualStage {
     RegStage<NR, RB, NTH> hi, lo;
-    MMVAE_DEV void load(const char* src, int64_t ld, int64_t plane_bytes) {
-        hi.load(src, ld);
-        if constexpr (X) lo.load(src + plane_bytes, ld);
+    MMVAE_DEV void load(const char* src, int64_t ld, int64_t plane_bytes, int tx = (int)threadIdx.x) {
+        hi.load(src, ld, tx);
+        if constexpr (X) lo.load(src + plane_bytes, ld, tx);
     }
-    MMVAE_DEV void store(char* dst, int img_bytes) const {
-        hi.store(dst);
-        if constexpr (X) lo.store(dst + img_bytes);
+    MMVAE_DEV void store(char* dst, int img_bytes, int tx = (int)threadIdx.x) const {
+        hi.store(dst, tx);
+        if constexpr (X) lo.store(dst + img_bytes, tx);
     }
 };
 

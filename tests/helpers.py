@@ -86,3 +86,37 @@ def assert_adam_close(got, want, grads, lr=1e-3, atol=2e-5, ctx="", noisy_keys=(
             i = int(np.argmax(d - lim))
             bad.append((k, float(d[i]), float(g[i])))
     assert not bad, f"{ctx} parameter mismatch after Adam: {bad}"
+
+
+def kappa_grad_atol(D, kappa, record=None):
+    """Absolute tolerance of the vMF ln_kappa gradient, from its f32 cancellation.
+
+    d loss / d kappa holds two terms of size df / kappa that nearly cancel: the likelihood's
+    -df (B / n) / kappa and the lbessel backward's Baricz bound (lb + ub) / (2 kappa) with
+    lb, ub ~ df (operators.hh:33-35, vmf.hh:419-440); the difference is O(kappa / df).  The
+    reference evaluates them in f32, and so do the oracle and the engine, each in its own order:
+    every evaluation carries up to ~4 ulp of df / kappa (sqrt, product, sum, quotient), and the
+    two being compared round independently, hence 8 ulp_f32(df / kappa), times kappa for the
+    ln_kappa chain rule (d / d ln kappa = kappa d / d kappa).  At configs[2] (D = 20k, df = 9999,
+    kappa = 4): 8 * 2^-12 * 4 = 7.8e-3."""
+    df = max(0.5 * D - 1.0, 0.0)
+    if df <= 0:
+        return 1e-6
+    t = df / kappa
+    ulp = 2.0 ** (np.floor(np.log2(t)) - 23)
+    atol = 8.0 * ulp * kappa
+    if record is not None:
+        record.append({"D": D, "kappa": kappa, "atol": atol})
+    return atol
+
+
+def record_kappa_err(tag, D, kappa, got, want, atol):
+    """Appends the measured ln_kappa gradient difference to gpurun_out/kappa_grad_err.jsonl."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = os.path.join(root, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "kappa_grad_err.jsonl"), "a") as f:
+        f.write(json.dumps({"test": tag, "D": int(D), "kappa": float(kappa), "got": float(got), "want": float(want),
+                            "abs_err": abs(float(got) - float(want)), "atol": float(atol),
+                            "rel_err": abs(float(got) - float(want)) / max(abs(float(want)), 1e-30)}) + "\n")
