@@ -107,8 +107,13 @@ int mmvae_upload_csr(mmvae_h h, const int64_t* rowptr, const int32_t* col, const
                      int64_t N, int64_t D, const float* covar);
 /* Host-resident dataset for data beyond HBM (the reference streams each batch from its BGZF
  * file, mtx_data_block_t::read, mmvae_io.hh:208-245): the caller's cell-major CSR (and covariates,
- * or NULL for ones) stays in host memory, registered here as mapped pinned memory; the caller keeps
- * the arrays alive and unchanged until mmvae_destroy or the next upload / synth / stream.  Every
+ * or NULL for ones) stays in host memory; the caller keeps the arrays alive and unchanged until
+ * mmvae_destroy or the next upload / synth / stream (host threads read them there).  The caller's
+ * memory is never page-locked: what the GPU reads over PCIe is an engine-owned mapped pinned copy
+ * — of the row offsets (8 B per row) and covariates (4 C B per row) always, and of col / val
+ * (8 B per nonzero) only in the unpacked case (non-integer values or D > 65536); for 16-bit integer
+ * counts the packed copy (4 B per nonzero) replaces them.  So pinned host memory is 8 B per row +
+ * 4 B (packed) or 8 B (unpacked) per nonzero beyond the caller's arrays.  Every
  * step's rows are gathered over PCIe into a per-step batch CSR in HBM (two slots, alternating with
  * the staging slots) and indexed; the gather runs on its own stream as soon as the step is staged,
  * under the previous step's kernels, and the step waits for it.  When D <= 65536 and every value
@@ -226,13 +231,17 @@ int mmvae_debug_poison(mmvae_h h, int32_t byte);
  * replay it; the step's variable scalars (Philox step / row offset, Adam's bias corrections)
  * travel in the staged copy.  Results are identical to eager launches.  Not used while kernel
  * timing is on.  With an active communicator (world > 1, or a 1-rank one under
- * MMVAE_FORCE_COMM=1) the RCCL bucket all-reduces are captured into the step graph too (unless
- * MMVAE_COMM_GRAPH=0 was set at mmvae_comm_init: eager steps).  Every rank then captures at the
- * same steps: before the first such step the ranks agree (ncclMax) on the largest batch any of
- * them can stage and size the batch-dependent buffers for it once; each capture's outcome is
- * agreed (ncclMin) before any rank launches; if any rank's capture failed, all of them run that
- * handle's communicator steps eagerly from then on.  Dataset and communicator calls are then
- * collective (every rank makes them at the same point of its step sequence).
+ * MMVAE_FORCE_COMM=1) the steps run eagerly with one flat all-reduce of the gradient, unless
+ * MMVAE_COMM_GRAPH=1 was set at mmvae_comm_init: then the two RCCL bucket all-reduces are captured
+ * into the step graph too.  Every rank then captures at the same steps: the graph key is a
+ * function of values all ranks share (csrc/graph_key.hpp; a step needs B * world == n_total),
+ * before the first such step the ranks agree (ncclMax) on the largest batch any of them can stage
+ * (Bpad x the largest dataset row: Bpad * max_nnz * 8 B of entry lists, doubled plus pinned DMA
+ * buffers for a streamed dataset) and size the batch-dependent buffers for it once; each capture's
+ * outcome and key are agreed (ncclMin) before any rank launches; if any rank's capture failed or
+ * its key differed, all of them run that handle's communicator steps eagerly from then on.
+ * Dataset, communicator, graph and timing calls are then collective (every rank makes them at the
+ * same point of its step sequence).
  * graph_stats: captures and replays so far. */
 int mmvae_graph_enable(mmvae_h h, int32_t on);
 int mmvae_graph_stats(mmvae_h h, int64_t* captures, int64_t* replays);

@@ -1649,19 +1649,44 @@ int comm_sync_capacity(Engine* e) {
     const int64_t need = w[0];
     e->no_balance = w[1] != 0;
     if (e->gstream) HIPCHK(e, hipStreamSynchronize(e->gstream));
+    // the worst-case buffers; an allocation that fails leaves the buffer empty (eager steps grow
+    // it per batch again) and, once the ranks agree on it below, every rank runs its communicator
+    // steps eagerly instead of failing
+    bool ok = true;
     if (!e->wide && need + 64 > e->ent_cap) {
         if (e->d_ents) hipFree(e->d_ents);
         e->d_ents = nullptr;
-        e->ent_cap = need + 64;
-        HIPCHK(e, hipMalloc(&e->d_ents, sizeof(uint2) * e->ent_cap));
-        HIPCHK(e, hipMemset(e->d_ents, 0, sizeof(uint2) * e->ent_cap));
+        e->ent_cap = 0;
+        if (hipMalloc(&e->d_ents, sizeof(uint2) * (need + 64)) == hipSuccess &&
+            hipMemset(e->d_ents, 0, sizeof(uint2) * (need + 64)) == hipSuccess) {
+            e->ent_cap = need + 64;
+        } else {
+            if (e->d_ents) hipFree(e->d_ents);
+            e->d_ents = nullptr;
+            ok = false;
+        }
     }
     if (e->streamed) {
-        for (int s = 0; s < 2; ++s) {
-            if (e->bset[s].cap < need) HIPCHK(e, batch_set_alloc(e, s, need));
-            if (e->stream_dma && e->hs_packed && e->bpk_cap[s] < need) HIPCHK(e, stream_bpk_alloc(e, s, need));
+        for (int s = 0; s < 2 && ok; ++s) {
+            if (e->bset[s].cap < need && batch_set_alloc(e, s, need) != hipSuccess) ok = false;
+            if (ok && e->stream_dma && e->hs_packed && e->bpk_cap[s] < need && stream_bpk_alloc(e, s, need) != hipSuccess)
+                ok = false;
         }
         stream_bind(e, e->cur_slot);
+    }
+    if (!ok) (void)hipGetLastError();
+    {
+        int64_t okw = ok ? 1 : 0;
+        HIPCHK(e, hipMemcpyAsync(dw, &okw, sizeof(okw), hipMemcpyHostToDevice, e->stream));
+        if (ncclAllReduce(dw, dw, 1, ncclInt64, ncclMin, e->comm, e->stream) != ncclSuccess)
+            FAIL(e, MMVAE_E_COMM, "comm_sync_capacity: ncclAllReduce failed");
+        HIPCHK(e, hipMemcpyAsync(&okw, dw, sizeof(okw), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (!okw) e->comm_graph_failed = true;  // on every rank: eager communicator steps from here
+        if (getenv_is("MMVAE_VERBOSE", "1"))
+            std::fprintf(stderr, "[mmvae] rank %d: agreed batch capacity %lld entries (%.1f MB of entry lists)%s\n",
+                         e->rank, (long long)need, 8e-6 * (double)need,
+                         okw ? "" : "; an allocation failed on some rank: eager communicator steps");
     }
     ++e->graph_gen;  // on every rank at the same step
     e->cap_synced = true;
