@@ -999,9 +999,12 @@ struct DecNBLds {
             o_cc = 16 * 64 * 4;       // p dq plane per 16-gene block, 1 KB blocks (pq hi / lo aliased)
             o_q1 = o_cc;
             o_du = o_cc + 16 * 64 * 4;  // du sums: [64] genes, [64] genes x z_nu, [16] rows x w_nu
+            // no LDS tile offsets (read from HBM with scalar loads) and two row scalars (d, z_nu):
+            // 3 x 53,056 bytes fit the CU's 160 KB at its 2 KB allocation granule (4 x 9,200 + 17.5 KB
+            // did not: 54,272 bytes ran two workgroups per CU)
             o_toff = o_du + (64 + 64 + 16) * 4;
-            o_rsc = o_toff + ((S * 4 + 15) / 16) * 16;
-            wave_bytes = o_rsc + ((16 * NRS * 4 + 15) / 16) * 16;
+            o_rsc = o_toff;
+            wave_bytes = o_rsc + 16 * 2 * 4;
             bytes = o_wave + NW * wave_bytes;
             return;
         }
@@ -1114,6 +1117,8 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
     CT* cc = reinterpret_cast<CT*>(wp + L.o_cc);
     int32_t* toffl = reinterpret_cast<int32_t*>(wp + L.o_toff);
     float* rsc = reinterpret_cast<float*>(wp + L.o_rsc);
+    // row scalars per row: NRS (d, w, valid, z_nu[R], c[C]); D3 keeps only d and z_nu
+    constexpr int RSS = D3 ? 2 : NRS, RSZ = D3 ? 1 : 3;
     float* duacc = reinterpret_cast<float*>(wp + L.o_du);  // D3: [64] sum du, [64] sum du z_nu, [16] sum du w_nu
     // the p tile's element (r, g): D3 unpadded with the gene XOR-swizzled by row (8-gene groups
     // stay contiguous for the dz GEMM's fragment reads), else a 68-float row stride
@@ -1219,9 +1224,15 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
     constexpr bool SPAIR = !std::is_same<P, float>::value;
     // ---- per-wave row data for the sparse pass ----
     const int wbk = row0 >> 4;  // this wave's 16-row block of the batch entry lists
-    fill_toffl(toffl, S, t0, d.NT, Q.toff, wbk, lane);
+    if constexpr (D3) toffl = const_cast<int32_t*>(Q.toff) + (int64_t)wbk * (d.NT + 1) + t0;  // (HBM, read-only)
+    else fill_toffl(toffl, S, t0, d.NT, Q.toff, wbk, lane);
     const int64_t segw = Q.seg[wbk];
-    if (lane < 16) {
+    if (D3 && lane < 16) {
+        const int b = row0 + lane;
+        const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
+        rsc[lane * 2] = Lr[d.LAT_D];
+        rsc[lane * 2 + 1] = Lr[d.LAT_ZNU];
+    } else if (lane < 16) {
         const int b = row0 + lane;
         const int64_t cell = Q.cells[b];  // padding rows hold the empty row N
         const float* Lr = Q.lat + (int64_t)b * d.lat_stride;
@@ -1307,8 +1318,8 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
                 const int ra = (int)(ea.x >> 6), ga = (int)(ea.x & 63);
                 const int rb = (int)(eb.x >> 6), gb2 = (int)(eb.x & 63);
                 const f2 x = f2{__uint_as_float(ea.y), vb ? __uint_as_float(eb.y) : 0.f};
-                const float* rsa = rsc + ra * NRS;
-                const float* rsb = rsc + rb * NRS;
+                const float* rsa = rsc + ra * RSS;
+                const float* rsb = rsc + rb * RSS;
                 const f2 p = f2{q2[qx(ra, ga)], q2[qx(rb, gb2)]};
                 const f2 mu = fma2(p, f2{rsa[0], rsb[0]}, splat2(1e-4f));  // nb.hh:519
                 const float4 g4a = gsb[ga], g4b = gsb[gb2];
@@ -1318,7 +1329,7 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
                     const f2 wn = q == 0 ? f2{g4a.w, g4b.w}
                                          : ((q < R) ? f2{Q.Wnd[(int64_t)(64 * t + ga) * R + q], Q.Wnd[(int64_t)(64 * t + gb2) * R + q]}
                                                     : splat2(0.f));
-                    u = fma2(wn, f2{rsa[3 + q], rsb[3 + q]}, u);
+                    u = fma2(wn, f2{rsa[RSZ + q], rsb[RSZ + q]}, u);
                 }
                 f2 nup, sgm;
                 nb_nu2(u, nup, sgm);  // nb.hh:458-459
@@ -1368,7 +1379,7 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
                     put(ra, ga, pdq.x, ddu.x);
                     if (vb) put(rb, gb2, pdq.y, ddu.y);
                     if constexpr (D3) {  // the d du terms into the wave's du sums (R = 1)
-                        const f2 dz = ddu * f2{rsa[3], rsb[3]};  // x z_nu of the entry's row
+                        const f2 dz = ddu * f2{rsa[RSZ], rsb[RSZ]};  // x z_nu of the entry's row
                         const f2 dw = ddu * f2{g4a.w, g4b.w};    // x w_nu of the entry's gene
                         atomicAdd(&duacc[ga], ddu.x);
                         atomicAdd(&duacc[64 + ga], dz.x);
@@ -1676,6 +1687,16 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
             const TileCtx c = ctx(t);
             phase_ls(c);
             phase_ez(c);
+            if constexpr (D3) {
+                // the logit GEMM's z fragments are re-read (L2) after the dz GEMM, through an
+                // address the compiler cannot prove loop-invariant: they are live from here to the
+                // next tile's logits only, not through its sparse pass and epilogue
+                const T* Zo = Z;
+                asm volatile("" : "+s"(Zo));
+#pragma unroll
+                for (int s = 0; s < KSL; ++s)
+                    zfr[s] = M::load(&Zo[(int64_t)(row0 + (lane & 15)) * KP + s * ML::KSTEP + (lane >> 4) * ML::EPL], Q.zplane);
+            }
             // double-buffered (NW = 8): the next tile's stage goes into the other buffer before the
             // tile's single barrier; buffer b is rewritten only after the next barrier, which every
             // wave reaches after its combine reads of b
@@ -2644,7 +2665,7 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     // x3 with MMVAE_DEC3=1 (read at create, Engine::dec3): the three-waves-per-SIMD instance
     // (4-wave workgroups, three per CU; the gene split was sized for three at create)
     const size_t lds3 = DecNBLds(KP, (int)sizeof(T), d.tpsD + 1, nqB, 3 + 1 + 1, csz, 4, 1, NPL, (int)sizeof(TL), false, true, true).bytes;
-    const bool use_d3 = X && e->dec3 && small_cr && lds3 <= 160 * 1024 / 3;
+    const bool use_d3 = X && e->dec3 && small_cr && 3 * ((lds3 + 2047) / 2048 * 2048) <= 160 * 1024;  // 2 KB LDS granule
     const int nwB = use_d3 ? 4 : (small_cr && bf && ldsB8 <= 160 * 1024 && !nw4) ? 8 : 4;
     const dim3 gdecB(nrb / (nwB / 4) * d.nsD);
     const dim3 gdecA(nrb / 2 * d.nsA);  // passes A / C: 128 rows per workgroup

@@ -14,7 +14,7 @@ for i in range(3):  # UPDATE=1: the training instance (outputs invalid under sta
     else:
         eng.eval_loss(np.arange(B), 1.0, step_id=i)
 nsd = int(os.environ.get("NSD", "8"))
-NW = 8  # waves per pass-B workgroup (DEC_NW)
+NW = int(os.environ.get("NW", "8"))  # waves per pass-B workgroup (DEC_NW; 4 for MMVAE_DEC3=1)
 nwg = (B // (16 * NW)) * nsd
 buf = np.zeros(nwg * NW * 16, np.float32)
 rc = mmvae_amd.lib().mmvae_debug_copy(eng._h, 1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), buf.size)
