@@ -60,7 +60,8 @@ MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __res
     constexpr int HN = H1 ? 1 : HMAX;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int sp = bid % d.nsB, rb = bid / d.nsB;
+    int sp, rb;
+    xcd_split_major(bid, d.nrb, d.nsB, sp, rb);
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * d.tpsB, t1 = min(d.NT, t0 + d.tpsB);
     const int S = d.tpsB + 1;

@@ -126,6 +126,26 @@ MMVAE_DEV void split_sum4(const float* __restrict__ p, int ns, int64_t sstride, 
     split_sum<4>(p, ns, sstride, off, cstride, on, out);
 }
 
+// (gene split sp, row block rb) of flat workgroup id bid < nrb * ns.  Workgroups b and b + 8
+// share an XCD and its L2 (round-robin dispatch, MI355X_MICROARCH.md "Workgroup dispatch"), so
+// the nrb * ns / 8 items of one XCD are taken consecutively in split-major order: the workgroups
+// reading a gene split's weight tiles sit on one or two XCDs, and each L2 holds about 1/8 of the
+// weights instead of all of them.  (MMVAE_XCD_MAJOR=0 at build: bid % ns, bid / ns.)
+#ifndef MMVAE_XCD_MAJOR
+#define MMVAE_XCD_MAJOR 1
+#endif
+MMVAE_DEV void xcd_split_major(int bid, int nrb, int ns, int& sp, int& rb) {
+    const int n = nrb * ns;
+    if (MMVAE_XCD_MAJOR && (n & 7) == 0) {
+        const int j = (bid & 7) * (n >> 3) + (bid >> 3);
+        sp = j / nrb;
+        rb = j - sp * nrb;
+    } else {
+        sp = bid % ns;
+        rb = bid / ns;
+    }
+}
+
 MMVAE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

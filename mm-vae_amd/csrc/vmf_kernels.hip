@@ -476,7 +476,8 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsp = PASS ? d.nsD : d.nsF, tps = PASS ? d.tpsD : d.tpsF;  // the forward pass: own split
-    const int sp = blockIdx.x % nsp, rb = blockIdx.x / nsp;
+    int sp, rb;
+    xcd_split_major((int)blockIdx.x, (int)gridDim.x / nsp, nsp, sp, rb);
     const int row0 = rb * 64 + 16 * w;
     const int t0 = sp * tps, t1 = min(d.NT, t0 + tps);
     const int S = tps + 1;
