@@ -2,15 +2,17 @@
 // tile), so every tile kernel reads a tile's entries of its 16 rows as one contiguous, lane-
 // balanced list — no per-tile prefix scans over the rows, no per-row pointers in LDS.
 //
-//   ents  uint2 [E + 64]: (pos = row-in-block << 6 | gene-in-tile, bits of x), row-major inside a
-//         tile (rows ascending, genes ascending — the order of the reference's dense row read,
-//         mmvae_io.hh:208-245)
+//   ents  uint32 [E + 64]: pos = row-in-block << 6 | gene-in-tile in bits 0-9, the count in bits
+//         10-31 (integer counts below 2^22); other data keep the value as a float in a parallel
+//         array (Engine::ent_xm, tiles.hpp EntList).  Row-major inside a tile (rows ascending,
+//         genes ascending — the order of the reference's dense row read, mmvae_io.hh:208-245)
 //   seg   int64 [WB + 1]: first entry of wave block wb (host prefix of the rows' nonzero counts)
 //   toff  int32 [WB][NT + 1]: first entry of tile t inside the block's segment
 // Built from the per-dataset tile index (rtp) by one launch, k_batch_lists (one workgroup per
 // wave block).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 #include "engine.hpp"
@@ -25,19 +27,23 @@ namespace mmvae {
 //      drops its row's entries of the chunk's tiles at their final positions, then the workgroup
 //      streams the chunk out with contiguous, full-line stores (no partial lines written from
 //      different waves or CUs).
-static constexpr int COPY_CAP_MAX = 16384;  // entries per LDS chunk (<= 128 KB), less for wide D
+//   XM = false: the chunk is staged as entry words (4 B: a 16-row block of ~26k entries at the
+//   headline is one chunk); XM = true: as (pos, value) pairs, streamed out to both arrays.
+static constexpr int COPY_CAP_MAX = 32768;  // entries per LDS chunk (<= 128 KB), less for wide D
+template <bool XM>
 __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict__ cells,
                                                       const int64_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const float* __restrict__ val,
                                                       const int32_t* __restrict__ rtp, const int64_t* __restrict__ seg,
                                                       int NT, int cap, int32_t* __restrict__ toff,
-                                                      uint2* __restrict__ ents, int dbg,
+                                                      uint32_t* __restrict__ ents, int64_t xoff, int dbg,
                                                       const float2* __restrict__ dotw, const float* __restrict__ Wne,
                                                       int H, int D, float* __restrict__ rowdots,
                                                       const StepScalars* __restrict__ ss, int64_t* ticket_out) {
     extern __shared__ __attribute__((aligned(16))) char csm[];
-    uint2* stage = reinterpret_cast<uint2*>(csm);                      // [cap]
-    int32_t* tw = reinterpret_cast<int32_t*>(csm + 8 * (size_t)cap);    // [NT + 1] tile offsets
+    using SE = typename std::conditional<XM, uint2, uint32_t>::type;  // staged entry
+    SE* stage = reinterpret_cast<SE*>(csm);                            // [cap]
+    int32_t* tw = reinterpret_cast<int32_t*>(csm + sizeof(SE) * (size_t)cap);  // [NT + 1] tile offsets
     int32_t* srt = tw + (NT + 1);                                       // [16][NT + 1] rows' tile pointers
     int32_t* sbase = srt + 16 * (NT + 1);                               // [16][NT] rows' list bases
     __shared__ int32_t wsum[16];
@@ -153,7 +159,11 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u + lane;
-            if (j < jB) stage[pos[u] + j - cb] = uint2{(uint32_t)((w << 6) | (g[u] & 63)), __float_as_uint(x[u])};
+            if (j < jB) {
+                const uint32_t p = (uint32_t)((w << 6) | (g[u] & 63));
+                if constexpr (XM) stage[pos[u] + j - cb] = uint2{p, __float_as_uint(x[u])};
+                else stage[pos[u] + j - cb] = p | ((uint32_t)x[u] << 10);
+            }
         }
         if (dots) {
 #pragma unroll
@@ -179,17 +189,27 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
         lds_barrier();
         const int tC = tB < NT ? chunk_end(tB) : NT;
         if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
-        uint2* dst = ents + base + cb;
+        uint32_t* dst = ents + base + cb;
         if (!dbg_bit(dbg, 8192)) {  // 8192: diagnostic, stream-out skipped (lists invalid)
-            // 16-byte stores (two entries each) from the first 16-byte-aligned entry on
-            const int head = (cnt > 0) ? (int)((base + cb) & 1) : 0, n2 = (cnt - head) >> 1;
-            if (tid == 0 && head) dst[0] = stage[0];
-            uint4* d4 = reinterpret_cast<uint4*>(dst + head);
-            for (int i = tid; i < n2; i += 1024) {
-                const uint2 a = stage[head + 2 * i], b2 = stage[head + 2 * i + 1];
-                d4[i] = uint4{a.x, a.y, b2.x, b2.y};
+            if constexpr (XM) {
+                float* dx = reinterpret_cast<float*>(ents) + xoff + base + cb;
+                for (int i = tid; i < cnt; i += 1024) {
+                    const uint2 a = stage[i];
+                    dst[i] = a.x;
+                    dx[i] = __uint_as_float(a.y);
+                }
+            } else {
+                // 16-byte stores (four entries each) from the first 16-byte-aligned entry on
+                const int head = min(cnt, (int)((4 - ((base + cb) & 3)) & 3)), n4 = (cnt - head) >> 2;
+                if (tid < head) dst[tid] = stage[tid];
+                uint4* d4 = reinterpret_cast<uint4*>(dst + head);
+                for (int i = tid; i < n4; i += 1024) {
+                    const int k = head + 4 * i;
+                    d4[i] = uint4{stage[k], stage[k + 1], stage[k + 2], stage[k + 3]};
+                }
+                const int rest = head + 4 * n4;
+                if (tid < cnt - rest) dst[rest + tid] = stage[rest + tid];
             }
-            if (tid == 0 && cnt > head && ((cnt - head) & 1)) dst[cnt - 1] = stage[cnt - 1];
         }
         lds_barrier();  // stage reusable (the stores carry register copies)
         tA = tB;
@@ -211,9 +231,12 @@ hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const flo
     ScopedTimer tm(e, "k_batch_lists");
     const size_t tab = sizeof(int32_t) * ((size_t)e->NT + 1 + 16 * ((size_t)e->NT + 1) + 16 * (size_t)e->NT);
     if (tab + 8 * 1024 > 160 * 1024) return hipErrorInvalidValue;  // D beyond ~75k genes
-    const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - 256 - tab) / 8) & ~1;  // 256: static LDS
-    hipLaunchKernelGGL(k_batch_lists, dim3((unsigned)WB), dim3(1024), 8 * (size_t)cap + tab, e->stream, e->d_cells,
-                       e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff, e->d_ents,
+    const EntList L = ent_list(e);
+    const size_t esz = L.xoff ? sizeof(uint2) : sizeof(uint32_t);
+    const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - 256 - tab) / esz) & ~3;  // 256: static LDS
+    hipLaunchKernelGGL(L.xoff ? k_batch_lists<true> : k_batch_lists<false>, dim3((unsigned)WB), dim3(1024), esz * (size_t)cap + tab,
+                       e->stream, e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff,
+                       reinterpret_cast<uint32_t*>(e->d_ents), L.xoff,
 #ifdef MMVAE_DIAG
                        [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(),
 #else

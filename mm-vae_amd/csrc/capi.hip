@@ -858,6 +858,30 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     e->hs_packed_dev = packed_dev;
     e->hs_packed_bytes = packed_map;
     e->hs_packed_reg = packed_reg;
+    {
+        // the batch lists carry integer counts below 2^22 in the entry word (tiles.hpp EntList);
+        // the packed copy already proved counts below 2^16
+        bool xm = getenv_is("MMVAE_LISTS_XM", "1");
+        if (!packed && !xm) {
+            const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+            std::vector<char> bad(nth, 0);
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nth; ++t)
+                th.emplace_back([&, t] {
+                    const int64_t a = nnz * t / nth, b = nnz * (t + 1) / nth;
+                    for (int64_t i = a; i < b; ++i) {
+                        const float v = val[i];
+                        if (std::signbit(v) || !(v < 4194304.f && v == std::floor(v))) {
+                            bad[t] = 1;
+                            break;
+                        }
+                    }
+                });
+            for (auto& x : th) x.join();
+            for (char b : bad) xm = xm || b;
+        }
+        e->ent_xm = xm;
+    }
     e->hs_cmax = cmax;
     e->hs_col = hs_col;
     e->hs_val = hs_val;

@@ -7,6 +7,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MMVAE_DEV __device__ __forceinline__
+
+// the per-step batch entry lists as the tile kernels read them (format: tiles.hpp ListEntries)
+struct EntList {
+    const uint32_t* w;
+    int64_t xoff;  // word offset of the float values; 0: counts in the entry word
+};
 #define MMVAE_HOSTDEV __host__ __device__ __forceinline__
 
 // ---------------------------------------------------------------------------------------

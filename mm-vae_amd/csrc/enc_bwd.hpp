@@ -41,7 +41,7 @@ template <class P> struct WEnc { typedef typename Elem<P>::type type; };
 template <> struct WEnc<X3> { typedef float type; };
 
 template <class P, int KP, bool H1, bool RAW>
-MMVAE_DEV void enc_bwd_body(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+MMVAE_DEV void enc_bwd_body(EntList ents, const int64_t* __restrict__ seg,
                             const int32_t* __restrict__ toff, const float* __restrict__ lat,
                             const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
                             const typename WEnc<P>::type* __restrict__ WeP,

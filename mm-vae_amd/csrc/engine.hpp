@@ -177,7 +177,10 @@ struct Engine {
     bool no_balance = false;         // MMVAE_NO_BALANCE at create (max-agreed over the ranks, comm_sync_capacity)
     std::vector<int32_t> cell_nnz;   // host copy of every cell's nonzero count (row balancing, lists)
     // per-step batch entry lists (batch.hip)
-    uint2* d_ents = nullptr;         // [ent_cap]
+    // [ent_cap] uint2 of storage: the 32-bit entry words [0, ent_cap), and with ent_xm the float
+    // values [ent_cap, 2 ent_cap) (tiles.hpp EntList / ListEntries)
+    uint2* d_ents = nullptr;
+    bool ent_xm = false;             // some dataset value is not an integer in [0, 2^22)
     int64_t ent_cap = 0;
     int64_t* d_seg = nullptr;        // [Bpad/16 + 1]
     int64_t* h_seg_pin = nullptr;    // pinned staging of seg
@@ -325,6 +328,10 @@ struct ScopedTimer {
         if (e->timing && a) timer_end(e, a);
     }
 };
+
+inline EntList ent_list(const Engine* e) {
+    return EntList{reinterpret_cast<const uint32_t*>(e->d_ents), e->ent_xm ? e->ent_cap : 0};
+}
 
 // NB launchers (nb_kernels.hip)
 hipError_t nb_prepare_frozen(Engine* e);

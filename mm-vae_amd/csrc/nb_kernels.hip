@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void k_prep(NBPtrs P, Dims d, float* gene, con
 #define MMVAE_ENC_NBW 2
 #endif
 template <class P, int KP, bool SB = false, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void k_enc_fwd(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+__global__ __launch_bounds__(64 * NW) void k_enc_fwd(EntList ents, const int64_t* __restrict__ seg,
                                                  const int32_t* __restrict__ toff,
                                                  const typename Elem<P>::type* __restrict__ WeS, int64_t wplane, Dims d,
                                                  float* __restrict__ hpart, const float* __restrict__ oscale) {
@@ -615,7 +615,7 @@ struct DecPtrs {
     float* slabB;     // [nrb][nqB][DP]
     float* slabC;     // [nrb][1+C][DP]
     float* lossp;     // [grid]
-    const uint2* ents;     // per-step batch entry lists (batch.hip)
+    EntList ents;          // per-step batch entry lists (batch.hip)
     const int64_t* seg;    // [Bpad/16 + 1]
     const int32_t* toff;   // [Bpad/16][NT+1]
     int64_t zplane;        // x3 mode: element offset of the lo plane of zb
@@ -1314,10 +1314,10 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
         // epilogue's own overdispersion arithmetic, so an entry's nu is the dense pass's).  The f32
         // mode keeps one entry per lane (its pass B already spills).
         if constexpr (SPAIR) {
-            if (!dbg_bit(d.dbg, 1)) pend.visit2(Q.ents, lane, [&](uint2 ea, uint2 eb, bool vb) {
-                const int ra = (int)(ea.x >> 6), ga = (int)(ea.x & 63);
-                const int rb = (int)(eb.x >> 6), gb2 = (int)(eb.x & 63);
-                const f2 x = f2{__uint_as_float(ea.y), vb ? __uint_as_float(eb.y) : 0.f};
+            if (!dbg_bit(d.dbg, 1)) pend.visit2(Q.ents, lane, [&](uint32_t ea, float xa, uint32_t eb, float xb, bool vb) {
+                const int ra = ent_row(ea), ga = ent_gene(ea);
+                const int rb = ent_row(eb), gb2 = ent_gene(eb);
+                const f2 x = f2{xa, vb ? xb : 0.f};
                 const float* rsa = rsc + ra * RSS;
                 const float* rsb = rsc + rb * RSS;
                 const f2 p = f2{q2[qx(ra, ga)], q2[qx(rb, gb2)]};
@@ -2167,7 +2167,7 @@ __global__ __launch_bounds__(256) void k_grad_small(Dims d, const float* __restr
 // gradient blocks (appended after the encoder blocks) run beside the encoder tail instead of as
 // a separate kernel on the chain
 template <class P, int KP, bool H1>
-__global__ __launch_bounds__(256) void k_enc_bwd_small(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+__global__ __launch_bounds__(256) void k_enc_bwd_small(EntList ents, const int64_t* __restrict__ seg,
                                                        const int32_t* __restrict__ toff, const float* __restrict__ lat,
                                                        const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
                                                        const typename WEnc<P>::type* __restrict__ WeP, Dims d,
@@ -2560,7 +2560,7 @@ template <class P, int KP>
 static void enc_fwd_run(Engine* e, const Dims& d, float* hpart, hipStream_t st) {
     constexpr int NW = EncNW<P>::value;
     hipLaunchKernelGGL((k_enc_fwd<P, KP, EncSB<P>::value, NW>), dim3(d.nrb * 4 / NW * d.nsE), dim3(64 * NW),
-                       (enc_fwd_lds<P, KP>(d)), st, e->d_ents,
+                       (enc_fwd_lds<P, KP>(d)), st, ent_list(e),
                        e->d_seg, e->d_toff, enc_img<P>(e), (int64_t)e->KP * e->DP, d, hpart,
                        (const float*)e->d_escale);
 }
@@ -2584,7 +2584,7 @@ static DecPtrs dec_ptrs(Engine* e, const Dims& d, const NBPtrs& P, bool bf) {
     Q.col = e->d_col;
     Q.val = e->d_val;
     Q.rtp = e->d_rtp;
-    Q.ents = e->d_ents;
+    Q.ents = ent_list(e);
     Q.seg = e->d_seg;
     Q.toff = e->d_toff;
     Q.WdP = e->cfg.dtype == MMVAE_DTYPE_FP8 ? (const void*)e->d_WdP8 : bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
@@ -2784,12 +2784,12 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         const int nenc = nrb * d.nsB;
         if (d.H == 1)
             hipLaunchKernelGGL((k_enc_bwd_small<PB, KP, true>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PB, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
+                               ent_list(e), e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
         else
             hipLaunchKernelGGL((k_enc_bwd_small<PB, KP, false>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PB, KP>(d)), st,
-                               e->d_ents, e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
+                               ent_list(e), e->d_seg, e->d_toff, e->d_lat, dhT, dpl, WeT, d, e->d_slabE, nenc, e->d_small,
                                e->n_lat_wg, G, e->d_smallg, e->d_lossp, (int)gdecB.x, e->d_lossp + e->klp_off,
                                e->n_lat_wg, e->d_out, sqS);
     }

@@ -147,7 +147,8 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
 // =======================================================================================
 __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                        const float* __restrict__ val, int64_t N, int NT, float epsD,
-                                                       int32_t* __restrict__ rtp, float2* __restrict__ cellnorm) {
+                                                       int32_t* __restrict__ rtp, float2* __restrict__ cellnorm,
+                                                       int32_t* __restrict__ xflag) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     // log1pf of the integer counts 0 .. 511 from a workgroup table (the same log1pf values, so the
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
     const int32_t* cr = col + s;
     const float* vr = val + s;
     float sl2 = 0.f, sy = 0.f;
+    bool nonint = false;  // a value the batch lists cannot carry in the entry word (tiles.hpp EntList)
     // four entries per lane per round, every load issued first (the per-step batch index of the
     // streamed dataset is latency-bound); each lane still sums its entries j = lane, lane + 64, ...
     // in order, so the norms are those of one entry per round
@@ -185,6 +187,7 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
             const int j = j0 + 64 * u;
             if (j < n) {
                 const float xv = x[u];
+                nonint |= !((__float_as_uint(xv) >> 31) == 0u && xv < 4194304.f && xv == floorf(xv));  // (-0 and NaN too)
                 const int xi = (int)fminf(fmaxf(xv, 0.f), 511.f);
                 // (x >= 0: log1pf(max(x, 0)) is l itself; else log1pf(0) = 0)
                 const float l = ((float)xi == xv) ? l1tab[xi] : log1pf(xv);
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
     sl2 = wave_sum(sl2);
     sy = wave_sum(sy);
     if (lane == 0) cellnorm[row] = float2{sl2, sy};
+    if (xflag && __ballot(nonint) != 0ull && lane == 0) *xflag = 1;  // (plain store: every writer stores 1)
 }
 
 // the index of rows [0, N] of a CSR (row N: the empty row) on the handle's stream, no sync
@@ -207,7 +211,7 @@ hipError_t index_rows(Engine* e, const int64_t* rowptr, const int32_t* col, cons
                       float* cellnorm, hipStream_t st) {
     const float epsD = (float)(1e-2 / (double)(float)e->D);
     hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((N + 1 + 3) / 4)), dim3(256), 0, st ? st : e->stream, rowptr, col, val, N,
-                       (int)e->NT, epsD, rtp, (float2*)cellnorm);
+                       (int)e->NT, epsD, rtp, (float2*)cellnorm, nullptr);
     return hipGetLastError();
 }
 
@@ -221,11 +225,24 @@ hipError_t build_dataset_index(Engine* e) {
     if ((er = hipMalloc(&e->d_rtp, sizeof(int32_t) * (size_t)(e->N + 1) * (size_t)(e->NT + 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_cellnorm, sizeof(float2) * (size_t)(e->N + 1))) != hipSuccess) return er;
     const float epsD = (float)(1e-2 / (double)(float)e->D);
-    ScopedTimer tm(e, "k_dataset_index");
-    hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((e->N + 1 + 3) / 4)), dim3(256), 0, e->stream, e->d_rowptr,
-                       e->d_col, e->d_val, e->N, (int)e->NT, epsD, e->d_rtp, (float2*)e->d_cellnorm);
+    int32_t* d_xf = nullptr;  // set when some value is not an integer count in [0, 2^22)
+    if ((er = hipMalloc(&d_xf, sizeof(int32_t))) != hipSuccess) return er;
+    if ((er = hipMemsetAsync(d_xf, 0, sizeof(int32_t), e->stream)) != hipSuccess) return er;
+    {
+        ScopedTimer tm(e, "k_dataset_index");
+        hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((e->N + 1 + 3) / 4)), dim3(256), 0, e->stream, e->d_rowptr,
+                           e->d_col, e->d_val, e->N, (int)e->NT, epsD, e->d_rtp, (float2*)e->d_cellnorm, d_xf);
+    }
     if ((er = hipGetLastError()) != hipSuccess) return er;
-    return hipStreamSynchronize(e->stream);
+    int32_t xf = 0;
+    er = hipMemcpyAsync(&xf, d_xf, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
+    if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
+    hipFree(d_xf);
+    if (er != hipSuccess) return er;
+    const bool xm = xf != 0 || getenv_is("MMVAE_LISTS_XM", "1");  // (test hook: the float-value lists)
+    if (xm != e->ent_xm) ++e->graph_gen;  // the lists' format is baked into captured steps
+    e->ent_xm = xm;
+    return hipSuccess;
 }
 
 }  // namespace mmvae

@@ -165,46 +165,65 @@ MMVAE_DEV float block_sum(float v, float* sbuf) {
     return t;  // valid in thread 0
 }
 
-// One tile's entries of a wave's 16 rows from the per-step batch lists (batch.hip): lane l
-// takes entries l and l + 64 (prefetched a tile ahead), entries past 128 are read on the spot.
-// toffl = the wave block's tile offsets t0 .. t0 + S - 1 (LDS), seg = the block's first entry.
+// The per-step batch entry lists (batch.hip): one 32-bit word per entry, bits 0-9 the position
+// (row-in-block << 6 | gene-in-tile), bits 10-31 the count when every value of the dataset is an
+// integer in [0, 2^22) (Engine::ent_xm false, the counts of scRNA data and of the bench).  Other
+// data (fractional values) keep the value as a float in a parallel array, words xoff.. of the
+// same buffer.  The x word is loaded unconditionally (index 0 when xoff = 0: one broadcast word),
+// so every load of a tile stays statically counted.
+MMVAE_DEV int ent_row(uint32_t e) { return (int)((e >> 6) & 15); }
+MMVAE_DEV int ent_gene(uint32_t e) { return (int)(e & 63); }
+MMVAE_DEV float ent_x(const EntList& L, uint32_t e, float xw) { return L.xoff ? xw : (float)(e >> 10); }
+MMVAE_DEV float ent_xload(const EntList& L, int64_t i) {
+    return reinterpret_cast<const float*>(L.w)[L.xoff ? L.xoff + i : 0];
+}
+// One tile's entries of a wave's 16 rows: lane l takes entries l and l + 64 (prefetched a tile
+// ahead), entries past 128 are read on the spot.  toffl = the wave block's tile offsets
+// t0 .. t0 + S - 1 (LDS), seg = the block's first entry.
 struct ListEntries {
     int n;
     int64_t base;
-    uint2 raw[2];  // the loaded words as they are: nothing reads them before visit (a select on
-                   // them at fetch time would make the compiler wait for the loads right there)
-    MMVAE_DEV void fetch(const uint2* __restrict__ ents, int64_t seg, const int32_t* toffl, int tl, int lane) {
+    uint32_t raw[2];  // the loaded words as they are: nothing reads them before visit (a select on
+    float xw[2];      // them at fetch time would make the compiler wait for the loads right there)
+    MMVAE_DEV void fetch(const EntList& L, int64_t seg, const int32_t* toffl, int tl, int lane) {
         const int a = toffl[tl];
         n = toffl[tl + 1] - a;
         base = seg + a;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // unconditional loads (the list buffer has 64 spare entries)
             const int e = lane + 64 * k;
-            raw[k] = ents[base + (e < n ? e : 0)];
+            const int64_t i = base + (e < n ? e : 0);
+            raw[k] = L.w[i];
+            xw[k] = ent_xload(L, i);
         }
     }
     // packed position (row-in-block << 6 | gene-in-tile) of register entry k, -1 past the list
-    MMVAE_DEV int pos(int k, int lane) const { return (lane + 64 * k < n) ? (int)raw[k].x : -1; }
-    // f(entry A, entry B, B valid) for the tile's entries two at a time: A = lane, B = lane + 64,
-    // then lane + 128 / + 192, ... (the packed-pair sparse passes; an invalid B holds a real entry
-    // of the tile, to be neither stored nor counted)
+    MMVAE_DEV int pos(int k, int lane) const { return (lane + 64 * k < n) ? (int)(raw[k] & 1023u) : -1; }
+    MMVAE_DEV float x(const EntList& L, int k) const { return ent_x(L, raw[k], xw[k]); }
+    // f(pos A, x A, pos B, x B, B valid) for the tile's entries two at a time: A = lane,
+    // B = lane + 64, then lane + 128 / + 192, ... (the packed-pair sparse passes; an invalid B
+    // holds a real entry of the tile, to be neither stored nor counted)
     template <class F>
-    MMVAE_DEV void visit2(const uint2* __restrict__ ents, int lane, F&& f) const {
-        if (lane < n) f(raw[0], raw[1], lane + 64 < n);
+    MMVAE_DEV void visit2(const EntList& L, int lane, F&& f) const {
+        if (lane < n) f(raw[0], x(L, 0), raw[1], x(L, 1), lane + 64 < n);
         for (int e = 128 + lane; e < n; e += 128) {
             const bool vb = e + 64 < n;
-            f(ents[base + e], ents[base + (vb ? e + 64 : e)], vb);
+            const int64_t ia = base + e, ib = base + (vb ? e + 64 : e);
+            const uint32_t ea = L.w[ia], eb = L.w[ib];
+            const float xa = ent_xload(L, ia), xb = ent_xload(L, ib);
+            f(ea, ent_x(L, ea, xa), eb, ent_x(L, eb, xb), vb);
         }
     }
     // f(row-in-block, gene-in-tile, x) for every entry of the tile
     template <class F>
-    MMVAE_DEV void visit(const uint2* __restrict__ ents, int lane, F&& f) const {
+    MMVAE_DEV void visit(const EntList& L, int lane, F&& f) const {
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (lane + 64 * k < n) f((int)(raw[k].x >> 6), (int)(raw[k].x & 63), __uint_as_float(raw[k].y));
+            if (lane + 64 * k < n) f(ent_row(raw[k]), ent_gene(raw[k]), x(L, k));
         for (int e = 128 + lane; e < n; e += 64) {
-            const uint2 r = ents[base + e];
-            f((int)(r.x >> 6), (int)(r.x & 63), __uint_as_float(r.y));
+            const uint32_t r = L.w[base + e];
+            const float xv = ent_xload(L, base + e);
+            f(ent_row(r), ent_gene(r), ent_x(L, r, xv));
         }
     }
 };

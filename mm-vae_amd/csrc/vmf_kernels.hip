@@ -374,7 +374,7 @@ struct VDecPtrs {
     const float* Wcd;
     const float* covar;
     const int64_t* cells;
-    const uint2* ents;     // batch entry lists (k_batch_lists)
+    EntList ents;          // batch entry lists (k_batch_lists)
     const int64_t* seg;
     const int32_t* toff;
     const void* WdP;       // [DP][KP] T
@@ -586,7 +586,7 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
     float lvA[2] = {0.f, 0.f}, lvB[2] = {0.f, 0.f};
     auto lookup = [&](const ListEntries& p, float (&lv)[2]) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) lv[k] = VTabT::value(ltab, fmaxf(__uint_as_float(p.raw[k].y), 0.f));
+        for (int k = 0; k < 2; ++k) lv[k] = VTabT::value(ltab, fmaxf(p.x(Q.ents, k), 0.f));
     };
     if (PRE && t0 < t1) lookup(pendA, lvA);
     // diagnostic (MMVAE_DBG & 256, -DMMVAE_DIAG builds): per-wave phase cycles into dzp
@@ -614,10 +614,11 @@ MMVAE_DEV void vdec_body(VDecPtrs Q, Dims d, float epsD) {
         if constexpr (PRE) {
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                if (lane + 64 * k < pend.n) lt[(int)(pend.raw[k].x >> 6) * LS + (int)(pend.raw[k].x & 63)] = lv[k];
+                if (lane + 64 * k < pend.n) lt[ent_row(pend.raw[k]) * LS + ent_gene(pend.raw[k])] = lv[k];
             for (int e = 128 + lane; e < pend.n; e += 64) {  // past the register pair: read here
-                const uint2 r = Q.ents[pend.base + e];
-                VTabT::put(ltab, lt, (int)(r.x >> 6) * LS + (int)(r.x & 63), 0, fmaxf(__uint_as_float(r.y), 0.f));
+                const uint32_t r = Q.ents.w[pend.base + e];
+                const float xv = ent_x(Q.ents, r, ent_xload(Q.ents, pend.base + e));
+                VTabT::put(ltab, lt, ent_row(r) * LS + ent_gene(r), 0, fmaxf(xv, 0.f));
             }
         } else {
             pend.visit(Q.ents, lane, [&](int r, int gl, float x) { VTabT::put(ltab, lt, r * LS + gl, 0, fmaxf(x, 0.f)); });
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_vgrad_small(Dims d, VScal sc, const flo
 
 // the encoder backward (log1p term only) and the small-gradient / loss blocks in one launch
 template <class P, int KP>
-__global__ __launch_bounds__(256) void k_enc_bwd_vsmall(const uint2* __restrict__ ents, const int64_t* __restrict__ seg,
+__global__ __launch_bounds__(256) void k_enc_bwd_vsmall(EntList ents, const int64_t* __restrict__ seg,
                                                         const int32_t* __restrict__ toff, const float* __restrict__ lat,
                                                         const typename Elem<P>::type* __restrict__ dhT, int64_t dplane,
                                                         const typename WEnc<P>::type* __restrict__ WeP, Dims d,
@@ -1366,7 +1367,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
     Q.Wcd = P.Wcd;
     Q.covar = e->d_covar;
     Q.cells = e->d_cells;
-    Q.ents = e->d_ents;
+    Q.ents = ent_list(e);
     Q.seg = e->d_seg;
     Q.toff = e->d_toff;
     Q.WdP = bf ? (const void*)e->d_WdP_b : (const void*)e->d_WdP_f;
@@ -1441,7 +1442,7 @@ static hipError_t vmf_launch_all(Engine* e, const Dims& d, const VPtrs& P, const
         const T* dhT = reinterpret_cast<const T*>(bf ? (const void*)e->d_dhT_b : (const void*)e->d_dhT_f);
         const auto* WeT = reinterpret_cast<const typename WEnc<PM>::type*>(
             std::is_same<typename WEnc<PM>::type, __bf16>::value ? (const void*)e->d_WeP_b : (const void*)e->d_WeP_f);
-        hipLaunchKernelGGL((k_enc_bwd_vsmall<PM, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP, false>(d)), st, e->d_ents,
+        hipLaunchKernelGGL((k_enc_bwd_vsmall<PM, KP>), dim3(nenc + gS), dim3(256), (enc_bwd_lds<PM, KP, false>(d)), st, ent_list(e),
                            e->d_seg, e->d_toff, e->d_lat, dhT, (int64_t)KP * d.Bpad, WeT, d, e->d_slabE, nenc, sc,
                            e->d_small, e->n_lat_wg, G, e->d_smallg, e->d_rowv, e->d_lossp, e->n_lat_wg, e->d_vk,
                            e->d_out, sqS);
