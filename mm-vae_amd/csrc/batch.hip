@@ -29,11 +29,15 @@ namespace mmvae {
 //      different waves or CUs).
 //   XM = false: the chunk is staged as entry words (4 B: a 16-row block of ~26k entries at the
 //   headline is one chunk); XM = true: as (pos, value) pairs, streamed out to both arrays.
+//   PK = true: the rows are read from the dataset's packed copy (gene << 16 | count, one word per
+//   entry, Engine::d_pk), so a row's first 2048 entries are in flight before the index phase in
+//   the registers the unpacked (col, val) pairs of 1024 take.
 static constexpr int COPY_CAP_MAX = 32768;  // entries per LDS chunk (<= 128 KB), less for wide D
-template <bool XM>
+template <bool XM, bool PK>
 __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict__ cells,
                                                       const int64_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const float* __restrict__ val,
+                                                      const uint32_t* __restrict__ pk,
                                                       const int32_t* __restrict__ rtp, const int64_t* __restrict__ seg,
                                                       int NT, int cap, int32_t* __restrict__ toff,
                                                       uint32_t* __restrict__ ents, int64_t xoff, int dbg,
@@ -59,17 +63,35 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     // the row's first 1024 entries are requested before the index phase (chunk 0 starts at
     // entry 0 of every row) so their latency hides behind it
     constexpr int U = 16;
-    int g[U];
-    float x[U];
-    auto load = [&](int jA, int jB) {
+    struct GrpU {  // 64 U entries of the row: gene ids and values
+        int g_[U];
+        float x_[U];
+        MMVAE_DEV int g(int u) const { return g_[u]; }
+        MMVAE_DEV float x(int u) const { return x_[u]; }
+    };
+    struct GrpP {  // 64 U packed entries
+        uint32_t w_[U];
+        MMVAE_DEV int g(int u) const { return (int)(w_[u] >> 16); }
+        MMVAE_DEV float x(int u) const { return (float)(w_[u] & 0xffffu); }
+    };
+    using Grp = typename std::conditional<PK, GrpP, GrpU>::type;
+    Grp gA, gB;  // gB: PK only (the group after gA, in flight with it)
+    auto load = [&](Grp& G, int jA, int jB) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads
             const int j = min(jA + 64 * u + lane, max(jB - 1, 0));
-            g[u] = col[s + j];
-            x[u] = val[s + j];
+            if constexpr (PK) {
+                G.w_[u] = pk[s + j];
+            } else {
+                G.g_[u] = col[s + j];
+                G.x_[u] = val[s + j];
+            }
         }
     };
-    if (!dbg_bit(dbg, 512)) load(0, rn);
+    if (!dbg_bit(dbg, 512)) {
+        load(gA, 0, rn);
+        if constexpr (PK) load(gB, 64 * U, rn);
+    }
     // the row's tile pointers: all loads of a group of 8 issued before the first LDS store
     {
         const int32_t* src = rtp + c * (int64_t)(NT + 1);
@@ -144,36 +166,36 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     float dpre = 0.f, dhn[HMAX];
 #pragma unroll
     for (int h = 0; h < HMAX; ++h) dhn[h] = 0.f;
-    auto drop = [&](int j0, int jB, int cb) {  // masked LDS stores at the final positions
+    auto drop = [&](const Grp& G, int j0, int jB, int cb) {  // masked LDS stores at the final positions
         float2 wv[U];
         if (dots) {  // every weight gather of the group in flight at once (clamped gene ids)
 #pragma unroll
-            for (int u = 0; u < U; ++u) wv[u] = dotw[(unsigned)g[u] < (unsigned)D ? g[u] : 0];
+            for (int u = 0; u < U; ++u) wv[u] = dotw[(unsigned)G.g(u) < (unsigned)D ? G.g(u) : 0];
         }
         // every tile-base lookup first (the clamped loads give real gene ids, so each index is in
         // range), then the masked stores: a lookup inside each store's branch waited for its own
         // LDS round trip, sixteen in a row
         int pos[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) pos[u] = sb[min(g[u] >> 6, NT - 1)];
+        for (int u = 0; u < U; ++u) pos[u] = sb[min(G.g(u) >> 6, NT - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = j0 + 64 * u + lane;
             if (j < jB) {
-                const uint32_t p = (uint32_t)((w << 6) | (g[u] & 63));
-                if constexpr (XM) stage[pos[u] + j - cb] = uint2{p, __float_as_uint(x[u])};
-                else stage[pos[u] + j - cb] = p | ((uint32_t)x[u] << 10);
+                const uint32_t p = (uint32_t)((w << 6) | (G.g(u) & 63));
+                if constexpr (XM) stage[pos[u] + j - cb] = uint2{p, __float_as_uint(G.x(u))};
+                else stage[pos[u] + j - cb] = p | ((uint32_t)G.x(u) << 10);
             }
         }
         if (dots) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const bool in = j0 + 64 * u + lane < jB;
-                const float xv = in ? x[u] : 0.f;
+                const float xv = in ? G.x(u) : 0.f;
                 dpre = fmaf(xv, wv[u].x, dpre);
                 dhn[0] = fmaf(xv, wv[u].y, dhn[0]);
                 for (int h = 1; h < H; ++h)
-                    if (in) dhn[h < HMAX ? h : 0] = fmaf(xv, Wne[(int64_t)h * D + g[u]], dhn[h < HMAX ? h : 0]);
+                    if (in) dhn[h < HMAX ? h : 0] = fmaf(xv, Wne[(int64_t)h * D + G.g(u)], dhn[h < HMAX ? h : 0]);
             }
         }
     };
@@ -181,14 +203,27 @@ __global__ __launch_bounds__(1024) void k_batch_lists(const int64_t* __restrict_
     while (tA < NT) {
         const int cb = tw[tA], cnt = tw[tB] - cb;
         const int jA = rt[tA], jB = rt[tB];
-        drop(jA, jB, cb);
-        for (int j0 = jA + 64 * U; j0 < jB; j0 += 64 * U) {  // rows with more than 1024 entries in the chunk
-            load(j0, jB);
-            drop(j0, jB, cb);
+        if constexpr (PK) {
+            // gA, gB hold the chunk's first two groups; each is refilled two groups ahead
+            for (int j0 = jA; j0 < jB; j0 += 2 * 64 * U) {
+                drop(gA, j0, jB, cb);
+                if (j0 + 2 * 64 * U < jB) load(gA, j0 + 2 * 64 * U, jB);
+                if (j0 + 64 * U < jB) drop(gB, j0 + 64 * U, jB, cb);
+                if (j0 + 3 * 64 * U < jB) load(gB, j0 + 3 * 64 * U, jB);
+            }
+        } else {
+            drop(gA, jA, jB, cb);
+            for (int j0 = jA + 64 * U; j0 < jB; j0 += 64 * U) {  // rows with more than 1024 entries in the chunk
+                load(gA, j0, jB);
+                drop(gA, j0, jB, cb);
+            }
         }
         lds_barrier();
         const int tC = tB < NT ? chunk_end(tB) : NT;
-        if (tB < NT) load(rt[tB], rt[tC]);  // next chunk in flight during the stream-out
+        if (tB < NT) {  // next chunk in flight during the stream-out
+            load(gA, rt[tB], rt[tC]);
+            if constexpr (PK) load(gB, rt[tB] + 64 * U, rt[tC]);
+        }
         uint32_t* dst = ents + base + cb;
         if (!dbg_bit(dbg, 8192)) {  // 8192: diagnostic, stream-out skipped (lists invalid)
             if constexpr (XM) {
@@ -234,8 +269,10 @@ hipError_t build_batch_lists(Engine* e, int64_t B, const float2* dotw, const flo
     const EntList L = ent_list(e);
     const size_t esz = L.xoff ? sizeof(uint2) : sizeof(uint32_t);
     const int cap = (int)std::min<size_t>(COPY_CAP_MAX, (160 * 1024 - 256 - tab) / esz) & ~3;  // 256: static LDS
-    hipLaunchKernelGGL(L.xoff ? k_batch_lists<true> : k_batch_lists<false>, dim3((unsigned)WB), dim3(1024), esz * (size_t)cap + tab,
-                       e->stream, e->d_cells, e->d_rowptr, e->d_col, e->d_val, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff,
+    const bool pk = !L.xoff && e->pk_on && e->d_pk;  // the packed dataset (counts below 2^16)
+    auto kern = L.xoff ? k_batch_lists<true, false> : pk ? k_batch_lists<false, true> : k_batch_lists<false, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)WB), dim3(1024), esz * (size_t)cap + tab, e->stream, e->d_cells, e->d_rowptr, e->d_col,
+                       e->d_val, e->d_pk, e->d_rtp, e->d_seg, (int)e->NT, cap, e->d_toff,
                        reinterpret_cast<uint32_t*>(e->d_ents), L.xoff,
 #ifdef MMVAE_DIAG
                        [] { const char* v = std::getenv("MMVAE_DBG"); return v ? std::atoi(v) : 0; }(),

@@ -505,7 +505,7 @@ int mmvae_destroy(mmvae_h e) {
     wide_destroy(e);
     void* bufs[] = {e->d_rowptr, e->d_col, e->d_val, e->d_covar, e->d_params, e->d_grads, e->d_m, e->d_v,
                     e->d_frozen, e->d_WeP_f, e->d_WeP_b, e->d_WdP_f, e->d_WdP_b, e->d_WdT_f, e->d_WdT_b, e->d_WeS_f, e->d_WeS_b,
-                    e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
+                    e->d_cells, e->d_eps, e->d_gene, e->d_mvec, e->d_rtp, e->d_cellnorm, e->d_pk, e->d_rowx, e->d_rowxp, e->d_hpart, e->d_lat,
                     e->d_zf, e->d_zb, e->d_lsep, e->d_rowB, e->d_rowfin, e->d_dzp, e->d_dh, e->d_dhT_f, e->d_dhT_b,
                     e->d_slabB, e->d_slabC, e->d_slabE, e->d_lossp, e->d_small, e->d_smallg, e->d_sumsq,
                     e->d_tmp, e->d_rowv, e->d_vk, e->d_tmp_ar, e->d_chain, e->d_WdP8, e->d_WeS8, e->d_escale, e->d_flag};
@@ -842,8 +842,9 @@ int mmvae_stream_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     }
     // the new dataset is in place: the resident one (if any) goes
     for (void* b : {(void*)e->d_rowptr, (void*)e->d_col, (void*)e->d_val, (void*)e->d_covar, (void*)e->d_rtp,
-                    (void*)e->d_cellnorm})
+                    (void*)e->d_cellnorm, (void*)e->d_pk})
         if (b) hipFree(b);
+    e->d_pk = nullptr;
     e->d_rowptr = nullptr;
     e->d_col = nullptr;
     e->d_val = nullptr;

@@ -190,6 +190,10 @@ struct Engine {
     float* d_gene = nullptr;         // per-gene prep (k_prep / k_vprep): [10][DP] floats
     float* d_mvec = nullptr;         // [DP/256][KP] partials of mvec (k_prep / k_vprep)
     int32_t* d_rtp = nullptr;        // [N+1][NT+1] per-cell tile pointers (dataset index; row N = empty)
+    // resident data with D <= 65536: the packed copy gene << 16 | count [nnz] written by the dataset
+    // index kernel; pk_on when every value is an integer count below 2^16 (k_batch_lists reads it)
+    uint32_t* d_pk = nullptr;
+    bool pk_on = false;
     float* d_cellnorm = nullptr;     // [N+1] float2: vMF row norms of log1p(x) (dataset index)
     float* d_rowx = nullptr;         // [Bpad][2+H]  pre_depth, lnorm2, hnu[H]
     float* d_rowxp = nullptr;        // [nsE][Bpad][1+H]  gene-split partials of depth(x), nu_enc(x)

@@ -148,7 +148,7 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
 __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                        const float* __restrict__ val, int64_t N, int NT, float epsD,
                                                        int32_t* __restrict__ rtp, float2* __restrict__ cellnorm,
-                                                       int32_t* __restrict__ xflag) {
+                                                       int32_t* __restrict__ xflag, uint32_t* __restrict__ pk) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     // log1pf of the integer counts 0 .. 511 from a workgroup table (the same log1pf values, so the
@@ -168,6 +168,7 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
     const float* vr = val + s;
     float sl2 = 0.f, sy = 0.f;
     bool nonint = false;  // a value the batch lists cannot carry in the entry word (tiles.hpp EntList)
+    bool nonpk = false;   // a value the packed copy cannot carry (an integer count below 2^16)
     // four entries per lane per round, every load issued first (the per-step batch index of the
     // streamed dataset is latency-bound); each lane still sums its entries j = lane, lane + 64, ...
     // in order, so the norms are those of one entry per round
@@ -188,6 +189,8 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
             if (j < n) {
                 const float xv = x[u];
                 nonint |= !((__float_as_uint(xv) >> 31) == 0u && xv < 4194304.f && xv == floorf(xv));  // (-0 and NaN too)
+                nonpk |= !((__float_as_uint(xv) >> 31) == 0u && xv < 65536.f && xv == floorf(xv));
+                if (pk) pk[s + j] = ((uint32_t)g[u] << 16) | (uint32_t)fminf(fmaxf(xv, 0.f), 65535.f);
                 const int xi = (int)fminf(fmaxf(xv, 0.f), 511.f);
                 // (x >= 0: log1pf(max(x, 0)) is l itself; else log1pf(0) = 0)
                 const float l = ((float)xi == xv) ? l1tab[xi] : log1pf(xv);
@@ -203,7 +206,9 @@ __global__ __launch_bounds__(256) void k_dataset_index(const int64_t* __restrict
     sl2 = wave_sum(sl2);
     sy = wave_sum(sy);
     if (lane == 0) cellnorm[row] = float2{sl2, sy};
-    if (xflag && __ballot(nonint) != 0ull && lane == 0) *xflag = 1;  // (plain store: every writer stores 1)
+    // (plain stores: every writer of a word stores the same value)
+    if (xflag && __ballot(nonint) != 0ull && lane == 0) xflag[0] = 1;
+    if (xflag && __ballot(nonpk) != 0ull && lane == 0) xflag[1] = 1;
 }
 
 // the index of rows [0, N] of a CSR (row N: the empty row) on the handle's stream, no sync
@@ -211,7 +216,7 @@ hipError_t index_rows(Engine* e, const int64_t* rowptr, const int32_t* col, cons
                       float* cellnorm, hipStream_t st) {
     const float epsD = (float)(1e-2 / (double)(float)e->D);
     hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((N + 1 + 3) / 4)), dim3(256), 0, st ? st : e->stream, rowptr, col, val, N,
-                       (int)e->NT, epsD, rtp, (float2*)cellnorm, nullptr);
+                       (int)e->NT, epsD, rtp, (float2*)cellnorm, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -219,26 +224,38 @@ hipError_t build_dataset_index(Engine* e) {
     if (e->wide) return hipSuccess;  // the wide path densifies straight from the CSR rows
     hipFree(e->d_rtp);
     hipFree(e->d_cellnorm);
+    hipFree(e->d_pk);
+    e->d_pk = nullptr;
+    e->pk_on = false;
     e->d_rtp = nullptr;
     e->d_cellnorm = nullptr;
     hipError_t er;
     if ((er = hipMalloc(&e->d_rtp, sizeof(int32_t) * (size_t)(e->N + 1) * (size_t)(e->NT + 1))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_cellnorm, sizeof(float2) * (size_t)(e->N + 1))) != hipSuccess) return er;
     const float epsD = (float)(1e-2 / (double)(float)e->D);
-    int32_t* d_xf = nullptr;  // set when some value is not an integer count in [0, 2^22)
-    if ((er = hipMalloc(&d_xf, sizeof(int32_t))) != hipSuccess) return er;
-    if ((er = hipMemsetAsync(d_xf, 0, sizeof(int32_t), e->stream)) != hipSuccess) return er;
+    // the packed copy for the list builder (MMVAE_LISTS_PK=0: none)
+    if (e->D <= 65536 && e->nnz > 0 && !getenv_is("MMVAE_LISTS_PK", "0"))
+        if ((er = hipMalloc(&e->d_pk, sizeof(uint32_t) * (size_t)e->nnz)) != hipSuccess) return er;
+    int32_t* d_xf = nullptr;  // [0]: some value is not an integer count in [0, 2^22); [1]: in [0, 2^16)
+    if ((er = hipMalloc(&d_xf, 2 * sizeof(int32_t))) != hipSuccess) return er;
+    if ((er = hipMemsetAsync(d_xf, 0, 2 * sizeof(int32_t), e->stream)) != hipSuccess) return er;
     {
         ScopedTimer tm(e, "k_dataset_index");
         hipLaunchKernelGGL(k_dataset_index, dim3((unsigned)((e->N + 1 + 3) / 4)), dim3(256), 0, e->stream, e->d_rowptr,
-                           e->d_col, e->d_val, e->N, (int)e->NT, epsD, e->d_rtp, (float2*)e->d_cellnorm, d_xf);
+                           e->d_col, e->d_val, e->N, (int)e->NT, epsD, e->d_rtp, (float2*)e->d_cellnorm, d_xf, e->d_pk);
     }
     if ((er = hipGetLastError()) != hipSuccess) return er;
-    int32_t xf = 0;
-    er = hipMemcpyAsync(&xf, d_xf, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
+    int32_t xf = 0, xp[2] = {0, 0};
+    er = hipMemcpyAsync(xp, d_xf, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream);
     if (er == hipSuccess) er = hipStreamSynchronize(e->stream);
     hipFree(d_xf);
     if (er != hipSuccess) return er;
+    xf = xp[0];
+    e->pk_on = e->d_pk && !xp[1];
+    if (e->d_pk && xp[1]) {  // not counts: no packed copy
+        hipFree(e->d_pk);
+        e->d_pk = nullptr;
+    }
     const bool xm = xf != 0 || getenv_is("MMVAE_LISTS_XM", "1");  // (test hook: the float-value lists)
     if (xm != e->ent_xm) ++e->graph_gen;  // the lists' format is baked into captured steps
     e->ent_xm = xm;
