@@ -856,12 +856,12 @@ MMVAE_DEV void dec_ac_body(DecPtrs Q, Dims d) {
         if (t + 1 < t1) st(hold, ghold, buf ^ 1);
         lds_barrier();
         lap(1);
-        if (PASS == 2) {  // 64-row slab block h = waves 2h, 2h + 1
+        if (PASS == 2) {  // one slab row per 128-row workgroup: (waves 0 + 1) + (waves 2 + 3)
             const float* pb = part + (buf * 4 * nq) * 64;
-            for (int i = threadIdx.x; i < 2 * nq * 64; i += 256) {
-                const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
-                Q.slabC[((int64_t)(2 * rbw + h) * nq + q) * d.DP + 64 * t + g] =
-                    pb[((2 * h) * nq + q) * 64 + g] + pb[((2 * h + 1) * nq + q) * 64 + g];
+            for (int i = threadIdx.x; i < nq * 64; i += 256) {
+                const int q = i >> 6, g = i & 63;
+                Q.slabC[((int64_t)rbw * nq + q) * d.DP + 64 * t + g] =
+                    (pb[(0 * nq + q) * 64 + g] + pb[(1 * nq + q) * 64 + g]) + (pb[(2 * nq + q) * 64 + g] + pb[(3 * nq + q) * 64 + g]);
             }
         }
     };
@@ -1627,18 +1627,22 @@ __global__ __launch_bounds__(64 * NW, D3 ? 3 : ((LOSS && NW == 8) ? 2 : 8 / NW))
     //      [th0, th0 + nth) ----
     auto combine = [&](const TileCtx& c, int th0, int nth) {
         if (LOSS || dbg_bit(d.dbg, 16384)) return;  // 16384: diagnostic, slab stores skipped
-        for (int i = (D3 ? tido : (int)threadIdx.x) - th0; i < (NW / 4) * nq * 64; i += nth) {  // per 64-row slab block h
-            const int h = i / (nq * 64), q = (i >> 6) % nq, g = i & 63;
+        // one slab row per workgroup (64 or 128 rows): the waves' partials in fixed order
+        for (int i = (D3 ? tido : (int)threadIdx.x) - th0; i < nq * 64; i += nth) {
+            const int q = i >> 6, g = i & 63;
             float v;
             if constexpr (D3) {  // each wave's partials in its p tile
                 auto pw_ = [&](int wv) { return reinterpret_cast<const float*>(smem + L.o_wave + wv * L.wave_bytes + L.o_q2); };
                 v = pw_(0)[q * 64 + g] + pw_(1)[q * 64 + g] + pw_(2)[q * 64 + g] + pw_(3)[q * 64 + g];
             } else {
-                const float* ph = c.pb + 4 * h * nq * 64;
-                v = ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
-                    ph[(3 * nq + q) * 64 + g];
+                auto half = [&](int h) {
+                    const float* ph = c.pb + 4 * h * nq * 64;
+                    return ph[(0 * nq + q) * 64 + g] + ph[(1 * nq + q) * 64 + g] + ph[(2 * nq + q) * 64 + g] +
+                           ph[(3 * nq + q) * 64 + g];
+                };
+                v = NW == 8 ? half(0) + half(1) : half(0);
             }
-            Q.slabB[((int64_t)(rbw * (NW / 4) + h) * nq + q) * d.DP + 64 * c.t + g] = v;
+            Q.slabB[((int64_t)rbw * nq + q) * d.DP + 64 * c.t + g] = v;
         }
     };
     if constexpr (SG) {
@@ -2198,7 +2202,7 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
                                                     const float* __restrict__ slabB,
                                                     const float* __restrict__ slabC,
                                                     const float* __restrict__ slabE,
-                                                    const float* __restrict__ smallg, int nrb,
+                                                    const float* __restrict__ smallg, int nrb, int nrbB, int nrbC,
                                                     double* __restrict__ sqpart) {
     constexpr int NQMAX = SMALL ? 9 : (1 + CMAX) + 1 + RMAX + (1 + CMAX) + 2 + HMAX;
     constexpr int NQR = NQMAX + 1;         // + the column dot sum_k cdh[k] W_enc[k][g]
@@ -2232,14 +2236,17 @@ __global__ __launch_bounds__(256) void k_grad_genes(NBPtrs P, Dims d, NBGrads G,
             }
     }
 #pragma unroll 2  // (4 at the headline shape: 15.4 -> 19.4 us)
+    // slab rows: pass B one per workgroup (nrbB: 128 or 64 rows), pass C one per 128 rows (nrbC),
+    // the encoder backward one per 64 rows (nrb)
     for (int rb = part; rb < nrb; rb += NPART) {
+        const bool inB = rb < nrbB, inC = rb < nrbC;
         const float* sB = slabB + (int64_t)rb * nqB * d.DP + g0 + gq;
         const float* sC = slabC + (int64_t)rb * nqC * d.DP + g0 + gq;
         const float* sE = slabE + (int64_t)rb * nqE * d.DP + g0 + gq;
 #pragma unroll
         for (int q = 0; q < NQMAX; ++q) {
-            if (q < nqB) { if (PART != 2) acc[q] += ld(sB + (int64_t)q * d.DP); }
-            else if (q < nqB + nqC) { if (PART != 2) acc[q] += ld(sC + (int64_t)(q - nqB) * d.DP); }
+            if (q < nqB) { if (PART != 2 && inB) acc[q] += ld(sB + (int64_t)q * d.DP); }
+            else if (q < nqB + nqC) { if (PART != 2 && inC) acc[q] += ld(sC + (int64_t)(q - nqB) * d.DP); }
             else if (q < nq) { if (PART != 1) acc[q] += ld(sE + (int64_t)(q - nqB - nqC) * d.DP); }
         }
     }
@@ -2744,14 +2751,15 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
     }
     const bool split = split_grads(e);
     const bool small_genes = d.C == 1 && d.R == 1 && d.H == 1;
+    const int nrbB = nrb / (nwB / 4), nrbC = nrb / 2;  // slab rows of passes B and C
     if (split) {  // decoder-side gene gradients final: all-reduce them under the encoder backward
         ScopedTimer tm(e, "k_grad_genes_dec");
         if (small_genes)
             hipLaunchKernelGGL((k_grad_genes<true, 1>), dim3((d.D + GG_GENES - 1) / GG_GENES), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, nullptr);
         else
             hipLaunchKernelGGL((k_grad_genes<false, 1>), dim3((d.D + GG_GENES - 1) / GG_GENES), dim3(256), 0, st, P, d, G, gene,
-                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nullptr);
+                               e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, nullptr);
         hipError_t er = comm_bucket(e, 0);
         if (er != hipSuccess) return er;
     }
@@ -2798,17 +2806,17 @@ static hipError_t nb_launch_all(Engine* e, const Dims& d, const NBPtrs& P, bool 
         if (small_genes) {
             if (split)
                 hipLaunchKernelGGL((k_grad_genes<true, 2>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, sqG);
             else
                 hipLaunchKernelGGL((k_grad_genes<true, 0>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, sqG);
         } else {
             if (split)
                 hipLaunchKernelGGL((k_grad_genes<false, 2>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, sqG);
             else
                 hipLaunchKernelGGL((k_grad_genes<false, 0>), dim3(gG), dim3(256), 0, st, P, d, G, gene,
-                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, sqG);
+                                   e->d_slabB, e->d_slabC, e->d_slabE, e->d_smallg, nrb, nrbB, nrbC, sqG);
         }
     }
     if (split) {
