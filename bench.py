@@ -599,12 +599,11 @@ def main():
             # the DP=8 configs' per-GPU shapes (one rank's step; the all-reduce is absent at N = 1)
             lines.append(secondary(mmvae_amd, "nb", 30000, 64, 4096, "bf16x3", 1000000, args.lib_size,
                                    label="BASELINE configs[3] per GPU: NB 1M x 30k, 4096 of the 32k global batch, bf16x3"))
-            # configs[4] per GPU.  Its fp8 mode (e4m3 forward GEMMs, `--dtype fp8`) is not a line here:
-            # the step is bound by the decoder's VALU work, and fp8 measured below the bf16 line at
-            # this shape (7.43M vs 7.59M cells/s, round 5), so it earns no place in the default run
-            # (DESIGN §7); `python bench.py --dtype fp8 --genes 30000 --batch 8192` measures it
-            lines.append(secondary(mmvae_amd, "nb", 30000, 64, 8192, "bf16", 1000000, args.lib_size,
-                                   label="BASELINE configs[4] per GPU: NB 1M x 30k, 8192 of the 65k global batch, bf16"))
+            # configs[4] per GPU, bf16, and its named precision (e4m3 forward GEMMs) beside it.  The
+            # step is bound by the decoder's VALU work, so fp8 is not faster than bf16 here
+            for dt_ in ("bf16", "fp8"):
+                lines.append(secondary(mmvae_amd, "nb", 30000, 64, 8192, dt_, 1000000, args.lib_size,
+                                       label=f"BASELINE configs[4] per GPU: NB 1M x 30k, 8192 of the 65k global batch, {dt_}"))
             # the wide path (shapes beyond the fused kernels: here --mean_latent 128): its GEMMs on
             # the bf16 MFMA in the x3 (fp32-accurate) mode, and the exact f32 MFMA line beside it
             for dt_ in ("bf16x3", "f32"):
