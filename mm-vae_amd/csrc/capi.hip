@@ -631,8 +631,9 @@ int mmvae_upload_csr(mmvae_h e, const int64_t* rowptr, const int32_t* col, const
     // N + 2 row pointers: rowptr[N + 1] = nnz makes the empty padding row N (every row past the
     // batch points there) a valid zero-length row for readers that take rowptr[c + 1]
     HIPCHK(e, dalloc(&e->d_rowptr, N + 2));
-    HIPCHK(e, dalloc(&e->d_col, nnz));
-    HIPCHK(e, dalloc(&e->d_val, nnz));
+    // +64: the clamped (unconditional) row loads of the empty padding row N read entry nnz
+    HIPCHK(e, dalloc(&e->d_col, nnz + 64));
+    HIPCHK(e, dalloc(&e->d_val, nnz + 64));
     HIPCHK(e, dalloc(&e->d_covar, (N + 1) * e->C));  // row N: zeros (padding rows)
     HIPCHK(e, hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C));
     HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (N + 1), hipMemcpyHostToDevice));

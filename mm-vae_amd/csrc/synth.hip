@@ -114,8 +114,8 @@ hipError_t synth_dataset(Engine* e, int64_t N, double lib, uint64_t seed, int64_
     e->d_val = nullptr;
     e->d_covar = nullptr;
     if ((er = hipMalloc(&e->d_rowptr, sizeof(int64_t) * (N + 2))) != hipSuccess) return er;
-    if ((er = hipMalloc(&e->d_col, sizeof(int32_t) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
-    if ((er = hipMalloc(&e->d_val, sizeof(float) * (nnz > 0 ? nnz : 1))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_col, sizeof(int32_t) * (nnz + 64))) != hipSuccess) return er;
+    if ((er = hipMalloc(&e->d_val, sizeof(float) * (nnz + 64))) != hipSuccess) return er;
     if ((er = hipMalloc(&e->d_covar, sizeof(float) * (N + 1) * e->C)) != hipSuccess) return er;  // row N: zeros
     if ((er = hipMemset(e->d_covar + N * e->C, 0, sizeof(float) * e->C)) != hipSuccess) return er;
     hipMemcpy(e->d_rowptr, rp.data(), sizeof(int64_t) * (N + 2), hipMemcpyHostToDevice);
@@ -235,7 +235,7 @@ hipError_t build_dataset_index(Engine* e) {
     const float epsD = (float)(1e-2 / (double)(float)e->D);
     // the packed copy for the list builder (MMVAE_LISTS_PK=0: none)
     if (e->D <= 65536 && e->nnz > 0 && !getenv_is("MMVAE_LISTS_PK", "0"))
-        if ((er = hipMalloc(&e->d_pk, sizeof(uint32_t) * (size_t)e->nnz)) != hipSuccess) return er;
+        if ((er = hipMalloc(&e->d_pk, sizeof(uint32_t) * ((size_t)e->nnz + 64))) != hipSuccess) return er;  // (+64: the clamped loads of an empty row read word nnz)
     int32_t* d_xf = nullptr;  // [0]: some value is not an integer count in [0, 2^22); [1]: in [0, 2^16)
     if ((er = hipMalloc(&d_xf, 2 * sizeof(int32_t))) != hipSuccess) return er;
     if ((er = hipMemsetAsync(d_xf, 0, 2 * sizeof(int32_t), e->stream)) != hipSuccess) return er;

@@ -90,3 +90,50 @@ def test_float_lists_meet_the_reference_fixtures(monkeypatch, path):
     loss, _ = eng.step(z["s0/cells"], float(z["s0/beta"]), eps=eps_of(z, "s0"))
     want = float(z["s0/loss"])
     assert abs(loss - want) <= 2e-5 * abs(want), (loss, want)
+
+
+@pytest.mark.parametrize("model", ["nb", "vmf"])
+def test_dense_rows_many_chunks_packed_reads(monkeypatch, model):
+    """Rows of several thousand entries (the packed reads' refill of two groups ahead) and 16-row
+    blocks past one LDS chunk (~30k entries: several chunks per block): the packed-dataset list
+    builder and the unpacked one (MMVAE_LISTS_PK=0) agree bit for bit.  The float-value lists stage
+    8 bytes an entry, so their chunks end at other tiles; the raw-count dots riding in the builder
+    then sum a row's entries in another lane order, and that format agrees to f32 rounding."""
+    from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
+    D, K, B, N = 20000, 64 if model == "nb" else 32, 256, 600
+
+    def run():
+        eng = Engine(D=D, K=K, max_batch=B, dtype="bf16x3", model=MODEL_VMF if model == "vmf" else MODEL_NB, seed=3)
+        nnz = eng.synth_csr(N, lib_size=40000.0, seed=5)
+        eng.init_params(seed=5)
+        out = []
+        for t in range(2):
+            cells = (np.arange(B, dtype=np.int64) * (3 + 2 * t) + 1) % N
+            out.append(eng.step(cells, 0.7, step_id=t))
+        res = (out, eng.grads(), eng.params(registered_only=True))
+        eng.close()
+        return res, nnz
+
+    for k in ("MMVAE_LISTS_PK", "MMVAE_LISTS_XM"):
+        monkeypatch.delenv(k, raising=False)
+    a, nnz = run()
+    assert nnz / N > 2500, nnz / N  # rows longer than two 1024-entry groups; blocks past one chunk
+    monkeypatch.setenv("MMVAE_LISTS_PK", "0")
+    b, _ = run()
+    monkeypatch.delenv("MMVAE_LISTS_PK")
+    monkeypatch.setenv("MMVAE_LISTS_XM", "1")
+    c, _ = run()
+    _same(a, b)
+    from helpers import rel_err
+    for (la, na), (lc, nc) in zip(a[0], c[0]):
+        assert abs(la - lc) <= 1e-6 * abs(la) and abs(na - nc) <= 1e-5 * abs(na), (la, lc, na, nc)
+    for k in a[1]:
+        assert rel_err(c[1][k], a[1][k]) <= 1e-5, k
+
+
+@pytest.mark.parametrize("model", ["nb", "vmf"])
+def test_dense_rows_live_oracle(model):
+    """The same dense rows (several list chunks per 16-row block) against the live oracle
+    (the reference's op sequence): loss 2e-5, gradients 2e-4 in x3."""
+    from test_gpu_tiling import _run_live
+    _run_live(model, 20000, 64 if model == "nb" else 32, 256, "bf16x3", N=600, lib_size=40000.0, many_tiles=False)

@@ -81,18 +81,19 @@ def _engine_params(eng, shapes):
     return {n: torch.from_numpy(eng.get_param(n, info[n]).reshape(v.shape)) for n, v in shapes.items()}
 
 
-def _run_live(model, D, K, B, dtype, N, relu=False, beta=0.8):
+def _run_live(model, D, K, B, dtype, N, relu=False, beta=0.8, lib_size=2000.0, many_tiles=True):
     from mmvae_amd import MODEL_NB, MODEL_VMF, Engine
     from oracle import nb_oracle, vmf_oracle
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     vmf = model == "vmf"
     eng = Engine(D=D, K=K, max_batch=B, dtype=dtype, seed=1, relu=relu, model=MODEL_VMF if vmf else MODEL_NB)
-    eng.synth_csr(N, lib_size=2000.0, seed=3)
+    eng.synth_csr(N, lib_size=lib_size, seed=3)
     eng.init_params(seed=7)
     if vmf:  # kappa off its floor so its gradient is live (Q4)
         eng.set_param("ln_kappa", np.array([np.log(np.float32(4.0))], np.float32))
     til = eng.tiling()
-    assert til["tps_dec"] > 1 and til["tps_enc"] > 1 and til["tps_ac"] > 1 and til["tps_encb"] > 1, til
+    if many_tiles:
+        assert til["tps_dec"] > 1 and til["tps_enc"] > 1 and til["tps_ac"] > 1 and til["tps_encb"] > 1, til
     cells = (np.arange(B, dtype=np.int64) * 7 + 11) % N  # scattered dataset rows
     rng = np.random.default_rng(5)
     em = rng.standard_normal((B, K)).astype(np.float32)
