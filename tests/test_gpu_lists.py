@@ -137,3 +137,38 @@ def test_dense_rows_live_oracle(model):
     (the reference's op sequence): loss 2e-5, gradients 2e-4 in x3."""
     from test_gpu_tiling import _run_live
     _run_live(model, 20000, 64 if model == "nb" else 32, 256, "bf16x3", N=600, lib_size=40000.0, many_tiles=False)
+
+
+def test_format_switches_on_one_handle(monkeypatch):
+    """One handle through resident integer counts (packed copy, count words), the same data streamed
+    from host memory, a fractional dataset (float-value lists), and integer counts again: every step
+    equals a fresh handle's on the same data bit for bit (the list format, the packed copy and the
+    step graphs follow each upload)."""
+    from mmvae_amd import MODEL_NB, Engine
+    for k in ("MMVAE_LISTS_PK", "MMVAE_LISTS_XM"):
+        monkeypatch.delenv(k, raising=False)
+    D, K, B, N = 3000, 32, 256, 1200
+    ints = _csr(N, D, 23)
+    frac = _csr(N, D, 29, frac=True)
+    cells = (np.arange(B, dtype=np.int64) * 7 + 2) % N
+
+    def fresh(csr, streamed=False):
+        eng = Engine(D=D, K=K, max_batch=B, dtype="bf16x3", model=MODEL_NB, seed=3)
+        (eng.stream_csr if streamed else eng.upload_csr)(*csr)
+        eng.init_params(seed=5)
+        out = eng.step(cells, 0.7, step_id=0), eng.grads()
+        eng.close()
+        return out
+
+    eng = Engine(D=D, K=K, max_batch=B, dtype="bf16x3", model=MODEL_NB, seed=3)
+    eng.graph(True)
+    for csr, streamed in ((ints, False), (ints, True), (frac, False), (ints, False)):
+        (eng.stream_csr if streamed else eng.upload_csr)(*csr)
+        eng.init_params(seed=5)
+        eng.reset_optimizer()
+        got = eng.step(cells, 0.7, step_id=0), eng.grads()
+        want = fresh(csr, streamed)
+        assert got[0] == want[0], (streamed, got[0], want[0])
+        for k in want[1]:
+            np.testing.assert_array_equal(got[1][k], want[1][k], err_msg=f"{k} streamed={streamed}")
+    eng.close()
